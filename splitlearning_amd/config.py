@@ -1,0 +1,143 @@
+"""Command-line configuration, validation and protocol constants.
+
+Flag names, types and defaults mirror the reference launcher
+(`/root/reference/split_nn.py:152-166`) so an existing command line keeps
+working; validation mirrors `split_nn.py:169-174`.  Constants the reference
+hard-codes (`split_nn.py:27-28,44-45`, `models.py:50,52`,
+`data_entities_vanilla_sisa.py:48,266`, `data_entities_vanilla.py:41`) become
+configurable with the same defaults.  Everything below the "framework" banner
+is new: device/placement, dtype, seeding and quirk switches.
+"""
+from __future__ import annotations
+
+import argparse
+from dataclasses import dataclass
+
+# Protocol constants (reference defaults).
+DEFAULT_OMIT_LABEL = 9                 # split_nn.py:45
+DEFAULT_UNLEARN_CLIENTS = (1,)         # split_nn.py:44
+DROPOUT_P = 0.5                        # models.py:50,52
+ADAM_WEIGHT_DECAY = 1e-5               # data_entities_vanilla_sisa.py:48,266
+SGD_MOMENTUM = 0.9                     # data_entities_vanilla.py:41
+TEST_PARTITION = 0.2                   # mnist_flat_generator.py:37
+MIN_SAMPLES_PER_CLIENT = 10            # noniid_partition.py:44
+CUT_FEATURES = 32 * 13 * 13            # models.py:35,49 (5408)
+NUM_CLASSES = 10                       # MNIST
+
+
+MODES = ("ushape", "vanilla", "sisa", "concat", "control")
+
+
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(description="Split Learning Initialization (MI355X-native)")
+    # ---- reference flags (split_nn.py:153-166) ----
+    p.add_argument("--world_size", type=int, default=3,
+                   help="1 server (Bob) + (world_size - 1) clients (Alices)")
+    p.add_argument("--epochs", type=int, default=1,
+                   help="client epochs per train request (local epochs in SISA)")
+    p.add_argument("--iterations", type=int, default=5,
+                   help="round-robin rounds (ignored by SISA / concat, as in the reference)")
+    p.add_argument("--batch_size", type=int, default=16)
+    p.add_argument("--partition_alpha", type=float, default=0.5,
+                   help="Dirichlet concentration for the non-IID partition")
+    p.add_argument("--datapath", type=str, default="data/mnist_flat",
+                   help="directory holding data_worker{k}_{train,test}.pt shards")
+    p.add_argument("--lr", type=float, default=0.001)
+    p.add_argument("--server_epochs", type=int, default=3,
+                   help="Bob's server epochs (SISA)")
+    p.add_argument("--vanilla", action="store_true", help="vanilla split-NN (labels to Bob)")
+    p.add_argument("--sisa", action="store_true", help="SISA split learning + unlearning")
+    p.add_argument("--concat", action="store_true", help="SISA with concatenated client embeddings")
+    p.add_argument("--control", action="store_true", help="retrain-from-scratch control group")
+    # ---- framework flags (new) ----
+    g = p.add_argument_group("framework")
+    g.add_argument("--device", choices=("auto", "cpu", "cuda"), default="auto",
+                   help="auto = one process per visible GPU if any, else CPU processes")
+    g.add_argument("--nprocs", type=int, default=0,
+                   help="number of OS processes (0 = #GPUs on GPU, world_size on CPU)")
+    g.add_argument("--bob_tp", type=int, default=0,
+                   help="tensor-parallel degree of Bob's server tail (0 = all processes on GPU, 1 on CPU)")
+    g.add_argument("--backend", choices=("auto", "nccl", "gloo"), default="auto")
+    g.add_argument("--kernels", choices=("auto", "hip", "torch"), default="auto",
+                   help="compute path: hand-written HIP kernels (GPU) or torch ops")
+    g.add_argument("--seed", type=int, default=None, help="seed everything (reference is unseeded)")
+    g.add_argument("--num_samples", type=int, default=70000,
+                   help="synthetic MNIST-shaped dataset size (no network: fetch_openml unavailable)")
+    g.add_argument("--mnist_npz", type=str, default="",
+                   help="optional local MNIST .npz (x uint8 [N,28,28], y [N]) used instead of synthetic")
+    g.add_argument("--reuse_data", action="store_true",
+                   help="reuse existing shards instead of regenerating (reference regenerates, Q12)")
+    g.add_argument("--log_dir", type=str, default="logs")
+    g.add_argument("--save_dir", type=str, default="",
+                   help="write checkpoints (reference state_dict key names) at the end of the run")
+    g.add_argument("--resume_dir", type=str, default="",
+                   help="load checkpoints written by --save_dir before the schedule starts")
+    g.add_argument("--master_addr", type=str, default="127.0.0.1")
+    g.add_argument("--master_port", type=int, default=5689)
+    g.add_argument("--omit_label", type=int, default=DEFAULT_OMIT_LABEL)
+    g.add_argument("--unlearn_clients", type=str, default="1",
+                   help="comma-separated Alice ids that request unlearning")
+    g.add_argument("--true_reset", action="store_true",
+                   help="re-initialise the client front on unlearn (reference reset is a no-op, Q4)")
+    g.add_argument("--eval_dropout_fix", action="store_true",
+                   help="put Bob in eval mode for vanilla evaluation (reference keeps dropout on, Q7)")
+    g.add_argument("--concat_unlearn", action="store_true",
+                   help="extend the concat schedule with unlearning + retrain (BASELINE config 5)")
+    g.add_argument("--timeout_s", type=float, default=1800.0,
+                   help="bounded wait for every collective / control message")
+    g.add_argument("--no_tqdm", action="store_true")
+    g.add_argument("--graphs", choices=("auto", "on", "off"), default="auto",
+                   help="capture Bob's fixed-shape server step in a HIP graph")
+    return p
+
+
+def validate(args: argparse.Namespace) -> argparse.Namespace:
+    """Reference validation (`split_nn.py:169-174`) plus derived fields."""
+    if args.concat and not args.sisa:
+        raise ValueError("The --concat option can only be used with the --sisa option.")
+    if args.vanilla and (args.sisa or args.concat):
+        raise ValueError("The --vanilla option cannot be used with --sisa or --concat.")
+    if args.control and (args.vanilla or args.sisa or args.concat):
+        raise ValueError("The --control option cannot be used with any other options.")
+    if args.world_size < 2:
+        raise ValueError("--world_size must be >= 2 (one Bob and at least one Alice)")
+    if args.batch_size < 1:
+        raise ValueError("--batch_size must be >= 1")
+    args.client_num_in_total = args.world_size - 1          # split_nn.py:176
+    args.class_num = NUM_CLASSES
+    args.mode = mode_of(args)
+    ids = [int(s) for s in str(args.unlearn_clients).split(",") if s.strip()]
+    for i in ids:
+        if not 1 <= i <= args.client_num_in_total:
+            raise ValueError(f"unlearn client {i} is not an Alice id in 1..{args.client_num_in_total}")
+    args.unlearn_client_ids = ids
+    return args
+
+
+def mode_of(args) -> str:
+    """Dispatch precedence of `split_nn.py:13-23`; --control gets SISA semantics (Q2)."""
+    if args.vanilla:
+        return "vanilla"
+    if args.concat:
+        return "concat"
+    if args.sisa:
+        return "sisa"
+    if args.control:
+        return "control"
+    return "ushape"
+
+
+def parse_args(argv=None) -> argparse.Namespace:
+    return validate(build_parser().parse_args(argv))
+
+
+@dataclass
+class OptimCfg:
+    """Hyper-parameters of one optimizer slot (fused kernels read these)."""
+    kind: str            # "adam" | "sgd"
+    lr: float
+    beta1: float = 0.9
+    beta2: float = 0.999
+    eps: float = 1e-8
+    weight_decay: float = 0.0
+    momentum: float = 0.0

@@ -1,0 +1,294 @@
+// Python bindings for the gfx950 kernels (pybind11 module `splitlearning_amd._C`).
+//
+// Thin by design: validate shapes/dtypes/devices on the host (a kernel must never
+// see an operand its grid does not assume), fetch the current HIP stream from the
+// PyTorch-ROCm stream registry, and call the launcher.  All buffers are
+// caller-allocated so the same calls can be captured into a HIP graph.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+#include "common.h"
+
+namespace sl {
+hipError_t conv_fwd(const void* x, bool x_u8, const int64_t* idx, int64_t row0, int B, const float* w,
+                    const float* b, float* y, uint8_t* am, hipStream_t st);
+hipError_t conv_bwd_opt(const float* dy, const float* y, const uint8_t* am, const void* x, bool x_u8,
+                        const int64_t* idx, int64_t row0, int B, float* w, float* b, float* s0w, float* s1w,
+                        float* s0b, float* s1b, SlOpt o, hipStream_t st);
+hipError_t linear_fwd(const float* X, int ldx, const float* W, int ldw, float* Y, int ldy, int M, int N, int K,
+                      Epi e, hipStream_t st);
+hipError_t linear_dgrad(const float* dZ, int ldz, const float* W, int ldw, const float* hprev, int ldh,
+                        float scale, float* dX, int ldx, float* ws, int64_t ws_elems, int M, int N, int K,
+                        hipStream_t st);
+hipError_t linear_epilogue(const float* P, int ldp, float* Y, int ldy, int M, int N, Epi e, hipStream_t st);
+hipError_t linear_wgrad_opt(const float* dZ, int ldz, const float* A, int lda, float* W, int ldw, float* s0,
+                            float* s1, float* bias, float* sb0, float* sb1, int M, int N, int K, SlOpt o,
+                            hipStream_t st);
+hipError_t opt_flat(float* p, const float* g, float* s0, float* s1, int64_t n, SlOpt o, hipStream_t st);
+hipError_t softmax_ce(const float* x, int ldx, const int64_t* y, int64_t ignore, float scale, float* loss_rows,
+                      float* d, int ldd, int M, int C, hipStream_t st);
+hipError_t eval_counters(const float* x, int ldx, const int64_t* y, int64_t omit, unsigned long long* counters,
+                         int M, int C, hipStream_t st);
+}  // namespace sl
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check(hipError_t e, const char* what) {
+  TORCH_CHECK(e == hipSuccess, what, ": ", hipGetErrorString(e));
+}
+
+void need_cuda(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+}
+void need_f32(const at::Tensor& t, const char* name) {
+  need_cuda(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kFloat, name, " must be float32");
+}
+// row-major 2-D with unit column stride, 16-byte aligned rows (float4 loads)
+void need_rows(const at::Tensor& t, const char* name) {
+  need_f32(t, name);
+  TORCH_CHECK(t.dim() == 2 && t.stride(1) == 1, name, " must be 2-D with unit column stride");
+  TORCH_CHECK(t.stride(0) % 4 == 0 && (reinterpret_cast<uintptr_t>(t.data_ptr()) % 16) == 0, name,
+              " rows must be 16-byte aligned");
+}
+// 2-D with unit column stride (scalar access only)
+void need_2d(const at::Tensor& t, const char* name) {
+  need_f32(t, name);
+  TORCH_CHECK(t.dim() == 2 && t.stride(1) == 1, name, " must be 2-D with unit column stride");
+}
+float* fptr(const c10::optional<at::Tensor>& t) {
+  return t.has_value() && t->defined() ? t->data_ptr<float>() : nullptr;
+}
+
+SlOpt make_opt(int64_t kind, double lr, double beta1, double beta2, double eps, double wd, double momentum,
+                   int64_t t) {
+  SlOpt o{};
+  o.kind = (int)kind;
+  o.lr = (float)lr;
+  o.beta1 = (float)beta1;
+  o.beta2 = (float)beta2;
+  o.eps = (float)eps;
+  o.wd = (float)wd;
+  o.momentum = (float)momentum;
+  if (kind == 2) {
+    TORCH_CHECK(t >= 1, "Adam step count must be >= 1");
+    const double bc1 = 1.0 - std::pow(beta1, (double)t);
+    const double bc2 = 1.0 - std::pow(beta2, (double)t);
+    o.step_size = (float)(lr / bc1);
+    o.inv_bc2_sqrt = (float)(1.0 / std::sqrt(bc2));
+  }
+  return o;
+}
+
+Epi make_epi(const c10::optional<at::Tensor>& bias, bool relu, double drop_p, uint64_t seed, int64_t col_off) {
+  Epi e{};
+  e.bias = bias.has_value() && bias->defined() ? bias->data_ptr<float>() : nullptr;
+  e.relu = relu ? 1 : 0;
+  e.thresh = drop_p > 0 ? (uint32_t)(drop_p * 4294967296.0) : 0u;
+  e.dscale = drop_p > 0 ? (float)(1.0 / (1.0 - drop_p)) : 1.f;
+  e.seed_lo = (uint32_t)(seed & 0xffffffffull);
+  e.seed_hi = (uint32_t)(seed >> 32);
+  e.col_off = (int)col_off;
+  return e;
+}
+
+// ---------------------------------------------------------------- conv
+void conv_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& idx, int64_t row0, int64_t B,
+              const at::Tensor& w, const at::Tensor& b, at::Tensor& y, at::Tensor& am) {
+  need_cuda(x, "x");
+  TORCH_CHECK(x.is_contiguous() && x.numel() % 784 == 0, "x must be contiguous [N,784]");
+  const bool u8 = x.scalar_type() == at::kByte;
+  TORCH_CHECK(u8 || x.scalar_type() == at::kFloat, "x must be uint8 or float32");
+  const int64_t nrows = x.numel() / 784;
+  need_f32(w, "w");
+  need_f32(b, "b");
+  TORCH_CHECK(w.numel() == 288 && b.numel() == 32 && w.is_contiguous() && b.is_contiguous(), "conv params 32x1x3x3");
+  need_f32(y, "y");
+  TORCH_CHECK(y.is_contiguous() && y.numel() >= B * 5408, "y too small");
+  TORCH_CHECK(am.scalar_type() == at::kByte && am.is_contiguous() && am.numel() >= B * 5408, "am too small");
+  const int64_t* ip = nullptr;
+  if (idx.has_value() && idx->defined()) {
+    TORCH_CHECK(idx->scalar_type() == at::kLong && idx->is_contiguous() && idx->numel() >= B, "idx int64 [B]");
+    need_cuda(*idx, "idx");
+    ip = idx->data_ptr<int64_t>();
+  } else {
+    TORCH_CHECK(row0 >= 0 && row0 + B <= nrows, "row range out of bounds");
+  }
+  check(sl::conv_fwd(x.data_ptr(), u8, ip, row0, (int)B, w.data_ptr<float>(), b.data_ptr<float>(),
+                     y.data_ptr<float>(), am.data_ptr<uint8_t>(), cur_stream()),
+        "conv_fwd");
+}
+
+void conv_bwd_opt(const at::Tensor& dy, const at::Tensor& y, const at::Tensor& am, const at::Tensor& x,
+                  const c10::optional<at::Tensor>& idx, int64_t row0, int64_t B, at::Tensor& w, at::Tensor& b,
+                  at::Tensor& s0w, const c10::optional<at::Tensor>& s1w, at::Tensor& s0b,
+                  const c10::optional<at::Tensor>& s1b, int64_t kind, double lr, double beta1, double beta2,
+                  double eps, double wd, double momentum, int64_t t) {
+  need_f32(dy, "dy");
+  need_f32(y, "y");
+  TORCH_CHECK(dy.is_contiguous() && y.is_contiguous() && dy.numel() >= B * 5408 && y.numel() >= B * 5408, "dy/y");
+  TORCH_CHECK(am.scalar_type() == at::kByte && am.numel() >= B * 5408, "am");
+  need_cuda(x, "x");
+  const bool u8 = x.scalar_type() == at::kByte;
+  const int64_t nrows = x.numel() / 784;
+  const int64_t* ip = nullptr;
+  if (idx.has_value() && idx->defined()) {
+    TORCH_CHECK(idx->scalar_type() == at::kLong && idx->numel() >= B, "idx int64 [B]");
+    ip = idx->data_ptr<int64_t>();
+  } else {
+    TORCH_CHECK(row0 >= 0 && row0 + B <= nrows, "row range out of bounds");
+  }
+  TORCH_CHECK(w.numel() == 288 && b.numel() == 32 && s0w.numel() == 288 && s0b.numel() == 32, "conv param/state");
+  check(sl::conv_bwd_opt(dy.data_ptr<float>(), y.data_ptr<float>(), am.data_ptr<uint8_t>(), x.data_ptr(), u8, ip,
+                         row0, (int)B, w.data_ptr<float>(), b.data_ptr<float>(), s0w.data_ptr<float>(), fptr(s1w),
+                         s0b.data_ptr<float>(), fptr(s1b), make_opt(kind, lr, beta1, beta2, eps, wd, momentum, t),
+                         cur_stream()),
+        "conv_bwd_opt");
+}
+
+// ---------------------------------------------------------------- linear
+void linear_fwd(const at::Tensor& X, const at::Tensor& W, const c10::optional<at::Tensor>& bias, at::Tensor& Y,
+                bool relu, double drop_p, uint64_t seed, int64_t col_off) {
+  need_rows(X, "X");
+  need_rows(W, "W");
+  need_2d(Y, "Y");
+  const int64_t M = X.size(0), K = X.size(1), N = W.size(0);
+  TORCH_CHECK(W.size(1) == K && K % 4 == 0, "W must be [N,K] with K % 4 == 0");
+  TORCH_CHECK(Y.size(0) == M && Y.size(1) == N, "Y must be [M,N]");
+  if (bias.has_value() && bias->defined()) TORCH_CHECK(bias->numel() == N && bias->is_contiguous(), "bias [N]");
+  check(sl::linear_fwd(X.data_ptr<float>(), (int)X.stride(0), W.data_ptr<float>(), (int)W.stride(0),
+                       Y.data_ptr<float>(), (int)Y.stride(0), (int)M, (int)N, (int)K,
+                       make_epi(bias, relu, drop_p, seed, col_off), cur_stream()),
+        "linear_fwd");
+}
+
+void linear_epilogue(const at::Tensor& P, const c10::optional<at::Tensor>& bias, at::Tensor& Y, bool relu,
+                     double drop_p, uint64_t seed, int64_t col_off) {
+  need_f32(P, "P");
+  need_f32(Y, "Y");
+  TORCH_CHECK(P.dim() == 2 && Y.dim() == 2 && P.stride(1) == 1 && Y.stride(1) == 1, "2-D row-major");
+  TORCH_CHECK(P.sizes() == Y.sizes(), "P/Y shape");
+  check(sl::linear_epilogue(P.data_ptr<float>(), (int)P.stride(0), Y.data_ptr<float>(), (int)Y.stride(0),
+                            (int)P.size(0), (int)P.size(1), make_epi(bias, relu, drop_p, seed, col_off),
+                            cur_stream()),
+        "linear_epilogue");
+}
+
+void linear_dgrad(const at::Tensor& dZ, const at::Tensor& W, const c10::optional<at::Tensor>& hprev, double scale,
+                  at::Tensor& dX, const c10::optional<at::Tensor>& ws) {
+  need_2d(dZ, "dZ");
+  need_rows(W, "W");
+  need_2d(dX, "dX");
+  const int64_t M = dZ.size(0), N = dZ.size(1), K = W.size(1);
+  TORCH_CHECK(W.size(0) == N && K % 4 == 0, "W must be [N,K]");
+  TORCH_CHECK(dX.size(0) == M && dX.size(1) == K, "dX must be [M,K]");
+  const float* hp = nullptr;
+  int ldh = 0;
+  if (hprev.has_value() && hprev->defined()) {
+    need_f32(*hprev, "hprev");
+    TORCH_CHECK(hprev->dim() == 2 && hprev->size(0) == M && hprev->size(1) == K && hprev->stride(1) == 1, "hprev");
+    hp = hprev->data_ptr<float>();
+    ldh = (int)hprev->stride(0);
+  }
+  float* wp = nullptr;
+  int64_t wn = 0;
+  if (ws.has_value() && ws->defined()) {
+    need_f32(*ws, "ws");
+    TORCH_CHECK(ws->is_contiguous(), "ws contiguous");
+    wp = ws->data_ptr<float>();
+    wn = ws->numel();
+  }
+  check(sl::linear_dgrad(dZ.data_ptr<float>(), (int)dZ.stride(0), W.data_ptr<float>(), (int)W.stride(0), hp, ldh,
+                         (float)scale, dX.data_ptr<float>(), (int)dX.stride(0), wp, wn, (int)M, (int)N, (int)K,
+                         cur_stream()),
+        "linear_dgrad");
+}
+
+void linear_wgrad_opt(const at::Tensor& dZ, const at::Tensor& A, at::Tensor& W, at::Tensor& s0,
+                      const c10::optional<at::Tensor>& s1, const c10::optional<at::Tensor>& bias,
+                      const c10::optional<at::Tensor>& sb0, const c10::optional<at::Tensor>& sb1, int64_t kind,
+                      double lr, double beta1, double beta2, double eps, double wd, double momentum, int64_t t) {
+  need_2d(dZ, "dZ");
+  need_rows(A, "A");
+  need_rows(W, "W");
+  need_rows(s0, "s0");
+  const int64_t M = dZ.size(0), N = dZ.size(1), K = A.size(1);
+  TORCH_CHECK(A.size(0) == M && W.size(0) == N && W.size(1) == K && K % 4 == 0, "shapes");
+  TORCH_CHECK(s0.sizes() == W.sizes() && s0.stride(0) == W.stride(0), "s0 like W");
+  if (s1.has_value() && s1->defined()) TORCH_CHECK(s1->sizes() == W.sizes() && s1->stride(0) == W.stride(0), "s1");
+  if (kind == 2) TORCH_CHECK(s1.has_value() && s1->defined(), "Adam needs s1");
+  if (bias.has_value() && bias->defined())
+    TORCH_CHECK(bias->numel() == N && sb0.has_value() && sb0->numel() == N, "bias state");
+  check(sl::linear_wgrad_opt(dZ.data_ptr<float>(), (int)dZ.stride(0), A.data_ptr<float>(), (int)A.stride(0),
+                             W.data_ptr<float>(), (int)W.stride(0), s0.data_ptr<float>(), fptr(s1), fptr(bias),
+                             fptr(sb0), fptr(sb1), (int)M, (int)N, (int)K,
+                             make_opt(kind, lr, beta1, beta2, eps, wd, momentum, t), cur_stream()),
+        "linear_wgrad_opt");
+}
+
+void opt_flat(at::Tensor& p, const at::Tensor& g, at::Tensor& s0, const c10::optional<at::Tensor>& s1,
+              int64_t kind, double lr, double beta1, double beta2, double eps, double wd, double momentum,
+              int64_t t) {
+  need_f32(p, "p");
+  need_f32(g, "g");
+  need_f32(s0, "s0");
+  TORCH_CHECK(p.is_contiguous() && g.is_contiguous() && s0.is_contiguous(), "contiguous");
+  TORCH_CHECK(g.numel() == p.numel() && s0.numel() == p.numel(), "sizes");
+  check(sl::opt_flat(p.data_ptr<float>(), g.data_ptr<float>(), s0.data_ptr<float>(), fptr(s1), p.numel(),
+                     make_opt(kind, lr, beta1, beta2, eps, wd, momentum, t), cur_stream()),
+        "opt_flat");
+}
+
+// ---------------------------------------------------------------- loss / metrics
+void softmax_ce(const at::Tensor& x, const at::Tensor& y, int64_t ignore, double scale, at::Tensor& loss_rows,
+                const c10::optional<at::Tensor>& d) {
+  need_f32(x, "logits");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "logits 2-D");
+  const int64_t M = x.size(0), C = x.size(1);
+  need_cuda(y, "labels");
+  TORCH_CHECK(y.scalar_type() == at::kLong && y.numel() == M && y.is_contiguous(), "labels int64 [M]");
+  need_f32(loss_rows, "loss_rows");
+  TORCH_CHECK(loss_rows.numel() >= M, "loss_rows");
+  float* dp = nullptr;
+  int ldd = 0;
+  if (d.has_value() && d->defined()) {
+    need_f32(*d, "dlogits");
+    TORCH_CHECK(d->dim() == 2 && d->size(0) == M && d->size(1) == C && d->stride(1) == 1, "dlogits");
+    dp = d->data_ptr<float>();
+    ldd = (int)d->stride(0);
+  }
+  check(sl::softmax_ce(x.data_ptr<float>(), (int)x.stride(0), y.data_ptr<int64_t>(), ignore, (float)scale,
+                       loss_rows.data_ptr<float>(), dp, ldd, (int)M, (int)C, cur_stream()),
+        "softmax_ce");
+}
+
+void eval_counters(const at::Tensor& x, const at::Tensor& y, int64_t omit, at::Tensor& counters) {
+  need_f32(x, "logits");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "logits 2-D");
+  TORCH_CHECK(y.scalar_type() == at::kLong && y.numel() == x.size(0) && y.is_contiguous(), "labels");
+  TORCH_CHECK(counters.scalar_type() == at::kLong && counters.numel() >= 6 && counters.is_contiguous(), "counters");
+  need_cuda(counters, "counters");
+  check(sl::eval_counters(x.data_ptr<float>(), (int)x.stride(0), y.data_ptr<int64_t>(), omit,
+                          reinterpret_cast<unsigned long long*>(counters.data_ptr<int64_t>()), (int)x.size(0),
+                          (int)x.size(1), cur_stream()),
+        "eval_counters");
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "splitlearning_amd gfx950 (MI355X) HIP kernels";
+  m.def("conv_fwd", &conv_fwd);
+  m.def("conv_bwd_opt", &conv_bwd_opt);
+  m.def("linear_fwd", &linear_fwd);
+  m.def("linear_epilogue", &linear_epilogue);
+  m.def("linear_dgrad", &linear_dgrad);
+  m.def("linear_wgrad_opt", &linear_wgrad_opt);
+  m.def("opt_flat", &opt_flat);
+  m.def("softmax_ce", &softmax_ce);
+  m.def("eval_counters", &eval_counters);
+  m.attr("arch") = "gfx950";
+}

@@ -1,0 +1,78 @@
+// Shared device helpers for the splitlearning_amd gfx950 kernels.
+//
+// Everything here is CDNA4-native: wave64 reductions, counter-based dropout
+// hash (bit-identical to ops/rng.py), and the fused optimizer update used by
+// every "gradient + step" kernel (torch.optim.SGD / Adam semantics, see
+// ops/torch_ops.py::adam_update_ / sgd_update_).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define SL_WAVE 64
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------------ RNG
+__device__ __forceinline__ uint32_t sl_fmix32(uint32_t x) {
+  x ^= x >> 16; x *= 0x85EBCA6Bu; x ^= x >> 13; x *= 0xC2B2AE35u; x ^= x >> 16;
+  return x;
+}
+// keep iff hash >= thresh, thresh = p * 2^32 (host computes it).
+__device__ __forceinline__ bool sl_hash_keep(uint32_t seed_lo, uint32_t seed_hi, uint32_t row,
+                                             uint32_t col, uint32_t thresh) {
+  uint32_t a = sl_fmix32((row * 0x9E3779B1u) ^ seed_lo);
+  uint32_t h = sl_fmix32(a ^ ((col * 0x85EBCA77u) ^ seed_hi));
+  return h >= thresh;
+}
+
+// ------------------------------------------------------------------ reductions
+__device__ __forceinline__ float sl_wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float sl_wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ------------------------------------------------------------------ optimizer
+// kind: 0 = write gradient only (p untouched, grad -> s0), 1 = SGD(momentum), 2 = Adam (L2 wd).
+struct SlOpt {
+  int kind;
+  float lr;
+  float beta1, beta2, eps, wd, momentum;
+  float step_size;     // Adam: lr / (1 - beta1^t)
+  float inv_bc2_sqrt;  // Adam: 1 / sqrt(1 - beta2^t)
+};
+
+// Update one element. s0 = m (Adam) / momentum buffer (SGD) / grad out (kind 0); s1 = v (Adam).
+__device__ __forceinline__ void sl_opt_update(const SlOpt& o, float& p, float g, float& s0, float& s1) {
+  if (o.kind == 0) { s0 = g; return; }
+  if (o.wd != 0.f) g = fmaf(o.wd, p, g);
+  if (o.kind == 1) {
+    float b = (o.momentum != 0.f) ? fmaf(o.momentum, s0, g) : g;
+    s0 = b;
+    p = fmaf(-o.lr, b, p);
+  } else {
+    float m = fmaf(o.beta1, s0, (1.f - o.beta1) * g);
+    float v = fmaf(o.beta2, s1, (1.f - o.beta2) * g * g);
+    s0 = m; s1 = v;
+    float denom = sqrtf(v) * o.inv_bc2_sqrt + o.eps;
+    p = p - o.step_size * (m / denom);
+  }
+}
+
+
+// Fused GEMM epilogue: bias, ReLU, counter-hash dropout (global column index).
+struct Epi {
+  const float* bias;
+  int relu;
+  uint32_t thresh;      // dropout keep iff hash >= thresh (0 = no dropout)
+  float dscale;         // 1/(1-p)
+  uint32_t seed_lo, seed_hi;
+  int col_off;          // global column index of column 0 (tensor-parallel shards)
+};
+
+#define SL_CHECK_LAUNCH() (hipGetLastError())

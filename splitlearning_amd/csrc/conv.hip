@@ -1,0 +1,150 @@
+// Client-front kernels: fused gather + conv3x3(1->32) + bias + ReLU + maxpool2x2
+// forward, and fused pool/ReLU backward + weight/bias gradient + optimizer step.
+//
+// Reference ops: models.py:8-9,21-23 (Conv2d(1,32,3) -> ReLU -> MaxPool(2,2)),
+// trained with Adam(wd=1e-5) (data_entities_vanilla_sisa.py:48) or SGD-m via the
+// DistributedOptimizer (data_entities_vanilla.py:37-42).  SURVEY §2.7 K1-K3, K13.
+//
+// The conv has K = 9 (one input channel), far too small for MFMA, so it is a
+// direct LDS-tiled convolution: one 256-thread workgroup per sample stages the
+// 28x28 image (converted from the uint8 shard row it gathers itself, so there
+// is no separate collate/convert kernel) and 32x9 weights in LDS and writes the
+// pooled, NCHW-flattened [5408] activation plus a 2-bit argmax for backward.
+#include "common.h"
+
+namespace sl {
+
+template <typename XT>
+__global__ void __launch_bounds__(256)
+conv_relu_pool_fwd_kernel(const XT* __restrict__ x, const int64_t* __restrict__ idx, int64_t row0,
+                          const float* __restrict__ w, const float* __restrict__ b,
+                          float* __restrict__ y, uint8_t* __restrict__ am) {
+  __shared__ float img[28 * 28];
+  __shared__ float sw[32 * 9];
+  __shared__ float sb[32];
+  const int s = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int64_t src = idx ? idx[s] : row0 + s;
+  const XT* xr = x + src * 784;
+  for (int i = tid; i < 784; i += 256) img[i] = (float)xr[i];
+  for (int i = tid; i < 288; i += 256) sw[i] = w[i];
+  if (tid < 32) sb[tid] = b[tid];
+  __syncthreads();
+  float* yo = y + (int64_t)s * 5408;
+  uint8_t* ao = am + (int64_t)s * 5408;
+  for (int o = tid; o < 5408; o += 256) {
+    const int oc = o / 169;
+    const int r = o - oc * 169;
+    const int ph = r / 13;
+    const int pw = r - ph * 13;
+    const float* wk = sw + oc * 9;
+    const float* base = img + (2 * ph) * 28 + 2 * pw;
+    float patch[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) patch[i][j] = base[i * 28 + j];
+    float best = 0.f;
+    int arg = 0;
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < 2; ++dx) {
+        float acc = 0.f;
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+          for (int kw = 0; kw < 3; ++kw) acc = fmaf(wk[kh * 3 + kw], patch[dy + kh][dx + kw], acc);
+        acc += sb[oc];
+        const int pos = dy * 2 + dx;
+        if (pos == 0 || acc > best) { best = acc; arg = pos; }   // first max (torch order)
+      }
+    yo[o] = fmaxf(best, 0.f);
+    ao[o] = (uint8_t)arg;
+  }
+}
+
+// One workgroup per output channel: reduce dW[oc,0:9], db[oc] over the batch, then
+// apply the optimizer to this channel's 10 parameters (no cross-block dependency).
+template <typename XT>
+__global__ void __launch_bounds__(256)
+conv_bwd_opt_kernel(const float* __restrict__ dy, const float* __restrict__ y,
+                    const uint8_t* __restrict__ am, const XT* __restrict__ x,
+                    const int64_t* __restrict__ idx, int64_t row0, int B,
+                    float* __restrict__ w, float* __restrict__ b,
+                    float* __restrict__ s0w, float* __restrict__ s1w,
+                    float* __restrict__ s0b, float* __restrict__ s1b, SlOpt o) {
+  const int oc = blockIdx.x;
+  const int tid = threadIdx.x;
+  float acc[10];
+#pragma unroll
+  for (int j = 0; j < 10; ++j) acc[j] = 0.f;
+  const int total = B * 169;
+  for (int t = tid; t < total; t += 256) {
+    const int s = t / 169;
+    const int r = t - s * 169;
+    const int64_t off = (int64_t)s * 5408 + oc * 169 + r;
+    if (y[off] <= 0.f) continue;
+    const float g = dy[off];
+    const int a = am[off];
+    const int ph = r / 13, pw = r - (r / 13) * 13;
+    const int row = 2 * ph + (a >> 1), col = 2 * pw + (a & 1);
+    const int64_t src = idx ? idx[s] : row0 + s;
+    const XT* xr = x + src * 784 + row * 28 + col;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) acc[kh * 3 + kw] = fmaf(g, (float)xr[kh * 28 + kw], acc[kh * 3 + kw]);
+    acc[9] += g;
+  }
+  __shared__ float red[4][10];
+  const int lane = tid & 63, wv = tid >> 6;
+#pragma unroll
+  for (int j = 0; j < 10; ++j) {
+    float v = sl_wave_sum(acc[j]);
+    if (lane == 0) red[wv][j] = v;
+  }
+  __syncthreads();
+  if (tid < 10) {
+    const float g = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+    if (tid < 9) {
+      const int k = oc * 9 + tid;
+      float p = w[k], a0 = s0w[k], a1 = s1w ? s1w[k] : 0.f;
+      sl_opt_update(o, p, g, a0, a1);
+      if (o.kind != 0) w[k] = p;
+      s0w[k] = a0;
+      if (s1w) s1w[k] = a1;
+    } else {
+      float p = b[oc], a0 = s0b[oc], a1 = s1b ? s1b[oc] : 0.f;
+      sl_opt_update(o, p, g, a0, a1);
+      if (o.kind != 0) b[oc] = p;
+      s0b[oc] = a0;
+      if (s1b) s1b[oc] = a1;
+    }
+  }
+}
+
+hipError_t conv_fwd(const void* x, bool x_u8, const int64_t* idx, int64_t row0, int B,
+                    const float* w, const float* b, float* y, uint8_t* am, hipStream_t st) {
+  if (B <= 0) return hipSuccess;
+  if (x_u8)
+    conv_relu_pool_fwd_kernel<uint8_t><<<B, 256, 0, st>>>((const uint8_t*)x, idx, row0, w, b, y, am);
+  else
+    conv_relu_pool_fwd_kernel<float><<<B, 256, 0, st>>>((const float*)x, idx, row0, w, b, y, am);
+  return hipGetLastError();
+}
+
+hipError_t conv_bwd_opt(const float* dy, const float* y, const uint8_t* am, const void* x, bool x_u8,
+                        const int64_t* idx, int64_t row0, int B, float* w, float* b, float* s0w,
+                        float* s1w, float* s0b, float* s1b, SlOpt o, hipStream_t st) {
+  if (B <= 0) return hipSuccess;
+  if (x_u8)
+    conv_bwd_opt_kernel<uint8_t><<<32, 256, 0, st>>>(dy, y, am, (const uint8_t*)x, idx, row0, B, w, b,
+                                                     s0w, s1w, s0b, s1b, o);
+  else
+    conv_bwd_opt_kernel<float><<<32, 256, 0, st>>>(dy, y, am, (const float*)x, idx, row0, B, w, b,
+                                                   s0w, s1w, s0b, s1b, o);
+  return hipGetLastError();
+}
+
+}  // namespace sl

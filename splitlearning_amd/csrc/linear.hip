@@ -1,0 +1,342 @@
+// Skinny Linear-layer kernels for Bob's server tail and the U-shape head.
+//
+// Reference ops: nn.Linear fc1/fc2/fc3 (models.py:36-37,49-53,69-73,90) with the
+// ReLU / Dropout(0.5) that follow them, trained by SGD-m (vanilla,
+// data_entities_vanilla.py:37-42) or Adam (U-shape data_entities.py:43-47; SISA
+// Adam(wd=1e-5) data_entities_vanilla_sisa.py:266).  SURVEY §2.7 K5-K8, K11-K12.
+//
+// Shape regime: M = batch (16 by default) rows against weights of up to
+// 5000 x 5408 (108 MB fp32).  At M = 16 every kernel is bound by streaming the
+// weight / optimizer state through HBM, so the design goal is bytes, not FLOPs:
+//   * forward  Y = X W^T: exact-fp32 MFMA (v_mfma_f32_16x16x4_f32), one 16-column
+//     tile per workgroup, the workgroup's waves split K and reduce through LDS,
+//     bias + ReLU + dropout fused in the epilogue (no second pass over Y);
+//   * dgrad    dX = dZ W: same MFMA, a 64-column K tile per workgroup, waves split
+//     N, optional split-N across workgroups, ReLU/dropout backward of the *previous*
+//     layer fused into the store;
+//   * wgrad + optimizer: dW is never materialised.  Each thread owns 4 adjacent
+//     weights of R rows, recomputes g = sum_m dZ[m,n] X[m,k] from registers, and
+//     applies SGD-momentum / Adam in place: 24 B of HBM traffic per parameter
+//     (p, m, v read + write) instead of 36 B for wgrad-then-optimizer.
+#include "common.h"
+
+namespace sl {
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+
+__device__ __forceinline__ float apply_epi(const Epi& e, float v, int m, int n) {
+  if (e.bias) v += e.bias[n];
+  if (e.relu) v = fmaxf(v, 0.f);
+  if (e.thresh) v = sl_hash_keep(e.seed_lo, e.seed_hi, (uint32_t)m, (uint32_t)(e.col_off + n), e.thresh) ? v * e.dscale : 0.f;
+  return v;
+}
+
+// ---------------------------------------------------------------------------- forward
+// grid (ceil(N/16), ceil(M/16)), block NW*64.  Requires K % 4 == 0, ldx/ldw % 4 == 0.
+template <int NW>
+__global__ void __launch_bounds__(NW * 64)
+skinny_fwd_kernel(const float* __restrict__ X, int ldx, const float* __restrict__ W, int ldw,
+                  float* __restrict__ Y, int ldy, int M, int N, int K, Epi e) {
+  __shared__ f32x4 red[NW][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int n0 = blockIdx.x * 16, m0 = blockIdx.y * 16;
+  const int kper = ((K + 16 * NW - 1) / (16 * NW)) * 16;
+  const int kb = wv * kper;
+  const int ke = min(K, kb + kper);
+  const int ra = m0 + (lane & 15), rb = n0 + (lane & 15);
+  const int kq = (lane >> 4) * 4;
+  const bool va = ra < M, vb = rb < N;
+  const float* pa = X + (int64_t)(va ? ra : 0) * ldx;
+  const float* pb = W + (int64_t)(vb ? rb : 0) * ldw;
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  int k = kb;
+  // main loop: 64 k per iteration, 4 independent float4 pairs in flight per lane
+  for (; k + 64 <= ke; k += 64) {
+    float4 a[4], w[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      a[u] = va ? ld4(pa + k + 16 * u + kq) : z4;
+      w[u] = vb ? ld4(pb + k + 16 * u + kq) : z4;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      acc0 = mfma4(a[u].x, w[u].x, acc0);
+      acc1 = mfma4(a[u].y, w[u].y, acc1);
+      acc0 = mfma4(a[u].z, w[u].z, acc0);
+      acc1 = mfma4(a[u].w, w[u].w, acc1);
+    }
+  }
+  for (; k < ke; k += 16) {
+    const int kk = k + kq;
+    const bool in = kk < ke;
+    float4 a = (va && in) ? ld4(pa + kk) : z4;
+    float4 w = (vb && in) ? ld4(pb + kk) : z4;
+    acc0 = mfma4(a.x, w.x, acc0);
+    acc1 = mfma4(a.y, w.y, acc1);
+    acc0 = mfma4(a.z, w.z, acc0);
+    acc1 = mfma4(a.w, w.w, acc1);
+  }
+  red[wv][lane] = acc0 + acc1;
+  __syncthreads();
+  if (wv == 0) {
+    f32x4 s = red[0][lane];
+#pragma unroll
+    for (int i = 1; i < NW; ++i) s += red[i][lane];
+    const int n = n0 + (lane & 15);
+    if (n < N) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + (lane >> 4) * 4 + r;
+        if (m < M) Y[(int64_t)m * ldy + n] = apply_epi(e, s[r], m, n);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------- dgrad
+// dX[M,K] = dZ[M,N] . W[N,K]; grid (ceil(K/64), ceil(M/16), S), block NW*64.
+// S == 1: store with the fused mask (h_prev > 0) * scale.  S > 1: store raw partial
+// sums to P[s][M][K] (reduced by dgrad_reduce_kernel).  Requires K % 4 == 0.
+template <int NW>
+__global__ void __launch_bounds__(NW * 64)
+skinny_dgrad_kernel(const float* __restrict__ dZ, int ldz, const float* __restrict__ W, int ldw,
+                    const float* __restrict__ hprev, int ldh, float scale,
+                    float* __restrict__ out, int ldo, int64_t slab, int M, int N, int K) {
+  __shared__ f32x4 red[NW][4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int k0 = blockIdx.x * 64, m0 = blockIdx.y * 16;
+  const int S = gridDim.z, sidx = blockIdx.z;
+  // N range for this workgroup, then for this wave (multiples of 4)
+  const int nblk = ((N + 4 * S - 1) / (4 * S)) * 4;
+  const int nb0 = sidx * nblk, ne0 = min(N, nb0 + nblk);
+  const int nper = (((ne0 - nb0) + 4 * NW - 1) / (4 * NW)) * 4;
+  const int nb = nb0 + wv * nper;
+  const int ne = min(ne0, nb + nper);
+  const int i = lane & 15, q = lane >> 4;
+  const int kcol = k0 + 4 * i;
+  const bool vk = kcol < K;
+  const bool vm = (m0 + i) < M;
+  const float* za = dZ + (int64_t)(vm ? m0 + i : 0) * ldz;
+  f32x4 acc[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) acc[c] = {0.f, 0.f, 0.f, 0.f};
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  int n = nb;
+  for (; n + 16 <= ne; n += 16) {
+    float a[4];
+    float4 w[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int nn = n + 4 * u + q;
+      a[u] = vm ? za[nn] : 0.f;
+      w[u] = vk ? ld4(W + (int64_t)nn * ldw + kcol) : z4;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      acc[0] = mfma4(a[u], w[u].x, acc[0]);
+      acc[1] = mfma4(a[u], w[u].y, acc[1]);
+      acc[2] = mfma4(a[u], w[u].z, acc[2]);
+      acc[3] = mfma4(a[u], w[u].w, acc[3]);
+    }
+  }
+  for (; n < ne; n += 4) {
+    const int nn = n + q;
+    const bool vn = nn < ne;
+    const float a = (vm && vn) ? za[nn] : 0.f;
+    const float4 w = (vk && vn) ? ld4(W + (int64_t)nn * ldw + kcol) : z4;
+    acc[0] = mfma4(a, w.x, acc[0]);
+    acc[1] = mfma4(a, w.y, acc[1]);
+    acc[2] = mfma4(a, w.z, acc[2]);
+    acc[3] = mfma4(a, w.w, acc[3]);
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) red[wv][c][lane] = acc[c];
+  __syncthreads();
+  // 4 waves finish: wave c' reduces column-group c' (needs NW >= 4)
+  if (wv < 4) {
+    const int c = wv;
+    f32x4 s = red[0][c][lane];
+#pragma unroll
+    for (int v = 1; v < NW; ++v) s += red[v][c][lane];
+    // D_c[row][j]: row = (lane>>4)*4 + r, j = lane & 15 -> k = k0 + 4j + c
+    const int kk = k0 + 4 * (lane & 15) + c;
+    if (kk < K) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + (lane >> 4) * 4 + r;
+        if (m >= M) continue;
+        float v = s[r];
+        if (S == 1) {
+          if (hprev) v = (hprev[(int64_t)m * ldh + kk] > 0.f) ? v * scale : 0.f;
+          out[(int64_t)m * ldo + kk] = v;
+        } else {
+          out[(int64_t)sidx * slab + (int64_t)m * K + kk] = v;
+        }
+      }
+    }
+  }
+}
+
+__global__ void dgrad_reduce_kernel(const float* __restrict__ P, int S, int64_t slab,
+                                    const float* __restrict__ hprev, int ldh, float scale,
+                                    float* __restrict__ out, int ldo, int M, int K) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)M * K) return;
+  const int m = (int)(t / K), k = (int)(t - (int64_t)m * K);
+  float v = 0.f;
+  for (int s = 0; s < S; ++s) v += P[s * slab + t];
+  if (hprev) v = (hprev[(int64_t)m * ldh + k] > 0.f) ? v * scale : 0.f;
+  out[(int64_t)m * ldo + k] = v;
+}
+
+// Y = epilogue(P) for a GEMM done elsewhere (large-M eval path): P [M,N] with ld ldp.
+__global__ void epilogue_kernel(const float* __restrict__ P, int ldp, float* __restrict__ Y, int ldy,
+                                int M, int N, Epi e) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)M * N) return;
+  const int m = (int)(t / N), n = (int)(t - (int64_t)m * N);
+  Y[(int64_t)m * ldy + n] = apply_epi(e, P[(int64_t)m * ldp + n], m, n);
+}
+
+// ---------------------------------------------------------------------------- wgrad + optimizer
+// For rows n in [blockIdx.y*R, +R) and 4 columns per thread starting at
+// (blockIdx.x*256 + tid)*4:  g = sum_m dZ[m,n] A[m,k];  p <- opt(p, g).
+// Bias rows handled by blockIdx.x == 0.  Requires K % 4 == 0, ld % 4 == 0.
+template <int R>
+__global__ void __launch_bounds__(256)
+wgrad_opt_kernel(const float* __restrict__ dZ, int ldz, const float* __restrict__ A, int lda,
+                 float* __restrict__ W, int ldw, float* __restrict__ s0, float* __restrict__ s1,
+                 float* __restrict__ bias, float* __restrict__ sb0, float* __restrict__ sb1,
+                 int M, int N, int K, SlOpt o) {
+  const int tid = threadIdx.x;
+  const int kq = (blockIdx.x * 256 + tid) * 4;
+  const int n0 = blockIdx.y * R;
+  const int nr = min(R, N - n0);
+  if (kq < K) {
+    float4 g[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) g[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int mc = 0; mc < M; mc += 16) {
+      float4 a[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        a[j] = (mc + j < M) ? ld4(A + (int64_t)(mc + j) * lda + kq) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (r < nr) {
+#pragma unroll
+          for (int j = 0; j < 16; ++j) {
+            const float d = (mc + j < M) ? dZ[(int64_t)(mc + j) * ldz + n0 + r] : 0.f;
+            g[r].x = fmaf(d, a[j].x, g[r].x);
+            g[r].y = fmaf(d, a[j].y, g[r].y);
+            g[r].z = fmaf(d, a[j].z, g[r].z);
+            g[r].w = fmaf(d, a[j].w, g[r].w);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (r >= nr) break;
+      const int64_t off = (int64_t)(n0 + r) * ldw + kq;
+      float4 p = ld4(W + off);
+      float4 m0 = ld4(s0 + off);
+      float4 m1 = s1 ? ld4(s1 + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+      sl_opt_update(o, p.x, g[r].x, m0.x, m1.x);
+      sl_opt_update(o, p.y, g[r].y, m0.y, m1.y);
+      sl_opt_update(o, p.z, g[r].z, m0.z, m1.z);
+      sl_opt_update(o, p.w, g[r].w, m0.w, m1.w);
+      if (o.kind != 0) *reinterpret_cast<float4*>(W + off) = p;
+      *reinterpret_cast<float4*>(s0 + off) = m0;
+      if (s1) *reinterpret_cast<float4*>(s1 + off) = m1;
+    }
+  }
+  if (bias && blockIdx.x == 0 && tid < nr) {
+    const int n = n0 + tid;
+    float g = 0.f;
+    for (int m = 0; m < M; ++m) g += dZ[(int64_t)m * ldz + n];
+    float p = bias[n], b0 = sb0[n], b1 = sb1 ? sb1[n] : 0.f;
+    sl_opt_update(o, p, g, b0, b1);
+    if (o.kind != 0) bias[n] = p;
+    sb0[n] = b0;
+    if (sb1) sb1[n] = b1;
+  }
+}
+
+// Plain elementwise optimizer over a flat parameter (generic fallback / tests).
+__global__ void opt_flat_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ s0,
+                                float* __restrict__ s1, int64_t n, SlOpt o) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float pp = p[i], a0 = s0[i], a1 = s1 ? s1[i] : 0.f;
+  sl_opt_update(o, pp, g[i], a0, a1);
+  if (o.kind != 0) p[i] = pp;
+  s0[i] = a0;
+  if (s1) s1[i] = a1;
+}
+
+// ---------------------------------------------------------------------------- host launchers
+hipError_t linear_fwd(const float* X, int ldx, const float* W, int ldw, float* Y, int ldy, int M, int N,
+                      int K, Epi e, hipStream_t st) {
+  if (M <= 0 || N <= 0) return hipSuccess;
+  dim3 grid((N + 15) / 16, (M + 15) / 16);
+  // enough waves per column tile to keep HBM busy; fewer when K is short
+  if (K >= 2048)
+    skinny_fwd_kernel<8><<<grid, 512, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e);
+  else
+    skinny_fwd_kernel<4><<<grid, 256, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e);
+  return hipGetLastError();
+}
+
+hipError_t linear_dgrad(const float* dZ, int ldz, const float* W, int ldw, const float* hprev, int ldh,
+                        float scale, float* dX, int ldx, float* ws, int64_t ws_elems, int M, int N, int K,
+                        hipStream_t st) {
+  if (M <= 0 || K <= 0) return hipSuccess;
+  const int kt = (K + 63) / 64, mt = (M + 15) / 16;
+  int S = 1;
+  // aim for >= ~256 workgroups on the 256-CU part; split N when there are few K tiles
+  while (S < 8 && kt * mt * S < 192 && N / (S * 2) >= 64) S *= 2;
+  const int64_t slab = (int64_t)M * K;
+  if (S > 1 && (ws == nullptr || ws_elems < slab * S)) S = 1;
+  dim3 grid(kt, mt, S);
+  if (S == 1) {
+    skinny_dgrad_kernel<8><<<grid, 512, 0, st>>>(dZ, ldz, W, ldw, hprev, ldh, scale, dX, ldx, 0, M, N, K);
+  } else {
+    skinny_dgrad_kernel<8><<<grid, 512, 0, st>>>(dZ, ldz, W, ldw, nullptr, 0, 1.f, ws, 0, slab, M, N, K);
+    const int64_t tot = (int64_t)M * K;
+    dgrad_reduce_kernel<<<(unsigned)((tot + 255) / 256), 256, 0, st>>>(ws, S, slab, hprev, ldh, scale, dX, ldx,
+                                                                        M, K);
+  }
+  return hipGetLastError();
+}
+
+hipError_t linear_epilogue(const float* P, int ldp, float* Y, int ldy, int M, int N, Epi e, hipStream_t st) {
+  const int64_t tot = (int64_t)M * N;
+  if (tot <= 0) return hipSuccess;
+  epilogue_kernel<<<(unsigned)((tot + 255) / 256), 256, 0, st>>>(P, ldp, Y, ldy, M, N, e);
+  return hipGetLastError();
+}
+
+hipError_t linear_wgrad_opt(const float* dZ, int ldz, const float* A, int lda, float* W, int ldw, float* s0,
+                            float* s1, float* bias, float* sb0, float* sb1, int M, int N, int K, SlOpt o,
+                            hipStream_t st) {
+  if (N <= 0 || K <= 0) return hipSuccess;
+  constexpr int R = 8;
+  dim3 grid((K / 4 + 255) / 256, (N + R - 1) / R);
+  wgrad_opt_kernel<R><<<grid, 256, 0, st>>>(dZ, ldz, A, lda, W, ldw, s0, s1, bias, sb0, sb1, M, N, K, o);
+  return hipGetLastError();
+}
+
+hipError_t opt_flat(float* p, const float* g, float* s0, float* s1, int64_t n, SlOpt o, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  opt_flat_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(p, g, s0, s1, n, o);
+  return hipGetLastError();
+}
+
+}  // namespace sl

@@ -1,0 +1,99 @@
+// Fused softmax-cross-entropy forward+backward and fused evaluation counters.
+//
+// Reference ops: nn.CrossEntropyLoss (mean) on Bob's 100 logits
+// (data_entities_vanilla.py:229-230, data_entities_vanilla_sisa.py:307-308), on the
+// U-shape head's 10 logits (data_entities.py:76) and on the SISA Alice's 5408-wide
+// activation treated as logits (Q5, data_entities_vanilla_sisa.py:64-65); and the
+// torch.max + mask counting of eval_breakdown (data_entities_vanilla.py:181-194).
+// SURVEY §2.7 K9, K10.  One wave64 per row; all reductions are in-register
+// shuffles, no LDS.
+#include "common.h"
+
+namespace sl {
+
+// loss_rows[m] = logsumexp(x_m) - x_m[y_m];  d[m,:] = scale * (softmax(x_m) - onehot(y_m)).
+// Rows with label == ignore get loss 0 and a zero gradient row.
+__global__ void __launch_bounds__(256)
+softmax_ce_kernel(const float* __restrict__ x, int ldx, const int64_t* __restrict__ y, int64_t ignore,
+                  float scale, float* __restrict__ loss_rows, float* __restrict__ d, int ldd, int M, int C) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const float* xr = x + (int64_t)row * ldx;
+  float* dr = d ? d + (int64_t)row * ldd : nullptr;
+  const int64_t lab = y[row];
+  if (lab == ignore) {
+    if (lane == 0) loss_rows[row] = 0.f;
+    if (dr)
+      for (int c = lane; c < C; c += 64) dr[c] = 0.f;
+    return;
+  }
+  float mx = -INFINITY;
+  for (int c = lane; c < C; c += 64) mx = fmaxf(mx, xr[c]);
+  mx = sl_wave_max(mx);
+  float s = 0.f;
+  for (int c = lane; c < C; c += 64) s += expf(xr[c] - mx);
+  s = sl_wave_sum(s);
+  const float inv = 1.f / s;
+  const float lse = mx + logf(s);
+  if (lane == 0) loss_rows[row] = lse - xr[lab];
+  if (dr) {
+    for (int c = lane; c < C; c += 64) {
+      float p = expf(xr[c] - mx) * inv;
+      if (c == lab) p -= 1.f;
+      dr[c] = p * scale;
+    }
+  }
+}
+
+// counters[6] += {correct, total, correct_unlearned, total_unlearned, correct_remaining, total_remaining}
+__global__ void __launch_bounds__(256)
+eval_counters_kernel(const float* __restrict__ x, int ldx, const int64_t* __restrict__ y, int64_t omit,
+                     unsigned long long* __restrict__ counters, int M, int C) {
+  __shared__ unsigned int part[6];
+  if (threadIdx.x < 6) part[threadIdx.x] = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row < M) {
+    const float* xr = x + (int64_t)row * ldx;
+    float best = -INFINITY;
+    int arg = 0x7fffffff;
+    for (int c = lane; c < C; c += 64) {
+      const float v = xr[c];
+      if (v > best) { best = v; arg = c; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ob = __shfl_xor(best, o, 64);
+      const int oa = __shfl_xor(arg, o, 64);
+      if (ob > best || (ob == best && oa < arg)) { best = ob; arg = oa; }
+    }
+    if (lane == 0) {
+      const int64_t lab = y[row];
+      const unsigned ok = (arg == lab) ? 1u : 0u;
+      atomicAdd(&part[0], ok);
+      atomicAdd(&part[1], 1u);
+      if (lab == omit) { atomicAdd(&part[2], ok); atomicAdd(&part[3], 1u); }
+      else { atomicAdd(&part[4], ok); atomicAdd(&part[5], 1u); }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 6 && part[threadIdx.x]) atomicAdd(&counters[threadIdx.x], (unsigned long long)part[threadIdx.x]);
+}
+
+hipError_t softmax_ce(const float* x, int ldx, const int64_t* y, int64_t ignore, float scale, float* loss_rows,
+                      float* d, int ldd, int M, int C, hipStream_t st) {
+  if (M <= 0) return hipSuccess;
+  softmax_ce_kernel<<<(M + 3) / 4, 256, 0, st>>>(x, ldx, y, ignore, scale, loss_rows, d, ldd, M, C);
+  return hipGetLastError();
+}
+
+hipError_t eval_counters(const float* x, int ldx, const int64_t* y, int64_t omit, unsigned long long* counters,
+                         int M, int C, hipStream_t st) {
+  if (M <= 0) return hipSuccess;
+  eval_counters_kernel<<<(M + 3) / 4, 256, 0, st>>>(x, ldx, y, omit, counters, M, C);
+  return hipGetLastError();
+}
+
+}  // namespace sl

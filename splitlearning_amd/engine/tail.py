@@ -1,0 +1,212 @@
+"""MLP-tail executor: Bob's server tail (optionally tensor-parallel) and the
+U-shape head on Alice.
+
+Reference semantics: `model2` / `model2_sisa` / `model2_sisa_concat` / `model3`
+(models.py:33-94) trained with per-batch optimizer steps; the backward of Bob's
+tail is what `dist_autograd.backward` ran on Bob (data_entities_vanilla.py:231)
+and Bob's own `loss.backward(); optimizer.step()` in SISA
+(data_entities_vanilla_sisa.py:305-313).
+
+MI355X design:
+* every Linear runs on the fused skinny kernels (fwd with bias/ReLU/dropout
+  epilogue; dgrad with the previous layer's ReLU/dropout backward fused; wgrad
+  fused into the optimizer so dW never touches HBM);
+* backward is split in two phases — all dgrads first (`backward_dgrad`, which
+  yields dL/d(cut activation) for the client as early as possible), then all
+  wgrad+optimizer kernels (`backward_step`) — so the cut-layer gradient's
+  transfer overlaps the parameter update (SURVEY §3.2 "legal overlap");
+* tensor parallelism over a process group (Megatron-style, semantics-preserving):
+  fc1 column-parallel (output features sharded, dropout mask hashed on the global
+  column so it is TP-invariant), fc2 row-parallel (one all-reduce of the [B,·]
+  partial sums per forward), fc3 replicated.  At TP degree T each GPU streams
+  1/T of the fc1/fc2 weights and optimizer state — the HBM-bound part of the
+  step — and at T >= 2 a shard of Bob's fp32 Adam state (384 MB in total) fits in
+  the 256 MB Infinity Cache.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from .. import ops
+from ..models.zoo import LinearSpec, TailSpec
+from ..ops.rng import step_seed
+from .slots import OptSlot
+
+
+@dataclass
+class _Layer:
+    spec: LinearSpec
+    style: str               # "rep" | "col" | "row"
+    W: torch.Tensor          # [N_local, K_local]
+    b: torch.Tensor          # [N_local]
+    col_off: int             # global index of local output column 0
+    in_off: int              # global index of local input column 0 (row-parallel)
+
+
+class TailEngine:
+    def __init__(self, module: torch.nn.Module, spec: TailSpec, device: torch.device,
+                 tp_rank: int = 0, tp_size: int = 1, allreduce=None, seed_base: int = 0):
+        self.spec = spec
+        self.device = device
+        self.ops = ops.impl(device)
+        self.tp_rank, self.tp_size = tp_rank, tp_size
+        self.allreduce = allreduce
+        self.seed_base = seed_base
+        self.training = True
+        self.fwd_count = 0
+        self.module = module
+        self.layers: list[_Layer] = []
+        lin = module.linears()
+        nl = len(lin)
+        for i, (ls, mod) in enumerate(zip(spec.layers, lin)):
+            style = "rep"
+            if tp_size > 1 and nl >= 2:
+                style = "col" if i == 0 else ("row" if i == 1 else "rep")
+            W, b = mod.weight.data, mod.bias.data
+            col_off = in_off = 0
+            if style == "col":
+                n = W.shape[0]
+                s, e = _shard_range(n, tp_rank, tp_size)
+                W, b, col_off = W[s:e], b[s:e], s
+            elif style == "row":
+                k = W.shape[1]
+                s, e = _shard_range(k, tp_rank, tp_size)
+                W, in_off = W[:, s:e], s
+            W = W.to(device).contiguous()
+            b = b.to(device).contiguous()
+            if tp_size == 1:
+                # the module's parameters *are* the device tensors (state_dict works directly)
+                mod.weight.data = W
+                mod.bias.data = b
+            self.layers.append(_Layer(ls, style, W, b, col_off, in_off))
+        self.acts: list[torch.Tensor] = []
+        self.dz: list[torch.Tensor] = []
+        self._train_fwd = False
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, x: torch.Tensor, train: bool | None = None) -> torch.Tensor:
+        train = self.training if train is None else train
+        self.fwd_count += 1
+        step = self.fwd_count
+        acts = [x]
+        h = x
+        for i, L in enumerate(self.layers):
+            ls = L.spec
+            drop = ls.dropout if train else 0.0
+            seed = step_seed(self.seed_base, i, step)
+            if L.style == "row":
+                part = self.ops.linear_fwd(h, L.W, None, False, 0.0, 0, 0)
+                self.allreduce(part)
+                h = self.ops.linear_epilogue(part, L.b, ls.relu, drop, seed, 0)
+            else:
+                h = self.ops.linear_fwd(h, L.W, L.b, ls.relu, drop, seed, L.col_off)
+            acts.append(h)
+        self.acts = acts
+        self._train_fwd = train
+        return h
+
+    __call__ = forward
+
+    # ------------------------------------------------------------------ backward
+    def backward_dgrad(self, dout: torch.Tensor, need_dx: bool):
+        """Phase 1: all data gradients.  Returns dL/dx (a *partial sum* across TP
+        ranks when fc1 is column-parallel) if `need_dx`, else None."""
+        L = self.layers
+        n = len(L)
+        last = L[-1].spec
+        dz = dout
+        if last.relu or (last.dropout and self._train_fwd):
+            scale = 1.0 / (1.0 - last.dropout) if (last.dropout and self._train_fwd) else 1.0
+            dz = dout * (self.acts[-1] > 0) * scale
+        dzs = [None] * n
+        dzs[n - 1] = dz
+        dx = None
+        for i in range(n - 1, -1, -1):
+            if i > 0:
+                prev = L[i - 1].spec
+                drop_on = prev.dropout > 0 and self._train_fwd
+                scale = 1.0 / (1.0 - prev.dropout) if drop_on else 1.0
+                hprev = self.acts[i] if (prev.relu or drop_on) else None
+                dzs[i - 1] = self.ops.linear_dgrad(dzs[i], L[i].W, hprev, scale)
+            elif need_dx:
+                dx = self.ops.linear_dgrad(dzs[0], L[0].W, None, 1.0)
+        self.dz = dzs
+        return dx
+
+    def backward_step(self, slot: OptSlot, t: int | None = None, prefix: str = ""):
+        """Phase 2: fused wgrad + optimizer update of every layer (one optimizer step)."""
+        t = slot.tick() if t is None else t
+        for i, L in enumerate(self.layers):
+            self.ops.linear_wgrad_step_(self.dz[i], self.acts[i], L.W, L.b, slot.cfg,
+                                        slot.state(f"{prefix}{L.spec.name}.weight", L.W),
+                                        slot.state(f"{prefix}{L.spec.name}.bias", L.b), t)
+        self.dz = []
+
+    # ------------------------------------------------------------------ state
+    def local_state(self) -> dict:
+        out = {}
+        for L in self.layers:
+            out[f"{L.spec.name}.weight"] = L.W
+            out[f"{L.spec.name}.bias"] = L.b
+        return out
+
+    def full_state_dict(self, gather=None) -> dict:
+        """Reference-layout state_dict (full tensors).  `gather(t) -> list[t]` collects the
+        TP shards (all ranks must call it)."""
+        sd = {}
+        for L in self.layers:
+            W, b = L.W, L.b
+            if L.style == "col":
+                W = torch.cat(gather(W), 0)
+                b = torch.cat(gather(b), 0)
+            elif L.style == "row":
+                W = torch.cat(gather(W.t().contiguous()), 0).t()
+            sd[f"{L.spec.name}.weight"] = W.detach().cpu().clone()
+            sd[f"{L.spec.name}.bias"] = b.detach().cpu().clone()
+        return sd
+
+    def load_full_state_dict(self, sd: dict):
+        with torch.no_grad():
+            for L in self.layers:
+                W = sd[f"{L.spec.name}.weight"]
+                b = sd[f"{L.spec.name}.bias"]
+                if L.style == "col":
+                    s, e = _shard_range(W.shape[0], self.tp_rank, self.tp_size)
+                    W, b = W[s:e], b[s:e]
+                elif L.style == "row":
+                    s, e = _shard_range(W.shape[1], self.tp_rank, self.tp_size)
+                    W = W[:, s:e]
+                L.W.copy_(W)
+                L.b.copy_(b)
+
+    def flat_weights(self) -> torch.Tensor:
+        return torch.cat([t.reshape(-1) for L in self.layers for t in (L.W, L.b)])
+
+    def load_flat_weights(self, flat: torch.Tensor):
+        o = 0
+        for L in self.layers:
+            for t in (L.W, L.b):
+                t.copy_(flat[o:o + t.numel()].view_as(t))
+                o += t.numel()
+
+    @property
+    def flat_numel(self) -> int:
+        return sum(t.numel() for L in self.layers for t in (L.W, L.b))
+
+    def reset_parameters(self):
+        for L, mod in zip(self.layers, self.module.linears()):
+            if self.tp_size == 1:
+                mod.reset_parameters()
+            else:
+                raise NotImplementedError("reset of a tensor-parallel tail")
+
+
+def _shard_range(n: int, r: int, t: int) -> tuple[int, int]:
+    """Contiguous, 4-aligned shard boundaries (float4 loads need K % 4 == 0)."""
+    per = -(-n // t)
+    per = -(-per // 4) * 4
+    s = min(n, r * per)
+    e = min(n, s + per)
+    return s, e

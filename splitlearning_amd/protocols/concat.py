@@ -1,0 +1,96 @@
+"""SISA with concatenated client embeddings (`--sisa --concat`).
+
+Reference: `/root/reference/data_entities_sisa_concat.py` + `models.py:66-82`
+(`model2_sisa_concat(k)`: fc1 takes 5408*k inputs, fc3 emits 100*k logits).
+The reference concatenates along the *batch* dimension, then iterates single
+samples and crashes in `torch.flatten(x, 1)` (Q3); its eval is a TODO.  The
+layer shapes only make sense for a **feature** concatenation, so this module
+pins the semantics SURVEY H6 recommends (documented in docs/DEVIATIONS.md):
+
+* server step t takes batch t of every Alice's cached activations and lays them
+  side by side: row b = [act_1[b] | act_2[b] | ... | act_k[b]] (zeros for an Alice
+  whose cache is exhausted or whose last batch is shorter);
+* logits are k heads of 100: loss = sum_j CE(logits[:, 100j:100j+100], y_j), each
+  a mean over Alice j's valid rows (rows without a sample carry ignore_index);
+* eval feeds Alice j's activation in slot j and zeros elsewhere and reads head j;
+* with `--concat_unlearn` the SISA unlearn/retrain tail is appended (BASELINE
+  config 5; the reference concat schedule has no unlearning step).
+
+The activation caches are replicated on every Bob TP rank by the dump (p2p
+multicast = the all-gather of client embeddings), so the per-step concat is a
+device-local gather into one [B, 5408k] buffer.
+"""
+from __future__ import annotations
+
+import torch
+
+from ..config import CUT_FEATURES
+from ..models import ServerTailSisaConcat, sisa_server_spec
+from .base import _progress
+from .sisa import SisaSession
+
+
+class ConcatSession(SisaSession):
+    mode = "concat"
+
+    def bob_module_and_spec(self):
+        return (self.make_bob_module(ServerTailSisaConcat, self.k),
+                sisa_server_spec(self.k, concat=True))
+
+    def cut_width_in(self) -> int:
+        return CUT_FEATURES
+
+    def bob_out_width(self) -> int:
+        return 100
+
+    def bob_infer(self, act, cid):
+        """Eval: Alice_cid's activation in slot cid, zeros elsewhere; returns head cid."""
+        j = cid - 1
+        outs = []
+        for s in range(0, act.shape[0], 2048):
+            a = act[s:s + 2048]
+            X = torch.zeros(a.shape[0], CUT_FEATURES * self.k, device=self.device)
+            X[:, j * CUT_FEATURES:(j + 1) * CUT_FEATURES] = a
+            outs.append(self.tail.forward(X)[:, 100 * j:100 * (j + 1)].contiguous())
+        return torch.cat(outs, 0) if len(outs) > 1 else outs[0]
+
+    def concat_step(self, caches, t: int):
+        k, B = self.k, self.B
+        rows = []
+        for acts, labels in caches:
+            rows.append(max(0, min(B, labels.numel() - t * B)))
+        M = max(rows)
+        X = torch.zeros(M, CUT_FEATURES * k, device=self.device)
+        Y = torch.full((M, k), -100, dtype=torch.int64, device=self.device)
+        scale = torch.zeros(M, k, device=self.device)
+        for j, ((acts, labels), r) in enumerate(zip(caches, rows)):
+            if r == 0:
+                continue
+            X[:r, j * CUT_FEATURES:(j + 1) * CUT_FEATURES] = acts[t * B:t * B + r]
+            Y[:r, j] = labels[t * B:t * B + r]
+            scale[:r, j] = 1.0 / r
+        out = self.tail.forward(X, train=True)                       # [M, 100k]
+        _, d = self.ops.softmax_ce(out.view(M * k, 100), Y.view(-1), 1.0)
+        d = (d.view(M, k, 100) * scale.view(M, k, 1)).view(M, 100 * k)
+        self.tail.backward_dgrad(d, need_dx=False)
+        self.tail.backward_step(self.bob_slot)
+        return sum(rows)
+
+    def train_and_backward(self, unlearn_request_from_alices, unlearn_id):
+        self.bob_log.info("Global Training")
+        self.switch_mode_to_train()
+        samples = 0
+        for _ in _progress(range(self.args.server_epochs), self.show, desc="Epochs", ascii=" >="):
+            caches = []
+            for cid in range(1, self.k + 1):
+                if cid in unlearn_request_from_alices:
+                    caches.append(self.get_activation_and_labels(cid, unlearned=True, unlearn_id=unlearn_id))
+                else:
+                    caches.append(self.get_activation_and_labels(cid, unlearned=False))
+            if self.is_bob:
+                T = max(-(-c[1].numel() // self.B) for c in caches)
+                for t in range(T):
+                    samples += self.concat_step(caches, t)
+        self.bob_log.info("Global training completed.")
+        self.comm.barrier()
+        return samples

@@ -1,0 +1,192 @@
+"""SISA split learning + unlearning (`--sisa`) and the retrain-from-scratch
+control group (`--control`).
+
+Reference: `/root/reference/data_entities_vanilla_sisa.py` (alice `:35-250`,
+bob `:253-419`), schedules `split_nn.py:74-117` (SISA) and `:119-135` (control;
+the reference routes `--control` to the wrong module and crashes, Q2 — here it
+gets the SISA semantics its methods were written for).
+
+Phases and their MI355X mapping:
+* local training — every Alice trains her conv front alone (CE on the 5408-wide
+  activation, Q5; Adam wd=1e-5), all Alices concurrently, one per GPU, each
+  batch = 3 kernels (gather+conv, softmax-CE, conv-backward+Adam), zero comm;
+* activation dump — on first use per cache key `(client, unlearned, unlearn_id)`
+  the client's whole shard goes through the frozen front and the activations +
+  labels are multicast p2p to every Bob TP rank, where they stay resident in HBM
+  (`activation_and_labels_cache`, SISA's isolated-slice cache, Q17);
+* server training — Bob's Adam(wd=1e-5) epochs over the cached activations, no
+  communication except the TP all-reduce inside each step;
+* unlearning — only the requesting Alice retrains (without the omitted label);
+  only her cache entry is recomputed; Bob retrains on top of his current weights.
+"""
+from __future__ import annotations
+
+import torch
+
+from ..config import ADAM_WEIGHT_DECAY, CUT_FEATURES
+from ..engine.slots import OptSlot, adam
+from ..models import ServerTailSisa, sisa_server_spec
+from .base import AliceState, Session, _progress
+
+
+class SisaSession(Session):
+    mode = "sisa"
+
+    def alice_optim(self):
+        return adam(self.args.lr, ADAM_WEIGHT_DECAY)
+
+    def bob_optim(self):
+        return adam(self.args.lr, ADAM_WEIGHT_DECAY)
+
+    def bob_module_and_spec(self):
+        return self.make_bob_module(ServerTailSisa), sisa_server_spec()
+
+    def _build_bob(self):
+        super()._build_bob()
+        self.bob_slots["server"] = OptSlot(self.bob_optim())
+
+    @property
+    def bob_slot(self) -> OptSlot:
+        return self.bob_slots["server"]
+
+    def before_eval(self):
+        # each reference Alice calls bob.switch_mode_to_eval() before evaluating
+        self.switch_mode_to_eval()
+
+    # ------------------------------------------------------------------ Alice-local training
+    def local_step(self, a: AliceState, idx):
+        act, am = a.front.forward(a.train, idx)
+        _, d = self.ops.softmax_ce(act, a.train.y[idx], 1.0 / idx.numel())
+        a.front.backward_step(d, act, am, a.train, idx, a.slot)
+
+    def local_train(self, a: AliceState, fixed_order=None):
+        """`epochs` local epochs; reshuffled every epoch unless a fixed (unlearn /
+        filtered, shuffle=False) order is given."""
+        for _ in _progress(range(self.args.epochs), self.show, desc="Epochs", ascii=" >="):
+            order = fixed_order if fixed_order is not None else a.train.shuffled_order(a.gen)
+            n = order.numel()
+            for s in range(0, n, self.B):
+                self.local_step(a, order[s:s + self.B])
+
+    def train(self, cid: int):
+        a = self.alices[cid]
+        a.logger.info("Local Training")
+        self.local_train(a)
+
+    # ------------------------------------------------------------------ Bob API
+    def train_request(self, client_id: int):
+        self.bob_log.info(f"Train Request for Alice-{client_id}")
+        if self.hosts(client_id):
+            self.train(client_id)
+        self.comm.barrier()
+
+    def train_request_parallel(self):
+        self.bob_log.info("Train all Alices in parallel")
+        for cid in sorted(self.alices):
+            self.train(cid)
+        self.comm.barrier()        # "wait for all futures"
+
+    def train_request_control(self, client_id: int, omit_label: int):
+        self.bob_log.info(f"Train Request for Alice-{client_id}")
+        if self.hosts(client_id):
+            self.train_control(client_id, omit_label)
+        self.comm.barrier()
+
+    def train_control(self, cid: int, omit_label: int):
+        """Reference `alice.train_control` (data_entities_vanilla_sisa.py:230-250)."""
+        a = self.alices[cid]
+        order = self.filtered_order(a, omit_label)
+        a.unlearn_order = order
+        a.logger.info("Filtered dataset: {}".format(self.label_counter(a, order)))
+        self.local_train(a, fixed_order=order)
+
+    def unlearn_request(self, client_id: int, omit_label: int):
+        self.bob_log.info(f"Unlearn Request for Alice-{client_id} upon the label-{omit_label}")
+        if self.hosts(client_id):
+            self.unlearn(client_id, omit_label)
+        self.comm.barrier()
+
+    def unlearn(self, cid: int, omit_label: int):
+        """Reference `alice.unlearn` (data_entities_vanilla_sisa.py:139-168)."""
+        a = self.alices[cid]
+        a.logger.info(f"Unlearning label: {omit_label}, and reset the model")
+        self.reset_model(cid)
+        a.slot = OptSlot(self.alice_optim())
+        order = self.filtered_order(a, omit_label)
+        a.unlearn_order = order
+        a.logger.info("Retraining dataset: {}".format(self.label_counter(a, order)))
+        a.logger.info("Test dataset (retraining): {}".format(a.test.label_counter()))
+        self.local_train(a, fixed_order=order)
+
+    def give_activation_and_labels(self, cid: int, unlearned: bool = False):
+        """Alice side of the dump: (activations [n,5408], labels [n]) over the train loader
+        (fresh shuffle) or the unlearn loader (fixed order)."""
+        a = self.alices[cid]
+        if unlearned:
+            if a.unlearn_order is None:
+                raise RuntimeError(f"Alice-{cid} has no unlearn dataloader (unlearn/train_control first)")
+            order = a.unlearn_order
+        else:
+            order = a.train.shuffled_order(a.gen)
+        return a.front.forward_chunked(a.train, order), a.train.y[order]
+
+    def get_activation_and_labels(self, client_id: int, unlearned: bool = False, unlearn_id=None):
+        key = (client_id, unlearned, unlearn_id)
+        hit = self.activation_and_labels_cache.get(key) if self.is_bob else None
+        # every rank must agree on hit/miss: the cache is replicated on all Bob ranks and
+        # keys are inserted in schedule order, so a Bob-side membership test is enough —
+        # non-Bob ranks track the key set too
+        known = key in self._cache_keys
+        if known:
+            return hit
+        acts = labels = None
+        if self.hosts(client_id):
+            acts, labels = self.give_activation_and_labels(client_id, unlearned)
+        acts = self.to_bob_var(client_id, acts, (CUT_FEATURES,), torch.float32)
+        labels = self.to_bob_var(client_id, labels, (), torch.int64)
+        self._cache_keys.add(key)
+        if self.is_bob:
+            self.activation_and_labels_cache[key] = (acts, labels)
+            return acts, labels
+        return None
+
+    @property
+    def _cache_keys(self) -> set:
+        if not hasattr(self, "_ck"):
+            self._ck = set()
+        return self._ck
+
+    def server_step(self, x, y):
+        out = self.tail.forward(x, train=True)
+        _, d = self.ops.softmax_ce(out, y, 1.0 / x.shape[0])
+        self.tail.backward_dgrad(d, need_dx=False)
+        self.tail.backward_step(self.bob_slot)
+
+    def train_and_backward(self, unlearn_request_from_alices, unlearn_id):
+        """Reference `bob.train_and_backward` (data_entities_vanilla_sisa.py:294-315)."""
+        self.bob_log.info("Global Training")
+        self.switch_mode_to_train()
+        samples = 0
+        for _ in _progress(range(self.args.server_epochs), self.show, desc="Epochs", ascii=" >="):
+            for cid in range(1, self.k + 1):
+                if cid in unlearn_request_from_alices:
+                    got = self.get_activation_and_labels(cid, unlearned=True, unlearn_id=unlearn_id)
+                else:
+                    got = self.get_activation_and_labels(cid, unlearned=False)
+                if self.is_bob:
+                    acts, labels = got
+                    n = labels.numel()
+                    for s in range(0, n, self.B):
+                        self.server_step(acts[s:s + self.B], labels[s:s + self.B])
+                    samples += n
+        self.bob_log.info("Global training completed.")
+        self.comm.barrier()
+        return samples
+
+    def inference(self, x):
+        return self.tail.forward(x)
+
+
+class ControlSession(SisaSession):
+    """`--control`: SISA semantics with Alice_1 trained on filtered data from the start."""
+    mode = "control"

@@ -1,0 +1,161 @@
+"""U-shape split learning (default mode): Alice conv front -> Bob MLP middle ->
+Alice head + loss.  Labels never leave the client.
+
+Reference: `/root/reference/data_entities.py` (alice `:23-128`, bob `:131-180`),
+schedule `split_nn.py:47-60`.  Per batch (data_entities.py:65-81) the reference
+does an `inference` RPC forward and a dist-autograd backward that crosses the
+process boundary twice, then a DistributedOptimizer Adam step over
+model3 + Bob + model1.  Here: activation Alice->Bob, Bob's [B,100] output
+Bob->Alice, head forward/CE/backward on Alice, dL/d(Bob output) Alice->Bob,
+Bob dgrad -> cut gradient Bob->Alice (posted async, overlapping Bob's fused
+wgrad+Adam), Alice's fused conv backward+Adam.  Bob keeps one Adam slot per
+Alice (Q8).  The reference crashes after training because the U-shape bob has
+no `eval_request_breakdown` (Q1); this module implements it and the U-shape
+unlearn request so the reference schedule runs to completion.
+"""
+from __future__ import annotations
+
+import torch
+
+from ..config import CUT_FEATURES
+from ..engine.slots import OptSlot, adam
+from ..engine.tail import TailEngine
+from ..models import ClientFront, Head, ServerTailUShape, head_spec, ushape_server_spec
+from .base import AliceState, Session, _progress
+
+
+class UShapeSession(Session):
+    mode = "ushape"
+
+    def front_module(self):
+        return ClientFront()
+
+    def alice_optim(self):
+        return adam(self.args.lr)
+
+    def bob_optim(self):
+        return adam(self.args.lr)
+
+    def bob_module_and_spec(self):
+        return self.make_bob_module(ServerTailUShape), ushape_server_spec()
+
+    def _extend_alice(self, a: AliceState):
+        torch.manual_seed(self.seed + 2000 + a.cid)
+        a.head = TailEngine(Head(), head_spec(), self.device)
+
+    def bob_slot(self, cid: int) -> OptSlot:
+        s = self.bob_slots.get(cid)
+        if s is None:
+            s = self.bob_slots[cid] = OptSlot(self.bob_optim())
+        return s
+
+    # ------------------------------------------------------------------ weights (model1 + model3)
+    def give_weights(self, cid: int):
+        a = self.alices[cid]
+        return [{k: v.detach().clone() for k, v in a.front.module.state_dict().items()},
+                {k: v.detach().clone() for k, v in a.head.module.state_dict().items()}]
+
+    def _flat_client_weights(self, a):
+        return torch.cat([a.front.flat_weights(), a.head.flat_weights()])
+
+    def _load_flat_client_weights(self, a, flat):
+        n = a.front.flat_numel
+        a.front.load_flat_weights(flat[:n])
+        a.head.load_flat_weights(flat[n:])
+
+    def _client_flat_numel(self) -> int:
+        return 32 * 9 + 32 + 100 * 10 + 10
+
+    def _client_state(self, a):
+        return {"model1": {k: v.detach().cpu() for k, v in a.front.module.state_dict().items()},
+                "model3": {k: v.detach().cpu() for k, v in a.head.module.state_dict().items()}}
+
+    def _load_client_state(self, a, sd):
+        a.front.module.load_state_dict({k: v.to(self.device) for k, v in sd["model1"].items()})
+        a.head.load_full_state_dict(sd["model3"])
+
+    def reset_model(self, cid: int):
+        a = self.alices[cid]
+        a.front.reset_parameters(self.args.true_reset)
+        with torch.no_grad():
+            a.head.reset_parameters()
+
+    # ------------------------------------------------------------------ one U-shape step
+    def split_step(self, cid: int, idx, B: int):
+        host = self.host(cid)
+        a = self.alices.get(cid)
+        act = am = None
+        if a is not None:
+            act, am = a.front.forward(a.train, idx)
+        act_b = self.to_bob(cid, act, (B, CUT_FEATURES))
+        out = self.tail.forward(act_b, train=True) if self.is_bob else None
+        mid = self.from_bob(cid, out, (B, 100))
+        dmid = None
+        t = None
+        if a is not None:
+            logits = a.head.forward(mid, train=True)
+            _, dlog = self.ops.softmax_ce(logits, a.train.y[idx], 1.0 / B)
+            dmid = a.head.backward_dgrad(dlog, need_dx=True)
+            t = a.slot.tick()
+            a.head.backward_step(a.slot, t, prefix="head.")
+        dmid_b = self.to_bob(cid, dmid, (B, 100))
+        dxp = self.tail.backward_dgrad(dmid_b, need_dx=True) if self.is_bob else None
+        fin = self.comm.reduce_to_async(dxp, host, self.bob_ranks, (B, CUT_FEATURES), torch.float32)
+        if self.is_bob:
+            self.tail.backward_step(self.bob_slot(cid))
+        dx = fin()
+        if a is not None:
+            a.front.backward_step(dx, act, am, a.train, idx, a.slot, t=t, prefix="front.")
+
+    def _run_epochs(self, cid: int, order_fn, n: int):
+        for _ in _progress(range(self.args.epochs), self.show, desc="Epochs", ascii=" >="):
+            a = self.alices.get(cid)
+            order = order_fn(a) if a is not None else None
+            for s in range(0, n, self.B):
+                e = min(s + self.B, n)
+                self.split_step(cid, order[s:e] if order is not None else None, e - s)
+
+    # ------------------------------------------------------------------ Bob API
+    def train_request(self, client_id: int):
+        self.bob_log.info(f"Train Request for Alice-{client_id}")
+        a = self.alices.get(client_id)
+        if a is not None:
+            a.logger.info("Training")
+            if self.last_alice_id is None:
+                a.logger.info(f"Alice-{client_id} is first client to train")
+            else:
+                a.logger.info(f"Alice-{client_id} receiving weights from Alice-{self.last_alice_id}")
+        if self.last_alice_id is not None:
+            self.relay_weights(self.last_alice_id, client_id)
+        self._run_epochs(client_id, lambda al: al.train.shuffled_order(al.gen), self.n_train[client_id])
+        self.last_alice_id = client_id
+
+    def unlearn_request(self, client_id: int, omit_label: int):
+        """U-shape unlearning (absent in the reference, Q1): reset + fresh Adam states
+        (client and Bob-side slot) + retrain on the filtered shard."""
+        self.bob_log.info(f"Unlearn Request for Alice-{client_id}")
+        a = self.alices.get(client_id)
+        order = None
+        if a is not None:
+            a.logger.info("Retraining")
+            self.reset_model(client_id)
+            a.slot = OptSlot(self.alice_optim())
+            order = self.filtered_order(a, omit_label)
+            a.unlearn_order = order
+            a.logger.info("Retraining dataset: {}".format(self.label_counter(a, order)))
+            a.logger.info("Test dataset (retraining): {}".format(a.test.label_counter()))
+        self.bob_slots[client_id] = OptSlot(self.bob_optim())
+        n = torch.tensor([order.numel() if order is not None else 0], dtype=torch.int64, device=self.device)
+        n = int(self.comm.multicast(n if a is not None else None, self.host(client_id),
+                                    range(self.comm.world), (1,), torch.int64).item())
+        self._run_epochs(client_id, lambda al: al.unlearn_order, n)
+
+    # ------------------------------------------------------------------ eval hooks
+    def bob_out_width(self) -> int:
+        return 100
+
+    def client_logits(self, cid: int, bob_out):
+        return self.alices[cid].head.forward(bob_out, train=False)
+
+    def inference(self, x):
+        return self.tail.forward(x)

@@ -1,0 +1,145 @@
+"""Process launcher: argument resolution, data generation, process spawn, per-rank entry.
+
+Reference: `split_nn.py:148-186` (argparse, validation, `load_mnist_image`, then
+`mp.spawn(example, nprocs=world_size)`) and `example()` (`:34-146`).
+
+MI355X mapping:
+* GPU: one process per visible GPU (`--nprocs` default = #GPUs), each pinned to
+  its device; roles are placed on processes (`parallel.dist.Placement`), so
+  world_size = #GPUs + 1 puts Bob's TP shard and one Alice on every GPU;
+* CPU: one process per role (`nprocs = world_size`), gloo, like the reference;
+* already running under `torchrun` (RANK/WORLD_SIZE in the environment): no
+  spawn, this process is its rank.
+The parent never touches the GPU (device count only), so spawned children own it.
+"""
+from __future__ import annotations
+
+import json
+import os
+import resource
+import sys
+
+import torch
+
+from ..config import parse_args
+
+
+def raise_fd_limit():
+    """Reference split_nn.py:7-10 (needed there by TensorPipe's shm fds; harmless here)."""
+    try:
+        soft, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
+        resource.setrlimit(resource.RLIMIT_NOFILE, (hard, hard))
+    except (ValueError, OSError):
+        pass
+
+
+def resolve(args):
+    ngpu = torch.cuda.device_count() if args.device in ("auto", "cuda") else 0
+    if args.device == "cuda" and ngpu == 0:
+        raise RuntimeError("--device cuda but no GPU is visible")
+    use_gpu = ngpu > 0
+    args.use_gpu = use_gpu
+    if args.nprocs <= 0:
+        args.nprocs = min(ngpu, args.world_size) if use_gpu else args.world_size
+    if use_gpu and args.nprocs > ngpu:
+        raise RuntimeError(f"{args.nprocs} processes but only {ngpu} GPUs (one process per GPU)")
+    if args.backend == "auto":
+        args.backend = "nccl" if use_gpu else "gloo"
+    if args.bob_tp <= 0:
+        args.bob_tp = args.nprocs if use_gpu else 1
+    if args.kernels == "torch":
+        from .. import ops
+        ops.set_backend("torch")
+    return args
+
+
+def worker(rank: int, nprocs: int, args, result_q=None):
+    from .. import ops
+    from ..parallel.dist import Comm, Placement, init_process, make_tp_group
+    from ..protocols import make_session, run_schedule
+
+    if args.kernels == "torch":
+        ops.set_backend("torch")
+    if args.use_gpu:
+        dev = torch.device("cuda", rank % torch.cuda.device_count())
+        torch.cuda.set_device(dev)
+    else:
+        dev = torch.device("cpu")
+        torch.set_num_threads(max(1, (os.cpu_count() or 1) // nprocs))
+    pl = Placement.make(args.world_size, nprocs, args.bob_tp)
+    tp_group = None
+    if nprocs > 1:
+        init_process(rank, nprocs, args.backend, args.master_addr, args.master_port, args.timeout_s, dev)
+        tp_group = make_tp_group(pl, args.backend)
+    comm = Comm(rank, nprocs, dev, pl, tp_group)
+    if getattr(args, "prep_in_worker", False):
+        if rank == 0:
+            prepare_data(args)
+        comm.barrier()
+    sess = make_session(args, comm, dev)
+    if args.resume_dir:
+        sess.load_checkpoints(args.resume_dir)
+    out = run_schedule(sess, args)
+    if args.save_dir:
+        sess.save_checkpoints(args.save_dir)
+    if rank == 0:
+        extra = {"mode": args.mode, "world_size": args.world_size, "nprocs": nprocs, "bob_tp": pl.bob_tp,
+                 "device": str(dev), "kernels": ops.get_backend() if dev.type == "cuda" else "torch",
+                 "last_eval": getattr(sess, "last_eval", None)}
+        sess.timer.dump(os.path.join(args.log_dir, "metrics.json"), extra)
+        if result_q is not None:
+            result_q.put({"phases": out["phases"], **extra})
+    sess.close()
+    if nprocs > 1:
+        import torch.distributed as dist
+        comm.barrier()
+        dist.destroy_process_group()
+    return out
+
+
+def _spawn_entry(rank, nprocs, args):
+    worker(rank, nprocs, args)
+
+
+def launch(args):
+    """Run the whole job (all ranks). Returns rank 0's metrics dict when run here."""
+    env_rank = os.environ.get("RANK")
+    if env_rank is not None and os.environ.get("WORLD_SIZE"):
+        args.nprocs = int(os.environ["WORLD_SIZE"])
+        args.master_addr = os.environ.get("MASTER_ADDR", args.master_addr)
+        args.master_port = int(os.environ.get("MASTER_PORT", args.master_port))
+        return worker(int(env_rank), args.nprocs, args)
+    if args.nprocs == 1:
+        return worker(0, 1, args)
+    import torch.multiprocessing as mp
+    mp.spawn(_spawn_entry, args=(args.nprocs, args), nprocs=args.nprocs, join=True)
+    path = os.path.join(args.log_dir, "metrics.json")
+    if os.path.exists(path):
+        with open(path) as f:
+            return json.load(f)
+    return None
+
+
+def prepare_data(args, verbose=True):
+    from ..data.mnist import shards_exist, write_shards
+    if args.reuse_data and shards_exist(args.datapath, args.client_num_in_total):
+        return
+    write_shards(args, verbose=verbose)
+
+
+def main(argv=None):
+    raise_fd_limit()
+    args = resolve(parse_args(argv))
+    os.makedirs(args.log_dir, exist_ok=True)           # Q15: loggers write here
+    if os.environ.get("RANK") is not None and os.environ.get("WORLD_SIZE"):
+        args.prep_in_worker = True                       # torchrun: rank 0 writes, then a barrier
+    else:
+        prepare_data(args)                               # split_nn.py:179 (every run, Q12)
+    if os.environ.get("RANK", "0") == "0":
+        print("Initialize Meetup Spot", flush=True)
+    return launch(args)
+
+
+if __name__ == "__main__":
+    main()
+    sys.exit(0)

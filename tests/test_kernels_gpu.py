@@ -1,0 +1,155 @@
+"""Numerics of every HIP kernel against the fp32 eager-PyTorch reference of the same op."""
+import pytest
+import torch
+
+from splitlearning_amd.config import OptimCfg
+from splitlearning_amd.ops import hip_ops, torch_ops
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(a, b, rtol=1e-4, atol=1e-4):
+    torch.testing.assert_close(a.float().cpu(), b.float().cpu(), rtol=rtol, atol=atol)
+
+
+def _shard(n, dev, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randint(0, 256, (n, 784), generator=g, dtype=torch.uint8)
+    return x.to(dev)
+
+
+def _conv_params(dev, seed=1):
+    g = torch.Generator().manual_seed(seed)
+    w = (torch.rand(32, 1, 3, 3, generator=g) - 0.5) * 0.1
+    b = (torch.rand(32, generator=g) - 0.5) * 0.1
+    return w.to(dev), b.to(dev)
+
+
+@pytest.mark.parametrize("B", [1, 7, 16, 300])
+def test_conv_fwd(cuda, B):
+    x = _shard(1000, cuda)
+    idx = torch.randperm(1000, device=cuda)[:B]
+    w, b = _conv_params(cuda)
+    y, am = hip_ops.conv_front_fwd(x, idx, w, b)
+    yr, amr = torch_ops.conv_front_fwd(x, idx, w, b)
+    _close(y, yr, rtol=1e-5, atol=2e-4)
+    pos = (yr > 1e-3)
+    assert torch.equal(am[pos], amr[pos])
+
+
+@pytest.mark.parametrize("kind", ["grad", "sgd", "adam"])
+def test_conv_bwd(cuda, kind):
+    B = 16
+    x = _shard(500, cuda)
+    idx = torch.randperm(500, device=cuda)[:B]
+    w, b = _conv_params(cuda)
+    y, am = torch_ops.conv_front_fwd(x, idx, w, b)
+    dy = torch.randn(B, 5408, device=cuda)
+    dwr, dbr = torch_ops.conv_front_bwd(dy, y, am, x, idx, w, b)
+    if kind == "grad":
+        dw, db = hip_ops.conv_front_bwd(dy, y, am, x, idx, w, b)
+        _close(dw, dwr, rtol=1e-4, atol=1e-2)
+        _close(db, dbr, rtol=1e-4, atol=1e-3)
+        return
+    cfg = OptimCfg("adam", 1e-3, weight_decay=1e-5) if kind == "adam" else OptimCfg("sgd", 1e-3, momentum=0.9)
+    def st(p):
+        return {"m": torch.full_like(p, 0.01), "v": torch.full_like(p, 0.02)} if kind == "adam" else \
+            {"buf": torch.full_like(p, 0.01)}
+    w1, b1, w2, b2 = w.clone(), b.clone(), w.clone(), b.clone()
+    sw1, sb1, sw2, sb2 = st(w), st(b), st(w), st(b)
+    hip_ops.conv_front_bwd_step_(dy, y, am, x, idx, w1, b1, cfg, sw1, sb1, 3)
+    torch_ops.apply_update_(w2, dwr, sw2, cfg, 3)
+    torch_ops.apply_update_(b2, dbr, sb2, cfg, 3)
+    _close(w1, w2, rtol=1e-4, atol=1e-6)
+    _close(b1, b2, rtol=1e-4, atol=1e-6)
+    for k in sw1:
+        _close(sw1[k], sw2[k], rtol=1e-3, atol=1e-4)
+
+
+@pytest.mark.parametrize("M,N,K", [(16, 5000, 5408), (16, 1000, 5000), (16, 100, 1000), (5, 10, 100),
+                                    (16, 37, 52), (200, 100, 1000)])
+@pytest.mark.parametrize("relu,drop", [(False, 0.0), (True, 0.0), (True, 0.5)])
+def test_linear_fwd(cuda, M, N, K, relu, drop):
+    x = torch.randn(M, K, device=cuda)
+    w = torch.randn(N, K, device=cuda) / K ** 0.5
+    b = torch.randn(N, device=cuda)
+    seed = 0x1234_5678_9ABC
+    y = hip_ops.linear_fwd(x, w, b, relu, drop, seed, col_offset=3)
+    yr = torch_ops.linear_fwd(x, w, b, relu, drop, seed, col_offset=3)
+    _close(y, yr, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("M,N,K", [(16, 5000, 5408), (16, 1000, 5000), (16, 100, 1000), (16, 10, 100),
+                                    (3, 37, 52)])
+@pytest.mark.parametrize("masked", [False, True])
+def test_linear_dgrad(cuda, M, N, K, masked):
+    dz = torch.randn(M, N, device=cuda)
+    w = torch.randn(N, K, device=cuda) / N ** 0.5
+    h = torch.relu(torch.randn(M, K, device=cuda)) if masked else None
+    dx = hip_ops.linear_dgrad(dz, w, h, 2.0)
+    dxr = torch_ops.linear_dgrad(dz, w, h, 2.0)
+    _close(dx, dxr, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("M,N,K", [(16, 5000, 5408), (16, 100, 1000), (7, 10, 100), (40, 33, 20)])
+@pytest.mark.parametrize("kind", ["grad", "sgd", "adam"])
+def test_linear_wgrad_opt(cuda, M, N, K, kind):
+    dz = torch.randn(M, N, device=cuda)
+    a = torch.randn(M, K, device=cuda)
+    if kind == "grad":
+        dw, db = hip_ops.linear_wgrad(dz, a)
+        dwr, dbr = torch_ops.linear_wgrad(dz, a)
+        _close(dw, dwr, rtol=1e-4, atol=1e-4)
+        _close(db, dbr, rtol=1e-4, atol=1e-4)
+        return
+    cfg = OptimCfg("adam", 1e-3, weight_decay=1e-5) if kind == "adam" else OptimCfg("sgd", 1e-2, momentum=0.9)
+    w = torch.randn(N, K, device=cuda)
+    b = torch.randn(N, device=cuda)
+    def st(p):
+        return {"m": torch.randn_like(p) * 0.1, "v": torch.rand_like(p) * 0.1} if kind == "adam" else \
+            {"buf": torch.randn_like(p) * 0.1}
+    sw, sb = st(w), st(b)
+    sw2 = {k: v.clone() for k, v in sw.items()}
+    sb2 = {k: v.clone() for k, v in sb.items()}
+    w2, b2 = w.clone(), b.clone()
+    hip_ops.linear_wgrad_step_(dz, a, w, b, cfg, sw, sb, 5)
+    torch_ops.linear_wgrad_step_(dz, a, w2, b2, cfg, sw2, sb2, 5)
+    _close(w, w2, rtol=1e-4, atol=1e-5)
+    _close(b, b2, rtol=1e-4, atol=1e-5)
+    for k in sw:
+        _close(sw[k], sw2[k], rtol=1e-4, atol=1e-5)
+        _close(sb[k], sb2[k], rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("M,C", [(16, 100), (16, 10), (16, 5408), (9, 100), (1000, 100)])
+def test_softmax_ce(cuda, M, C):
+    x = torch.randn(M, C, device=cuda) * 3
+    y = torch.randint(0, min(C, 10), (M,), device=cuda)
+    y[0] = -100
+    loss, d = hip_ops.softmax_ce(x, y, 1.0 / M)
+    lr, dr = torch_ops.softmax_ce(x, y, 1.0 / M)
+    _close(loss, lr, rtol=1e-5, atol=1e-5)
+    _close(d, dr, rtol=1e-5, atol=1e-6)
+    ref = torch.nn.functional.cross_entropy(x, y, reduction="sum") / M
+    assert abs(loss.sum().item() / M - ref.item()) < 1e-4
+
+
+@pytest.mark.parametrize("M,C", [(16, 100), (3001, 100), (77, 10)])
+def test_eval_counters(cuda, M, C):
+    x = torch.randn(M, C, device=cuda)
+    y = torch.randint(0, 10, (M,), device=cuda)
+    x[torch.arange(M // 2, device=cuda), y[: M // 2]] += 10.0
+    c = hip_ops.eval_counters(x, y, 9)
+    cr = torch_ops.eval_counters(x, y, 9)
+    assert c.cpu().tolist() == cr.cpu().tolist()
+
+
+def test_opt_flat(cuda):
+    p = torch.randn(1001, device=cuda)
+    g = torch.randn(1001, device=cuda)
+    cfg = OptimCfg("adam", 1e-3, weight_decay=1e-5)
+    st = {"m": torch.zeros_like(p), "v": torch.zeros_like(p)}
+    p2, st2 = p.clone(), {k: v.clone() for k, v in st.items()}
+    hip_ops.apply_update_(p, g, st, cfg, 1)
+    torch_ops.apply_update_(p2, g, st2, cfg, 1)
+    _close(p, p2, rtol=1e-5, atol=1e-6)
