@@ -1,0 +1,126 @@
+"""CLI parity, data pipeline invariants and checkpoint (state_dict) layout."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from splitlearning_amd.config import build_parser, parse_args
+from splitlearning_amd.data import (dirichlet_partition, make_client_shards, synthetic_mnist, write_shards,
+                                    load_shard, shard_paths)
+from splitlearning_amd.models import (model1, model1_sisa, model2, model2_sisa, model2_sisa_concat, model3)
+
+
+def test_reference_flags_and_defaults():
+    a = parse_args([])
+    assert (a.world_size, a.epochs, a.iterations, a.batch_size) == (3, 1, 5, 16)
+    assert a.partition_alpha == 0.5 and a.datapath == "data/mnist_flat" and a.lr == 0.001
+    assert a.server_epochs == 3 and not (a.vanilla or a.sisa or a.concat or a.control)
+    assert a.mode == "ushape" and a.client_num_in_total == 2
+    assert parse_args(["--vanilla"]).mode == "vanilla"
+    assert parse_args(["--sisa"]).mode == "sisa"
+    assert parse_args(["--sisa", "--concat"]).mode == "concat"
+    assert parse_args(["--control"]).mode == "control"
+    flags = {a.dest for a in build_parser()._actions}
+    for f in ["world_size", "epochs", "iterations", "batch_size", "partition_alpha", "datapath", "lr",
+              "server_epochs", "vanilla", "sisa", "concat", "control"]:
+        assert f in flags
+
+
+@pytest.mark.parametrize("argv,msg", [
+    (["--concat"], "--concat option can only be used with the --sisa"),
+    (["--vanilla", "--sisa"], "--vanilla option cannot be used"),
+    (["--vanilla", "--sisa", "--concat"], "--vanilla option cannot be used"),
+    (["--control", "--sisa"], "--control option cannot be used"),
+])
+def test_reference_validation_errors(argv, msg):
+    with pytest.raises(ValueError, match=msg):
+        parse_args(argv)
+
+
+def test_dirichlet_partition_invariants():
+    y = np.random.default_rng(0).integers(0, 10, 5000)
+    for k in (1, 2, 4, 8):
+        parts = dirichlet_partition(y, k, 10, 0.5, rng=np.random.default_rng(k))
+        allidx = np.concatenate(list(parts.values()))
+        assert len(allidx) == len(y) and len(np.unique(allidx)) == len(y)
+        assert min(len(p) for p in parts.values()) >= 10
+    p1 = dirichlet_partition(y, 4, 10, 0.5, rng=np.random.default_rng(3))
+    p2 = dirichlet_partition(y, 4, 10, 0.5, rng=np.random.default_rng(3))
+    assert all(np.array_equal(p1[i], p2[i]) for i in range(4))
+
+
+def test_dirichlet_is_non_iid_at_small_alpha():
+    y = np.random.default_rng(0).integers(0, 10, 20000)
+    parts = dirichlet_partition(y, 4, 10, 0.1, rng=np.random.default_rng(0))
+    hist = np.stack([np.bincount(y[p], minlength=10) / len(p) for p in parts.values()])
+    assert hist.max(axis=1).mean() > 0.3          # skewed label mixtures
+
+
+def test_synthetic_mnist_shape_and_range():
+    x, y = synthetic_mnist(100, seed=0)
+    assert x.shape == (100, 1, 28, 28) and x.dtype == np.uint8 and y.dtype == np.int64
+    assert set(np.unique(y)) <= set(range(10))
+
+
+def test_shards_tensor_only_roundtrip(tmp_path):
+    class A:
+        pass
+    a = A()
+    a.datapath = str(tmp_path)
+    a.client_num_in_total = 3
+    a.partition_alpha = 0.5
+    a.num_samples = 900
+    a.seed = 1
+    a.mnist_npz = ""
+    sizes = write_shards(a, verbose=False)
+    total = 0
+    for cid in (1, 2, 3):
+        ptr, pte = shard_paths(str(tmp_path), cid)
+        assert os.path.basename(ptr) == f"data_worker{cid}_train.pt"
+        tr, te = load_shard(str(tmp_path), cid)          # weights_only=True inside
+        assert tr["x"].dtype == torch.uint8 and tr["x"].shape[1:] == (1, 28, 28)
+        assert sizes[cid] == (len(tr["y"]), len(te["y"]))
+        # 80/20 split per client (relational_table_preprocessor.py:80)
+        n = len(tr["y"]) + len(te["y"])
+        assert len(tr["y"]) == int(n * 0.8)
+        total += n
+    assert total == 900
+
+
+def test_make_client_shards_disjoint():
+    x, y = synthetic_mnist(500, seed=0)
+    sh = make_client_shards(x, y, 2, 0.5, seed=0)
+    assert sum(len(v[1]) + len(v[3]) for v in sh.values()) == 500
+
+
+REF_KEYS = {
+    model1: {"conv1.weight": (32, 1, 3, 3), "conv1.bias": (32,)},
+    model1_sisa: {"conv_layers.0.weight": (32, 1, 3, 3), "conv_layers.0.bias": (32,)},
+    model2: {"fc1.weight": (1000, 5408), "fc1.bias": (1000,), "fc2.weight": (100, 1000), "fc2.bias": (100,)},
+    model2_sisa: {"fc1.weight": (5000, 5408), "fc1.bias": (5000,), "fc2.weight": (1000, 5000),
+                  "fc2.bias": (1000,), "fc3.weight": (100, 1000), "fc3.bias": (100,)},
+    model3: {"fc3.weight": (10, 100), "fc3.bias": (10,)},
+}
+
+
+@pytest.mark.parametrize("cls", list(REF_KEYS))
+def test_state_dict_layout_matches_reference(cls):
+    sd = cls().state_dict()
+    assert {k: tuple(v.shape) for k, v in sd.items()} == REF_KEYS[cls]
+
+
+def test_param_counts_match_survey():
+    count = lambda m: sum(p.numel() for p in m.parameters())
+    assert count(model1()) == 320 and count(model1_sisa()) == 320
+    assert count(model2()) == 5_509_100 and count(model2_sisa()) == 32_146_100
+    assert count(model2_sisa_concat(4)) == 113_566_400 and count(model3()) == 1_010
+
+
+def test_model_forward_shapes():
+    x = torch.zeros(2, 1, 28, 28)
+    assert model1_sisa()(x).shape == (2, 5408)
+    assert model2_sisa()(torch.zeros(2, 5408)).shape == (2, 100)
+    assert model2_sisa_concat(3)(torch.zeros(2, 5408 * 3)).shape == (2, 300)
+    assert model2()(torch.zeros(2, 32, 13, 13)).shape == (2, 100)
+    assert model3()(torch.zeros(2, 100)).shape == (2, 10)
