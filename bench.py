@@ -48,7 +48,7 @@ def _session_args(a, world_size, log_dir):
         batch_size=a.batch_size, partition_alpha=0.5, datapath="", lr=1e-3, server_epochs=a.server_epochs,
         vanilla=False, sisa=True, concat=False, control=False, mode="sisa", seed=a.seed, log_dir=log_dir,
         no_tqdm=True, true_reset=False, eval_dropout_fix=False, concat_unlearn=False, omit_label=9,
-        unlearn_client_ids=[1], save_dir="", resume_dir="", kernels=a.kernels)
+        unlearn_client_ids=[1], save_dir="", resume_dir="", kernels=a.kernels, graphs=a.graphs)
 
 
 def main(argv=None):
@@ -64,6 +64,7 @@ def main(argv=None):
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--bob_tp", type=int, default=0, help="0 = all ranks")
     ap.add_argument("--json_out", type=str, default="")
+    ap.add_argument("--graphs", choices=("auto", "on", "off"), default="auto")
     a = ap.parse_args(argv)
 
     from splitlearning_amd import ops

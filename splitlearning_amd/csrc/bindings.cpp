@@ -4,6 +4,12 @@
 // see an operand its grid does not assume), fetch the current HIP stream from the
 // PyTorch-ROCm stream registry, and call the launcher.  All buffers are
 // caller-allocated so the same calls can be captured into a HIP graph.
+//
+// Optimizer hyper-parameters travel as (kind, lr, beta1, beta2, eps, wd, momentum, t, dyn):
+// kind 0 = write the gradient into s0, 1 = SGD(momentum), 2 = Adam (L2 weight decay);
+// `dyn` != 0 is the device address of {step_size, inv_bc2_sqrt} used instead of t
+// (graph replay).  Dropout seeds likewise: (seed, dseed) with dseed = device address
+// of {seed_lo, seed_hi} or 0.
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
@@ -13,11 +19,14 @@
 namespace sl {
 hipError_t conv_fwd(const void* x, bool x_u8, const int64_t* idx, int64_t row0, int B, const float* w,
                     const float* b, float* y, uint8_t* am, hipStream_t st);
-hipError_t conv_bwd_opt(const float* dy, const float* y, const uint8_t* am, const void* x, bool x_u8,
-                        const int64_t* idx, int64_t row0, int B, float* w, float* b, float* s0w, float* s1w,
-                        float* s0b, float* s1b, SlOpt o, hipStream_t st);
+hipError_t conv_local_step(const void* x, bool x_u8, const int64_t* idx, const int64_t* labels, int B, float* w,
+                           float* b, float* slab, float* loss_rows, float* s0w, float* s1w, float* s0b, float* s1b,
+                           SlOpt o, hipStream_t st);
+hipError_t conv_bwd_step(const float* dy, const float* y, const uint8_t* am, const void* x, bool x_u8,
+                         const int64_t* idx, int B, float* w, float* b, float* slab, float* s0w, float* s1w,
+                         float* s0b, float* s1b, SlOpt o, hipStream_t st);
 hipError_t linear_fwd(const float* X, int ldx, const float* W, int ldw, float* Y, int ldy, int M, int N, int K,
-                      Epi e, hipStream_t st);
+                      Epi e, float* ws, int64_t ws_elems, hipStream_t st);
 hipError_t linear_dgrad(const float* dZ, int ldz, const float* W, int ldw, const float* hprev, int ldh,
                         float scale, float* dX, int ldx, float* ws, int64_t ws_elems, int M, int N, int K,
                         hipStream_t st);
@@ -34,20 +43,18 @@ hipError_t eval_counters(const float* x, int ldx, const int64_t* y, int64_t omit
 
 namespace {
 
+using OptT = c10::optional<at::Tensor>;
+
 hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
-void check(hipError_t e, const char* what) {
-  TORCH_CHECK(e == hipSuccess, what, ": ", hipGetErrorString(e));
-}
+void check(hipError_t e, const char* what) { TORCH_CHECK(e == hipSuccess, what, ": ", hipGetErrorString(e)); }
 
-void need_cuda(const at::Tensor& t, const char* name) {
-  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
-}
+void need_cuda(const at::Tensor& t, const char* name) { TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor"); }
 void need_f32(const at::Tensor& t, const char* name) {
   need_cuda(t, name);
   TORCH_CHECK(t.scalar_type() == at::kFloat, name, " must be float32");
 }
-// row-major 2-D with unit column stride, 16-byte aligned rows (float4 loads)
+// row-major 2-D with unit column stride and 16-byte aligned rows (float4 loads)
 void need_rows(const at::Tensor& t, const char* name) {
   need_f32(t, name);
   TORCH_CHECK(t.dim() == 2 && t.stride(1) == 1, name, " must be 2-D with unit column stride");
@@ -59,12 +66,10 @@ void need_2d(const at::Tensor& t, const char* name) {
   need_f32(t, name);
   TORCH_CHECK(t.dim() == 2 && t.stride(1) == 1, name, " must be 2-D with unit column stride");
 }
-float* fptr(const c10::optional<at::Tensor>& t) {
-  return t.has_value() && t->defined() ? t->data_ptr<float>() : nullptr;
-}
+float* fptr(const OptT& t) { return t.has_value() && t->defined() ? t->data_ptr<float>() : nullptr; }
 
 SlOpt make_opt(int64_t kind, double lr, double beta1, double beta2, double eps, double wd, double momentum,
-                   int64_t t) {
+               int64_t t, int64_t dyn) {
   SlOpt o{};
   o.kind = (int)kind;
   o.lr = (float)lr;
@@ -73,7 +78,8 @@ SlOpt make_opt(int64_t kind, double lr, double beta1, double beta2, double eps, 
   o.eps = (float)eps;
   o.wd = (float)wd;
   o.momentum = (float)momentum;
-  if (kind == 2) {
+  o.dyn = reinterpret_cast<const float*>(dyn);
+  if (kind == 2 && !dyn) {
     TORCH_CHECK(t >= 1, "Adam step count must be >= 1");
     const double bc1 = 1.0 - std::pow(beta1, (double)t);
     const double bc2 = 1.0 - std::pow(beta2, (double)t);
@@ -83,75 +89,100 @@ SlOpt make_opt(int64_t kind, double lr, double beta1, double beta2, double eps, 
   return o;
 }
 
-Epi make_epi(const c10::optional<at::Tensor>& bias, bool relu, double drop_p, uint64_t seed, int64_t col_off) {
+Epi make_epi(const OptT& bias, bool relu, double drop_p, uint64_t seed, int64_t col_off, int64_t dseed) {
   Epi e{};
-  e.bias = bias.has_value() && bias->defined() ? bias->data_ptr<float>() : nullptr;
+  e.bias = fptr(bias);
   e.relu = relu ? 1 : 0;
   e.thresh = drop_p > 0 ? (uint32_t)(drop_p * 4294967296.0) : 0u;
   e.dscale = drop_p > 0 ? (float)(1.0 / (1.0 - drop_p)) : 1.f;
   e.seed_lo = (uint32_t)(seed & 0xffffffffull);
   e.seed_hi = (uint32_t)(seed >> 32);
   e.col_off = (int)col_off;
+  e.dseed = reinterpret_cast<const uint32_t*>(dseed);
   return e;
 }
 
+#define OPT_ARGS int64_t kind, double lr, double beta1, double beta2, double eps, double wd, double momentum, \
+                 int64_t t, int64_t dyn
+#define OPT_PASS make_opt(kind, lr, beta1, beta2, eps, wd, momentum, t, dyn)
+
 // ---------------------------------------------------------------- conv
-void conv_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& idx, int64_t row0, int64_t B,
-              const at::Tensor& w, const at::Tensor& b, at::Tensor& y, at::Tensor& am) {
+void check_x(const at::Tensor& x) {
   need_cuda(x, "x");
   TORCH_CHECK(x.is_contiguous() && x.numel() % 784 == 0, "x must be contiguous [N,784]");
-  const bool u8 = x.scalar_type() == at::kByte;
-  TORCH_CHECK(u8 || x.scalar_type() == at::kFloat, "x must be uint8 or float32");
-  const int64_t nrows = x.numel() / 784;
+  TORCH_CHECK(x.scalar_type() == at::kByte || x.scalar_type() == at::kFloat, "x must be uint8 or float32");
+}
+void check_params(const at::Tensor& w, const at::Tensor& b) {
   need_f32(w, "w");
   need_f32(b, "b");
   TORCH_CHECK(w.numel() == 288 && b.numel() == 32 && w.is_contiguous() && b.is_contiguous(), "conv params 32x1x3x3");
+}
+void check_idx(const at::Tensor& idx, int64_t B) {
+  need_cuda(idx, "idx");
+  TORCH_CHECK(idx.scalar_type() == at::kLong && idx.is_contiguous() && idx.numel() >= B, "idx int64 [B]");
+}
+void check_slab(const at::Tensor& slab, int64_t B) {
+  need_f32(slab, "slab");
+  TORCH_CHECK(slab.is_contiguous() && slab.numel() >= B * 320, "slab workspace [B,320]");
+}
+
+void conv_fwd(const at::Tensor& x, const at::Tensor& idx, int64_t B, const at::Tensor& w, const at::Tensor& b,
+              at::Tensor& y, at::Tensor& am) {
+  check_x(x);
+  check_params(w, b);
+  check_idx(idx, B);
   need_f32(y, "y");
   TORCH_CHECK(y.is_contiguous() && y.numel() >= B * 5408, "y too small");
   TORCH_CHECK(am.scalar_type() == at::kByte && am.is_contiguous() && am.numel() >= B * 5408, "am too small");
-  const int64_t* ip = nullptr;
-  if (idx.has_value() && idx->defined()) {
-    TORCH_CHECK(idx->scalar_type() == at::kLong && idx->is_contiguous() && idx->numel() >= B, "idx int64 [B]");
-    need_cuda(*idx, "idx");
-    ip = idx->data_ptr<int64_t>();
-  } else {
-    TORCH_CHECK(row0 >= 0 && row0 + B <= nrows, "row range out of bounds");
-  }
-  check(sl::conv_fwd(x.data_ptr(), u8, ip, row0, (int)B, w.data_ptr<float>(), b.data_ptr<float>(),
-                     y.data_ptr<float>(), am.data_ptr<uint8_t>(), cur_stream()),
+  check(sl::conv_fwd(x.data_ptr(), x.scalar_type() == at::kByte, idx.data_ptr<int64_t>(), 0, (int)B,
+                     w.data_ptr<float>(), b.data_ptr<float>(), y.data_ptr<float>(), am.data_ptr<uint8_t>(),
+                     cur_stream()),
         "conv_fwd");
 }
 
-void conv_bwd_opt(const at::Tensor& dy, const at::Tensor& y, const at::Tensor& am, const at::Tensor& x,
-                  const c10::optional<at::Tensor>& idx, int64_t row0, int64_t B, at::Tensor& w, at::Tensor& b,
-                  at::Tensor& s0w, const c10::optional<at::Tensor>& s1w, at::Tensor& s0b,
-                  const c10::optional<at::Tensor>& s1b, int64_t kind, double lr, double beta1, double beta2,
-                  double eps, double wd, double momentum, int64_t t) {
+// SISA local step: fused gather+conv+pool+softmax-CE(5408)+dW partials, then reduce+optimizer.
+void conv_local_step(const at::Tensor& x, const at::Tensor& idx, const at::Tensor& labels, int64_t B, at::Tensor& w,
+                     at::Tensor& b, at::Tensor& slab, at::Tensor& loss_rows, at::Tensor& s0w, const OptT& s1w,
+                     at::Tensor& s0b, const OptT& s1b, OPT_ARGS) {
+  check_x(x);
+  check_params(w, b);
+  check_idx(idx, B);
+  check_slab(slab, B);
+  need_cuda(labels, "labels");
+  TORCH_CHECK(labels.scalar_type() == at::kLong && labels.numel() == x.numel() / 784, "labels int64 [N]");
+  need_f32(loss_rows, "loss_rows");
+  TORCH_CHECK(loss_rows.numel() >= B, "loss_rows");
+  TORCH_CHECK(s0w.numel() == 288 && s0b.numel() == 32, "optimizer state");
+  check(sl::conv_local_step(x.data_ptr(), x.scalar_type() == at::kByte, idx.data_ptr<int64_t>(),
+                            labels.data_ptr<int64_t>(), (int)B, w.data_ptr<float>(), b.data_ptr<float>(),
+                            slab.data_ptr<float>(), loss_rows.data_ptr<float>(), s0w.data_ptr<float>(), fptr(s1w),
+                            s0b.data_ptr<float>(), fptr(s1b), OPT_PASS, cur_stream()),
+        "conv_local_step");
+}
+
+// Split-mode client backward: dW partials from the cut gradient, then reduce+optimizer.
+void conv_bwd_step(const at::Tensor& dy, const at::Tensor& y, const at::Tensor& am, const at::Tensor& x,
+                   const at::Tensor& idx, int64_t B, at::Tensor& w, at::Tensor& b, at::Tensor& slab, at::Tensor& s0w,
+                   const OptT& s1w, at::Tensor& s0b, const OptT& s1b, OPT_ARGS) {
+  check_x(x);
+  check_params(w, b);
+  check_idx(idx, B);
+  check_slab(slab, B);
   need_f32(dy, "dy");
   need_f32(y, "y");
   TORCH_CHECK(dy.is_contiguous() && y.is_contiguous() && dy.numel() >= B * 5408 && y.numel() >= B * 5408, "dy/y");
-  TORCH_CHECK(am.scalar_type() == at::kByte && am.numel() >= B * 5408, "am");
-  need_cuda(x, "x");
-  const bool u8 = x.scalar_type() == at::kByte;
-  const int64_t nrows = x.numel() / 784;
-  const int64_t* ip = nullptr;
-  if (idx.has_value() && idx->defined()) {
-    TORCH_CHECK(idx->scalar_type() == at::kLong && idx->numel() >= B, "idx int64 [B]");
-    ip = idx->data_ptr<int64_t>();
-  } else {
-    TORCH_CHECK(row0 >= 0 && row0 + B <= nrows, "row range out of bounds");
-  }
-  TORCH_CHECK(w.numel() == 288 && b.numel() == 32 && s0w.numel() == 288 && s0b.numel() == 32, "conv param/state");
-  check(sl::conv_bwd_opt(dy.data_ptr<float>(), y.data_ptr<float>(), am.data_ptr<uint8_t>(), x.data_ptr(), u8, ip,
-                         row0, (int)B, w.data_ptr<float>(), b.data_ptr<float>(), s0w.data_ptr<float>(), fptr(s1w),
-                         s0b.data_ptr<float>(), fptr(s1b), make_opt(kind, lr, beta1, beta2, eps, wd, momentum, t),
-                         cur_stream()),
-        "conv_bwd_opt");
+  TORCH_CHECK(am.scalar_type() == at::kByte && am.is_contiguous() && am.numel() >= B * 5408, "am");
+  TORCH_CHECK(s0w.numel() == 288 && s0b.numel() == 32, "optimizer state");
+  check(sl::conv_bwd_step(dy.data_ptr<float>(), y.data_ptr<float>(), am.data_ptr<uint8_t>(), x.data_ptr(),
+                          x.scalar_type() == at::kByte, idx.data_ptr<int64_t>(), (int)B, w.data_ptr<float>(),
+                          b.data_ptr<float>(), slab.data_ptr<float>(), s0w.data_ptr<float>(), fptr(s1w),
+                          s0b.data_ptr<float>(), fptr(s1b), OPT_PASS, cur_stream()),
+        "conv_bwd_step");
 }
 
 // ---------------------------------------------------------------- linear
-void linear_fwd(const at::Tensor& X, const at::Tensor& W, const c10::optional<at::Tensor>& bias, at::Tensor& Y,
-                bool relu, double drop_p, uint64_t seed, int64_t col_off) {
+void linear_fwd(const at::Tensor& X, const at::Tensor& W, const OptT& bias, at::Tensor& Y, bool relu, double drop_p,
+                uint64_t seed, int64_t col_off, int64_t dseed, const OptT& ws) {
   need_rows(X, "X");
   need_rows(W, "W");
   need_2d(Y, "Y");
@@ -159,26 +190,34 @@ void linear_fwd(const at::Tensor& X, const at::Tensor& W, const c10::optional<at
   TORCH_CHECK(W.size(1) == K && K % 4 == 0, "W must be [N,K] with K % 4 == 0");
   TORCH_CHECK(Y.size(0) == M && Y.size(1) == N, "Y must be [M,N]");
   if (bias.has_value() && bias->defined()) TORCH_CHECK(bias->numel() == N && bias->is_contiguous(), "bias [N]");
+  float* wp = nullptr;
+  int64_t wn = 0;
+  if (ws.has_value() && ws->defined()) {
+    need_f32(*ws, "ws");
+    TORCH_CHECK(ws->is_contiguous(), "ws contiguous");
+    wp = ws->data_ptr<float>();
+    wn = ws->numel();
+  }
   check(sl::linear_fwd(X.data_ptr<float>(), (int)X.stride(0), W.data_ptr<float>(), (int)W.stride(0),
                        Y.data_ptr<float>(), (int)Y.stride(0), (int)M, (int)N, (int)K,
-                       make_epi(bias, relu, drop_p, seed, col_off), cur_stream()),
+                       make_epi(bias, relu, drop_p, seed, col_off, dseed), wp, wn, cur_stream()),
         "linear_fwd");
 }
 
-void linear_epilogue(const at::Tensor& P, const c10::optional<at::Tensor>& bias, at::Tensor& Y, bool relu,
-                     double drop_p, uint64_t seed, int64_t col_off) {
-  need_f32(P, "P");
-  need_f32(Y, "Y");
-  TORCH_CHECK(P.dim() == 2 && Y.dim() == 2 && P.stride(1) == 1 && Y.stride(1) == 1, "2-D row-major");
+void linear_epilogue(const at::Tensor& P, const OptT& bias, at::Tensor& Y, bool relu, double drop_p, uint64_t seed,
+                     int64_t col_off, int64_t dseed) {
+  need_2d(P, "P");
+  need_2d(Y, "Y");
   TORCH_CHECK(P.sizes() == Y.sizes(), "P/Y shape");
+  if (bias.has_value() && bias->defined()) TORCH_CHECK(bias->numel() == P.size(1), "bias [N]");
   check(sl::linear_epilogue(P.data_ptr<float>(), (int)P.stride(0), Y.data_ptr<float>(), (int)Y.stride(0),
-                            (int)P.size(0), (int)P.size(1), make_epi(bias, relu, drop_p, seed, col_off),
+                            (int)P.size(0), (int)P.size(1), make_epi(bias, relu, drop_p, seed, col_off, dseed),
                             cur_stream()),
         "linear_epilogue");
 }
 
-void linear_dgrad(const at::Tensor& dZ, const at::Tensor& W, const c10::optional<at::Tensor>& hprev, double scale,
-                  at::Tensor& dX, const c10::optional<at::Tensor>& ws) {
+void linear_dgrad(const at::Tensor& dZ, const at::Tensor& W, const OptT& hprev, double scale, at::Tensor& dX,
+                  const OptT& ws) {
   need_2d(dZ, "dZ");
   need_rows(W, "W");
   need_2d(dX, "dX");
@@ -188,8 +227,8 @@ void linear_dgrad(const at::Tensor& dZ, const at::Tensor& W, const c10::optional
   const float* hp = nullptr;
   int ldh = 0;
   if (hprev.has_value() && hprev->defined()) {
-    need_f32(*hprev, "hprev");
-    TORCH_CHECK(hprev->dim() == 2 && hprev->size(0) == M && hprev->size(1) == K && hprev->stride(1) == 1, "hprev");
+    need_2d(*hprev, "hprev");
+    TORCH_CHECK(hprev->size(0) == M && hprev->size(1) == K, "hprev shape");
     hp = hprev->data_ptr<float>();
     ldh = (int)hprev->stride(0);
   }
@@ -207,10 +246,8 @@ void linear_dgrad(const at::Tensor& dZ, const at::Tensor& W, const c10::optional
         "linear_dgrad");
 }
 
-void linear_wgrad_opt(const at::Tensor& dZ, const at::Tensor& A, at::Tensor& W, at::Tensor& s0,
-                      const c10::optional<at::Tensor>& s1, const c10::optional<at::Tensor>& bias,
-                      const c10::optional<at::Tensor>& sb0, const c10::optional<at::Tensor>& sb1, int64_t kind,
-                      double lr, double beta1, double beta2, double eps, double wd, double momentum, int64_t t) {
+void linear_wgrad_opt(const at::Tensor& dZ, const at::Tensor& A, at::Tensor& W, at::Tensor& s0, const OptT& s1,
+                      const OptT& bias, const OptT& sb0, const OptT& sb1, OPT_ARGS) {
   need_2d(dZ, "dZ");
   need_rows(A, "A");
   need_rows(W, "W");
@@ -224,29 +261,25 @@ void linear_wgrad_opt(const at::Tensor& dZ, const at::Tensor& A, at::Tensor& W, 
     TORCH_CHECK(bias->numel() == N && sb0.has_value() && sb0->numel() == N, "bias state");
   check(sl::linear_wgrad_opt(dZ.data_ptr<float>(), (int)dZ.stride(0), A.data_ptr<float>(), (int)A.stride(0),
                              W.data_ptr<float>(), (int)W.stride(0), s0.data_ptr<float>(), fptr(s1), fptr(bias),
-                             fptr(sb0), fptr(sb1), (int)M, (int)N, (int)K,
-                             make_opt(kind, lr, beta1, beta2, eps, wd, momentum, t), cur_stream()),
+                             fptr(sb0), fptr(sb1), (int)M, (int)N, (int)K, OPT_PASS, cur_stream()),
         "linear_wgrad_opt");
 }
 
-void opt_flat(at::Tensor& p, const at::Tensor& g, at::Tensor& s0, const c10::optional<at::Tensor>& s1,
-              int64_t kind, double lr, double beta1, double beta2, double eps, double wd, double momentum,
-              int64_t t) {
+void opt_flat(at::Tensor& p, const at::Tensor& g, at::Tensor& s0, const OptT& s1, OPT_ARGS) {
   need_f32(p, "p");
   need_f32(g, "g");
   need_f32(s0, "s0");
   TORCH_CHECK(p.is_contiguous() && g.is_contiguous() && s0.is_contiguous(), "contiguous");
   TORCH_CHECK(g.numel() == p.numel() && s0.numel() == p.numel(), "sizes");
-  check(sl::opt_flat(p.data_ptr<float>(), g.data_ptr<float>(), s0.data_ptr<float>(), fptr(s1), p.numel(),
-                     make_opt(kind, lr, beta1, beta2, eps, wd, momentum, t), cur_stream()),
+  check(sl::opt_flat(p.data_ptr<float>(), g.data_ptr<float>(), s0.data_ptr<float>(), fptr(s1), p.numel(), OPT_PASS,
+                     cur_stream()),
         "opt_flat");
 }
 
 // ---------------------------------------------------------------- loss / metrics
 void softmax_ce(const at::Tensor& x, const at::Tensor& y, int64_t ignore, double scale, at::Tensor& loss_rows,
-                const c10::optional<at::Tensor>& d) {
-  need_f32(x, "logits");
-  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "logits 2-D");
+                const OptT& d) {
+  need_2d(x, "logits");
   const int64_t M = x.size(0), C = x.size(1);
   need_cuda(y, "labels");
   TORCH_CHECK(y.scalar_type() == at::kLong && y.numel() == M && y.is_contiguous(), "labels int64 [M]");
@@ -255,8 +288,8 @@ void softmax_ce(const at::Tensor& x, const at::Tensor& y, int64_t ignore, double
   float* dp = nullptr;
   int ldd = 0;
   if (d.has_value() && d->defined()) {
-    need_f32(*d, "dlogits");
-    TORCH_CHECK(d->dim() == 2 && d->size(0) == M && d->size(1) == C && d->stride(1) == 1, "dlogits");
+    need_2d(*d, "dlogits");
+    TORCH_CHECK(d->size(0) == M && d->size(1) == C, "dlogits shape");
     dp = d->data_ptr<float>();
     ldd = (int)d->stride(0);
   }
@@ -266,8 +299,7 @@ void softmax_ce(const at::Tensor& x, const at::Tensor& y, int64_t ignore, double
 }
 
 void eval_counters(const at::Tensor& x, const at::Tensor& y, int64_t omit, at::Tensor& counters) {
-  need_f32(x, "logits");
-  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "logits 2-D");
+  need_2d(x, "logits");
   TORCH_CHECK(y.scalar_type() == at::kLong && y.numel() == x.size(0) && y.is_contiguous(), "labels");
   TORCH_CHECK(counters.scalar_type() == at::kLong && counters.numel() >= 6 && counters.is_contiguous(), "counters");
   need_cuda(counters, "counters");
@@ -282,7 +314,8 @@ void eval_counters(const at::Tensor& x, const at::Tensor& y, int64_t omit, at::T
 PYBIND11_MODULE(_C, m) {
   m.doc() = "splitlearning_amd gfx950 (MI355X) HIP kernels";
   m.def("conv_fwd", &conv_fwd);
-  m.def("conv_bwd_opt", &conv_bwd_opt);
+  m.def("conv_local_step", &conv_local_step);
+  m.def("conv_bwd_step", &conv_bwd_step);
   m.def("linear_fwd", &linear_fwd);
   m.def("linear_epilogue", &linear_epilogue);
   m.def("linear_dgrad", &linear_dgrad);
@@ -290,5 +323,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("opt_flat", &opt_flat);
   m.def("softmax_ce", &softmax_ce);
   m.def("eval_counters", &eval_counters);
+  m.def("set_variant", [](int64_t slot, int64_t v) {
+    TORCH_CHECK(slot >= 0 && slot < 8, "variant slot");
+    sl::g_variant[slot] = (int)v;
+  });
+  m.def("get_variant", [](int64_t slot) { return (int64_t)sl::g_variant[slot]; });
   m.attr("arch") = "gfx950";
 }

@@ -45,6 +45,9 @@ struct SlOpt {
   float beta1, beta2, eps, wd, momentum;
   float step_size;     // Adam: lr / (1 - beta1^t)
   float inv_bc2_sqrt;  // Adam: 1 / sqrt(1 - beta2^t)
+  // graph replay: when set, {step_size, inv_bc2_sqrt} are read from device memory so a
+  // captured step can be replayed at any step count (the host refreshes the table).
+  const float* dyn;
 };
 
 // Update one element. s0 = m (Adam) / momentum buffer (SGD) / grad out (kind 0); s1 = v (Adam).
@@ -59,8 +62,10 @@ __device__ __forceinline__ void sl_opt_update(const SlOpt& o, float& p, float g,
     float m = fmaf(o.beta1, s0, (1.f - o.beta1) * g);
     float v = fmaf(o.beta2, s1, (1.f - o.beta2) * g * g);
     s0 = m; s1 = v;
-    float denom = sqrtf(v) * o.inv_bc2_sqrt + o.eps;
-    p = p - o.step_size * (m / denom);
+    const float ss = o.dyn ? o.dyn[0] : o.step_size;
+    const float ib = o.dyn ? o.dyn[1] : o.inv_bc2_sqrt;
+    float denom = sqrtf(v) * ib + o.eps;
+    p = p - ss * (m / denom);
   }
 }
 
@@ -73,6 +78,26 @@ struct Epi {
   float dscale;         // 1/(1-p)
   uint32_t seed_lo, seed_hi;
   int col_off;          // global column index of column 0 (tensor-parallel shards)
+  const uint32_t* dseed;  // graph replay: {seed_lo, seed_hi} from device memory when set
 };
+
+// Vector form of sl_opt_update (the f32x4 elements cannot bind to float&).
+template <bool ADAM>
+__device__ __forceinline__ void sl_opt_update4(const SlOpt& o, f32x4& p, f32x4 g, f32x4& s0, f32x4& s1) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float pp = p[i], a0 = s0[i], a1 = ADAM ? s1[i] : 0.f;
+    sl_opt_update(o, pp, g[i], a0, a1);
+    p[i] = pp;
+    s0[i] = a0;
+    if (ADAM) s1[i] = a1;
+  }
+}
+
+// Kernel-variant switches for in-process A/B measurement (set from Python via
+// _C.set_variant; 0 = the shipped default everywhere).
+namespace sl {
+extern int g_variant[8];
+}
 
 #define SL_CHECK_LAUNCH() (hipGetLastError())

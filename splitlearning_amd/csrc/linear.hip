@@ -22,6 +22,8 @@
 
 namespace sl {
 
+int g_variant[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
@@ -32,22 +34,36 @@ __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast
 __device__ __forceinline__ float apply_epi(const Epi& e, float v, int m, int n) {
   if (e.bias) v += e.bias[n];
   if (e.relu) v = fmaxf(v, 0.f);
-  if (e.thresh) v = sl_hash_keep(e.seed_lo, e.seed_hi, (uint32_t)m, (uint32_t)(e.col_off + n), e.thresh) ? v * e.dscale : 0.f;
+  if (e.thresh) {
+    const uint32_t lo = e.dseed ? e.dseed[0] : e.seed_lo, hi = e.dseed ? e.dseed[1] : e.seed_hi;
+    v = sl_hash_keep(lo, hi, (uint32_t)m, (uint32_t)(e.col_off + n), e.thresh) ? v * e.dscale : 0.f;
+  }
   return v;
 }
 
 // ---------------------------------------------------------------------------- forward
 // grid (ceil(N/16), ceil(M/16)), block NW*64.  Requires K % 4 == 0, ldx/ldw % 4 == 0.
-template <int NW>
+// U = float4 pairs in flight per lane per iteration; NT = non-temporal weight loads
+// (every weight is read by exactly one wave once per step, so keep it out of L2).
+// Split-K (gridDim.z = S > 1): workgroup z covers its own 16-aligned slice of K and stores
+// raw partial sums to P[z][M][N]; epilogue_kernel then reduces the S slabs and applies the
+// epilogue.  Splitting K is what balances the load: the fc1 GEMM has only 313 column
+// tiles for 256 CUs, and each CU's load issue rate (16 rows x 64 B per wave instruction)
+// is the limiter, so ~4 workgroups per CU beat 1-2 big ones.
+template <int NW, int U, bool NT>
 __global__ void __launch_bounds__(NW * 64)
 skinny_fwd_kernel(const float* __restrict__ X, int ldx, const float* __restrict__ W, int ldw,
-                  float* __restrict__ Y, int ldy, int M, int N, int K, Epi e) {
+                  float* __restrict__ Y, int ldy, int M, int N, int K, Epi e,
+                  float* __restrict__ P = nullptr, int64_t slab = 0) {
   __shared__ f32x4 red[NW][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int n0 = blockIdx.x * 16, m0 = blockIdx.y * 16;
-  const int kper = ((K + 16 * NW - 1) / (16 * NW)) * 16;
-  const int kb = wv * kper;
-  const int ke = min(K, kb + kper);
+  const int S = gridDim.z;
+  const int kz = ((K + 16 * S - 1) / (16 * S)) * 16;
+  const int kz0 = min(K, (int)blockIdx.z * kz), kz1 = min(K, kz0 + kz);
+  const int kper = ((kz1 - kz0 + 16 * NW - 1) / (16 * NW)) * 16;
+  const int kb = kz0 + wv * kper;
+  const int ke = min(kz1, kb + kper);
   const int ra = m0 + (lane & 15), rb = n0 + (lane & 15);
   const int kq = (lane >> 4) * 4;
   const bool va = ra < M, vb = rb < N;
@@ -55,21 +71,26 @@ skinny_fwd_kernel(const float* __restrict__ X, int ldx, const float* __restrict_
   const float* pb = W + (int64_t)(vb ? rb : 0) * ldw;
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  const f32x4 zv = {0.f, 0.f, 0.f, 0.f};
   int k = kb;
-  // main loop: 64 k per iteration, 4 independent float4 pairs in flight per lane
-  for (; k + 64 <= ke; k += 64) {
-    float4 a[4], w[4];
+  // main loop: 16*U k per iteration, U independent float4 pairs in flight per lane
+  for (; k + 16 * U <= ke; k += 16 * U) {
+    float4 a[U];
+    f32x4 w[U];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < U; ++u) {
       a[u] = va ? ld4(pa + k + 16 * u + kq) : z4;
-      w[u] = vb ? ld4(pb + k + 16 * u + kq) : z4;
+      if (NT)
+        w[u] = vb ? __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(pb + k + 16 * u + kq)) : zv;
+      else
+        w[u] = vb ? *reinterpret_cast<const f32x4*>(pb + k + 16 * u + kq) : zv;
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      acc0 = mfma4(a[u].x, w[u].x, acc0);
-      acc1 = mfma4(a[u].y, w[u].y, acc1);
-      acc0 = mfma4(a[u].z, w[u].z, acc0);
-      acc1 = mfma4(a[u].w, w[u].w, acc1);
+    for (int u = 0; u < U; ++u) {
+      acc0 = mfma4(a[u].x, w[u][0], acc0);
+      acc1 = mfma4(a[u].y, w[u][1], acc1);
+      acc0 = mfma4(a[u].z, w[u][2], acc0);
+      acc1 = mfma4(a[u].w, w[u][3], acc1);
     }
   }
   for (; k < ke; k += 16) {
@@ -81,6 +102,81 @@ skinny_fwd_kernel(const float* __restrict__ X, int ldx, const float* __restrict_
     acc1 = mfma4(a.y, w.y, acc1);
     acc0 = mfma4(a.z, w.z, acc0);
     acc1 = mfma4(a.w, w.w, acc1);
+  }
+  red[wv][lane] = acc0 + acc1;
+  __syncthreads();
+  if (wv == 0) {
+    f32x4 s = red[0][lane];
+#pragma unroll
+    for (int i = 1; i < NW; ++i) s += red[i][lane];
+    const int n = n0 + (lane & 15);
+    if (n < N) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + (lane >> 4) * 4 + r;
+        if (m >= M) continue;
+        if (S == 1)
+          Y[(int64_t)m * ldy + n] = apply_epi(e, s[r], m, n);
+        else
+          P[(int64_t)blockIdx.z * slab + (int64_t)m * N + n] = s[r];
+      }
+    }
+  }
+}
+
+// Software-pipelined forward: two register buffers, the next chunk's loads are issued
+// before the current chunk's MFMAs so a wave always has U float4 pairs in flight.
+template <int NW, int U>
+__global__ void __launch_bounds__(NW * 64)
+skinny_fwd_pipe_kernel(const float* __restrict__ X, int ldx, const float* __restrict__ W, int ldw,
+                       float* __restrict__ Y, int ldy, int M, int N, int K, Epi e) {
+  __shared__ f32x4 red[NW][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int n0 = blockIdx.x * 16, m0 = blockIdx.y * 16;
+  const int kper = ((K + 16 * NW - 1) / (16 * NW)) * 16;
+  const int kb = wv * kper;
+  const int ke = min(K, kb + kper);
+  const int ra = m0 + (lane & 15), rb = n0 + (lane & 15);
+  const int kq = (lane >> 4) * 4;
+  const bool va = ra < M, vb = rb < N;
+  const float* pa = X + (int64_t)(va ? ra : 0) * ldx + kq;
+  const float* pb = W + (int64_t)(vb ? rb : 0) * ldw + kq;
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  const f32x4 zv = {0.f, 0.f, 0.f, 0.f};
+  constexpr int CH = 16 * U;
+  const int nfull = ke > kb ? (ke - kb) / CH : 0;
+  f32x4 a0[U], w0[U], a1[U], w1[U];
+#define SL_LD(A_, W_, K0_)                                                           \
+  _Pragma("unroll") for (int u = 0; u < U; ++u) {                                    \
+    A_[u] = va ? *reinterpret_cast<const f32x4*>(pa + (K0_) + 16 * u) : zv;          \
+    W_[u] = vb ? *reinterpret_cast<const f32x4*>(pb + (K0_) + 16 * u) : zv;          \
+  }
+#define SL_MM(A_, W_)                                                                \
+  _Pragma("unroll") for (int u = 0; u < U; ++u) {                                    \
+    acc0 = mfma4(A_[u][0], W_[u][0], acc0);                                          \
+    acc1 = mfma4(A_[u][1], W_[u][1], acc1);                                          \
+    acc0 = mfma4(A_[u][2], W_[u][2], acc0);                                          \
+    acc1 = mfma4(A_[u][3], W_[u][3], acc1);                                          \
+  }
+  if (nfull > 0) { SL_LD(a0, w0, kb); }
+  int c = 0;
+  for (; c + 1 < nfull; c += 2) {
+    SL_LD(a1, w1, kb + (c + 1) * CH);
+    SL_MM(a0, w0);
+    if (c + 2 < nfull) { SL_LD(a0, w0, kb + (c + 2) * CH); }
+    SL_MM(a1, w1);
+  }
+  if (c < nfull) { SL_MM(a0, w0); }
+#undef SL_LD
+#undef SL_MM
+  for (int k = kb + nfull * CH; k < ke; k += 16) {
+    const bool in = k + kq < ke;
+    const f32x4 a = (va && in) ? *reinterpret_cast<const f32x4*>(pa + k) : zv;
+    const f32x4 w = (vb && in) ? *reinterpret_cast<const f32x4*>(pb + k) : zv;
+    acc0 = mfma4(a[0], w[0], acc0);
+    acc1 = mfma4(a[1], w[1], acc1);
+    acc0 = mfma4(a[2], w[2], acc0);
+    acc1 = mfma4(a[3], w[3], acc1);
   }
   red[wv][lane] = acc0 + acc1;
   __syncthreads();
@@ -197,11 +293,13 @@ __global__ void dgrad_reduce_kernel(const float* __restrict__ P, int S, int64_t 
 
 // Y = epilogue(P) for a GEMM done elsewhere (large-M eval path): P [M,N] with ld ldp.
 __global__ void epilogue_kernel(const float* __restrict__ P, int ldp, float* __restrict__ Y, int ldy,
-                                int M, int N, Epi e) {
+                                int M, int N, Epi e, int S = 1, int64_t slab = 0) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (int64_t)M * N) return;
   const int m = (int)(t / N), n = (int)(t - (int64_t)m * N);
-  Y[(int64_t)m * ldy + n] = apply_epi(e, P[(int64_t)m * ldp + n], m, n);
+  float v = P[(int64_t)m * ldp + n];
+  for (int s = 1; s < S; ++s) v += P[s * slab + (int64_t)m * ldp + n];
+  Y[(int64_t)m * ldy + n] = apply_epi(e, v, m, n);
 }
 
 // ---------------------------------------------------------------------------- wgrad + optimizer
@@ -269,6 +367,153 @@ wgrad_opt_kernel(const float* __restrict__ dZ, int ldz, const float* __restrict_
   }
 }
 
+// v2: all R rows' parameter/state loads are issued first (non-temporal, 3R float4 in
+// flight per lane), the block's dZ slice sits in LDS (broadcast reads), the batch rows
+// of A stream from L2 four at a time while the state loads are in flight.
+template <int R, bool ADAM, bool NT>
+__global__ void __launch_bounds__(256)
+wgrad_opt_v2_kernel(const float* __restrict__ dZ, int ldz, const float* __restrict__ A, int lda,
+                    float* __restrict__ W, int ldw, float* __restrict__ s0, float* __restrict__ s1,
+                    float* __restrict__ bias, float* __restrict__ sb0, float* __restrict__ sb1,
+                    int M, int N, int K, SlOpt o) {
+  __shared__ float sdz[16 * R];
+  const int tid = threadIdx.x;
+  const int kq = (blockIdx.x * 256 + tid) * 4;
+  const int n0 = blockIdx.y * R;
+  const int nr = min(R, N - n0);
+  const bool act = kq < K;
+  const f32x4 zv = {0.f, 0.f, 0.f, 0.f};
+  f32x4 p[R], q0[R], q1[R], g[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    g[r] = zv;
+    p[r] = q0[r] = q1[r] = zv;
+    if (act && r < nr) {
+      const int64_t off = (int64_t)(n0 + r) * ldw + kq;
+      if (NT) {
+        p[r] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(W + off));
+        q0[r] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(s0 + off));
+        if (ADAM) q1[r] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(s1 + off));
+      } else {
+        p[r] = *reinterpret_cast<const f32x4*>(W + off);
+        q0[r] = *reinterpret_cast<const f32x4*>(s0 + off);
+        if (ADAM) q1[r] = *reinterpret_cast<const f32x4*>(s1 + off);
+      }
+    }
+  }
+  for (int mc = 0; mc < M; mc += 16) {
+    __syncthreads();
+    if (tid < 16 * R) {
+      const int j = tid / R, r = tid - (tid / R) * R;
+      sdz[tid] = (mc + j < M && r < nr) ? dZ[(int64_t)(mc + j) * ldz + n0 + r] : 0.f;
+    }
+    __syncthreads();
+    if (act) {
+#pragma unroll
+      for (int j = 0; j < 16; j += 4) {
+        f32x4 a[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          a[u] = (mc + j + u < M) ? *reinterpret_cast<const f32x4*>(A + (int64_t)(mc + j + u) * lda + kq) : zv;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int r = 0; r < R; ++r) g[r] += sdz[(j + u) * R + r] * a[u];
+      }
+    }
+  }
+  if (act) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (r < nr) {
+        const int64_t off = (int64_t)(n0 + r) * ldw + kq;
+        sl_opt_update4<ADAM>(o, p[r], g[r], q0[r], q1[r]);
+        if (NT) {
+          if (o.kind != 0) __builtin_nontemporal_store(p[r], reinterpret_cast<f32x4*>(W + off));
+          __builtin_nontemporal_store(q0[r], reinterpret_cast<f32x4*>(s0 + off));
+          if (ADAM) __builtin_nontemporal_store(q1[r], reinterpret_cast<f32x4*>(s1 + off));
+        } else {
+          if (o.kind != 0) *reinterpret_cast<f32x4*>(W + off) = p[r];
+          *reinterpret_cast<f32x4*>(s0 + off) = q0[r];
+          if (ADAM) *reinterpret_cast<f32x4*>(s1 + off) = q1[r];
+        }
+      }
+    }
+  }
+  if (bias && blockIdx.x == 0 && tid < nr) {
+    const int n = n0 + tid;
+    float gb = 0.f;
+    for (int m = 0; m < M; ++m) gb += dZ[(int64_t)m * ldz + n];
+    float pb = bias[n], b0 = sb0[n], b1 = sb1 ? sb1[n] : 0.f;
+    sl_opt_update(o, pb, gb, b0, b1);
+    if (o.kind != 0) bias[n] = pb;
+    sb0[n] = b0;
+    if (sb1) sb1[n] = b1;
+  }
+}
+
+// v3: memory-level parallelism first.  A 1024-thread workgroup owns a 16-row x 256-column
+// tile; every wave covers one row's 256 contiguous weights (1 KB per instruction), so each
+// thread holds exactly one float4 of p/m/v, issues those loads before anything else, and
+// stays at ~40 VGPRs (32 waves/CU resident).  The tile's 16x256 slice of A and its 16x16
+// slice of dZ are staged once in LDS and shared by all 16 rows (A re-read from L2 once
+// per 16 rows); the per-thread dot product is 16 broadcast-free ds_read_b128 + 64 FMAs.
+template <bool ADAM>
+__global__ void __launch_bounds__(1024)
+wgrad_opt_v3_kernel(const float* __restrict__ dZ, int ldz, const float* __restrict__ A, int lda,
+                    float* __restrict__ W, int ldw, float* __restrict__ s0, float* __restrict__ s1,
+                    float* __restrict__ bias, float* __restrict__ sb0, float* __restrict__ sb1,
+                    int M, int N, int K, SlOpt o) {
+  __shared__ f32x4 sa[16][64];
+  __shared__ float sdz[16][16];
+  const int tid = threadIdx.x;
+  const int r = tid >> 6, lane = tid & 63;
+  const int n = blockIdx.y * 16 + r;
+  const int k = blockIdx.x * 256 + lane * 4;
+  const bool act = (n < N) && (k < K);
+  const f32x4 zv = {0.f, 0.f, 0.f, 0.f};
+  const int64_t off = (int64_t)n * ldw + k;
+  f32x4 p = zv, q0 = zv, q1 = zv;
+  if (act) {
+    p = *reinterpret_cast<const f32x4*>(W + off);
+    q0 = *reinterpret_cast<const f32x4*>(s0 + off);
+    if (ADAM) q1 = *reinterpret_cast<const f32x4*>(s1 + off);
+  }
+  f32x4 g = zv;
+  float gb = 0.f;
+  for (int mc = 0; mc < M; mc += 16) {
+    if (mc) __syncthreads();
+    {
+      const int m = mc + r, kk = blockIdx.x * 256 + lane * 4;
+      sa[r][lane] = (m < M && kk < K) ? *reinterpret_cast<const f32x4*>(A + (int64_t)m * lda + kk) : zv;
+      if (tid < 256) {
+        const int mm = mc + (tid >> 4), nn = blockIdx.y * 16 + (tid & 15);
+        sdz[tid >> 4][tid & 15] = (mm < M && nn < N) ? dZ[(int64_t)mm * ldz + nn] : 0.f;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      const float d = sdz[m][r];
+      g += d * sa[m][lane];
+      gb += d;
+    }
+  }
+  if (act) {
+    sl_opt_update4<ADAM>(o, p, g, q0, q1);
+    if (o.kind != 0) *reinterpret_cast<f32x4*>(W + off) = p;
+    *reinterpret_cast<f32x4*>(s0 + off) = q0;
+    if (ADAM) *reinterpret_cast<f32x4*>(s1 + off) = q1;
+  }
+  if (bias && blockIdx.x == 0 && lane == 0 && n < N) {
+    float pb = bias[n], b0 = sb0[n], b1 = sb1 ? sb1[n] : 0.f;
+    sl_opt_update(o, pb, gb, b0, b1);
+    if (o.kind != 0) bias[n] = pb;
+    sb0[n] = b0;
+    if (sb1) sb1[n] = b1;
+  }
+}
+
 // Plain elementwise optimizer over a flat parameter (generic fallback / tests).
 __global__ void opt_flat_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ s0,
                                 float* __restrict__ s1, int64_t n, SlOpt o) {
@@ -283,14 +528,47 @@ __global__ void opt_flat_kernel(float* __restrict__ p, const float* __restrict__
 
 // ---------------------------------------------------------------------------- host launchers
 hipError_t linear_fwd(const float* X, int ldx, const float* W, int ldw, float* Y, int ldy, int M, int N,
-                      int K, Epi e, hipStream_t st) {
+                      int K, Epi e, float* ws, int64_t ws_elems, hipStream_t st) {
   if (M <= 0 || N <= 0) return hipSuccess;
   dim3 grid((N + 15) / 16, (M + 15) / 16);
-  // enough waves per column tile to keep HBM busy; fewer when K is short
-  if (K >= 2048)
-    skinny_fwd_kernel<8><<<grid, 512, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e);
-  else
-    skinny_fwd_kernel<4><<<grid, 256, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e);
+  const int v = g_variant[0];
+  if (v == 0 || v >= 7) {
+    // split K until there are ~4 workgroups per CU, keeping >= 256 k per workgroup
+    const int tiles = grid.x * grid.y;
+    int S = 1;
+    const int target = (v == 8) ? 2048 : (v == 9 ? 512 : 1024);
+    while (S < 16 && tiles * S * 2 <= target && K / (S * 2) >= 256) S *= 2;
+    const int64_t slab = (int64_t)M * N;
+    if (S > 1 && (ws == nullptr || ws_elems < slab * S)) S = 1;
+    const int kz = (K + S - 1) / S;
+    const int nw = kz >= 1024 ? 8 : (kz >= 512 ? 4 : 2);
+    dim3 g3(grid.x, grid.y, S);
+    float* P = S > 1 ? ws : nullptr;
+    if (nw == 8)
+      skinny_fwd_kernel<8, 4, false><<<g3, 512, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e, P, slab);
+    else if (nw == 4)
+      skinny_fwd_kernel<4, 4, false><<<g3, 256, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e, P, slab);
+    else
+      skinny_fwd_kernel<2, 4, false><<<g3, 128, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e, P, slab);
+    if (S > 1) {
+      const int64_t tot = (int64_t)M * N;
+      epilogue_kernel<<<(unsigned)((tot + 255) / 256), 256, 0, st>>>(ws, N, Y, ldy, M, N, e, S, slab);
+    }
+    return hipGetLastError();
+  }
+  if (K >= 2048) {
+    switch (v) {
+      case 1: skinny_fwd_kernel<8, 4, true><<<grid, 512, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e); break;
+      case 2: skinny_fwd_kernel<8, 8, false><<<grid, 512, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e); break;
+      case 3: skinny_fwd_pipe_kernel<8, 4><<<grid, 512, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e); break;
+      case 4: skinny_fwd_pipe_kernel<8, 8><<<grid, 512, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e); break;
+      case 5: skinny_fwd_pipe_kernel<16, 4><<<grid, 1024, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e); break;
+      case 6: skinny_fwd_pipe_kernel<4, 8><<<grid, 256, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e); break;
+      default: skinny_fwd_kernel<8, 4, false><<<grid, 512, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e); break;
+    }
+  } else {
+    skinny_fwd_kernel<4, 4, false><<<grid, 256, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e);
+  }
   return hipGetLastError();
 }
 
@@ -301,7 +579,7 @@ hipError_t linear_dgrad(const float* dZ, int ldz, const float* W, int ldw, const
   const int kt = (K + 63) / 64, mt = (M + 15) / 16;
   int S = 1;
   // aim for >= ~256 workgroups on the 256-CU part; split N when there are few K tiles
-  while (S < 8 && kt * mt * S < 192 && N / (S * 2) >= 64) S *= 2;
+  while (S < 16 && kt * mt * S < 768 && N / (S * 2) >= 64) S *= 2;
   const int64_t slab = (int64_t)M * K;
   if (S > 1 && (ws == nullptr || ws_elems < slab * S)) S = 1;
   dim3 grid(kt, mt, S);
@@ -329,7 +607,24 @@ hipError_t linear_wgrad_opt(const float* dZ, int ldz, const float* A, int lda, f
   if (N <= 0 || K <= 0) return hipSuccess;
   constexpr int R = 8;
   dim3 grid((K / 4 + 255) / 256, (N + R - 1) / R);
-  wgrad_opt_kernel<R><<<grid, 256, 0, st>>>(dZ, ldz, A, lda, W, ldw, s0, s1, bias, sb0, sb1, M, N, K, o);
+  // default (0) = v3 (5.8 TB/s effective on fc1 at M = 16); 3 = v1, 1/2 = v2 variants
+  const int v = g_variant[1];
+  if (v == 3) {
+    wgrad_opt_kernel<R><<<grid, 256, 0, st>>>(dZ, ldz, A, lda, W, ldw, s0, s1, bias, sb0, sb1, M, N, K, o);
+  } else if (v == 1) {
+    if (o.kind == 2)
+      wgrad_opt_v2_kernel<R, true, false><<<grid, 256, 0, st>>>(dZ, ldz, A, lda, W, ldw, s0, s1, bias, sb0, sb1, M,
+                                                                N, K, o);
+    else
+      wgrad_opt_v2_kernel<R, false, false><<<grid, 256, 0, st>>>(dZ, ldz, A, lda, W, ldw, s0, s1, bias, sb0, sb1, M,
+                                                                 N, K, o);
+  } else {
+    dim3 g3((K + 255) / 256, (N + 15) / 16);
+    if (o.kind == 2)
+      wgrad_opt_v3_kernel<true><<<g3, 1024, 0, st>>>(dZ, ldz, A, lda, W, ldw, s0, s1, bias, sb0, sb1, M, N, K, o);
+    else
+      wgrad_opt_v3_kernel<false><<<g3, 1024, 0, st>>>(dZ, ldz, A, lda, W, ldw, s0, s1, bias, sb0, sb1, M, N, K, o);
+  }
   return hipGetLastError();
 }
 

@@ -46,6 +46,45 @@ softmax_ce_kernel(const float* __restrict__ x, int ldx, const int64_t* __restric
   }
 }
 
+// Wide rows (C in the thousands, e.g. the 5408-way SISA client loss): one 256-thread
+// workgroup per row, LDS reduction across its 4 waves.
+__global__ void __launch_bounds__(256)
+softmax_ce_wide_kernel(const float* __restrict__ x, int ldx, const int64_t* __restrict__ y, int64_t ignore,
+                       float scale, float* __restrict__ loss_rows, float* __restrict__ d, int ldd, int C) {
+  __shared__ float red[8];
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const float* xr = x + (int64_t)row * ldx;
+  float* dr = d ? d + (int64_t)row * ldd : nullptr;
+  const int64_t lab = y[row];
+  if (lab == ignore) {
+    if (tid == 0) loss_rows[row] = 0.f;
+    if (dr)
+      for (int c = tid; c < C; c += 256) dr[c] = 0.f;
+    return;
+  }
+  float mx = -INFINITY;
+  for (int c = tid; c < C; c += 256) mx = fmaxf(mx, xr[c]);
+  mx = sl_wave_max(mx);
+  if (lane == 0) red[wv] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  float s = 0.f;
+  for (int c = tid; c < C; c += 256) s += expf(xr[c] - mx);
+  s = sl_wave_sum(s);
+  if (lane == 0) red[4 + wv] = s;
+  __syncthreads();
+  s = red[4] + red[5] + red[6] + red[7];
+  const float inv = 1.f / s;
+  if (tid == 0) loss_rows[row] = mx + logf(s) - xr[lab];
+  if (dr) {
+    for (int c = tid; c < C; c += 256) {
+      float p = expf(xr[c] - mx) * inv;
+      if (c == lab) p -= 1.f;
+      dr[c] = p * scale;
+    }
+  }
+}
+
 // counters[6] += {correct, total, correct_unlearned, total_unlearned, correct_remaining, total_remaining}
 __global__ void __launch_bounds__(256)
 eval_counters_kernel(const float* __restrict__ x, int ldx, const int64_t* __restrict__ y, int64_t omit,
@@ -85,7 +124,10 @@ eval_counters_kernel(const float* __restrict__ x, int ldx, const int64_t* __rest
 hipError_t softmax_ce(const float* x, int ldx, const int64_t* y, int64_t ignore, float scale, float* loss_rows,
                       float* d, int ldd, int M, int C, hipStream_t st) {
   if (M <= 0) return hipSuccess;
-  softmax_ce_kernel<<<(M + 3) / 4, 256, 0, st>>>(x, ldx, y, ignore, scale, loss_rows, d, ldd, M, C);
+  if (C > 512)
+    softmax_ce_wide_kernel<<<M, 256, 0, st>>>(x, ldx, y, ignore, scale, loss_rows, d, ldd, C);
+  else
+    softmax_ce_kernel<<<(M + 3) / 4, 256, 0, st>>>(x, ldx, y, ignore, scale, loss_rows, d, ldd, M, C);
   return hipGetLastError();
 }
 

@@ -51,6 +51,16 @@ class FrontEngine:
                                       slot.state(prefix + "conv.weight", w),
                                       slot.state(prefix + "conv.bias", b), t)
 
+    def local_step(self, shard: DeviceShard, idx, slot: OptSlot):
+        """SISA client-only step: CE on the activation itself (Q5) + optimizer, fused."""
+        if self.frozen:
+            raise RuntimeError("element 0 of tensors does not require grad and does not have a grad_fn "
+                               "(client front is frozen: call unfreeze_weights first)")
+        w, b = self.params
+        t = slot.tick()
+        return self.ops.conv_local_step_(shard.x, shard.y, idx, w, b, slot.cfg,
+                                         slot.state("conv.weight", w), slot.state("conv.bias", b), t)
+
     def reset_parameters(self, true_reset: bool):
         """Reference `reset_model` (data_entities_vanilla.py:204-207): reset the direct
         children that have `reset_parameters`.  For model1_sisa that is nothing (Q4) unless

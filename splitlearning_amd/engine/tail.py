@@ -86,7 +86,8 @@ class TailEngine:
         self._train_fwd = False
 
     # ------------------------------------------------------------------ forward
-    def forward(self, x: torch.Tensor, train: bool | None = None) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, train: bool | None = None, dseeds=None) -> torch.Tensor:
+        """`dseeds[i]` (graph replay only): device int32[2] holding layer i's dropout seed."""
         train = self.training if train is None else train
         self.fwd_count += 1
         step = self.fwd_count
@@ -96,12 +97,13 @@ class TailEngine:
             ls = L.spec
             drop = ls.dropout if train else 0.0
             seed = step_seed(self.seed_base, i, step)
+            kw = {} if dseeds is None else {"dseed": dseeds[i]}
             if L.style == "row":
                 part = self.ops.linear_fwd(h, L.W, None, False, 0.0, 0, 0)
                 self.allreduce(part)
-                h = self.ops.linear_epilogue(part, L.b, ls.relu, drop, seed, 0)
+                h = self.ops.linear_epilogue(part, L.b, ls.relu, drop, seed, 0, **kw)
             else:
-                h = self.ops.linear_fwd(h, L.W, L.b, ls.relu, drop, seed, L.col_off)
+                h = self.ops.linear_fwd(h, L.W, L.b, ls.relu, drop, seed, L.col_off, **kw)
             acts.append(h)
         self.acts = acts
         self._train_fwd = train
@@ -135,13 +137,15 @@ class TailEngine:
         self.dz = dzs
         return dx
 
-    def backward_step(self, slot: OptSlot, t: int | None = None, prefix: str = ""):
-        """Phase 2: fused wgrad + optimizer update of every layer (one optimizer step)."""
+    def backward_step(self, slot: OptSlot, t: int | None = None, prefix: str = "", dyn=None):
+        """Phase 2: fused wgrad + optimizer update of every layer (one optimizer step).
+        `dyn` (graph replay only): device float[2] with Adam's {step_size, 1/sqrt(bc2)}."""
         t = slot.tick() if t is None else t
+        kw = {} if dyn is None else {"dyn": dyn}
         for i, L in enumerate(self.layers):
             self.ops.linear_wgrad_step_(self.dz[i], self.acts[i], L.W, L.b, slot.cfg,
                                         slot.state(f"{prefix}{L.spec.name}.weight", L.W),
-                                        slot.state(f"{prefix}{L.spec.name}.bias", L.b), t)
+                                        slot.state(f"{prefix}{L.spec.name}.bias", L.b), t, **kw)
         self.dz = []
 
     # ------------------------------------------------------------------ state

@@ -1,7 +1,9 @@
 """HIP (gfx950) implementations of the framework ops, over `splitlearning_amd._C`.
 
-Same signatures as `ops.torch_ops`.  Importing this module loads the in-tree
-extension and raises if it is missing: on a GPU the HIP path is the one that
+Same signatures as `ops.torch_ops` (plus optional graph-replay hooks: `dyn` = a device
+tensor holding {step_size, inv_bc2_sqrt} for Adam, `dseed` = a device tensor holding
+{seed_lo, seed_hi} for dropout).  Importing this module does not load the extension;
+the first call does, and raises if it is missing: on a GPU the HIP path is the one that
 runs, it never falls back silently.
 """
 from __future__ import annotations
@@ -12,24 +14,41 @@ from .. import _native
 
 CUT = 5408
 KIND = {"sgd": 1, "adam": 2}
+M64 = (1 << 64) - 1
 
 
 def C():
     return _native.load()
 
 
-def _opt_args(cfg, t):
+def _ptr(t):
+    return 0 if t is None else t.data_ptr()
+
+
+def _opt_args(cfg, t, dyn=None):
     if cfg is None:
-        return (0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 1)
-    return (KIND[cfg.kind], cfg.lr, cfg.beta1, cfg.beta2, cfg.eps, cfg.weight_decay, cfg.momentum, max(t, 1))
+        return (0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 1, 0)
+    return (KIND[cfg.kind], cfg.lr, cfg.beta1, cfg.beta2, cfg.eps, cfg.weight_decay, cfg.momentum, max(t, 1),
+            _ptr(dyn))
 
 
 def _s1(st):
-    return st.get("v") if "v" in st else None
+    return st.get("v")
 
 
 def _s0(st):
     return st["m"] if "m" in st else st["buf"]
+
+
+_SLAB: dict = {}
+
+
+def _slab(device, B):
+    s = _SLAB.get(device)
+    if s is None or s.numel() < B * 320:
+        s = torch.empty(max(B, 64) * 320, device=device, dtype=torch.float32)
+        _SLAB[device] = s
+    return s
 
 
 # ---------------------------------------------------------------- conv front
@@ -39,21 +58,36 @@ def conv_front_fwd(x_u8, idx, w, b, y=None, am=None):
         y = torch.empty(B, CUT, device=x_u8.device, dtype=torch.float32)
     if am is None:
         am = torch.empty(B, CUT, device=x_u8.device, dtype=torch.uint8)
-    C().conv_fwd(x_u8, idx, 0, B, w.detach(), b.detach(), y, am)
+    C().conv_fwd(x_u8, idx, B, w.detach(), b.detach(), y, am)
     return y, am
 
 
 def conv_front_bwd(dy, y, am, x_u8, idx, w, b):
+    """dW, db only (kind 0 writes the gradient into the state slot)."""
+    B = int(idx.numel())
     dw = torch.empty_like(w)
     db = torch.empty_like(b)
-    C().conv_bwd_opt(dy, y, am, x_u8, idx, 0, int(idx.numel()), w.detach(), b.detach(), dw, None, db, None,
-                     *_opt_args(None, 0))
+    C().conv_bwd_step(dy, y, am, x_u8, idx, B, w.detach(), b.detach(), _slab(dy.device, B), dw, None, db, None,
+                      *_opt_args(None, 0))
     return dw, db
 
 
-def conv_front_bwd_step_(dy, y, am, x_u8, idx, w, b, cfg, st_w, st_b, t):
-    C().conv_bwd_opt(dy, y, am, x_u8, idx, 0, int(idx.numel()), w.detach(), b.detach(), _s0(st_w), _s1(st_w),
-                     _s0(st_b), _s1(st_b), *_opt_args(cfg, t))
+def conv_front_bwd_step_(dy, y, am, x_u8, idx, w, b, cfg, st_w, st_b, t, dyn=None):
+    """Per-sample dW partials (one workgroup per sample) + reduce/optimizer (one workgroup)."""
+    B = int(idx.numel())
+    C().conv_bwd_step(dy, y, am, x_u8, idx, B, w.detach(), b.detach(), _slab(dy.device, B), _s0(st_w), _s1(st_w),
+                      _s0(st_b), _s1(st_b), *_opt_args(cfg, t, dyn))
+
+
+def conv_local_step_(x_u8, y_all, idx, w, b, cfg, st_w, st_b, t, loss_rows=None, dyn=None):
+    """SISA client step in two kernels: gather+conv+pool+softmax-CE(5408)+dW partials,
+    then reduce+optimizer.  Returns per-sample losses."""
+    B = int(idx.numel())
+    if loss_rows is None:
+        loss_rows = torch.empty(B, device=x_u8.device, dtype=torch.float32)
+    C().conv_local_step(x_u8, idx, y_all, B, w.detach(), b.detach(), _slab(x_u8.device, B), loss_rows,
+                        _s0(st_w), _s1(st_w), _s0(st_b), _s1(st_b), *_opt_args(cfg, t, dyn))
+    return loss_rows
 
 
 # ---------------------------------------------------------------- linear
@@ -62,7 +96,7 @@ def conv_front_bwd_step_(dy, y, am, x_u8, idx, w, b, cfg, st_w, st_b, t):
 LARGE_M = 128
 
 
-def linear_fwd(x, w, b, relu: bool, drop_p: float, seed: int, col_offset: int = 0, out=None):
+def linear_fwd(x, w, b, relu: bool, drop_p: float, seed: int, col_offset: int = 0, out=None, dseed=None):
     M, N = x.shape[0], w.shape[0]
     if out is None:
         out = torch.empty(M, N, device=x.device, dtype=torch.float32)
@@ -70,36 +104,44 @@ def linear_fwd(x, w, b, relu: bool, drop_p: float, seed: int, col_offset: int = 
     bias = b.detach() if b is not None else None
     if M > LARGE_M:
         P = torch.mm(x, w.t())
-        C().linear_epilogue(P, bias, out, relu, float(drop_p), seed & ((1 << 64) - 1), col_offset)
+        C().linear_epilogue(P, bias, out, relu, float(drop_p), seed & M64, col_offset, _ptr(dseed))
     else:
-        C().linear_fwd(x, w, bias, out, relu, float(drop_p), seed & ((1 << 64) - 1), col_offset)
+        C().linear_fwd(x, w, bias, out, relu, float(drop_p), seed & M64, col_offset, _ptr(dseed),
+                       _fwd_workspace(x.device, 16 * M * N))
     return out
 
 
-def linear_epilogue(P, b, relu: bool, drop_p: float, seed: int, col_offset: int = 0):
-    out = torch.empty_like(P)
-    C().linear_epilogue(P, b.detach() if b is not None else None, out, relu, float(drop_p),
-                        seed & ((1 << 64) - 1), col_offset)
+def linear_epilogue(P, b, relu: bool, drop_p: float, seed: int, col_offset: int = 0, out=None, dseed=None):
+    if out is None:
+        out = torch.empty_like(P)
+    C().linear_epilogue(P, b.detach() if b is not None else None, out, relu, float(drop_p), seed & M64, col_offset,
+                        _ptr(dseed))
     return out
 
 
 _WS: dict = {}
 
 
-def _workspace(device, n):
-    key = (device, torch.cuda.current_stream(device).cuda_stream)
-    ws = _WS.get(key)
+def _workspace(device, n, key="dgrad"):
+    """Split-K / split-N partial-sum slabs.  Separate buffers per op kind: a forward's
+    slabs must not alias the dgrad slabs of the same step (both can be live in a graph)."""
+    ws = _WS.get((device, key))
     if ws is None or ws.numel() < n:
         ws = torch.empty(max(n, 1 << 20), device=device, dtype=torch.float32)
-        _WS[key] = ws
+        _WS[(device, key)] = ws
     return ws
 
 
-def linear_dgrad(dz, w, h_prev=None, scale: float = 1.0, out=None):
+def _fwd_workspace(device, n):
+    return _workspace(device, n, "fwd")
+
+
+def linear_dgrad(dz, w, h_prev=None, scale: float = 1.0, out=None, ws=None):
     M, K = dz.shape[0], w.shape[1]
     if out is None:
         out = torch.empty(M, K, device=dz.device, dtype=torch.float32)
-    ws = _workspace(dz.device, 8 * M * K)
+    if ws is None:
+        ws = _workspace(dz.device, 16 * M * K)
     C().linear_dgrad(dz, w.detach(), h_prev, float(scale), out, ws)
     return out
 
@@ -114,10 +156,10 @@ def linear_wgrad(dz, a):
     return dw, db
 
 
-def linear_wgrad_step_(dz, a, w, b, cfg, st_w, st_b, t):
+def linear_wgrad_step_(dz, a, w, b, cfg, st_w, st_b, t, dyn=None):
     C().linear_wgrad_opt(dz, a, w.detach(), _s0(st_w), _s1(st_w), b.detach() if b is not None else None,
                          _s0(st_b) if b is not None else None, _s1(st_b) if b is not None else None,
-                         *_opt_args(cfg, t))
+                         *_opt_args(cfg, t, dyn))
 
 
 def apply_update_(p, g, st, cfg, t):
@@ -125,9 +167,9 @@ def apply_update_(p, g, st, cfg, t):
 
 
 # ---------------------------------------------------------------- loss / metrics
-def softmax_ce(logits, labels, scale: float, ignore_index: int = -100, d_out=None):
+def softmax_ce(logits, labels, scale: float, ignore_index: int = -100, d_out=None, loss_out=None):
     M = logits.shape[0]
-    loss = torch.empty(M, device=logits.device, dtype=torch.float32)
+    loss = torch.empty(M, device=logits.device, dtype=torch.float32) if loss_out is None else loss_out
     d = torch.empty_like(logits) if d_out is None else d_out
     C().softmax_ce(logits, labels, int(ignore_index), float(scale), loss, d)
     return loss, d

@@ -138,6 +138,15 @@ def conv_front_bwd_step_(dy, y, am, x_u8, idx, w, b, cfg, st_w, st_b, t):
         apply_update_(b, db, st_b, cfg, t)
 
 
+def conv_local_step_(x_u8, y_all, idx, w, b, cfg, st_w, st_b, t, loss_rows=None):
+    """SISA client step: CE over the 5408-wide activation (Q5), backward, optimizer."""
+    with torch.no_grad():
+        act, am = conv_front_fwd(x_u8, idx, w, b)
+        loss, d = softmax_ce(act, y_all[idx], 1.0 / idx.numel())
+        conv_front_bwd_step_(d, act, am, x_u8, idx, w, b, cfg, st_w, st_b, t)
+    return loss
+
+
 # ---------------------------------------------------------------- loss / metrics
 def softmax_ce(logits, labels, scale: float, ignore_index: int = -100):
     """Row-wise cross-entropy. Returns (per-row loss [M] (0 for ignored rows),

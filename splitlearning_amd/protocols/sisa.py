@@ -55,9 +55,8 @@ class SisaSession(Session):
 
     # ------------------------------------------------------------------ Alice-local training
     def local_step(self, a: AliceState, idx):
-        act, am = a.front.forward(a.train, idx)
-        _, d = self.ops.softmax_ce(act, a.train.y[idx], 1.0 / idx.numel())
-        a.front.backward_step(d, act, am, a.train, idx, a.slot)
+        """`zero_grad; CE(model(x), y).backward(); step` (data_entities_vanilla_sisa.py:60-70)."""
+        a.front.local_step(a.train, idx, a.slot)
 
     def local_train(self, a: AliceState, fixed_order=None):
         """`epochs` local epochs; reshuffled every epoch unless a fixed (unlearn /
@@ -162,6 +161,35 @@ class SisaSession(Session):
         self.tail.backward_dgrad(d, need_dx=False)
         self.tail.backward_step(self.bob_slot)
 
+    GRAPH_STEPS = 16
+
+    def _use_graphs(self) -> bool:
+        mode = getattr(self.args, "graphs", "auto")
+        if mode == "off" or self.device.type != "cuda" or self.tail.tp_size != 1:
+            return False
+        from .. import ops as _ops
+        return _ops.get_backend() != "torch"
+
+    def server_epoch(self, acts, labels):
+        """One pass of Bob's optimizer over one client's cached activations (batch order as
+        cached).  Full batches run as HIP-graph chunks of GRAPH_STEPS steps when possible."""
+        n, B = labels.numel(), self.B
+        s = 0
+        G = self.GRAPH_STEPS
+        if self._use_graphs() and n // B >= G:
+            key = (B, G, acts.shape[1])
+            gs = getattr(self, "_graphed", {}).get(key)
+            if gs is None:
+                from ..engine.graphs import GraphedServerSteps
+                if not hasattr(self, "_graphed"):
+                    self._graphed = {}
+                gs = self._graphed[key] = GraphedServerSteps(self.tail, self.bob_slot, B, G, acts.shape[1])
+            ng = (n // B // G) * G
+            gs.run(acts, labels, ng)
+            s = ng * B
+        for s in range(s, n, B):
+            self.server_step(acts[s:s + B], labels[s:s + B])
+
     def train_and_backward(self, unlearn_request_from_alices, unlearn_id):
         """Reference `bob.train_and_backward` (data_entities_vanilla_sisa.py:294-315)."""
         self.bob_log.info("Global Training")
@@ -175,10 +203,8 @@ class SisaSession(Session):
                     got = self.get_activation_and_labels(cid, unlearned=False)
                 if self.is_bob:
                     acts, labels = got
-                    n = labels.numel()
-                    for s in range(0, n, self.B):
-                        self.server_step(acts[s:s + self.B], labels[s:s + self.B])
-                    samples += n
+                    self.server_epoch(acts, labels)
+                    samples += labels.numel()
         self.bob_log.info("Global training completed.")
         self.comm.barrier()
         return samples

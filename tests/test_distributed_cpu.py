@@ -1,0 +1,133 @@
+"""Multi-process protocol tests on CPU (gloo): the distributed paths the 8-GPU node runs,
+exercised here with 2-3 processes.
+
+* tensor-parallel Bob (TP=2) equals the single-process Bob step for step;
+* every mode runs end-to-end through the real launcher with one process per role
+  (reference topology) and with fewer processes than roles (Alices co-located,
+  Bob tensor-parallel) — the MI355X placement;
+* log vocabulary and metrics are produced.
+"""
+import json
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from splitlearning_amd.runtime.launcher import main as launch_main
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _tp_worker(rank, world, port, out_dir, steps):
+    import torch.distributed as dist
+    from splitlearning_amd.config import OptimCfg
+    from splitlearning_amd.engine import OptSlot, TailEngine
+    from splitlearning_amd.models import ServerTailSisa, sisa_server_spec
+    from splitlearning_amd.ops import torch_ops as K
+    from splitlearning_amd.parallel.dist import Comm, Placement, make_tp_group
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    pl = Placement.make(world + 1, world, world)
+    comm = Comm(rank, world, torch.device("cpu"), pl, make_tp_group(pl, "gloo"))
+    torch.manual_seed(0)
+    tail = TailEngine(ServerTailSisa(), sisa_server_spec(), torch.device("cpu"), rank, world,
+                      allreduce=comm.tp_allreduce, seed_base=3)
+    slot = OptSlot(OptimCfg("adam", 1e-3, weight_decay=1e-5))
+    g = torch.Generator().manual_seed(1)
+    outs = []
+    for _ in range(steps):
+        x = torch.rand(16, 5408, generator=g) * 20
+        y = torch.randint(0, 10, (16,), generator=g)
+        o = tail.forward(x, train=True)
+        _, d = K.softmax_ce(o, y, 1 / 16)
+        dx = tail.backward_dgrad(d, need_dx=True)
+        dx = comm.reduce_to(dx, 0, pl.bob_ranks, dx.shape, dx.dtype)
+        tail.backward_step(slot)
+        if rank == 0:
+            outs.append((o.clone(), dx.clone()))
+    sd = tail.full_state_dict(comm.tp_allgather)
+    if rank == 0:
+        torch.save({"sd": sd, "outs": outs}, os.path.join(out_dir, f"tp{world}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.slow
+def test_tensor_parallel_bob_matches_single_process(tmp_path):
+    steps = 3
+    mp.spawn(_tp_worker, args=(2, _free_port(), str(tmp_path), steps), nprocs=2, join=True)
+    mp.spawn(_tp_worker, args=(1, _free_port(), str(tmp_path), steps), nprocs=1, join=True)
+    a = torch.load(tmp_path / "tp2.pt", weights_only=True)
+    b = torch.load(tmp_path / "tp1.pt", weights_only=True)
+    for (o2, dx2), (o1, dx1) in zip(a["outs"], b["outs"]):
+        torch.testing.assert_close(o2, o1, rtol=1e-4, atol=1e-4)
+        torch.testing.assert_close(dx2, dx1, rtol=1e-4, atol=1e-5)
+    for k in b["sd"]:
+        d = (a["sd"][k] - b["sd"][k]).abs()
+        assert a["sd"][k].shape == b["sd"][k].shape, k
+        assert d.max().item() < 7e-3 and (d > 1e-5).float().mean().item() < 1e-4, k
+
+
+def _run(tmp_path, mode_flags, world_size, nprocs, bob_tp=1, extra=()):
+    logs = tmp_path / "logs"
+    argv = list(mode_flags) + ["--world_size", str(world_size), "--nprocs", str(nprocs), "--bob_tp", str(bob_tp),
+                               "--iterations", "1", "--server_epochs", "1", "--num_samples", "700", "--seed", "3",
+                               "--no_tqdm", "--device", "cpu", "--datapath", str(tmp_path / "data"),
+                               "--log_dir", str(logs), "--master_port", str(_free_port())] + list(extra)
+    launch_main(argv)
+    with open(logs / "metrics.json") as f:
+        m = json.load(f)
+    bob = (logs / "bob.log").read_text()
+    return m, bob, logs
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("flags,ws,np_,tp", [
+    (["--vanilla"], 3, 3, 1),          # reference topology: 1 process per role
+    (["--vanilla"], 3, 2, 2),          # MI355X placement: Alices co-located, Bob TP=2
+    ([], 3, 2, 2),                     # U-shape
+    (["--sisa"], 3, 2, 2),
+    (["--control"], 3, 3, 1),
+    (["--sisa", "--concat", "--concat_unlearn"], 3, 2, 2),
+])
+def test_modes_end_to_end(tmp_path, flags, ws, np_, tp):
+    m, bob, logs = _run(tmp_path, flags, ws, np_, tp)
+    assert "Bob Started Getting Tipsy" in bob
+    assert "Accuracy over all data" in bob
+    assert m["nprocs"] == np_ and m["bob_tp"] == tp
+    for cid in range(1, ws):
+        alog = (logs / f"alice{cid}.log").read_text()
+        assert "Alice is going insane!" in alog and "Local Data Statistics:" in alog
+    if "--vanilla" in flags:
+        assert "Train Request for Alice-1" in bob and "Unlearn Request for Alice-1" in bob
+        assert "receiving weights from Alice-1" in (logs / "alice2.log").read_text()
+    if "--sisa" in flags and "--concat" not in flags:
+        for line in ["Train all Alices in parallel", "Server training starts. Freezing weights for Alices-1.",
+                     "Global Training", "Global training completed.", "Unfreezing weights for Alices-1.",
+                     "Unlearn Request for Alice-1 upon the label-9"]:
+            assert line in bob, line
+        assert "Unlearning label: 9, and reset the model" in (logs / "alice1.log").read_text()
+    if "--control" in flags:
+        assert "Filtered dataset:" in (logs / "alice1.log").read_text()
+
+
+@pytest.mark.slow
+def test_checkpoint_roundtrip(tmp_path):
+    ck = tmp_path / "ck"
+    _run(tmp_path, ["--vanilla"], 3, 2, 2, extra=["--save_dir", str(ck)])
+    bob = torch.load(ck / "bob.pt", weights_only=True)
+    assert tuple(bob["fc1.weight"].shape) == (5000, 5408) and tuple(bob["fc2.weight"].shape) == (1000, 5000)
+    a1 = torch.load(ck / "alice1.pt", weights_only=True)
+    assert set(a1) == {"conv_layers.0.weight", "conv_layers.0.bias"}
+    # resume into a fresh run: loads without error and trains on
+    _run(tmp_path, ["--vanilla"], 3, 2, 2, extra=["--resume_dir", str(ck)])
