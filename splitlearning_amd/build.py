@@ -24,7 +24,7 @@ ARCH = os.environ.get("SL_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 KERNEL_SOURCES = ["conv.hip", "linear.hip", "loss.hip"]
-BINDING_SOURCES = ["bindings.cpp"]
+BINDING_SOURCES = ["bindings.cpp", "comm.cpp"]
 
 
 def so_path() -> str:
@@ -42,7 +42,7 @@ def _torch_flags():
                                         "-DTORCH_API_INCLUDE_EXTENSION_H",
                                         "-DTORCH_EXTENSION_NAME=_C", "-DUSE_ROCM=1"]
     ldflags = [f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
-               "-ltorch_python", "-lamdhip64", f"-Wl,-rpath,{tlib}"]
+               "-ltorch_python", "-lamdhip64", "-lrccl", f"-Wl,-rpath,{tlib}"]
     return cflags, ldflags
 
 

@@ -311,8 +311,11 @@ void eval_counters(const at::Tensor& x, const at::Tensor& y, int64_t omit, at::T
 
 }  // namespace
 
+void sl_register_comm(pybind11::module& m);
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "splitlearning_amd gfx950 (MI355X) HIP kernels";
+  sl_register_comm(m);
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_local_step", &conv_local_step);
   m.def("conv_bwd_step", &conv_bwd_step);

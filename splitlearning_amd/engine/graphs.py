@@ -29,8 +29,8 @@ from .tail import TailEngine
 
 class GraphedServerSteps:
     def __init__(self, tail: TailEngine, slot: OptSlot, B: int, G: int, k_in: int):
-        if tail.tp_size != 1:
-            raise ValueError("graph capture needs a single-GPU tail")
+        if tail.tp_size != 1 and not getattr(tail.allreduce, "capturable", False):
+            raise ValueError("graph capture of a tensor-parallel tail needs the native RCCL all-reduce")
         if slot.cfg.kind != "adam":
             raise ValueError("graphed server steps implement the SISA Adam slot")
         self.tail, self.slot, self.B, self.G = tail, slot, B, G

@@ -73,6 +73,7 @@ class Session:
         self._build_alices()
         self._exchange_meta()
         self.is_bob = self.pl.is_bob(self.rank)
+        self.tp_allreduce = self._tp_allreduce()          # collective over all ranks
         self.tail: TailEngine | None = None
         self.bob_slots: dict = {}
         self.last_alice_id = None
@@ -142,12 +143,24 @@ class Session:
         dist.all_gather_object(out, obj)
         return out
 
+    def _tp_allreduce(self):
+        """Bob's TP all-reduce: a native RCCL communicator on GPUs (capturable in the
+        server-step graph), the torch.distributed group otherwise (gloo on CPU)."""
+        if self.pl.bob_tp <= 1:
+            return self.comm.tp_allreduce
+        if self.device.type == "cuda" and getattr(self.args, "native_comm", True):
+            from ..parallel.rccl import make_native_comm, native_allreduce
+            tpc = make_native_comm(self.pl.bob_ranks, self.rank)
+            self.tp_native_comm = tpc
+            return native_allreduce(tpc) if tpc is not None else self.comm.tp_allreduce
+        return self.comm.tp_allreduce
+
     def _build_bob(self):
         module, spec = self.bob_module_and_spec()
         tp_size = self.pl.bob_tp
         tp_rank = self.pl.bob_ranks.index(self.rank)
         self.tail = TailEngine(module, spec, self.device, tp_rank, tp_size,
-                               allreduce=self.comm.tp_allreduce, seed_base=self.seed)
+                               allreduce=self.tp_allreduce, seed_base=self.seed)
 
     def make_bob_module(self, cls, *a):
         # identical init on every TP rank: seed the default generator with the agreed seed

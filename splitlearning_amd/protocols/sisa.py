@@ -165,7 +165,9 @@ class SisaSession(Session):
 
     def _use_graphs(self) -> bool:
         mode = getattr(self.args, "graphs", "auto")
-        if mode == "off" or self.device.type != "cuda" or self.tail.tp_size != 1:
+        if mode == "off" or self.device.type != "cuda":
+            return False
+        if self.tail.tp_size != 1 and not getattr(self.tail.allreduce, "capturable", False):
             return False
         from .. import ops as _ops
         return _ops.get_backend() != "torch"
