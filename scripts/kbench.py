@@ -127,6 +127,34 @@ def main():
         tail.backward_dgrad(d, need_dx=True)
         tail.backward_step(slot)
     cases.append(("bob_step_with_dx", bob_step_dx, 32_146_100 * 32))
+    ftail = TailEngine(ServerTailSisa(), sisa_server_spec(), dev)
+    fslot = OptSlot(adam(1e-3, 1e-5))
+    # pieces of the fused step
+    L1, L2, L3 = ftail.layers
+    h1f = torch.relu(torch.randn(M, N1, device=dev))
+    P2 = H.linear_fwd_partial(h1f, L2.W)
+    cases.append(("fused:fc2_fwd_partial", lambda: H.linear_fwd_partial(h1f, L2.W), W2.numel() * 4))
+    cases.append(("fused:head3", lambda: H.server_head3(P2, L2.b, True, 0.5, 3, L3.W, L3.b, yl, 1 / 16), 0))
+    h2f, dlf, dz2f, _ = H.server_head3(P2, L2.b, True, 0.5, 3, L3.W, L3.b, yl, 1 / 16)
+    cases.append(("fused:fc2_dgrad_partial", lambda: H.linear_dgrad_partial(dz2f, L2.W), W2.numel() * 4))
+    dz1p = H.linear_dgrad_partial(dz2f, L2.W)
+    wst = [fslot.state(f"fc{i}.{n}", t) for i, L in ((1, L1), (2, L2), (3, L3)) for n, t in
+           (("weight", L.W), ("bias", L.b))]
+    grp = [(None, dz1p, h1f, 2.0, x, L1.W, wst[0], L1.b, wst[1]), (dz2f, None, None, 1.0, h1f, L2.W, wst[2], L2.b,
+                                                                     wst[3]),
+           (dlf, None, None, 1.0, h2f, L3.W, wst[4], L3.b, wst[5])]
+    cases.append(("fused:wgrad_group3", lambda: H.wgrad_group_(grp, M, cfg, 3), 32_146_100 * 24))
+    cases.append(("fused:wgrad_fc1_only", lambda: H.wgrad_group_(grp[:1], M, cfg, 3), W1.numel() * 24))
+    dz1r = torch.randn(M, N1, device=dev)
+    grp_plain = [(dz1r, None, None, 1.0, x, L1.W, wst[0], L1.b, wst[1])]
+    cases.append(("fused:wgrad_fc1_plain_dz", lambda: H.wgrad_group_(grp_plain, M, cfg, 3), W1.numel() * 24))
+    cases.append(("v3:wgrad_fc1_same_tensors", lambda: H.linear_wgrad_step_(dz1r, x, L1.W, L1.b, cfg, wst[0], wst[1], 3),
+                  W1.numel() * 24))
+
+    def bob_fused():
+        ftail.train_fwd_bwd3(x, yl, need_dx=False)
+        ftail.fused_step(fslot)
+    cases.append(("bob_fused_step", bob_fused, 32_146_100 * 28))
     # graph-replayed server steps (per-step time = one replay of 16 steps / 16)
     from splitlearning_amd.engine.graphs import GraphedServerSteps
     gtail = TailEngine(ServerTailSisa(), sisa_server_spec(), dev)

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include "common.h"
+#include "fused.h"
 
 namespace sl {
 hipError_t conv_fwd(const void* x, bool x_u8, const int64_t* idx, int64_t row0, int B, const float* w,
@@ -31,6 +32,10 @@ hipError_t linear_dgrad(const float* dZ, int ldz, const float* W, int ldw, const
                         float scale, float* dX, int ldx, float* ws, int64_t ws_elems, int M, int N, int K,
                         hipStream_t st);
 hipError_t linear_epilogue(const float* P, int ldp, float* Y, int ldy, int M, int N, Epi e, hipStream_t st);
+hipError_t linear_fwd_partial(const float* X, int ldx, const float* W, int ldw, int M, int N, int K, float* ws,
+                              int64_t ws_elems, int max_split, int* S_out, hipStream_t st);
+hipError_t linear_dgrad_partial(const float* dZ, int ldz, const float* W, int ldw, int M, int N, int K, float* ws,
+                                int64_t ws_elems, int* S_out, hipStream_t st);
 hipError_t linear_wgrad_opt(const float* dZ, int ldz, const float* A, int lda, float* W, int ldw, float* s0,
                             float* s1, float* bias, float* sb0, float* sb1, int M, int N, int K, SlOpt o,
                             hipStream_t st);
@@ -309,6 +314,121 @@ void eval_counters(const at::Tensor& x, const at::Tensor& y, int64_t omit, at::T
         "eval_counters");
 }
 
+// Partial products into a workspace; return the number of slabs S (result = ws[:S*M*cols]).
+int64_t linear_fwd_partial(const at::Tensor& X, const at::Tensor& W, at::Tensor& ws, int64_t max_split) {
+  need_rows(X, "X");
+  need_rows(W, "W");
+  need_f32(ws, "ws");
+  TORCH_CHECK(ws.is_contiguous(), "ws contiguous");
+  const int64_t M = X.size(0), K = X.size(1), N = W.size(0);
+  TORCH_CHECK(W.size(1) == K && K % 4 == 0, "W must be [N,K] with K % 4 == 0");
+  int S = 1;
+  check(sl::linear_fwd_partial(X.data_ptr<float>(), (int)X.stride(0), W.data_ptr<float>(), (int)W.stride(0), (int)M,
+                               (int)N, (int)K, ws.data_ptr<float>(), ws.numel(), (int)max_split, &S, cur_stream()),
+        "linear_fwd_partial");
+  return S;
+}
+
+int64_t linear_dgrad_partial(const at::Tensor& dZ, const at::Tensor& W, at::Tensor& ws) {
+  need_2d(dZ, "dZ");
+  need_rows(W, "W");
+  need_f32(ws, "ws");
+  TORCH_CHECK(ws.is_contiguous(), "ws contiguous");
+  const int64_t M = dZ.size(0), N = dZ.size(1), K = W.size(1);
+  TORCH_CHECK(W.size(0) == N && K % 4 == 0, "W must be [N,K]");
+  int S = 1;
+  check(sl::linear_dgrad_partial(dZ.data_ptr<float>(), (int)dZ.stride(0), W.data_ptr<float>(), (int)W.stride(0),
+                                 (int)M, (int)N, (int)K, ws.data_ptr<float>(), ws.numel(), &S, cur_stream()),
+        "linear_dgrad_partial");
+  return S;
+}
+
+// ---------------------------------------------------------------- fused server step
+// P2: fc2 partial sums, [S2, M, N2] split-K slabs or a reduced [M, N2] tensor.
+void server_head3(const at::Tensor& P2, const OptT& b2, bool relu2, double drop2, uint64_t seed2, int64_t dseed2,
+                  const at::Tensor& W3, const OptT& b3, const at::Tensor& y, int64_t ignore, double scale,
+                  at::Tensor& h2, at::Tensor& dlog, at::Tensor& dz2, at::Tensor& loss_rows) {
+  need_f32(P2, "P2");
+  TORCH_CHECK(P2.is_contiguous() && (P2.dim() == 2 || P2.dim() == 3), "P2 [S,M,N2] or [M,N2] contiguous");
+  const int64_t S2 = P2.dim() == 3 ? P2.size(0) : 1;
+  const int64_t M = P2.size(P2.dim() - 2), N2 = P2.size(P2.dim() - 1);
+  need_rows(W3, "W3");
+  const int64_t C = W3.size(0);
+  TORCH_CHECK(W3.size(1) == N2 && N2 % 4 == 0 && C <= 4096, "W3 [C, N2], N2 % 4 == 0");
+  need_cuda(y, "labels");
+  TORCH_CHECK(y.scalar_type() == at::kLong && y.numel() == M && y.is_contiguous(), "labels int64 [M]");
+  for (auto* t : {&h2, &dz2}) {
+    need_f32(*t, "h2/dz2");
+    TORCH_CHECK(t->is_contiguous() && t->size(0) == M && t->size(1) == N2, "h2/dz2 [M,N2]");
+  }
+  need_f32(dlog, "dlog");
+  TORCH_CHECK(dlog.is_contiguous() && dlog.size(0) == M && dlog.size(1) == C, "dlog [M,C]");
+  need_f32(loss_rows, "loss_rows");
+  TORCH_CHECK(loss_rows.numel() >= M, "loss_rows");
+  check(sl::server_head3(P2.data_ptr<float>(), (int)S2, M * N2, make_epi(b2, relu2, drop2, seed2, 0, dseed2),
+                         W3.data_ptr<float>(), fptr(b3), y.data_ptr<int64_t>(), ignore, (float)scale,
+                         h2.data_ptr<float>(), dlog.data_ptr<float>(), dz2.data_ptr<float>(),
+                         loss_rows.data_ptr<float>(), (int)M, (int)N2, (int)C, cur_stream()),
+        "server_head3");
+}
+
+// layers: up to 3 tuples (dz, dzp, hmask, mscale, A, W, s0, s1, bias, sb0, sb1); exactly one of dz / dzp
+// (dzp = [S, M, N] split-N partial slabs of the layer's output gradient, masked by hmask > 0).
+void wgrad_group(const std::vector<py::tuple>& layers, int64_t M, OPT_ARGS) {
+  TORCH_CHECK(!layers.empty() && layers.size() <= 3, "1..3 layers");
+  sl::WgGroup g{};
+  g.n = (int)layers.size();
+  for (size_t i = 0; i < layers.size(); ++i) {
+    const py::tuple& L = layers[i];
+    TORCH_CHECK(L.size() == 11, "layer tuple has 11 fields");
+    auto opt = [&](int j) -> OptT { return L[j].is_none() ? OptT() : OptT(L[j].cast<at::Tensor>()); };
+    const at::Tensor A = L[4].cast<at::Tensor>();
+    at::Tensor W = L[5].cast<at::Tensor>();
+    at::Tensor s0 = L[6].cast<at::Tensor>();
+    need_rows(A, "A");
+    need_rows(W, "W");
+    need_rows(s0, "s0");
+    const int64_t N = W.size(0), K = W.size(1);
+    TORCH_CHECK(A.size(0) == M && A.size(1) == K && K % 4 == 0, "A [M,K]");
+    TORCH_CHECK(s0.sizes() == W.sizes() && s0.stride(0) == W.stride(0), "s0 like W");
+    OptT s1 = opt(7), bias = opt(8), sb0 = opt(9), sb1 = opt(10), dz = opt(0), dzp = opt(1), hm = opt(2);
+    if (kind == 2) TORCH_CHECK(s1.has_value() && s1->sizes() == W.sizes() && s1->stride(0) == W.stride(0), "s1");
+    if (bias.has_value()) TORCH_CHECK(bias->numel() == N && sb0.has_value() && sb0->numel() == N, "bias state");
+    sl::WgDesc& d = g.d[i];
+    TORCH_CHECK(dz.has_value() != dzp.has_value(), "exactly one of dz / dzp");
+    if (dz.has_value()) {
+      need_2d(*dz, "dz");
+      TORCH_CHECK(dz->size(0) == M && dz->size(1) == N, "dz [M,N]");
+      d.dz = dz->data_ptr<float>();
+      d.ldz = (int)dz->stride(0);
+    } else {
+      need_f32(*dzp, "dzp");
+      TORCH_CHECK(dzp->is_contiguous() && dzp->numel() % (M * N) == 0, "dzp [S,M,N]");
+      d.dzp = dzp->data_ptr<float>();
+      d.S = (int)(dzp->numel() / (M * N));
+      d.slab = M * N;
+      if (hm.has_value()) {
+        need_f32(*hm, "hmask");
+        TORCH_CHECK(hm->is_contiguous() && hm->numel() == M * N, "hmask [M,N]");
+        d.hmask = hm->data_ptr<float>();
+      }
+      d.mscale = L[3].cast<float>();
+    }
+    d.A = A.data_ptr<float>();
+    d.lda = (int)A.stride(0);
+    d.W = W.data_ptr<float>();
+    d.ldw = (int)W.stride(0);
+    d.s0 = s0.data_ptr<float>();
+    d.s1 = fptr(s1);
+    d.bias = fptr(bias);
+    d.sb0 = fptr(sb0);
+    d.sb1 = fptr(sb1);
+    d.N = (int)N;
+    d.K = (int)K;
+  }
+  check(sl::wgrad_group(g, (int)M, OPT_PASS, cur_stream()), "wgrad_group");
+}
+
 }  // namespace
 
 void sl_register_comm(pybind11::module& m);
@@ -326,6 +446,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("opt_flat", &opt_flat);
   m.def("softmax_ce", &softmax_ce);
   m.def("eval_counters", &eval_counters);
+  m.def("server_head3", &server_head3);
+  m.def("linear_fwd_partial", &linear_fwd_partial);
+  m.def("linear_dgrad_partial", &linear_dgrad_partial);
+  m.def("wgrad_group", &wgrad_group);
   m.def("set_variant", [](int64_t slot, int64_t v) {
     TORCH_CHECK(slot >= 0 && slot < 8, "variant slot");
     sl::g_variant[slot] = (int)v;

@@ -81,6 +81,16 @@ struct Epi {
   const uint32_t* dseed;  // graph replay: {seed_lo, seed_hi} from device memory when set
 };
 
+__device__ __forceinline__ float apply_epi(const Epi& e, float v, int m, int n) {
+  if (e.bias) v += e.bias[n];
+  if (e.relu) v = fmaxf(v, 0.f);
+  if (e.thresh) {
+    const uint32_t lo = e.dseed ? e.dseed[0] : e.seed_lo, hi = e.dseed ? e.dseed[1] : e.seed_hi;
+    v = sl_hash_keep(lo, hi, (uint32_t)m, (uint32_t)(e.col_off + n), e.thresh) ? v * e.dscale : 0.f;
+  }
+  return v;
+}
+
 // Vector form of sl_opt_update (the f32x4 elements cannot bind to float&).
 template <bool ADAM>
 __device__ __forceinline__ void sl_opt_update4(const SlOpt& o, f32x4& p, f32x4 g, f32x4& s0, f32x4& s1) {

@@ -1,0 +1,37 @@
+// Descriptors shared by the fused server-step kernels (fused.hip) and the bindings.
+#pragma once
+#include "common.h"
+
+namespace sl {
+
+struct WgDesc {
+  const float* dz;      // [M, N] (ld ldz), or nullptr when given as partial slabs:
+  int ldz;
+  const float* dzp;     // [S][M][N] split-N partial sums of dZ (before the mask)
+  int S;
+  int64_t slab;
+  const float* hmask;   // [M, N] post-activation of this layer: dz *= mscale * [hmask > 0]
+  float mscale;
+  const float* A;       // [M, K] layer input
+  int lda;
+  float* W;
+  int ldw;
+  float* s0;
+  float* s1;
+  float* bias;
+  float* sb0;
+  float* sb1;
+  int N, K;
+  int yb0;              // first blockIdx.y of this layer
+};
+struct WgGroup {
+  WgDesc d[3];
+  int n;
+};
+
+hipError_t server_head3(const float* P2, int S2, int64_t slab2, Epi e2, const float* W3, const float* b3,
+                        const int64_t* y, int64_t ignore, float scale, float* h2, float* dlog, float* dz2,
+                        float* loss_rows, int M, int N2, int C, hipStream_t st);
+hipError_t wgrad_group(const WgGroup& g, int M, SlOpt o, hipStream_t st);
+
+}  // namespace sl

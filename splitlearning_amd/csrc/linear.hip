@@ -31,15 +31,6 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
 
-__device__ __forceinline__ float apply_epi(const Epi& e, float v, int m, int n) {
-  if (e.bias) v += e.bias[n];
-  if (e.relu) v = fmaxf(v, 0.f);
-  if (e.thresh) {
-    const uint32_t lo = e.dseed ? e.dseed[0] : e.seed_lo, hi = e.dseed ? e.dseed[1] : e.seed_hi;
-    v = sl_hash_keep(lo, hi, (uint32_t)m, (uint32_t)(e.col_off + n), e.thresh) ? v * e.dscale : 0.f;
-  }
-  return v;
-}
 
 // ---------------------------------------------------------------------------- forward
 // grid (ceil(N/16), ceil(M/16)), block NW*64.  Requires K % 4 == 0, ldx/ldw % 4 == 0.
@@ -591,6 +582,54 @@ hipError_t linear_dgrad(const float* dZ, int ldz, const float* W, int ldw, const
     dgrad_reduce_kernel<<<(unsigned)((tot + 255) / 256), 256, 0, st>>>(ws, S, slab, hprev, ldh, scale, dX, ldx,
                                                                         M, K);
   }
+  return hipGetLastError();
+}
+
+// Partial-output variants for fused consumers (server_head3 / wgrad_group reduce the slabs
+// themselves): the split-K (fwd) or split-N (dgrad) slabs, or the plain product when no
+// split is chosen, land in ws as [S][M][cols]; *S_out receives S.
+hipError_t linear_fwd_partial(const float* X, int ldx, const float* W, int ldw, int M, int N, int K, float* ws,
+                              int64_t ws_elems, int max_split, int* S_out, hipStream_t st) {
+  *S_out = 1;
+  if (M <= 0 || N <= 0) return hipSuccess;
+  dim3 grid((N + 15) / 16, (M + 15) / 16);
+  const int tiles = grid.x * grid.y;
+  int S = 1;
+  while (S < max_split && tiles * S * 2 <= 2048 && K / (S * 2) >= 256) S *= 2;
+  const int64_t slab = (int64_t)M * N;
+  if (ws_elems < slab * S) S = 1;
+  if (ws_elems < slab) return hipErrorInvalidValue;
+  const int kz = (K + S - 1) / S;
+  const int nw = kz >= 1024 ? 8 : (kz >= 512 ? 4 : 2);
+  dim3 g3(grid.x, grid.y, S);
+  Epi e{};
+  e.dscale = 1.f;
+  if (nw == 8)
+    skinny_fwd_kernel<8, 4, false><<<g3, 512, 0, st>>>(X, ldx, W, ldw, ws, N, M, N, K, e, ws, slab);
+  else if (nw == 4)
+    skinny_fwd_kernel<4, 4, false><<<g3, 256, 0, st>>>(X, ldx, W, ldw, ws, N, M, N, K, e, ws, slab);
+  else
+    skinny_fwd_kernel<2, 4, false><<<g3, 128, 0, st>>>(X, ldx, W, ldw, ws, N, M, N, K, e, ws, slab);
+  *S_out = S;
+  return hipGetLastError();
+}
+
+hipError_t linear_dgrad_partial(const float* dZ, int ldz, const float* W, int ldw, int M, int N, int K, float* ws,
+                                int64_t ws_elems, int* S_out, hipStream_t st) {
+  *S_out = 1;
+  if (M <= 0 || K <= 0) return hipSuccess;
+  const int kt = (K + 63) / 64, mt = (M + 15) / 16;
+  int S = 1;
+  while (S < 16 && kt * mt * S < 768 && N / (S * 2) >= 64) S *= 2;
+  const int64_t slab = (int64_t)M * K;
+  if (ws_elems < slab * S) S = 1;
+  if (ws_elems < slab) return hipErrorInvalidValue;
+  dim3 grid(kt, mt, S);
+  if (S == 1)
+    skinny_dgrad_kernel<8><<<grid, 512, 0, st>>>(dZ, ldz, W, ldw, nullptr, 0, 1.f, ws, K, 0, M, N, K);
+  else
+    skinny_dgrad_kernel<8><<<grid, 512, 0, st>>>(dZ, ldz, W, ldw, nullptr, 0, 1.f, ws, 0, slab, M, N, K);
+  *S_out = S;
   return hipGetLastError();
 }
 

@@ -47,8 +47,8 @@ class GraphedServerSteps:
         # scratch slabs must be allocated outside the capture (they are shared with eager calls)
         kmax = max(max(L.W.shape[1] for L in tail.layers), k_in)
         nmax = max(L.W.shape[0] for L in tail.layers)
-        ops._workspace(dev, 16 * B * kmax)
-        ops._fwd_workspace(dev, 16 * B * nmax)
+        for key, n in (("dgrad", kmax), ("fwd", nmax), ("fc2p", nmax), ("dz1p", kmax)):
+            ops._workspace(dev, 16 * B * n, key)
         torch.cuda.synchronize(dev)
         fwd0 = tail.fwd_count
         self.graph = torch.cuda.CUDAGraph()
@@ -56,13 +56,19 @@ class GraphedServerSteps:
         s.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s):
             with torch.cuda.graph(self.graph, stream=s):
+                fused = tail.fused3_ok()
                 for i in range(G):
                     xs = self.x[i * B:(i + 1) * B]
                     ys = self.y[i * B:(i + 1) * B]
-                    out = tail.forward(xs, train=True, dseeds=[self.seed_tab[i, l] for l in range(self.L)])
-                    _, d = ops.softmax_ce(out, ys, 1.0 / B)
-                    tail.backward_dgrad(d, need_dx=False)
-                    tail.backward_step(slot, t=1, dyn=self.opt_tab[i])
+                    dseeds = [self.seed_tab[i, l] for l in range(self.L)]
+                    if fused:
+                        tail.train_fwd_bwd3(xs, ys, need_dx=False, dseeds=dseeds)
+                        tail.fused_step(slot, t=1, dyn=self.opt_tab[i])
+                    else:
+                        out = tail.forward(xs, train=True, dseeds=dseeds)
+                        _, d = ops.softmax_ce(out, ys, 1.0 / B)
+                        tail.backward_dgrad(d, need_dx=False)
+                        tail.backward_step(slot, t=1, dyn=self.opt_tab[i])
         torch.cuda.current_stream(dev).wait_stream(s)
         tail.fwd_count = fwd0           # capture does not execute: restore the host counters
         self._tabs = None

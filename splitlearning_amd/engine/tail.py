@@ -148,6 +148,58 @@ class TailEngine:
                                         slot.state(f"{prefix}{L.spec.name}.bias", L.b), t, **kw)
         self.dz = []
 
+    # ------------------------------------------------------------------ fused 3-layer step
+    def fused3_ok(self) -> bool:
+        """The SISA/vanilla server tail (fc1 ReLU+Dropout, fc2 ReLU+Dropout, fc3 -> CE) on the
+        HIP kernels: 6 launches per step instead of 13 (csrc/fused.hip)."""
+        if not hasattr(self.ops, "server_head3") or len(self.layers) != 3:
+            return False
+        s = [L.spec for L in self.layers]
+        return (s[0].relu and s[1].relu and not s[2].relu and s[2].dropout == 0
+                and self.layers[2].style == "rep" and s[1].out_features % 4 == 0)
+
+    def train_fwd_bwd3(self, x, labels, need_dx: bool, dseeds=None):
+        """Training forward + softmax-CE + all data gradients of the 3-layer tail.
+        Returns (per-row loss, dL/dx or None); `fused_step` then applies the optimizer."""
+        ops = self.ops
+        L1, L2, L3 = self.layers
+        M = x.shape[0]
+        self.fwd_count += 1
+        seeds = [step_seed(self.seed_base, i, self.fwd_count) for i in range(3)]
+
+        def ds(i):
+            return {} if dseeds is None else {"dseed": dseeds[i]}
+        p1, p2 = L1.spec.dropout, L2.spec.dropout
+        h1 = ops.linear_fwd(x, L1.W, L1.b, True, p1, seeds[0], L1.col_off, **ds(0))
+        if L2.style == "row":
+            P2 = ops.linear_fwd(h1, L2.W, None, False, 0.0, 0, 0)
+            self.allreduce(P2)
+        else:
+            P2 = ops.linear_fwd_partial(h1, L2.W)
+        h2, dlog, dz2, loss = ops.server_head3(P2, L2.b, True, p2, seeds[1], L3.W, L3.b, labels, 1.0 / M, **ds(1))
+        s1 = 1.0 / (1.0 - p1) if p1 else 1.0
+        dx = None
+        # dz1 is materialised (split-N dgrad + reduce/mask kernel): reducing the split-N
+        # slabs inside the wgrad staging put ~9 dependent L2 loads per element on every
+        # workgroup's critical path (measured 166 vs 120 us on fc1), a net loss.
+        dz1 = ops.linear_dgrad(dz2, L2.W, h1, s1)
+        if need_dx:
+            dx = ops.linear_dgrad(dz1, L1.W, None, 1.0)
+        src1 = (dz1, None, None, 1.0)
+        self.acts = [x, h1, h2]
+        self._wg = [src1 + (x,), (dz2, None, None, 1.0, h1), (dlog, None, None, 1.0, h2)]
+        self._train_fwd = True
+        return loss, dx
+
+    def fused_step(self, slot: OptSlot, t: int | None = None, dyn=None, prefix: str = ""):
+        t = slot.tick() if t is None else t
+        layers = []
+        for (dz, dzp, hm, ms, A), L in zip(self._wg, self.layers):
+            layers.append((dz, dzp, hm, ms, A, L.W, slot.state(f"{prefix}{L.spec.name}.weight", L.W), L.b,
+                           slot.state(f"{prefix}{L.spec.name}.bias", L.b)))
+        self.ops.wgrad_group_(layers, self.acts[0].shape[0], slot.cfg, t, dyn)
+        self._wg = []
+
     # ------------------------------------------------------------------ state
     def local_state(self) -> dict:
         out = {}

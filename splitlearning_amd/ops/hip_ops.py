@@ -123,8 +123,9 @@ _WS: dict = {}
 
 
 def _workspace(device, n, key="dgrad"):
-    """Split-K / split-N partial-sum slabs.  Separate buffers per op kind: a forward's
-    slabs must not alias the dgrad slabs of the same step (both can be live in a graph)."""
+    """Split-K / split-N partial-sum slabs.  Separate buffers per producer: slabs handed to
+    a later fused consumer ("fc2p" -> server_head3, "dz1p" -> wgrad_group) must not be
+    overwritten by the scratch use ("fwd", "dgrad") of the kernels launched in between."""
     ws = _WS.get((device, key))
     if ws is None or ws.numel() < n:
         ws = torch.empty(max(n, 1 << 20), device=device, dtype=torch.float32)
@@ -164,6 +165,50 @@ def linear_wgrad_step_(dz, a, w, b, cfg, st_w, st_b, t, dyn=None):
 
 def apply_update_(p, g, st, cfg, t):
     C().opt_flat(p.detach(), g, _s0(st), _s1(st), *_opt_args(cfg, t))
+
+
+# ---------------------------------------------------------------- fused server step
+def linear_fwd_partial(x, w, max_split: int = 16, key: str = "fc2p"):
+    """x @ w.T as un-reduced split-K slabs [S, M, N] (S = 1: the plain product)."""
+    M, N = x.shape[0], w.shape[0]
+    ws = _workspace(x.device, 16 * M * N, key)
+    S = C().linear_fwd_partial(x, w.detach(), ws, max_split)
+    return ws[:S * M * N].view(S, M, N)
+
+
+def linear_dgrad_partial(dz, w, key: str = "dz1p"):
+    """dz @ w as un-reduced split-N slabs [S, M, K] (no mask)."""
+    M, K = dz.shape[0], w.shape[1]
+    ws = _workspace(dz.device, 16 * M * K, key)
+    S = C().linear_dgrad_partial(dz, w.detach(), ws)
+    return ws[:S * M * K].view(S, M, K)
+
+
+def server_head3(P2, b2, relu2: bool, drop2: float, seed2: int, W3, b3, labels, scale: float,
+                 ignore_index: int = -100, dseed=None):
+    """fc2 epilogue + fc3 + softmax-CE + fc3 dgrad + fc2 ReLU/dropout backward, one kernel.
+    Returns (h2, dlogits, dz2, loss_rows)."""
+    M, N2 = P2.shape[-2], P2.shape[-1]
+    dev = P2.device
+    h2 = torch.empty(M, N2, device=dev)
+    dz2 = torch.empty(M, N2, device=dev)
+    dlog = torch.empty(M, W3.shape[0], device=dev)
+    loss = torch.empty(M, device=dev)
+    C().server_head3(P2, b2.detach() if b2 is not None else None, relu2, float(drop2), seed2 & M64, _ptr(dseed),
+                     W3.detach(), b3.detach() if b3 is not None else None, labels, int(ignore_index), float(scale),
+                     h2, dlog, dz2, loss)
+    return h2, dlog, dz2, loss
+
+
+def wgrad_group_(layers, M: int, cfg, t: int, dyn=None):
+    """Fused wgrad+optimizer of up to 3 layers in one launch.  Each layer:
+    (dz, dzp, hmask, mscale, A, W, st_w, b, st_b) — exactly one of dz / dzp."""
+    tup = []
+    for dz, dzp, hm, ms, A, W, st_w, b, st_b in layers:
+        tup.append((dz, dzp, hm, float(ms), A, W.detach(), _s0(st_w), _s1(st_w),
+                    b.detach() if b is not None else None, _s0(st_b) if b is not None else None,
+                    _s1(st_b) if b is not None else None))
+    C().wgrad_group(tup, int(M), *_opt_args(cfg, t, dyn))
 
 
 # ---------------------------------------------------------------- loss / metrics

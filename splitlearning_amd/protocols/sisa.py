@@ -156,6 +156,11 @@ class SisaSession(Session):
         return self._ck
 
     def server_step(self, x, y):
+        """`zero_grad; CE(model(x), y).backward(); step` on Bob (data_entities_vanilla_sisa.py:305-313)."""
+        if self.tail.fused3_ok():
+            self.tail.train_fwd_bwd3(x, y, need_dx=False)
+            self.tail.fused_step(self.bob_slot)
+            return
         out = self.tail.forward(x, train=True)
         _, d = self.ops.softmax_ce(out, y, 1.0 / x.shape[0])
         self.tail.backward_dgrad(d, need_dx=False)

@@ -55,13 +55,20 @@ class VanillaSession(Session):
             labels = a.train.y[idx]
         act_b, lab_b = self.send_act_labels(cid, act, labels, B)
         dxp = None
+        fused = self.is_bob and self.tail.fused3_ok()
         if self.is_bob:
-            out = self.tail.forward(act_b, train=True)
-            _, dout = self.ops.softmax_ce(out, lab_b, 1.0 / B)
-            dxp = self.tail.backward_dgrad(dout, need_dx=True)
+            if fused:
+                _, dxp = self.tail.train_fwd_bwd3(act_b, lab_b, need_dx=True)
+            else:
+                out = self.tail.forward(act_b, train=True)
+                _, dout = self.ops.softmax_ce(out, lab_b, 1.0 / B)
+                dxp = self.tail.backward_dgrad(dout, need_dx=True)
         fin = self.comm.reduce_to_async(dxp, host, self.bob_ranks, (B, CUT_FEATURES), torch.float32)
         if self.is_bob:
-            self.tail.backward_step(self.bob_slot(cid))
+            if fused:
+                self.tail.fused_step(self.bob_slot(cid))
+            else:
+                self.tail.backward_step(self.bob_slot(cid))
         dx = fin()
         if a is not None:
             a.front.backward_step(dx, act, am, a.train, idx, a.slot)

@@ -15,27 +15,32 @@ def _tail(dev):
     return TailEngine(ServerTailSisa(), sisa_server_spec(), dev, seed_base=42)
 
 
+def _eager_step(t, slot, x, y):
+    if t.fused3_ok():
+        t.train_fwd_bwd3(x, y, need_dx=False)
+        t.fused_step(slot)
+        return
+    out = t.forward(x, train=True)
+    _, d = hip_ops.softmax_ce(out, y, 1.0 / x.shape[0])
+    t.backward_dgrad(d, need_dx=False)
+    t.backward_step(slot)
+
+
 def test_graph_replay_matches_eager(cuda):
     g = torch.Generator().manual_seed(0)
     n, B, G = 16 * 40, 16, 8
     acts = (torch.rand(n, 5408, generator=g) * 30).to(cuda)
     labels = torch.randint(0, 10, (n,), generator=g).to(cuda)
-    # eager
+    # eager (same kernel sequence as the graph: the fused path when available)
     te, se = _tail(cuda), OptSlot(adam(1e-3, 1e-5))
     for s in range(0, n, B):
-        out = te.forward(acts[s:s + B], train=True)
-        _, d = hip_ops.softmax_ce(out, labels[s:s + B], 1.0 / B)
-        te.backward_dgrad(d, need_dx=False)
-        te.backward_step(se)
+        _eager_step(te, se, acts[s:s + B], labels[s:s + B])
     # graphed (first 32 steps) + eager tail (8 steps)
     tg, sg = _tail(cuda), OptSlot(adam(1e-3, 1e-5))
     gs = GraphedServerSteps(tg, sg, B, G, 5408)
     gs.run(acts, labels, 32)
     for s in range(32 * B, n, B):
-        out = tg.forward(acts[s:s + B], train=True)
-        _, d = hip_ops.softmax_ce(out, labels[s:s + B], 1.0 / B)
-        tg.backward_dgrad(d, need_dx=False)
-        tg.backward_step(sg)
+        _eager_step(tg, sg, acts[s:s + B], labels[s:s + B])
     torch.cuda.synchronize()
     assert sg.t == se.t == 40 and tg.fwd_count == te.fwd_count
     for L1, L2 in zip(te.layers, tg.layers):
@@ -78,12 +83,41 @@ def test_graphed_tp_tail_with_native_allreduce(cuda):
                           seed_base=5)
     te, se = mk(), OptSlot(adam(1e-3, 1e-5))
     for s in range(0, n, B):
-        out = te.forward(acts[s:s + B], train=True)
-        _, d = hip_ops.softmax_ce(out, labels[s:s + B], 1.0 / B)
-        te.backward_dgrad(d, need_dx=False)
-        te.backward_step(se)
+        _eager_step(te, se, acts[s:s + B], labels[s:s + B])
     tg, sg = mk(), OptSlot(adam(1e-3, 1e-5))
     GraphedServerSteps(tg, sg, B, G, 5408).run(acts, labels, n // B)
     torch.cuda.synchronize()
     for L1, L2 in zip(te.layers, tg.layers):
         assert torch.equal(L1.W, L2.W) and torch.equal(L1.b, L2.b)
+
+
+@pytest.mark.parametrize("need_dx", [False, True])
+@pytest.mark.parametrize("kind", ["adam", "sgd"])
+def test_fused_server_step_matches_generic(cuda, need_dx, kind):
+    from splitlearning_amd.engine import sgd_momentum
+    g = torch.Generator().manual_seed(2)
+    B, steps = 16, 4
+    acts = (torch.rand(B * steps, 5408, generator=g) * 30).to(cuda)
+    labels = torch.randint(0, 10, (B * steps,), generator=g).to(cuda)
+    mk_slot = (lambda: OptSlot(adam(1e-3, 1e-5))) if kind == "adam" else (lambda: OptSlot(sgd_momentum(1e-2)))
+    ta, sa = _tail(cuda), mk_slot()
+    tb, sb = _tail(cuda), mk_slot()
+    assert tb.fused3_ok()
+    for s in range(0, B * steps, B):
+        x, y = acts[s:s + B], labels[s:s + B]
+        out = ta.forward(x, train=True)
+        loss_a, d = hip_ops.softmax_ce(out, y, 1.0 / B)
+        dxa = ta.backward_dgrad(d, need_dx=need_dx)
+        ta.backward_step(sa)
+        loss_b, dxb = tb.train_fwd_bwd3(x, y, need_dx=need_dx)
+        tb.fused_step(sb)
+        torch.testing.assert_close(loss_b, loss_a, rtol=1e-4, atol=1e-5)
+        if need_dx:
+            torch.testing.assert_close(dxb, dxa, rtol=1e-3, atol=1e-5)
+    torch.cuda.synchronize()
+    for L1, L2 in zip(ta.layers, tb.layers):
+        if kind == "sgd":   # plain SGD: parameter error = lr * gradient rounding difference
+            torch.testing.assert_close(L1.W, L2.W, rtol=1e-4, atol=1e-4)
+            continue
+        d = (L1.W - L2.W).abs()   # Adam: rounding noise on ~zero gradients moves by up to lr
+        assert d.max().item() < 1e-2 and (d > 1e-5).float().mean().item() < 1e-4
