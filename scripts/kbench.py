@@ -148,6 +148,18 @@ def main():
     dz1r = torch.randn(M, N1, device=dev)
     grp_plain = [(dz1r, None, None, 1.0, x, L1.W, wst[0], L1.b, wst[1])]
     cases.append(("fused:wgrad_fc1_plain_dz", lambda: H.wgrad_group_(grp_plain, M, cfg, 3), W1.numel() * 24))
+    pn = H.lookahead_slabs(dev, 5408, M, N1)
+    cases.append(("fused:wgrad_fc1_plain_dz_lookahead",
+                  lambda: H.wgrad_group_(grp_plain, M, cfg, 3, x_next=x, p_next=pn), W1.numel() * 24))
+    def _v1(fn):
+        def run():
+            C.set_variant(3, 1)
+            fn()
+            C.set_variant(3, 0)
+        return run
+    cases.append(("fused:wgrad_fc1_plain_dz[mfma]", _v1(lambda: H.wgrad_group_(grp_plain, M, cfg, 3)), W1.numel() * 24))
+    cases.append(("fused:wgrad_fc1_plain_dz_lookahead[mfma]",
+                  _v1(lambda: H.wgrad_group_(grp_plain, M, cfg, 3, x_next=x, p_next=pn)), W1.numel() * 24))
     cases.append(("v3:wgrad_fc1_same_tensors", lambda: H.linear_wgrad_step_(dz1r, x, L1.W, L1.b, cfg, wst[0], wst[1], 3),
                   W1.numel() * 24))
 
@@ -155,6 +167,14 @@ def main():
         ftail.train_fwd_bwd3(x, yl, need_dx=False)
         ftail.fused_step(fslot)
     cases.append(("bob_fused_step", bob_fused, 32_146_100 * 28))
+    ltail = TailEngine(ServerTailSisa(), sisa_server_spec(), dev)
+    lslot = OptSlot(adam(1e-3, 1e-5))
+    ltail.lookahead_prologue(x)
+
+    def bob_lookahead():
+        ltail.train_fwd_bwd3(x, yl, need_dx=False, pre=True)
+        ltail.fused_step(lslot, x_next=x)
+    cases.append(("bob_lookahead_step", bob_lookahead, 32_146_100 * 24))
     # graph-replayed server steps (per-step time = one replay of 16 steps / 16)
     from splitlearning_amd.engine.graphs import GraphedServerSteps
     gtail = TailEngine(ServerTailSisa(), sisa_server_spec(), dev)

@@ -1,0 +1,80 @@
+"""Drive Bob's server step for rocprofv3 (per-kernel device times):
+
+    rocprofv3 --kernel-trace --stats --output-format csv -d OUT -o step -- \
+        python3 scripts/prof_step.py --path fused --steps 200
+
+--path generic|fused|lookahead|graph|local (local = the SISA client step).
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from splitlearning_amd import ops  # noqa: E402
+from splitlearning_amd.engine import OptSlot, TailEngine, adam  # noqa: E402
+from splitlearning_amd.models import ServerTailSisa, sisa_server_spec  # noqa: E402
+from splitlearning_amd.ops import hip_ops as H  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--path", default="fused")
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--tp", type=int, default=1, help="simulate a TP shard (rank 0 of tp, 1-rank all-reduce)")
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    ops.set_backend("hip")
+    torch.manual_seed(0)
+    n = 16 * 64
+    acts = torch.rand(n, 5408, device=dev) * 20
+    labels = torch.randint(0, 10, (n,), device=dev)
+    ar = None
+    if a.tp > 1:
+        from splitlearning_amd.parallel.rccl import native_allreduce, self_comm
+        ar = native_allreduce(self_comm())
+    tail = TailEngine(ServerTailSisa(), sisa_server_spec(), dev, tp_rank=0, tp_size=a.tp, allreduce=ar)
+    slot = OptSlot(adam(1e-3, 1e-5))
+    if a.path == "local":
+        from splitlearning_amd.data.device_dataset import DeviceShard
+        from splitlearning_amd.engine import FrontEngine
+        from splitlearning_amd.models import ClientFrontSisa
+        x = torch.randint(0, 256, (4096, 784), dtype=torch.uint8)
+        y = torch.randint(0, 10, (4096,))
+        shard = DeviceShard(x, y, dev)
+        front = FrontEngine(ClientFrontSisa(), dev)
+        aslot = OptSlot(adam(1e-3, 1e-5))
+        order = shard.shuffled_order(torch.Generator().manual_seed(0))
+        for i in range(a.steps):
+            s = (i * 16) % 4096
+            front.local_step(shard, order[s:s + 16], aslot)
+    elif a.path == "graph":
+        from splitlearning_amd.engine.graphs import GraphedServerSteps
+        gs = GraphedServerSteps(tail, slot, 16, 16, 5408)
+        for _ in range(a.steps // 16):
+            gs.run(acts, labels, 16)
+    else:
+        if a.path == "lookahead":
+            tail.lookahead_prologue(acts[:16])
+        for i in range(a.steps):
+            s = (i * 16) % n
+            x, y = acts[s:s + 16], labels[s:s + 16]
+            if a.path == "lookahead":
+                tail.train_fwd_bwd3(x, y, need_dx=False, pre=True)
+                s2 = ((i + 1) * 16) % n
+                tail.fused_step(slot, x_next=acts[s2:s2 + 16])
+            elif a.path == "fused":
+                tail.train_fwd_bwd3(x, y, need_dx=False)
+                tail.fused_step(slot)
+            else:
+                out = tail.forward(x, train=True)
+                _, d = H.softmax_ce(out, y, 1 / 16)
+                tail.backward_dgrad(d, need_dx=False)
+                tail.backward_step(slot)
+    torch.cuda.synchronize()
+
+
+if __name__ == "__main__":
+    main()

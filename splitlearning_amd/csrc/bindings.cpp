@@ -31,7 +31,8 @@ hipError_t linear_fwd(const float* X, int ldx, const float* W, int ldw, float* Y
 hipError_t linear_dgrad(const float* dZ, int ldz, const float* W, int ldw, const float* hprev, int ldh,
                         float scale, float* dX, int ldx, float* ws, int64_t ws_elems, int M, int N, int K,
                         hipStream_t st);
-hipError_t linear_epilogue(const float* P, int ldp, float* Y, int ldy, int M, int N, Epi e, hipStream_t st);
+hipError_t linear_epilogue(const float* P, int ldp, float* Y, int ldy, int M, int N, Epi e, int S, int64_t slab,
+                           hipStream_t st);
 hipError_t linear_fwd_partial(const float* X, int ldx, const float* W, int ldw, int M, int N, int K, float* ws,
                               int64_t ws_elems, int max_split, int* S_out, hipStream_t st);
 hipError_t linear_dgrad_partial(const float* dZ, int ldz, const float* W, int ldw, int M, int N, int K, float* ws,
@@ -209,15 +210,25 @@ void linear_fwd(const at::Tensor& X, const at::Tensor& W, const OptT& bias, at::
         "linear_fwd");
 }
 
+// P: [M, N] pre-activations, or [S, M, N] contiguous split-K partial slabs (summed here).
 void linear_epilogue(const at::Tensor& P, const OptT& bias, at::Tensor& Y, bool relu, double drop_p, uint64_t seed,
                      int64_t col_off, int64_t dseed) {
-  need_2d(P, "P");
   need_2d(Y, "Y");
-  TORCH_CHECK(P.sizes() == Y.sizes(), "P/Y shape");
-  if (bias.has_value() && bias->defined()) TORCH_CHECK(bias->numel() == P.size(1), "bias [N]");
-  check(sl::linear_epilogue(P.data_ptr<float>(), (int)P.stride(0), Y.data_ptr<float>(), (int)Y.stride(0),
-                            (int)P.size(0), (int)P.size(1), make_epi(bias, relu, drop_p, seed, col_off, dseed),
-                            cur_stream()),
+  int S = 1;
+  int64_t slab = 0;
+  if (P.dim() == 3) {
+    need_f32(P, "P");
+    TORCH_CHECK(P.is_contiguous() && P.size(1) == Y.size(0) && P.size(2) == Y.size(1), "P [S,M,N]");
+    S = (int)P.size(0);
+    slab = P.size(1) * P.size(2);
+  } else {
+    need_2d(P, "P");
+    TORCH_CHECK(P.sizes() == Y.sizes(), "P/Y shape");
+  }
+  const int64_t M = Y.size(0), N = Y.size(1);
+  if (bias.has_value() && bias->defined()) TORCH_CHECK(bias->numel() == N, "bias [N]");
+  check(sl::linear_epilogue(P.data_ptr<float>(), (int)P.stride(P.dim() - 2), Y.data_ptr<float>(), (int)Y.stride(0),
+                            (int)M, (int)N, make_epi(bias, relu, drop_p, seed, col_off, dseed), S, slab, cur_stream()),
         "linear_epilogue");
 }
 
@@ -347,14 +358,16 @@ int64_t linear_dgrad_partial(const at::Tensor& dZ, const at::Tensor& W, at::Tens
 // P2: fc2 partial sums, [S2, M, N2] split-K slabs or a reduced [M, N2] tensor.
 void server_head3(const at::Tensor& P2, const OptT& b2, bool relu2, double drop2, uint64_t seed2, int64_t dseed2,
                   const at::Tensor& W3, const OptT& b3, const at::Tensor& y, int64_t ignore, double scale,
-                  at::Tensor& h2, at::Tensor& dlog, at::Tensor& dz2, at::Tensor& loss_rows) {
+                  at::Tensor& h2, at::Tensor& dlog, at::Tensor& dz2, at::Tensor& loss_rows, at::Tensor& ws) {
   need_f32(P2, "P2");
   TORCH_CHECK(P2.is_contiguous() && (P2.dim() == 2 || P2.dim() == 3), "P2 [S,M,N2] or [M,N2] contiguous");
   const int64_t S2 = P2.dim() == 3 ? P2.size(0) : 1;
   const int64_t M = P2.size(P2.dim() - 2), N2 = P2.size(P2.dim() - 1);
   need_rows(W3, "W3");
   const int64_t C = W3.size(0);
-  TORCH_CHECK(W3.size(1) == N2 && N2 % 4 == 0 && C <= 4096, "W3 [C, N2], N2 % 4 == 0");
+  TORCH_CHECK(W3.size(1) == N2 && N2 % 4 == 0 && W3.stride(0) % 4 == 0 && C <= 4096, "W3 [C, N2], N2 % 4 == 0");
+  need_f32(ws, "ws");
+  TORCH_CHECK(ws.is_contiguous() && ws.numel() >= (int64_t)sl::head3_slices((int)N2) * M * C, "head workspace");
   need_cuda(y, "labels");
   TORCH_CHECK(y.scalar_type() == at::kLong && y.numel() == M && y.is_contiguous(), "labels int64 [M]");
   for (auto* t : {&h2, &dz2}) {
@@ -366,15 +379,18 @@ void server_head3(const at::Tensor& P2, const OptT& b2, bool relu2, double drop2
   need_f32(loss_rows, "loss_rows");
   TORCH_CHECK(loss_rows.numel() >= M, "loss_rows");
   check(sl::server_head3(P2.data_ptr<float>(), (int)S2, M * N2, make_epi(b2, relu2, drop2, seed2, 0, dseed2),
-                         W3.data_ptr<float>(), fptr(b3), y.data_ptr<int64_t>(), ignore, (float)scale,
-                         h2.data_ptr<float>(), dlog.data_ptr<float>(), dz2.data_ptr<float>(),
-                         loss_rows.data_ptr<float>(), (int)M, (int)N2, (int)C, cur_stream()),
+                         W3.data_ptr<float>(), (int)W3.stride(0), fptr(b3), y.data_ptr<int64_t>(), ignore,
+                         (float)scale, h2.data_ptr<float>(), dlog.data_ptr<float>(), dz2.data_ptr<float>(),
+                         loss_rows.data_ptr<float>(), ws.data_ptr<float>(), ws.numel(), (int)M, (int)N2, (int)C,
+                         cur_stream()),
         "server_head3");
 }
 
 // layers: up to 3 tuples (dz, dzp, hmask, mscale, A, W, s0, s1, bias, sb0, sb1); exactly one of dz / dzp
 // (dzp = [S, M, N] split-N partial slabs of the layer's output gradient, masked by hmask > 0).
-void wgrad_group(const std::vector<py::tuple>& layers, int64_t M, OPT_ARGS) {
+// xn / pn (optional): next batch [mn, K0] -> its split-K partial pre-activations of layer 0
+// with the updated weights, pn = [ceil(K0/256), mn, N0].
+void wgrad_group(const std::vector<py::tuple>& layers, int64_t M, const OptT& xn, const OptT& pn, OPT_ARGS) {
   TORCH_CHECK(!layers.empty() && layers.size() <= 3, "1..3 layers");
   sl::WgGroup g{};
   g.n = (int)layers.size();
@@ -426,6 +442,18 @@ void wgrad_group(const std::vector<py::tuple>& layers, int64_t M, OPT_ARGS) {
     d.N = (int)N;
     d.K = (int)K;
   }
+  if (xn.has_value() && xn->defined()) {
+    TORCH_CHECK(pn.has_value() && pn->defined(), "pn needed with xn");
+    need_rows(*xn, "xn");
+    need_f32(*pn, "pn");
+    const int64_t K0 = g.d[0].K, N0 = g.d[0].N, mn = xn->size(0);
+    TORCH_CHECK(xn->size(1) == K0 && mn >= 1 && mn <= 16, "xn [mn<=16, K0]");
+    TORCH_CHECK(pn->is_contiguous() && pn->numel() >= (K0 + 255) / 256 * mn * N0, "pn [K0/256, mn, N0]");
+    g.xn = xn->data_ptr<float>();
+    g.ldxn = (int)xn->stride(0);
+    g.mn = (int)mn;
+    g.pn = pn->data_ptr<float>();
+  }
   check(sl::wgrad_group(g, (int)M, OPT_PASS, cur_stream()), "wgrad_group");
 }
 
@@ -447,6 +475,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("softmax_ce", &softmax_ce);
   m.def("eval_counters", &eval_counters);
   m.def("server_head3", &server_head3);
+  m.def("head3_slices", [](int64_t n2) { return (int64_t)sl::head3_slices((int)n2); });
   m.def("linear_fwd_partial", &linear_fwd_partial);
   m.def("linear_dgrad_partial", &linear_dgrad_partial);
   m.def("wgrad_group", &wgrad_group);

@@ -27,11 +27,19 @@ struct WgDesc {
 struct WgGroup {
   WgDesc d[3];
   int n;
+  // Optional look-ahead forward of layer 0 with its *updated* weights:
+  //   pn[kb][m][n] = sum_{k in k-block kb} xn[m, k] * W0_new[n, k]   (kb = 256-column blocks)
+  // i.e. the next batch's split-K partial pre-activations, written while W0 is in registers.
+  const float* xn;      // [mn, K0] next batch input (mn <= 16), or nullptr
+  int ldxn;
+  int mn;
+  float* pn;            // [ceil(K0/256)][mn][N0]
 };
 
-hipError_t server_head3(const float* P2, int S2, int64_t slab2, Epi e2, const float* W3, const float* b3,
+int head3_slices(int N2);
+hipError_t server_head3(const float* P2, int S2, int64_t slab2, Epi e2, const float* W3, int ldw3, const float* b3,
                         const int64_t* y, int64_t ignore, float scale, float* h2, float* dlog, float* dz2,
-                        float* loss_rows, int M, int N2, int C, hipStream_t st);
+                        float* loss_rows, float* ws, int64_t ws_elems, int M, int N2, int C, hipStream_t st);
 hipError_t wgrad_group(const WgGroup& g, int M, SlOpt o, hipStream_t st);
 
 }  // namespace sl

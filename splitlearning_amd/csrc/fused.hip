@@ -5,11 +5,13 @@
 // chain is 13 kernels, each with a ~1.5-2.5 us dependent-launch boundary, and on a
 // tensor-parallel shard (1/8 of the bytes) the boundaries dominate.  Two fusions:
 //
-//  head3_kernel  one workgroup per batch row: reduce fc2's split-K partial slabs, apply
-//                fc2's bias/ReLU/dropout (-> h2), fc3 logits, softmax-CE (loss, dlogits),
-//                fc3 data gradient and fc2's ReLU/dropout backward (-> dz2).  Replaces
-//                fc2-epilogue, fc3-forward(+epilogue), CE and fc3-dgrad (5 launches).
-//                fc3 is 100x1000: each workgroup streams W3 twice from L2.
+//  server_head3  two kernels over (row, 128-column slice) workgroups: reduce fc2's split-K
+//                partial slabs + fc2's bias/ReLU/dropout (-> h2) + partial fc3 logits; then
+//                logits, softmax-CE (loss, dlogits), fc3 data gradient and fc2's
+//                ReLU/dropout backward (-> dz2).  Replaces fc2-epilogue, fc3-forward,
+//                CE and fc3-dgrad.  (A one-workgroup-per-row version that recomputed the
+//                logits per slice measured 59 us under rocprofv3: each workgroup streamed
+//                all of W3 with dependent loads; this split measures in profiles/.)
 //
 //  wgrad_group_kernel   the fused wgrad+optimizer (v3 layout) for up to 3 layers in one
 //                launch; a layer's dZ may be given as un-reduced split-N partial slabs plus
@@ -19,62 +21,94 @@
 
 namespace sl {
 
+// Column slices of <= 32 float4 (128 columns) per workgroup; grid (M, Q) for both kernels.
+constexpr int HS = 32;
+
+__device__ __forceinline__ void head_slice(int n4, int Q, int q, int& a, int& b) {
+  a = (int)(((int64_t)n4 * q) / Q);
+  b = (int)(((int64_t)n4 * (q + 1)) / Q);
+}
+
+// head_fwd_kernel: workgroup (m, q) reduces fc2's split-K slabs for its column slice of row
+// m, applies fc2's epilogue (-> h2) and writes the slice's partial fc3 logits plog[q][m][:].
+// Every load of a phase is issued before the first is consumed (one memory round trip per
+// phase): at B = 16 this op is pure latency.
 __global__ void __launch_bounds__(256)
-head3_kernel(const float* __restrict__ P2, int S2, int64_t slab2, Epi e2, const float* __restrict__ W3,
-             const float* __restrict__ b3, const int64_t* __restrict__ y, int64_t ignore, float scale,
-             float* __restrict__ h2, float* __restrict__ dlog, float* __restrict__ dz2,
-             float* __restrict__ loss_rows, int N2, int C) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* hrow = sm;            // N2 (rounded up to 4)
-  float* lg = sm + ((N2 + 3) & ~3);   // C
-  // grid (M, Q): workgroup (m, q) recomputes row m's logits and CE (cheap, L2-resident W3)
-  // but owns only column quarter q of the h2 / dz2 outputs, so the dz2 phase is spread
-  // over M*Q workgroups.
-  const int m = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int Q = gridDim.y, q = blockIdx.y;
-  const int n4 = N2 >> 2;   // N2 % 4 == 0 (checked on the host)
-  const int q4a = (int)(((int64_t)n4 * q) / Q), q4b = (int)(((int64_t)n4 * (q + 1)) / Q);
-  // 1. h2 = epilogue(sum of fc2 partial slabs); float4 per thread, slab loads unrolled so
-  //    they are all in flight together
-  const float* prow = P2 + (int64_t)m * N2;
-  for (int c4 = tid; c4 < n4; c4 += 256) {
+head_fwd_kernel(const float* __restrict__ P2, int S2, int64_t slab2, Epi e2, const float* __restrict__ W3,
+                int ldw3, float* __restrict__ h2, float* __restrict__ plog, int M, int N2, int C) {
+  __shared__ f32x4 part[8][HS];
+  __shared__ f32x4 hs[HS];
+  const int m = blockIdx.x, q = blockIdx.y, Q = gridDim.y, tid = threadIdx.x;
+  int qa, qb;
+  head_slice(N2 >> 2, Q, q, qa, qb);
+  const int ncol = qb - qa;
+  // 1. slab reduction: 32 columns x 8 slab groups
+  {
+    const int c = tid & (HS - 1), sg = tid >> 5;
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 8
-    for (int s = 0; s < S2; ++s) v += reinterpret_cast<const f32x4*>(prow + s * slab2)[c4];
-    f32x4 o;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) o[i] = apply_epi(e2, v[i], m, 4 * c4 + i);
-    reinterpret_cast<f32x4*>(hrow)[c4] = o;
-    if (c4 >= q4a && c4 < q4b) reinterpret_cast<f32x4*>(h2 + (int64_t)m * N2)[c4] = o;
-  }
-  __syncthreads();
-  // 2. logits[o] = <h2, W3[o]> + b3[o]: a wave takes OG outputs at a time (OG independent
-  //    accumulators / loads in flight), lanes split K in float4 steps
-  constexpr int OG = 5;
-  const f32x4* hr = reinterpret_cast<const f32x4*>(hrow);
-  for (int o0 = wv * OG; o0 < C; o0 += 4 * OG) {
-    float acc[OG];
-#pragma unroll
-    for (int j = 0; j < OG; ++j) acc[j] = 0.f;
+    if (c < ncol) {
+      const f32x4* src = reinterpret_cast<const f32x4*>(P2 + (int64_t)m * N2) + qa + c;
 #pragma unroll 4
-    for (int qq = lane; qq < n4; qq += 64) {
-      const f32x4 a = hr[qq];
-#pragma unroll
-      for (int j = 0; j < OG; ++j) {
-        if (o0 + j < C) {
-          const f32x4 b = reinterpret_cast<const f32x4*>(W3 + (int64_t)(o0 + j) * N2)[qq];
-          acc[j] = fmaf(a[0], b[0], fmaf(a[1], b[1], fmaf(a[2], b[2], fmaf(a[3], b[3], acc[j]))));
-        }
-      }
+      for (int s = sg; s < S2; s += 8) v += src[s * (slab2 >> 2)];
     }
-#pragma unroll
-    for (int j = 0; j < OG; ++j) {
-      const float s = sl_wave_sum(acc[j]);
-      if (lane == 0 && o0 + j < C) lg[o0 + j] = s + (b3 ? b3[o0 + j] : 0.f);
-    }
+    part[sg][c] = v;
   }
   __syncthreads();
-  // 3. softmax cross-entropy of the row (wave 0)
+  if (tid < HS) {
+    f32x4 v = part[0][tid];
+#pragma unroll
+    for (int g = 1; g < 8; ++g) v += part[g][tid];
+    f32x4 o = {0.f, 0.f, 0.f, 0.f};
+    if (tid < ncol) {
+      const int col = 4 * (qa + tid);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[i] = apply_epi(e2, v[i], m, col + i);
+      reinterpret_cast<f32x4*>(h2 + (int64_t)m * N2)[qa + tid] = o;
+    }
+    hs[tid] = o;
+  }
+  __syncthreads();
+  // 2. partial logits: half-waves (32 lanes = the slice's columns) per output, 8 outputs
+  //    per wave instruction group; JU outputs' loads in flight per lane
+  const int lane = tid & 63, wv = tid >> 6, half = lane >> 5, c = lane & 31;
+  const f32x4 h = hs[c];
+  constexpr int JU = 13;
+  for (int j0 = 0; j0 * 8 < C; j0 += JU) {
+    f32x4 w[JU];
+#pragma unroll
+    for (int j = 0; j < JU; ++j) {
+      const int o = 8 * (j0 + j) + 2 * wv + half;
+      w[j] = (o < C && c < ncol) ? *reinterpret_cast<const f32x4*>(W3 + (int64_t)o * ldw3 + 4 * (qa + c))
+                                 : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int j = 0; j < JU; ++j) {
+      const int o = 8 * (j0 + j) + 2 * wv + half;
+      float d = w[j][0] * h[0] + w[j][1] * h[1] + w[j][2] * h[2] + w[j][3] * h[3];
+#pragma unroll
+      for (int off = 16; off > 0; off >>= 1) d += __shfl_xor(d, off);
+      if (c == 0 && o < C) plog[((int64_t)q * M + m) * C + o] = d;
+    }
+  }
+}
+
+// head_bwd_kernel: workgroup (m, q) sums row m's partial logits (+ b3), softmax-CE (loss and
+// dlogits written by q == 0), then dz2 = (dlogits . W3) * dscale * [h2 > 0] for its slice.
+__global__ void __launch_bounds__(256)
+head_bwd_kernel(const float* __restrict__ plog, const float* __restrict__ b3, const float* __restrict__ W3,
+                int ldw3, const int64_t* __restrict__ y, int64_t ignore, float scale, float dscale,
+                const float* __restrict__ h2, float* __restrict__ dlog, float* __restrict__ dz2,
+                float* __restrict__ loss_rows, int M, int N2, int C) {
+  extern __shared__ float lg[];   // C
+  __shared__ f32x4 part[8][HS];
+  const int m = blockIdx.x, q = blockIdx.y, Q = gridDim.y, tid = threadIdx.x;
+  const int lane = tid & 63, wv = tid >> 6;
+  for (int o = tid; o < C; o += 256) {
+    float v = b3 ? b3[o] : 0.f;
+    for (int s = 0; s < Q; ++s) v += plog[((int64_t)s * M + m) * C + o];
+    lg[o] = v;
+  }
+  __syncthreads();
   const int64_t lab = y[m];
   if (wv == 0) {
     if (lab == ignore) {
@@ -99,44 +133,51 @@ head3_kernel(const float* __restrict__ P2, int S2, int64_t slab2, Epi e2, const 
   __syncthreads();
   if (q == 0)
     for (int c = tid; c < C; c += 256) dlog[(int64_t)m * C + c] = lg[c];
-  // 4. dz2 = (dlogits . W3) * dscale * [h2 > 0] for this workgroup's column slice: the
-  //    slice's float4 columns x the C outputs are spread over all 256 threads (OGR output
-  //    groups per column), partial sums reduced through LDS (reuses the logits' tail).
-  const int ncol = q4b - q4a;                 // float4 columns of this slice (<= 64)
-  const int ogr = ncol > 0 ? max(1, 256 / ncol) : 1;
-  __shared__ f32x4 part[256];
-  {
-    const int col = tid % max(ncol, 1), grp = tid / max(ncol, 1);
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    if (ncol > 0 && grp < ogr) {
-      const int qq = q4a + col;
-#pragma unroll 4
-      for (int o = grp; o < C; o += ogr) acc += lg[o] * reinterpret_cast<const f32x4*>(W3 + (int64_t)o * N2)[qq];
+  int qa, qb;
+  head_slice(N2 >> 2, Q, q, qa, qb);
+  const int ncol = qb - qa;
+  const int c = tid & (HS - 1), g = tid >> 5;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  constexpr int JU = 13;
+  for (int j0 = 0; j0 * 8 < C; j0 += JU) {
+    f32x4 w[JU];
+#pragma unroll
+    for (int j = 0; j < JU; ++j) {
+      const int o = 8 * (j0 + j) + g;
+      w[j] = (o < C && c < ncol) ? *reinterpret_cast<const f32x4*>(W3 + (int64_t)o * ldw3 + 4 * (qa + c))
+                                 : f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    part[tid] = acc;
+#pragma unroll
+    for (int j = 0; j < JU; ++j) {
+      const int o = 8 * (j0 + j) + g;
+      acc += (o < C ? lg[o] : 0.f) * w[j];
+    }
   }
+  part[g][c] = acc;
   __syncthreads();
   if (tid < ncol) {
-    f32x4 acc = part[tid];
-    for (int gI = 1; gI < ogr; ++gI) acc += part[gI * ncol + tid];
-    const int qq = q4a + tid;
-    const f32x4 h = reinterpret_cast<const f32x4*>(hrow)[qq];
+    f32x4 v = part[0][tid];
+#pragma unroll
+    for (int gg = 1; gg < 8; ++gg) v += part[gg][tid];
+    const f32x4 hh = reinterpret_cast<const f32x4*>(h2 + (int64_t)m * N2)[qa + tid];
     f32x4 out;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) out[i] = h[i] > 0.f ? acc[i] * e2.dscale : 0.f;
-    reinterpret_cast<f32x4*>(dz2 + (int64_t)m * N2)[qq] = out;
+    for (int i = 0; i < 4; ++i) out[i] = hh[i] > 0.f ? v[i] * dscale : 0.f;
+    reinterpret_cast<f32x4*>(dz2 + (int64_t)m * N2)[qa + tid] = out;
   }
 }
 
-template <bool ADAM>
+template <bool ADAM, bool FWDN>
 __global__ void __launch_bounds__(1024)
 wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
   __shared__ f32x4 sa[16][64];
   __shared__ float sdz[16][16];
+  __shared__ f32x4 sw[FWDN ? 16 : 1][64];    // look-ahead: the updated W tile
+  __shared__ f32x4 red[FWDN ? 16 : 1][64];   // look-ahead: per-wave 16x16 partials
   // pick the layer with selects (no runtime-indexed access to the by-value argument)
   const int by = (int)blockIdx.y;
-  const WgDesc L = (grp.n > 2 && by >= grp.d[2].yb0) ? grp.d[2]
-                   : ((grp.n > 1 && by >= grp.d[1].yb0) ? grp.d[1] : grp.d[0]);
+  const bool l0 = !(grp.n > 1 && by >= grp.d[1].yb0);
+  const WgDesc L = (grp.n > 2 && by >= grp.d[2].yb0) ? grp.d[2] : (l0 ? grp.d[0] : grp.d[1]);
   const int kb = blockIdx.x * 256;
   if (kb >= L.K) return;                 // uniform per workgroup
   const int tid = threadIdx.x;
@@ -153,6 +194,11 @@ wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
     q0 = *reinterpret_cast<const f32x4*>(L.s0 + off);
     if (ADAM) q1 = *reinterpret_cast<const f32x4*>(L.s1 + off);
   }
+  // look-ahead A operand in MFMA layout: lane (li, lq) holds x_next[li][kb + 16*wave + 4*lq .. +3]
+  const int li = lane & 15, lq = lane >> 4;
+  const int kx = kb + 16 * r + 4 * lq;
+  f32x4 xv = zv;
+  if (FWDN && l0 && li < grp.mn && kx < L.K) xv = *reinterpret_cast<const f32x4*>(grp.xn + (int64_t)li * grp.ldxn + kx);
   f32x4 g = zv;
   float gb = 0.f;
   for (int mc = 0; mc < M; mc += 16) {
@@ -188,6 +234,26 @@ wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
     *reinterpret_cast<f32x4*>(L.s0 + off) = q0;
     if (ADAM) *reinterpret_cast<f32x4*>(L.s1 + off) = q1;
   }
+  if (FWDN && l0) {
+    // next batch's partial pre-activations with the updated tile: stage W_new through LDS
+    // into MFMA B layout; wave w covers columns [16w, 16w+16) with 4 exact-fp32 MFMAs
+    // (B[k][n] = W_new[n][k]: lane (n = li, k-group lq) reads one float4 of the tile)
+    sw[r][lane] = act ? p : zv;
+    __syncthreads();
+    const f32x4 wv4 = sw[li][4 * r + lq];
+    f32x4 z = zv;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) z = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[i], wv4[i], z, 0, 0, 0);
+    red[r][lane] = z;                     // z[j] = partial(m = 4*lq + j, n = n0 + li)
+    __syncthreads();
+    if (tid < 256) {
+      const int m = tid >> 4, nn = tid & 15;
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < 16; ++w) v += red[w][16 * (m >> 2) + nn][m & 3];
+      if (m < grp.mn && n0 + nn < L.N) grp.pn[((int64_t)blockIdx.x * grp.mn + m) * L.N + n0 + nn] = v;
+    }
+  }
   if (L.bias && blockIdx.x == 0 && lane == 0 && n < L.N) {
     float pb = L.bias[n], b0 = L.sb0[n], b1 = L.sb1 ? L.sb1[n] : 0.f;
     sl_opt_update(o, pb, gb, b0, b1);
@@ -197,16 +263,116 @@ wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
   }
 }
 
-hipError_t server_head3(const float* P2, int S2, int64_t slab2, Epi e2, const float* W3, const float* b3,
+// All-MFMA form of the grouped wgrad+optimizer (variant 1; NOT the default).  Workgroup = 16 waves over a
+// 16-row x 256-column tile of W; wave w owns columns [16w, 16w+16).  Per 16-row batch chunk
+// the wave forms its 16x16 tile of dW^T with 4 exact-fp32 v_mfma_f32_16x16x4f32:
+//   A[k][m] = X[m][k] (lane: k = lane&15, m = lane>>4), B[m][n] = dZ[m][n],
+// whose accumulator layout (lane: n = lane&15, k = 4*(lane>>4)+i) is exactly one float4 of
+// a W row -> the W / state streams are float4 loads and the batch operands come straight
+// from L2 (no LDS staging: the LDS version re-read the X tile once per wave, 16x).
+// Look-ahead (FWDN): with W_new in that same layout, 4 more MFMAs give the wave's share of
+// x_next @ W_new^T (A = x_next float4 component i, B = W_new component i); the 16 waves'
+// 16x16 partials are summed through LDS into one split-K slab per 256-column block.
+// Measured on MI355X (fc1, 5000x5408, Adam): 147 us vs 120 us for the LDS-staged kernel
+// below — each wave instruction here touches 16 rows x 64 B instead of 1 row x 1 KB, and
+// HBM streams the latter better; the X-tile LDS re-reads it avoids were not the limiter.
+template <bool ADAM, bool FWDN>
+__global__ void __launch_bounds__(1024)
+wgrad_group_mfma_kernel(WgGroup grp, int M, SlOpt o) {
+  __shared__ f32x4 red[FWDN ? 16 : 1][64];
+  const int by = (int)blockIdx.y;
+  const bool l0 = !(grp.n > 1 && by >= grp.d[1].yb0);
+  const WgDesc L = (grp.n > 2 && by >= grp.d[2].yb0) ? grp.d[2] : (l0 ? grp.d[0] : grp.d[1]);
+  const int kb = blockIdx.x * 256;
+  if (kb >= L.K) return;                 // uniform per workgroup
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, li = lane & 15, lq = lane >> 4;
+  const int n0 = (by - L.yb0) * 16;
+  const int kw = kb + wv * 16;
+  const int n = n0 + li, k4 = kw + 4 * lq;
+  const bool nin = n < L.N;
+  const bool act = nin && k4 < L.K;
+  const f32x4 zv = {0.f, 0.f, 0.f, 0.f};
+  const int64_t off = (int64_t)n * L.ldw + k4;
+  f32x4 p = zv, q0 = zv, q1 = zv;
+  if (act) {
+    p = *reinterpret_cast<const f32x4*>(L.W + off);
+    q0 = *reinterpret_cast<const f32x4*>(L.s0 + off);
+    if (ADAM) q1 = *reinterpret_cast<const f32x4*>(L.s1 + off);
+  }
+  f32x4 xv = zv;
+  if (FWDN && l0 && li < grp.mn && k4 < L.K) xv = *reinterpret_cast<const f32x4*>(grp.xn + (int64_t)li * grp.ldxn + k4);
+  const bool kin = kw + li < L.K;
+  f32x4 g = zv;
+  float gb = 0.f;
+  for (int mc = 0; mc < M; mc += 16) {
+    float a[4], b[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int m = mc + 4 * s + lq;
+      a[s] = (m < M && kin) ? L.A[(int64_t)m * L.lda + kw + li] : 0.f;
+      float v = 0.f;
+      if (m < M && nin) {
+        if (L.dzp) {
+          for (int z = 0; z < L.S; ++z) v += L.dzp[z * L.slab + (int64_t)m * L.N + n];
+          if (L.hmask) v = L.hmask[(int64_t)m * L.N + n] > 0.f ? v * L.mscale : 0.f;
+        } else {
+          v = L.dz[(int64_t)m * L.ldz + n];
+        }
+      }
+      b[s] = v;
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      g = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], g, 0, 0, 0);
+      gb += b[s];
+    }
+  }
+  if (act) {
+    sl_opt_update4<ADAM>(o, p, g, q0, q1);
+    if (o.kind != 0) *reinterpret_cast<f32x4*>(L.W + off) = p;
+    *reinterpret_cast<f32x4*>(L.s0 + off) = q0;
+    if (ADAM) *reinterpret_cast<f32x4*>(L.s1 + off) = q1;
+  } else {
+    p = zv;
+  }
+  if (FWDN && l0) {
+    f32x4 z = zv;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) z = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[i], p[i], z, 0, 0, 0);
+    red[wv][lane] = z;                    // z[j] = partial(m = 4*lq + j, n = n0 + li)
+    __syncthreads();
+    if (tid < 256) {
+      const int m = tid >> 4, nn = tid & 15;
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < 16; ++w) v += red[w][16 * (m >> 2) + nn][m & 3];
+      if (m < grp.mn && n0 + nn < L.N) grp.pn[((int64_t)blockIdx.x * grp.mn + m) * L.N + n0 + nn] = v;
+    }
+  }
+  if (L.bias && blockIdx.x == 0 && wv == 0) {
+    gb += __shfl_xor(gb, 16);
+    gb += __shfl_xor(gb, 32);
+    if (lq == 0 && nin) {
+      float pb = L.bias[n], b0 = L.sb0[n], b1 = L.sb1 ? L.sb1[n] : 0.f;
+      sl_opt_update(o, pb, gb, b0, b1);
+      if (o.kind != 0) L.bias[n] = pb;
+      L.sb0[n] = b0;
+      if (L.sb1) L.sb1[n] = b1;
+    }
+  }
+}
+
+int head3_slices(int N2) { return max(1, (N2 / 4 + HS - 1) / HS); }
+
+hipError_t server_head3(const float* P2, int S2, int64_t slab2, Epi e2, const float* W3, int ldw3, const float* b3,
                         const int64_t* y, int64_t ignore, float scale, float* h2, float* dlog, float* dz2,
-                        float* loss_rows, int M, int N2, int C, hipStream_t st) {
+                        float* loss_rows, float* ws, int64_t ws_elems, int M, int N2, int C, hipStream_t st) {
   if (M <= 0) return hipSuccess;
-  const size_t shmem = (size_t)(((N2 + 3) & ~3) + C) * sizeof(float);
-  // column slices of <= 64 float4 so phase 4 has >= 4 output groups per column
-  const int n4 = N2 / 4;
-  const int Q = max(1, (n4 + 63) / 64);
-  head3_kernel<<<dim3(M, Q), 256, shmem, st>>>(P2, S2, slab2, e2, W3, b3, y, ignore, scale, h2, dlog, dz2, loss_rows,
-                                               N2, C);
+  const int Q = head3_slices(N2);
+  if (ws_elems < (int64_t)Q * M * C || (N2 & 3) || (ldw3 & 3)) return hipErrorInvalidValue;
+  head_fwd_kernel<<<dim3(M, Q), 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C);
+  head_bwd_kernel<<<dim3(M, Q), 256, (size_t)C * sizeof(float), st>>>(ws, b3, W3, ldw3, y, ignore, scale, e2.dscale,
+                                                                      h2, dlog, dz2, loss_rows, M, N2, C);
   return hipGetLastError();
 }
 
@@ -220,10 +386,26 @@ hipError_t wgrad_group(const WgGroup& g, int M, SlOpt o, hipStream_t st) {
   }
   if (yb == 0 || kmax == 0) return hipSuccess;
   dim3 grid((kmax + 255) / 256, yb);
-  if (o.kind == 2)
-    wgrad_group_kernel<true><<<grid, 1024, 0, st>>>(gg, M, o);
-  else
-    wgrad_group_kernel<false><<<grid, 1024, 0, st>>>(gg, M, o);
+  if (gg.xn && (gg.mn <= 0 || gg.mn > 16 || !gg.pn)) return hipErrorInvalidValue;
+  const bool fw = gg.xn != nullptr;
+  if (g_variant[3] != 1) {   // default: LDS-staged VALU dW (row-contiguous W streams)
+    if (o.kind == 2) {
+      if (fw) wgrad_group_kernel<true, true><<<grid, 1024, 0, st>>>(gg, M, o);
+      else wgrad_group_kernel<true, false><<<grid, 1024, 0, st>>>(gg, M, o);
+    } else {
+      if (fw) wgrad_group_kernel<false, true><<<grid, 1024, 0, st>>>(gg, M, o);
+      else wgrad_group_kernel<false, false><<<grid, 1024, 0, st>>>(gg, M, o);
+    }
+    return hipGetLastError();
+  }
+  // variant 1: all-MFMA form (64-byte row segments per wave: measured slower, see above)
+  if (o.kind == 2) {
+    if (fw) wgrad_group_mfma_kernel<true, true><<<grid, 1024, 0, st>>>(gg, M, o);
+    else wgrad_group_mfma_kernel<true, false><<<grid, 1024, 0, st>>>(gg, M, o);
+  } else {
+    if (fw) wgrad_group_mfma_kernel<false, true><<<grid, 1024, 0, st>>>(gg, M, o);
+    else wgrad_group_mfma_kernel<false, false><<<grid, 1024, 0, st>>>(gg, M, o);
+  }
   return hipGetLastError();
 }
 

@@ -633,10 +633,11 @@ hipError_t linear_dgrad_partial(const float* dZ, int ldz, const float* W, int ld
   return hipGetLastError();
 }
 
-hipError_t linear_epilogue(const float* P, int ldp, float* Y, int ldy, int M, int N, Epi e, hipStream_t st) {
+hipError_t linear_epilogue(const float* P, int ldp, float* Y, int ldy, int M, int N, Epi e, int S, int64_t slab,
+                           hipStream_t st) {
   const int64_t tot = (int64_t)M * N;
   if (tot <= 0) return hipSuccess;
-  epilogue_kernel<<<(unsigned)((tot + 255) / 256), 256, 0, st>>>(P, ldp, Y, ldy, M, N, e);
+  epilogue_kernel<<<(unsigned)((tot + 255) / 256), 256, 0, st>>>(P, ldp, Y, ldy, M, N, e, S, slab);
   return hipGetLastError();
 }
 

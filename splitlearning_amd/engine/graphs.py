@@ -12,10 +12,15 @@ What varies between replays is handled without re-capture:
   seeds: kernels read them from small static device tables (`SlOpt.dyn`,
   `Epi.dseed`), refreshed per chunk by a device-to-device copy from per-epoch tables
   that the host fills once.
-Numerics are identical to the eager path (same step counts, same seeds).
+* the fc1 look-ahead (TailEngine.fused_step(x_next=...)): step i of the graph
+  pre-computes fc1's product for step i+1; the staging buffer holds G+1 batches so
+  the last step pre-computes the first batch of the next chunk, and `run` starts the
+  chain with an eager `lookahead_prologue`.
+Numerics are identical to the eager `SisaSession.server_epoch` loop (same step counts,
+seeds and kernel sequence).
 
-Requires a single-GPU tail (TP degree 1): a tensor-parallel step contains a
-collective and runs eagerly.
+A tensor-parallel tail is captured too when its all-reduce is the native
+(capturable) RCCL communicator (parallel/rccl.py).
 """
 from __future__ import annotations
 
@@ -36,7 +41,7 @@ class GraphedServerSteps:
         self.tail, self.slot, self.B, self.G = tail, slot, B, G
         dev = tail.device
         self.L = len(tail.layers)
-        self.x = torch.zeros(G * B, k_in, device=dev)
+        self.x = torch.zeros((G + 1) * B, k_in, device=dev)
         self.y = torch.zeros(G * B, dtype=torch.int64, device=dev)
         self.opt_tab = torch.zeros(G, 2, device=dev)
         self.seed_tab = torch.zeros(G, self.L, 2, dtype=torch.int32, device=dev)
@@ -47,8 +52,10 @@ class GraphedServerSteps:
         # scratch slabs must be allocated outside the capture (they are shared with eager calls)
         kmax = max(max(L.W.shape[1] for L in tail.layers), k_in)
         nmax = max(L.W.shape[0] for L in tail.layers)
-        for key, n in (("dgrad", kmax), ("fwd", nmax), ("fc2p", nmax), ("dz1p", kmax)):
+        for key, n in (("dgrad", kmax), ("fwd", nmax), ("fc2p", nmax), ("dz1p", kmax), ("head", nmax)):
             ops._workspace(dev, 16 * B * n, key)
+        if tail.lookahead_ok(B):
+            tail.lookahead_slabs(B)
         torch.cuda.synchronize(dev)
         fwd0 = tail.fwd_count
         self.graph = torch.cuda.CUDAGraph()
@@ -57,13 +64,17 @@ class GraphedServerSteps:
         with torch.cuda.stream(s):
             with torch.cuda.graph(self.graph, stream=s):
                 fused = tail.fused3_ok()
+                self.lookahead = fused and tail.lookahead_ok(B)
+                if self.lookahead:
+                    tail._pre = tail.lookahead_slabs(B)     # filled by run()'s prologue
                 for i in range(G):
                     xs = self.x[i * B:(i + 1) * B]
                     ys = self.y[i * B:(i + 1) * B]
                     dseeds = [self.seed_tab[i, l] for l in range(self.L)]
                     if fused:
-                        tail.train_fwd_bwd3(xs, ys, need_dx=False, dseeds=dseeds)
-                        tail.fused_step(slot, t=1, dyn=self.opt_tab[i])
+                        tail.train_fwd_bwd3(xs, ys, need_dx=False, dseeds=dseeds, pre=self.lookahead)
+                        xn = self.x[(i + 1) * B:(i + 2) * B] if self.lookahead else None
+                        tail.fused_step(slot, t=1, dyn=self.opt_tab[i], x_next=xn)
                     else:
                         out = tail.forward(xs, train=True, dseeds=dseeds)
                         _, d = ops.softmax_ce(out, ys, 1.0 / B)
@@ -71,7 +82,7 @@ class GraphedServerSteps:
                         tail.backward_step(slot, t=1, dyn=self.opt_tab[i])
         torch.cuda.current_stream(dev).wait_stream(s)
         tail.fwd_count = fwd0           # capture does not execute: restore the host counters
-        self._tabs = None
+        tail._pre = None
 
     def _epoch_tables(self, nsteps: int):
         """Per-step Adam scalars and dropout seeds for the next `nsteps` steps."""
@@ -88,17 +99,26 @@ class GraphedServerSteps:
         return (torch.from_numpy(opt.astype(np.float32)).to(dev),
                 torch.from_numpy(seeds.view(np.int32)).to(dev))
 
-    def run(self, acts: torch.Tensor, labels: torch.Tensor, nsteps: int):
-        """Run the first `nsteps` (a multiple of G) full batches of (acts, labels)."""
+    def run(self, acts: torch.Tensor, labels: torch.Tensor, nsteps: int) -> bool:
+        """Run the first `nsteps` (a multiple of G) full batches of (acts, labels).
+        Returns True when the look-ahead for the following full batch (rows
+        nsteps*B ... +B) is pending in the tail (pass `pre=True` to its step)."""
         G, B = self.G, self.B
-        assert nsteps % G == 0 and nsteps * B <= labels.numel()
+        n = labels.numel()
+        assert nsteps % G == 0 and nsteps * B <= n
         opt_all, seed_all = self._epoch_tables(nsteps)
+        if self.lookahead:
+            self.tail.lookahead_prologue(acts[:B])
         for c in range(nsteps // G):
             r0 = c * G * B
-            self.x.copy_(acts[r0:r0 + G * B])
+            r1 = min(n, r0 + (G + 1) * B)
+            self.x[:r1 - r0].copy_(acts[r0:r1])
             self.y.copy_(labels[r0:r0 + G * B])
             self.opt_tab.copy_(opt_all[c * G:(c + 1) * G])
             self.seed_tab.copy_(seed_all[c * G:(c + 1) * G])
             self.graph.replay()
         self.slot.t += nsteps
         self.tail.fwd_count += nsteps
+        pending = self.lookahead and nsteps * B + B <= n
+        self.tail._pre = self.tail.lookahead_slabs(B) if pending else None
+        return pending

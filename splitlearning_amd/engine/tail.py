@@ -84,6 +84,7 @@ class TailEngine:
         self.acts: list[torch.Tensor] = []
         self.dz: list[torch.Tensor] = []
         self._train_fwd = False
+        self._pre = None          # pending look-ahead fc1 partial slabs (see fused_step)
 
     # ------------------------------------------------------------------ forward
     def forward(self, x: torch.Tensor, train: bool | None = None, dseeds=None) -> torch.Tensor:
@@ -140,6 +141,7 @@ class TailEngine:
     def backward_step(self, slot: OptSlot, t: int | None = None, prefix: str = "", dyn=None):
         """Phase 2: fused wgrad + optimizer update of every layer (one optimizer step).
         `dyn` (graph replay only): device float[2] with Adam's {step_size, 1/sqrt(bc2)}."""
+        self._pre = None
         t = slot.tick() if t is None else t
         kw = {} if dyn is None else {"dyn": dyn}
         for i, L in enumerate(self.layers):
@@ -158,9 +160,27 @@ class TailEngine:
         return (s[0].relu and s[1].relu and not s[2].relu and s[2].dropout == 0
                 and self.layers[2].style == "rep" and s[1].out_features % 4 == 0)
 
-    def train_fwd_bwd3(self, x, labels, need_dx: bool, dseeds=None):
+    def lookahead_ok(self, m: int) -> bool:
+        """Whether `fused_step(x_next=...)` can pre-compute the next batch's fc1 product."""
+        return self.fused3_ok() and hasattr(self.ops, "lookahead_slabs") and 0 < m <= 16
+
+    def lookahead_slabs(self, m: int):
+        L1 = self.layers[0]
+        return self.ops.lookahead_slabs(self.device, L1.W.shape[1], m, L1.W.shape[0])
+
+    def lookahead_prologue(self, x0):
+        """Start a look-ahead chain: fc1's product for the first batch, in slab form."""
+        L1 = self.layers[0]
+        p = self.lookahead_slabs(x0.shape[0])
+        p.zero_()
+        p[0].copy_(self.ops.linear_fwd(x0, L1.W, None, False, 0.0, 0, 0))
+        self._pre = p
+
+    def train_fwd_bwd3(self, x, labels, need_dx: bool, dseeds=None, pre: bool = False):
         """Training forward + softmax-CE + all data gradients of the 3-layer tail.
-        Returns (per-row loss, dL/dx or None); `fused_step` then applies the optimizer."""
+        Returns (per-row loss, dL/dx or None); `fused_step` then applies the optimizer.
+        `pre`: fc1's product for `x` was already computed by the previous step's
+        `fused_step(x_next=x)` (or `lookahead_prologue(x)`); only its epilogue runs here."""
         ops = self.ops
         L1, L2, L3 = self.layers
         M = x.shape[0]
@@ -170,7 +190,14 @@ class TailEngine:
         def ds(i):
             return {} if dseeds is None else {"dseed": dseeds[i]}
         p1, p2 = L1.spec.dropout, L2.spec.dropout
-        h1 = ops.linear_fwd(x, L1.W, L1.b, True, p1, seeds[0], L1.col_off, **ds(0))
+        if pre:
+            P1 = self._pre
+            assert P1 is not None and P1.shape[1] == M, "no pending look-ahead for this batch"
+            self._pre = None
+            h1 = ops.linear_epilogue(P1, L1.b, True, p1, seeds[0], L1.col_off, **ds(0))
+        else:
+            self._pre = None
+            h1 = ops.linear_fwd(x, L1.W, L1.b, True, p1, seeds[0], L1.col_off, **ds(0))
         if L2.style == "row":
             P2 = ops.linear_fwd(h1, L2.W, None, False, 0.0, 0, 0)
             self.allreduce(P2)
@@ -191,13 +218,22 @@ class TailEngine:
         self._train_fwd = True
         return loss, dx
 
-    def fused_step(self, slot: OptSlot, t: int | None = None, dyn=None, prefix: str = ""):
+    def fused_step(self, slot: OptSlot, t: int | None = None, dyn=None, prefix: str = "", x_next=None):
+        """Optimizer step of all three layers in one launch.  `x_next`: the next batch's
+        input; while each fc1 weight tile is in registers after its update, the kernel also
+        forms that tile's share of x_next @ W1_new^T, so the next step reads W1 once instead
+        of twice (fc1's 108 MB forward read disappears; train_fwd_bwd3(pre=True) consumes)."""
         t = slot.tick() if t is None else t
         layers = []
         for (dz, dzp, hm, ms, A), L in zip(self._wg, self.layers):
             layers.append((dz, dzp, hm, ms, A, L.W, slot.state(f"{prefix}{L.spec.name}.weight", L.W), L.b,
                            slot.state(f"{prefix}{L.spec.name}.bias", L.b)))
-        self.ops.wgrad_group_(layers, self.acts[0].shape[0], slot.cfg, t, dyn)
+        pn = None
+        if x_next is not None:
+            assert self.lookahead_ok(x_next.shape[0])
+            pn = self.lookahead_slabs(x_next.shape[0])
+        self.ops.wgrad_group_(layers, self.acts[0].shape[0], slot.cfg, t, dyn, x_next=x_next, p_next=pn)
+        self._pre = pn
         self._wg = []
 
     # ------------------------------------------------------------------ state
@@ -224,6 +260,7 @@ class TailEngine:
         return sd
 
     def load_full_state_dict(self, sd: dict):
+        self._pre = None
         with torch.no_grad():
             for L in self.layers:
                 W = sd[f"{L.spec.name}.weight"]
@@ -241,6 +278,7 @@ class TailEngine:
         return torch.cat([t.reshape(-1) for L in self.layers for t in (L.W, L.b)])
 
     def load_flat_weights(self, flat: torch.Tensor):
+        self._pre = None
         o = 0
         for L in self.layers:
             for t in (L.W, L.b):
@@ -252,6 +290,7 @@ class TailEngine:
         return sum(t.numel() for L in self.layers for t in (L.W, L.b))
 
     def reset_parameters(self):
+        self._pre = None
         for L, mod in zip(self.layers, self.module.linears()):
             if self.tp_size == 1:
                 mod.reset_parameters()

@@ -112,8 +112,9 @@ def linear_fwd(x, w, b, relu: bool, drop_p: float, seed: int, col_offset: int = 
 
 
 def linear_epilogue(P, b, relu: bool, drop_p: float, seed: int, col_offset: int = 0, out=None, dseed=None):
+    """P: [M, N] pre-activations or [S, M, N] split-K partial slabs (reduced here)."""
     if out is None:
-        out = torch.empty_like(P)
+        out = torch.empty(P.shape[-2:], device=P.device, dtype=torch.float32)
     C().linear_epilogue(P, b.detach() if b is not None else None, out, relu, float(drop_p), seed & M64, col_offset,
                         _ptr(dseed))
     return out
@@ -194,21 +195,30 @@ def server_head3(P2, b2, relu2: bool, drop2: float, seed2: int, W3, b3, labels, 
     dz2 = torch.empty(M, N2, device=dev)
     dlog = torch.empty(M, W3.shape[0], device=dev)
     loss = torch.empty(M, device=dev)
+    ws = _workspace(dev, C().head3_slices(N2) * M * W3.shape[0], "head")
     C().server_head3(P2, b2.detach() if b2 is not None else None, relu2, float(drop2), seed2 & M64, _ptr(dseed),
                      W3.detach(), b3.detach() if b3 is not None else None, labels, int(ignore_index), float(scale),
-                     h2, dlog, dz2, loss)
+                     h2, dlog, dz2, loss, ws)
     return h2, dlog, dz2, loss
 
 
-def wgrad_group_(layers, M: int, cfg, t: int, dyn=None):
+def lookahead_slabs(device, K0: int, mn: int, N0: int):
+    """Workspace for wgrad_group_'s look-ahead forward: [ceil(K0/256), mn, N0]."""
+    S = (K0 + 255) // 256
+    return _workspace(device, S * mn * N0, "fc1n")[:S * mn * N0].view(S, mn, N0)
+
+
+def wgrad_group_(layers, M: int, cfg, t: int, dyn=None, x_next=None, p_next=None):
     """Fused wgrad+optimizer of up to 3 layers in one launch.  Each layer:
-    (dz, dzp, hmask, mscale, A, W, st_w, b, st_b) — exactly one of dz / dzp."""
+    (dz, dzp, hmask, mscale, A, W, st_w, b, st_b) — exactly one of dz / dzp.
+    With `x_next` (<= 16 rows), also writes layer 0's split-K partial pre-activations of
+    the next batch under the *updated* weights into `p_next` (see lookahead_slabs)."""
     tup = []
     for dz, dzp, hm, ms, A, W, st_w, b, st_b in layers:
         tup.append((dz, dzp, hm, float(ms), A, W.detach(), _s0(st_w), _s1(st_w),
                     b.detach() if b is not None else None, _s0(st_b) if b is not None else None,
                     _s1(st_b) if b is not None else None))
-    C().wgrad_group(tup, int(M), *_opt_args(cfg, t, dyn))
+    C().wgrad_group(tup, int(M), x_next, p_next, *_opt_args(cfg, t, dyn))
 
 
 # ---------------------------------------------------------------- loss / metrics

@@ -155,11 +155,12 @@ class SisaSession(Session):
             self._ck = set()
         return self._ck
 
-    def server_step(self, x, y):
-        """`zero_grad; CE(model(x), y).backward(); step` on Bob (data_entities_vanilla_sisa.py:305-313)."""
+    def server_step(self, x, y, pre: bool = False, x_next=None):
+        """`zero_grad; CE(model(x), y).backward(); step` on Bob (data_entities_vanilla_sisa.py:305-313).
+        `pre` / `x_next`: the fc1 look-ahead chain (TailEngine.fused_step)."""
         if self.tail.fused3_ok():
-            self.tail.train_fwd_bwd3(x, y, need_dx=False)
-            self.tail.fused_step(self.bob_slot)
+            self.tail.train_fwd_bwd3(x, y, need_dx=False, pre=pre)
+            self.tail.fused_step(self.bob_slot, x_next=x_next)
             return
         out = self.tail.forward(x, train=True)
         _, d = self.ops.softmax_ce(out, y, 1.0 / x.shape[0])
@@ -183,6 +184,8 @@ class SisaSession(Session):
         n, B = labels.numel(), self.B
         s = 0
         G = self.GRAPH_STEPS
+        la = self.tail.lookahead_ok(B)
+        pre = False
         if self._use_graphs() and n // B >= G:
             key = (B, G, acts.shape[1])
             gs = getattr(self, "_graphed", {}).get(key)
@@ -192,10 +195,16 @@ class SisaSession(Session):
                     self._graphed = {}
                 gs = self._graphed[key] = GraphedServerSteps(self.tail, self.bob_slot, B, G, acts.shape[1])
             ng = (n // B // G) * G
-            gs.run(acts, labels, ng)
+            pre = gs.run(acts, labels, ng)
             s = ng * B
+        elif la and n >= B:
+            self.tail.lookahead_prologue(acts[:B])
+            pre = True
         for s in range(s, n, B):
-            self.server_step(acts[s:s + B], labels[s:s + B])
+            # look ahead only to a full batch (the prologue / slabs are sized for B rows)
+            nxt = acts[s + B:s + 2 * B] if la and s + 2 * B <= n else None
+            self.server_step(acts[s:s + B], labels[s:s + B], pre=pre, x_next=nxt)
+            pre = nxt is not None
 
     def train_and_backward(self, unlearn_request_from_alices, unlearn_id):
         """Reference `bob.train_and_backward` (data_entities_vanilla_sisa.py:294-315)."""

@@ -214,3 +214,43 @@ def test_wgrad_v1_matches_v2(cuda):
     for other in outs[1:]:
         for p, q in zip(outs[0], other):
             _close(p, q, rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("variant", [0, 1])          # 0 = LDS-staged (default), 1 = all-MFMA
+@pytest.mark.parametrize("kind", ["sgd", "adam"])
+@pytest.mark.parametrize("M,shapes,mn", [(16, [(5000, 5408), (1000, 5000)], 16), (20, [(100, 1000), (33, 20)], 5),
+                                         (7, [(10, 100)], 0)])
+def test_wgrad_group(cuda, variant, kind, M, shapes, mn):
+    """Grouped wgrad+optimizer (+ layer-0 look-ahead forward) == per-layer fp32 reference."""
+    C = hip_ops.C()
+    cfg = OptimCfg("adam", 1e-3, weight_decay=1e-5) if kind == "adam" else OptimCfg("sgd", 1e-2, momentum=0.9)
+
+    def st(p):
+        return {"m": torch.randn_like(p) * 0.1, "v": torch.rand_like(p) * 0.1} if kind == "adam" else \
+            {"buf": torch.randn_like(p) * 0.1}
+    layers, refs = [], []
+    for N, K in shapes:
+        dz, a = torch.randn(M, N, device=cuda), torch.randn(M, K, device=cuda)
+        w, b = torch.randn(N, K, device=cuda), torch.randn(N, device=cuda)
+        sw, sb = st(w), st(b)
+        refs.append((dz, a, w.clone(), b.clone(), {k: v.clone() for k, v in sw.items()},
+                     {k: v.clone() for k, v in sb.items()}))
+        layers.append((dz, None, None, 1.0, a, w, sw, b, sb))
+    kw = {}
+    if mn:
+        xn = torch.randn(mn, shapes[0][1], device=cuda)
+        kw = {"x_next": xn, "p_next": hip_ops.lookahead_slabs(cuda, shapes[0][1], mn, shapes[0][0])}
+    try:
+        C.set_variant(3, variant)
+        hip_ops.wgrad_group_(layers, M, cfg, 4, **kw)
+    finally:
+        C.set_variant(3, 0)
+    for (dz, a, w2, b2, sw2, sb2), L in zip(refs, layers):
+        torch_ops.linear_wgrad_step_(dz, a, w2, b2, cfg, sw2, sb2, 4)
+        _close(L[5], w2, rtol=1e-4, atol=1e-5)
+        _close(L[7], b2, rtol=1e-4, atol=1e-5)
+        for k in sw2:
+            _close(L[6][k], sw2[k], rtol=1e-4, atol=1e-5)
+            _close(L[8][k], sb2[k], rtol=1e-4, atol=1e-5)
+    if mn:
+        _close(kw["p_next"].sum(0), kw["x_next"] @ layers[0][5].t(), rtol=1e-4, atol=2e-3)
