@@ -103,6 +103,22 @@ class Comm:
             return buf
         return None
 
+    def exchange(self, sends, recvs):
+        """One batched round of point-to-point transfers: `sends` = [(tensor, dst)],
+        `recvs` = [(buffer, src)] (this rank's side of every pair).  All transfers are
+        posted together (RCCL groups them), so distinct peers' xGMI links run
+        concurrently instead of one message after another."""
+        ops = [dist.P2POp(dist.isend, t.contiguous(), d) for t, d in sends if d != self.rank]
+        ops += [dist.P2POp(dist.irecv, b, s) for b, s in recvs if s != self.rank]
+        if not ops:
+            return
+        for r in dist.batch_isend_irecv(ops):
+            r.wait()
+        for t, d in sends:
+            if d != self.rank:
+                self.bytes_sent += t.numel() * t.element_size()
+                self.msgs_sent += 1
+
     def reduce_to_async(self, t: torch.Tensor | None, dst: int, srcs, shape=None, dtype=None):
         """Post the sum-to-`dst` of `t` over `srcs` (each src sends its partial, dst adds)
         and return a `finish()` callable giving the sum on dst (None elsewhere).  Work the

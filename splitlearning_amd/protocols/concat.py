@@ -80,6 +80,7 @@ class ConcatSession(SisaSession):
         self.bob_log.info("Global Training")
         self.switch_mode_to_train()
         samples = 0
+        self.prefetch_activations(unlearn_request_from_alices, unlearn_id)
         for _ in _progress(range(self.args.server_epochs), self.show, desc="Epochs", ascii=" >="):
             caches = []
             for cid in range(1, self.k + 1):

@@ -149,6 +149,52 @@ class SisaSession(Session):
             return acts, labels
         return None
 
+    def prefetch_activations(self, unlearn_request_from_alices=(), unlearn_id=None):
+        """Fill Bob's activation cache for every client in one batched transfer.
+
+        The reference pulls the dumps one client at a time (rpc_sync per client,
+        data_entities_vanilla_sisa.py:272-292, 299-302).  Here every host rank runs its
+        Alices' frozen fronts first, then all (client -> Bob rank) transfers are posted as
+        one batch of p2p ops, so N hosts stream into Bob's ranks over their own links at
+        once.  Collective; cache keys are identical to
+        `get_activation_and_labels`, which then hits."""
+        keys = []
+        for cid in range(1, self.k + 1):
+            unl = cid in unlearn_request_from_alices
+            key = (cid, unl, unlearn_id if unl else None)
+            if key not in self._cache_keys:
+                keys.append(key)
+        if not keys:
+            return
+        if not self.comm.distributed:
+            for cid, unl, uid in keys:
+                self.get_activation_and_labels(cid, unlearned=unl, unlearn_id=uid)
+            return
+        local = {}
+        counts = torch.zeros(self.k + 1, dtype=torch.int64, device=self.device)
+        for cid, unl, _ in keys:
+            if self.hosts(cid):
+                acts, labels = self.give_activation_and_labels(cid, unl)
+                local[cid] = self.pack(acts, labels)
+                counts[cid] = labels.numel()
+        self.comm.allreduce_sum_(counts)
+        counts = counts.tolist()
+        sends, recvs, got = [], [], {}
+        for cid, _, _ in keys:
+            n, h = counts[cid], self.host(cid)
+            if self.rank == h:
+                sends += [(local[cid], b) for b in self.bob_ranks if b != h]
+                got[cid] = local[cid]
+            elif self.is_bob:
+                got[cid] = torch.empty(n * CUT_FEATURES + n, device=self.device, dtype=torch.float32)
+                recvs.append((got[cid], h))
+        self.comm.exchange(sends, recvs)
+        for key in keys:
+            cid = key[0]
+            self._cache_keys.add(key)
+            if self.is_bob:
+                self.activation_and_labels_cache[key] = self.unpack(got[cid], counts[cid])
+
     @property
     def _cache_keys(self) -> set:
         if not hasattr(self, "_ck"):
@@ -211,6 +257,7 @@ class SisaSession(Session):
         self.bob_log.info("Global Training")
         self.switch_mode_to_train()
         samples = 0
+        self.prefetch_activations(unlearn_request_from_alices, unlearn_id)
         for _ in _progress(range(self.args.server_epochs), self.show, desc="Epochs", ascii=" >="):
             for cid in range(1, self.k + 1):
                 if cid in unlearn_request_from_alices:
