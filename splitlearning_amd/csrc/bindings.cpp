@@ -166,6 +166,37 @@ void conv_local_step(const at::Tensor& x, const at::Tensor& idx, const at::Tenso
         "conv_local_step");
 }
 
+// A whole SISA local epoch: ceil(n/B) client steps over `order` (the last one partial, like
+// DataLoader(drop_last=False)), launched from C++ back to back (2 kernels per step, the
+// optimizer step count advancing from t0) so the host never throttles the ~18 us steps.
+void conv_local_epoch(const at::Tensor& x, const at::Tensor& order, const at::Tensor& labels, int64_t B,
+                      at::Tensor& w, at::Tensor& b, at::Tensor& slab, at::Tensor& loss_rows, at::Tensor& s0w,
+                      const OptT& s1w, at::Tensor& s0b, const OptT& s1b, int64_t kind, double lr, double beta1,
+                      double beta2, double eps, double wd, double momentum, int64_t t0) {
+  check_x(x);
+  check_params(w, b);
+  need_cuda(order, "order");
+  TORCH_CHECK(order.scalar_type() == at::kLong && order.is_contiguous() && order.dim() == 1, "order int64 [n]");
+  const int64_t n = order.numel();
+  TORCH_CHECK(B >= 1 && B <= 4096, "batch size");
+  check_slab(slab, B);
+  need_cuda(labels, "labels");
+  TORCH_CHECK(labels.scalar_type() == at::kLong && labels.numel() == x.numel() / 784, "labels int64 [N]");
+  need_f32(loss_rows, "loss_rows");
+  TORCH_CHECK(loss_rows.is_contiguous() && loss_rows.numel() >= n, "loss_rows [n]");
+  TORCH_CHECK(s0w.numel() == 288 && s0b.numel() == 32, "optimizer state");
+  const hipStream_t st = cur_stream();
+  for (int64_t s = 0, t = t0; s < n; s += B, ++t) {
+    const int bs = (int)std::min<int64_t>(B, n - s);
+    check(sl::conv_local_step(x.data_ptr(), x.scalar_type() == at::kByte, order.data_ptr<int64_t>() + s,
+                              labels.data_ptr<int64_t>(), bs, w.data_ptr<float>(), b.data_ptr<float>(),
+                              slab.data_ptr<float>(), loss_rows.data_ptr<float>() + s, s0w.data_ptr<float>(),
+                              fptr(s1w), s0b.data_ptr<float>(), fptr(s1b),
+                              make_opt(kind, lr, beta1, beta2, eps, wd, momentum, t, 0), st),
+          "conv_local_epoch");
+  }
+}
+
 // Split-mode client backward: dW partials from the cut gradient, then reduce+optimizer.
 void conv_bwd_step(const at::Tensor& dy, const at::Tensor& y, const at::Tensor& am, const at::Tensor& x,
                    const at::Tensor& idx, int64_t B, at::Tensor& w, at::Tensor& b, at::Tensor& slab, at::Tensor& s0w,
@@ -467,6 +498,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_local_step", &conv_local_step);
   m.def("conv_bwd_step", &conv_bwd_step);
+  m.def("conv_local_epoch", &conv_local_epoch);
   m.def("linear_fwd", &linear_fwd);
   m.def("linear_epilogue", &linear_epilogue);
   m.def("linear_dgrad", &linear_dgrad);

@@ -61,6 +61,22 @@ class FrontEngine:
         return self.ops.conv_local_step_(shard.x, shard.y, idx, w, b, slot.cfg,
                                          slot.state("conv.weight", w), slot.state("conv.bias", b), t)
 
+    def local_epoch(self, shard: DeviceShard, order, B: int, slot: OptSlot):
+        """ceil(len(order)/B) consecutive `local_step`s (last batch partial) in one host call."""
+        if self.frozen:
+            raise RuntimeError("element 0 of tensors does not require grad and does not have a grad_fn "
+                               "(client front is frozen: call unfreeze_weights first)")
+        w, b = self.params
+        n = int(order.numel())
+        nsteps = -(-n // B)
+        if nsteps == 0:
+            return None
+        t0 = slot.t + 1
+        st_w, st_b = slot.state("conv.weight", w), slot.state("conv.bias", b)
+        loss = self.ops.conv_local_epoch_(shard.x, shard.y, order, B, w, b, slot.cfg, st_w, st_b, t0)
+        slot.t += nsteps
+        return loss
+
     def reset_parameters(self, true_reset: bool):
         """Reference `reset_model` (data_entities_vanilla.py:204-207): reset the direct
         children that have `reset_parameters`.  For model1_sisa that is nothing (Q4) unless

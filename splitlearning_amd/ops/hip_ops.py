@@ -90,6 +90,19 @@ def conv_local_step_(x_u8, y_all, idx, w, b, cfg, st_w, st_b, t, loss_rows=None,
     return loss_rows
 
 
+def conv_local_epoch_(x_u8, y_all, order, B: int, w, b, cfg, st_w, st_b, t0: int):
+    """ceil(n/B) SISA client steps over `order` in one host call (steps t0, t0+1, ...).
+    Returns the per-sample losses [n]."""
+    n = int(order.numel())
+    loss_rows = torch.empty(n, device=x_u8.device, dtype=torch.float32)
+    if n == 0:
+        return loss_rows
+    args = _opt_args(cfg, t0)
+    C().conv_local_epoch(x_u8, order, y_all, int(B), w.detach(), b.detach(), _slab(x_u8.device, B), loss_rows,
+                         _s0(st_w), _s1(st_w), _s0(st_b), _s1(st_b), *args[:7], int(t0))
+    return loss_rows
+
+
 # ---------------------------------------------------------------- linear
 # eval-time inference with many rows goes through hipBLASLt (plain library GEMM)
 # plus the fused epilogue kernel; the skinny kernels cover the training batch sizes.

@@ -147,6 +147,14 @@ def conv_local_step_(x_u8, y_all, idx, w, b, cfg, st_w, st_b, t, loss_rows=None)
     return loss
 
 
+def conv_local_epoch_(x_u8, y_all, order, B: int, w, b, cfg, st_w, st_b, t0: int):
+    """ceil(n/B) client steps over `order` (steps t0, t0+1, ...); per-sample losses [n]."""
+    out = []
+    for i, s in enumerate(range(0, order.numel(), B)):
+        out.append(conv_local_step_(x_u8, y_all, order[s:s + B], w, b, cfg, st_w, st_b, t0 + i))
+    return torch.cat(out) if out else torch.empty(0, device=x_u8.device)
+
+
 # ---------------------------------------------------------------- loss / metrics
 def softmax_ce(logits, labels, scale: float, ignore_index: int = -100):
     """Row-wise cross-entropy. Returns (per-row loss [M] (0 for ignored rows),

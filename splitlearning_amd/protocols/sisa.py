@@ -63,9 +63,7 @@ class SisaSession(Session):
         filtered, shuffle=False) order is given."""
         for _ in _progress(range(self.args.epochs), self.show, desc="Epochs", ascii=" >="):
             order = fixed_order if fixed_order is not None else a.train.shuffled_order(a.gen)
-            n = order.numel()
-            for s in range(0, n, self.B):
-                self.local_step(a, order[s:s + self.B])
+            a.front.local_epoch(a.train, order, self.B, a.slot)
 
     def train(self, cid: int):
         a = self.alices[cid]

@@ -254,3 +254,24 @@ def test_wgrad_group(cuda, variant, kind, M, shapes, mn):
             _close(L[8][k], sb2[k], rtol=1e-4, atol=1e-5)
     if mn:
         _close(kw["p_next"].sum(0), kw["x_next"] @ layers[0][5].t(), rtol=1e-4, atol=2e-3)
+
+
+@pytest.mark.parametrize("kind", ["sgd", "adam"])
+def test_conv_local_epoch_matches_steps(cuda, kind):
+    """The C++-looped epoch == the per-step calls (bitwise), incl. a partial last batch."""
+    x = _shard(300, cuda)
+    y_all = torch.randint(0, 10, (300,), device=cuda)
+    order = torch.randperm(300, device=cuda)[:109]
+    w, b = _conv_params(cuda)
+    cfg = OptimCfg("adam", 1e-3, weight_decay=1e-5) if kind == "adam" else OptimCfg("sgd", 1e-3, momentum=0.9)
+
+    def st(p):
+        return {"m": torch.zeros_like(p), "v": torch.zeros_like(p)} if kind == "adam" else \
+            {"buf": torch.zeros_like(p)}
+    w1, b1, w2, b2 = w.clone(), b.clone(), w.clone(), b.clone()
+    s = [st(w), st(b), st(w), st(b)]
+    l1 = hip_ops.conv_local_epoch_(x, y_all, order, 16, w1, b1, cfg, s[0], s[1], 3)
+    l2 = torch.cat([hip_ops.conv_local_step_(x, y_all, order[i:i + 16], w2, b2, cfg, s[2], s[3], 3 + j)
+                    for j, i in enumerate(range(0, 109, 16))])
+    torch.cuda.synchronize()
+    assert torch.equal(l1, l2) and torch.equal(w1, w2) and torch.equal(b1, b2)
