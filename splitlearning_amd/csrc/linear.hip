@@ -288,8 +288,18 @@ __global__ void epilogue_kernel(const float* __restrict__ P, int ldp, float* __r
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (int64_t)M * N) return;
   const int m = (int)(t / N), n = (int)(t - (int64_t)m * N);
-  float v = P[(int64_t)m * ldp + n];
-  for (int s = 1; s < S; ++s) v += P[s * slab + (int64_t)m * ldp + n];
+  const float* src = P + (int64_t)m * ldp + n;
+  float v = src[0];
+  // independent slab loads in flight together (the look-ahead hands over ~22 slabs)
+  int s = 1;
+  for (; s + 4 <= S; s += 4) {
+    const float a = src[s * slab], b = src[(s + 1) * slab], c = src[(s + 2) * slab], d = src[(s + 3) * slab];
+    v += a;
+    v += b;
+    v += c;
+    v += d;
+  }
+  for (; s < S; ++s) v += src[s * slab];
   Y[(int64_t)m * ldy + n] = apply_epi(e, v, m, n);
 }
 
