@@ -160,15 +160,6 @@ def main():
     cases.append(("fused:wgrad_fc1_plain_dz[mfma]", _v1(lambda: H.wgrad_group_(grp_plain, M, cfg, 3)), W1.numel() * 24))
     cases.append(("fused:wgrad_fc1_plain_dz_lookahead[mfma]",
                   _v1(lambda: H.wgrad_group_(grp_plain, M, cfg, 3, x_next=x, p_next=pn)), W1.numel() * 24))
-    def _nt(mask, fn):
-        def run():
-            C.set_variant(4, mask)
-            fn()
-            C.set_variant(4, 0)
-        return run
-    for mask in (0b011011, 0b001001, 0b010010, 0b100100, 0b111111, 0b110110):
-        cases.append((f"fused:wgrad_fc1_lookahead_nt{mask:06b}",
-                      _nt(mask, lambda: H.wgrad_group_(grp_plain, M, cfg, 3, x_next=x, p_next=pn)), W1.numel() * 24))
     cases.append(("v3:wgrad_fc1_same_tensors", lambda: H.linear_wgrad_step_(dz1r, x, L1.W, L1.b, cfg, wst[0], wst[1], 3),
                   W1.numel() * 24))
 

@@ -34,7 +34,6 @@ struct WgGroup {
   int ldxn;
   int mn;
   float* pn;            // [ceil(K0/256)][mn][N0]
-  int ntmask;           // cache-policy experiment: bit i = non-temporal {ld W, ld s0, ld s1, st W, st s0, st s1}
 };
 
 int head3_slices(int N2);

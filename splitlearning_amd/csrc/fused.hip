@@ -189,14 +189,10 @@ wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
   const f32x4 zv = {0.f, 0.f, 0.f, 0.f};
   const int64_t off = (int64_t)n * L.ldw + k;
   f32x4 p = zv, q0 = zv, q1 = zv;
-  const int nt = grp.ntmask;
   if (act) {
-    const f32x4* pw = reinterpret_cast<const f32x4*>(L.W + off);
-    const f32x4* p0 = reinterpret_cast<const f32x4*>(L.s0 + off);
-    const f32x4* p1 = reinterpret_cast<const f32x4*>(L.s1 + off);
-    p = (nt & 1) ? __builtin_nontemporal_load(pw) : *pw;
-    q0 = (nt & 2) ? __builtin_nontemporal_load(p0) : *p0;
-    if (ADAM) q1 = (nt & 4) ? __builtin_nontemporal_load(p1) : *p1;
+    p = *reinterpret_cast<const f32x4*>(L.W + off);
+    q0 = *reinterpret_cast<const f32x4*>(L.s0 + off);
+    if (ADAM) q1 = *reinterpret_cast<const f32x4*>(L.s1 + off);
   }
   // look-ahead A operand in MFMA layout: lane (li, lq) holds x_next[li][kb + 16*wave + 4*lq .. +3]
   const int li = lane & 15, lq = lane >> 4;
@@ -234,16 +230,9 @@ wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
   }
   if (act) {
     sl_opt_update4<ADAM>(o, p, g, q0, q1);
-    f32x4* pw = reinterpret_cast<f32x4*>(L.W + off);
-    f32x4* p0 = reinterpret_cast<f32x4*>(L.s0 + off);
-    f32x4* p1 = reinterpret_cast<f32x4*>(L.s1 + off);
-    if (o.kind != 0) {
-      if (nt & 8) __builtin_nontemporal_store(p, pw); else *pw = p;
-    }
-    if (nt & 16) __builtin_nontemporal_store(q0, p0); else *p0 = q0;
-    if (ADAM) {
-      if (nt & 32) __builtin_nontemporal_store(q1, p1); else *p1 = q1;
-    }
+    if (o.kind != 0) *reinterpret_cast<f32x4*>(L.W + off) = p;
+    *reinterpret_cast<f32x4*>(L.s0 + off) = q0;
+    if (ADAM) *reinterpret_cast<f32x4*>(L.s1 + off) = q1;
   }
   if (FWDN && l0) {
     // next batch's partial pre-activations with the updated tile: stage W_new through LDS
@@ -398,7 +387,6 @@ hipError_t wgrad_group(const WgGroup& g, int M, SlOpt o, hipStream_t st) {
   if (yb == 0 || kmax == 0) return hipSuccess;
   dim3 grid((kmax + 255) / 256, yb);
   if (gg.xn && (gg.mn <= 0 || gg.mn > 16 || !gg.pn)) return hipErrorInvalidValue;
-  gg.ntmask = g_variant[4];
   const bool fw = gg.xn != nullptr;
   if (g_variant[3] != 1) {   // default: LDS-staged VALU dW (row-contiguous W streams)
     if (o.kind == 2) {
