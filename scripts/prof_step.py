@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--path", default="fused")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--tp", type=int, default=1, help="simulate a TP shard (rank 0 of tp, 1-rank all-reduce)")
+    ap.add_argument("--time", action="store_true", help="print wall-clock us/step (second half of the run)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     ops.set_backend("hip")
@@ -53,12 +54,27 @@ def main():
     elif a.path == "graph":
         from splitlearning_amd.engine.graphs import GraphedServerSteps
         gs = GraphedServerSteps(tail, slot, 16, 16, 5408)
-        for _ in range(a.steps // 16):
-            gs.run(acts, labels, 16)
+        # one run() per epoch of n // 16 steps, like SisaSession.server_epoch
+        per = n // 16
+        reps = max(1, a.steps // per)
+        import time
+        for i in range(reps):
+            if i == reps // 2:
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+            gs.run(acts, labels, per)
+        torch.cuda.synchronize()
+        if a.time:
+            dt = time.perf_counter() - t0
+            print(f"path=graph tp={a.tp} us_per_step={dt / ((reps - reps // 2) * per) * 1e6:.2f}")
     else:
         if a.path == "lookahead":
             tail.lookahead_prologue(acts[:16])
+        import time
         for i in range(a.steps):
+            if i == a.steps // 2:
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
             s = (i * 16) % n
             x, y = acts[s:s + 16], labels[s:s + 16]
             if a.path == "lookahead":
@@ -73,6 +89,10 @@ def main():
                 _, d = H.softmax_ce(out, y, 1 / 16)
                 tail.backward_dgrad(d, need_dx=False)
                 tail.backward_step(slot)
+        torch.cuda.synchronize()
+        if a.time:
+            dt = time.perf_counter() - t0
+            print(f"path={a.path} tp={a.tp} us_per_step={dt / (a.steps - a.steps // 2) * 1e6:.2f}")
     torch.cuda.synchronize()
 
 

@@ -87,7 +87,8 @@ def build_parser() -> argparse.ArgumentParser:
                    help="bounded wait for every collective / control message")
     g.add_argument("--no_tqdm", action="store_true")
     g.add_argument("--graphs", choices=("auto", "on", "off"), default="auto",
-                   help="capture Bob's fixed-shape server step in a HIP graph")
+                   help="capture Bob's fixed-shape server steps in HIP graphs (auto: single-GPU "
+                        "tail only; on: also a tensor-parallel tail, all-reduce inside the graph)")
     return p
 
 

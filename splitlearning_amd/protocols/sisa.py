@@ -217,8 +217,12 @@ class SisaSession(Session):
         mode = getattr(self.args, "graphs", "auto")
         if mode == "off" or self.device.type != "cuda":
             return False
-        if self.tail.tp_size != 1 and not getattr(self.tail.allreduce, "capturable", False):
-            return False
+        if self.tail.tp_size != 1:
+            # A TP shard step is GPU-bound even eagerly (measured 58 us eager vs 59 us
+            # replayed at TP=8, docs/PERF.md), so "auto" keeps the collective out of the
+            # graph; "on" captures it when the all-reduce is the native RCCL communicator.
+            if mode != "on" or not getattr(self.tail.allreduce, "capturable", False):
+                return False
         from .. import ops as _ops
         return _ops.get_backend() != "torch"
 
