@@ -64,69 +64,9 @@ conv_relu_pool_fwd_kernel(const XT* __restrict__ x, const int64_t* __restrict__ 
   }
 }
 
-// One workgroup per output channel: reduce dW[oc,0:9], db[oc] over the batch, then
-// apply the optimizer to this channel's 10 parameters (no cross-block dependency).
-template <typename XT>
-__global__ void __launch_bounds__(256)
-conv_bwd_opt_kernel(const float* __restrict__ dy, const float* __restrict__ y,
-                    const uint8_t* __restrict__ am, const XT* __restrict__ x,
-                    const int64_t* __restrict__ idx, int64_t row0, int B,
-                    float* __restrict__ w, float* __restrict__ b,
-                    float* __restrict__ s0w, float* __restrict__ s1w,
-                    float* __restrict__ s0b, float* __restrict__ s1b, SlOpt o) {
-  const int oc = blockIdx.x;
-  const int tid = threadIdx.x;
-  float acc[10];
-#pragma unroll
-  for (int j = 0; j < 10; ++j) acc[j] = 0.f;
-  const int total = B * 169;
-  for (int t = tid; t < total; t += 256) {
-    const int s = t / 169;
-    const int r = t - s * 169;
-    const int64_t off = (int64_t)s * 5408 + oc * 169 + r;
-    if (y[off] <= 0.f) continue;
-    const float g = dy[off];
-    const int a = am[off];
-    const int ph = r / 13, pw = r - (r / 13) * 13;
-    const int row = 2 * ph + (a >> 1), col = 2 * pw + (a & 1);
-    const int64_t src = idx ? idx[s] : row0 + s;
-    const XT* xr = x + src * 784 + row * 28 + col;
-#pragma unroll
-    for (int kh = 0; kh < 3; ++kh)
-#pragma unroll
-      for (int kw = 0; kw < 3; ++kw) acc[kh * 3 + kw] = fmaf(g, (float)xr[kh * 28 + kw], acc[kh * 3 + kw]);
-    acc[9] += g;
-  }
-  __shared__ float red[4][10];
-  const int lane = tid & 63, wv = tid >> 6;
-#pragma unroll
-  for (int j = 0; j < 10; ++j) {
-    float v = sl_wave_sum(acc[j]);
-    if (lane == 0) red[wv][j] = v;
-  }
-  __syncthreads();
-  if (tid < 10) {
-    const float g = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
-    if (tid < 9) {
-      const int k = oc * 9 + tid;
-      float p = w[k], a0 = s0w[k], a1 = s1w ? s1w[k] : 0.f;
-      sl_opt_update(o, p, g, a0, a1);
-      if (o.kind != 0) w[k] = p;
-      s0w[k] = a0;
-      if (s1w) s1w[k] = a1;
-    } else {
-      float p = b[oc], a0 = s0b[oc], a1 = s1b ? s1b[oc] : 0.f;
-      sl_opt_update(o, p, g, a0, a1);
-      if (o.kind != 0) b[oc] = p;
-      s0b[oc] = a0;
-      if (s1b) s1b[oc] = a1;
-    }
-  }
-}
-
 // ---------------------------------------------------------------------------------------
-// Two-stage backward used by the training loops (replaces conv_bwd_opt_kernel's 32-block
-// reduction over the whole batch):
+// Two-stage backward + optimizer (a first single-kernel version, 32 workgroups each reducing
+// one channel over the whole batch, left most of the GPU idle):
 //   stage 1, one workgroup per sample: thread t owns output channel t>>3 and every 8th
 //   pooled position of it, so its dW/db contributions all go to ONE channel and are
 //   reduced by three xor-shuffles inside 8-lane groups -> slab[s][oc*10 + j];
@@ -340,19 +280,6 @@ hipError_t conv_fwd(const void* x, bool x_u8, const int64_t* idx, int64_t row0, 
     conv_relu_pool_fwd_kernel<uint8_t><<<B, 256, 0, st>>>((const uint8_t*)x, idx, row0, w, b, y, am);
   else
     conv_relu_pool_fwd_kernel<float><<<B, 256, 0, st>>>((const float*)x, idx, row0, w, b, y, am);
-  return hipGetLastError();
-}
-
-hipError_t conv_bwd_opt(const float* dy, const float* y, const uint8_t* am, const void* x, bool x_u8,
-                        const int64_t* idx, int64_t row0, int B, float* w, float* b, float* s0w,
-                        float* s1w, float* s0b, float* s1b, SlOpt o, hipStream_t st) {
-  if (B <= 0) return hipSuccess;
-  if (x_u8)
-    conv_bwd_opt_kernel<uint8_t><<<32, 256, 0, st>>>(dy, y, am, (const uint8_t*)x, idx, row0, B, w, b,
-                                                     s0w, s1w, s0b, s1b, o);
-  else
-    conv_bwd_opt_kernel<float><<<32, 256, 0, st>>>(dy, y, am, (const float*)x, idx, row0, B, w, b,
-                                                   s0w, s1w, s0b, s1b, o);
   return hipGetLastError();
 }
 

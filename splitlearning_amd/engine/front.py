@@ -1,8 +1,11 @@
 """Client-front executor (Alice's conv stack) over the fused conv kernels.
 
 Forward = one kernel (`conv_fwd`: gather uint8 rows by index, conv3x3, bias,
-ReLU, maxpool, flatten); backward+step = one kernel (`conv_bwd_opt`: pool/ReLU
-backward, dW/db reduction, SGD-m or Adam update in place).  Parameters are the
+ReLU, maxpool, flatten); backward+step = two (`conv_bwd_step`: per-sample pool/ReLU
+backward + dW/db partials, then one reduce + SGD-m / Adam update in place).  The SISA
+client step is forward + 5408-way CE + partials in one kernel plus the reduce/update
+(`conv_local_step`), and a whole local epoch is one host call (`local_epoch`).
+Reference: models.py:16-30 (model1_sisa), data_entities_vanilla_sisa.py:55-70.  Parameters are the
 `nn.Module`'s own tensors, so `state_dict()` keeps the reference key names
 (`conv_layers.0.*` for model1_sisa, `conv1.*` for model1).
 """
