@@ -160,6 +160,9 @@ def main():
     cases.append(("fused:wgrad_fc1_plain_dz[mfma]", _v1(lambda: H.wgrad_group_(grp_plain, M, cfg, 3)), W1.numel() * 24))
     cases.append(("fused:wgrad_fc1_plain_dz_lookahead[mfma]",
                   _v1(lambda: H.wgrad_group_(grp_plain, M, cfg, 3, x_next=x, p_next=pn)), W1.numel() * 24))
+    grp3_plain = [grp_plain[0], grp[1], grp[2]]
+    cases.append(("fused:wgrad_group3_plain_lookahead",
+                  lambda: H.wgrad_group_(grp3_plain, M, cfg, 3, x_next=x, p_next=pn), 32_146_100 * 24))
     cases.append(("v3:wgrad_fc1_same_tensors", lambda: H.linear_wgrad_step_(dz1r, x, L1.W, L1.b, cfg, wst[0], wst[1], 3),
                   W1.numel() * 24))
 

@@ -19,6 +19,8 @@
 //                reduce kernel).
 #include "fused.h"
 
+#include <algorithm>
+
 namespace sl {
 
 // Column slices of <= 32 float4 (128 columns) per workgroup; grid (M, Q) for both kernels.
@@ -167,7 +169,7 @@ head_bwd_kernel(const float* __restrict__ plog, const float* __restrict__ b3, co
   }
 }
 
-template <bool ADAM, bool FWDN>
+template <bool ADAM, bool FWDN, bool PART>
 __global__ void __launch_bounds__(1024)
 wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
   __shared__ f32x4 sa[16][64];
@@ -210,7 +212,7 @@ wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
         const int mr = mc + (tid >> 4), nn = n0 + (tid & 15);
         float v = 0.f;
         if (mr < M && nn < L.N) {
-          if (L.dzp) {
+          if (PART && L.dzp) {
             for (int s = 0; s < L.S; ++s) v += L.dzp[s * L.slab + (int64_t)mr * L.N + nn];
             if (L.hmask) v = L.hmask[(int64_t)mr * L.N + nn] > 0.f ? v * L.mscale : 0.f;
           } else {
@@ -388,14 +390,18 @@ hipError_t wgrad_group(const WgGroup& g, int M, SlOpt o, hipStream_t st) {
   dim3 grid((kmax + 255) / 256, yb);
   if (gg.xn && (gg.mn <= 0 || gg.mn > 16 || !gg.pn)) return hipErrorInvalidValue;
   const bool fw = gg.xn != nullptr;
+  bool part = false;
+  for (int i = 0; i < gg.n; ++i) part = part || gg.d[i].dzp != nullptr;
   if (g_variant[3] != 1) {   // default: LDS-staged VALU dW (row-contiguous W streams)
-    if (o.kind == 2) {
-      if (fw) wgrad_group_kernel<true, true><<<grid, 1024, 0, st>>>(gg, M, o);
-      else wgrad_group_kernel<true, false><<<grid, 1024, 0, st>>>(gg, M, o);
+#define SL_WG(A, F, P) wgrad_group_kernel<A, F, P><<<grid, 1024, 0, st>>>(gg, M, o)
+    if (part) {
+      if (o.kind == 2) { if (fw) SL_WG(true, true, true); else SL_WG(true, false, true); }
+      else { if (fw) SL_WG(false, true, true); else SL_WG(false, false, true); }
     } else {
-      if (fw) wgrad_group_kernel<false, true><<<grid, 1024, 0, st>>>(gg, M, o);
-      else wgrad_group_kernel<false, false><<<grid, 1024, 0, st>>>(gg, M, o);
+      if (o.kind == 2) { if (fw) SL_WG(true, true, false); else SL_WG(true, false, false); }
+      else { if (fw) SL_WG(false, true, false); else SL_WG(false, false, false); }
     }
+#undef SL_WG
     return hipGetLastError();
   }
   // variant 1: all-MFMA form (64-byte row segments per wave: measured slower, see above)
