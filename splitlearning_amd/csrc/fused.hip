@@ -44,6 +44,20 @@ head_fwd_kernel(const float* __restrict__ P2, int S2, int64_t slab2, Epi e2, con
   int qa, qb;
   head_slice(N2 >> 2, Q, q, qa, qb);
   const int ncol = qb - qa;
+  const int lane = tid & 63, wv = tid >> 6, half = lane >> 5, c = lane & 31;
+  constexpr int JU = 13;
+  // W3 loads of the first output group do not depend on anything: issue them first so
+  // they overlap the slab reduction (one memory round trip for the whole kernel at C <= 104)
+  f32x4 w[JU];
+  auto load_w = [&](int j0) {
+#pragma unroll
+    for (int j = 0; j < JU; ++j) {
+      const int o = 8 * (j0 + j) + 2 * wv + half;
+      w[j] = (o < C && c < ncol) ? *reinterpret_cast<const f32x4*>(W3 + (int64_t)o * ldw3 + 4 * (qa + c))
+                                 : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  load_w(0);
   // 1. slab reduction: 32 columns x 8 slab groups
   {
     const int c = tid & (HS - 1), sg = tid >> 5;
@@ -72,17 +86,9 @@ head_fwd_kernel(const float* __restrict__ P2, int S2, int64_t slab2, Epi e2, con
   __syncthreads();
   // 2. partial logits: half-waves (32 lanes = the slice's columns) per output, 8 outputs
   //    per wave instruction group; JU outputs' loads in flight per lane
-  const int lane = tid & 63, wv = tid >> 6, half = lane >> 5, c = lane & 31;
   const f32x4 h = hs[c];
-  constexpr int JU = 13;
   for (int j0 = 0; j0 * 8 < C; j0 += JU) {
-    f32x4 w[JU];
-#pragma unroll
-    for (int j = 0; j < JU; ++j) {
-      const int o = 8 * (j0 + j) + 2 * wv + half;
-      w[j] = (o < C && c < ncol) ? *reinterpret_cast<const f32x4*>(W3 + (int64_t)o * ldw3 + 4 * (qa + c))
-                                 : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
+    if (j0) load_w(j0);
 #pragma unroll
     for (int j = 0; j < JU; ++j) {
       const int o = 8 * (j0 + j) + 2 * wv + half;
@@ -105,8 +111,27 @@ head_bwd_kernel(const float* __restrict__ plog, const float* __restrict__ b3, co
   __shared__ f32x4 part[8][HS];
   const int m = blockIdx.x, q = blockIdx.y, Q = gridDim.y, tid = threadIdx.x;
   const int lane = tid & 63, wv = tid >> 6;
+  int qa, qb;
+  head_slice(N2 >> 2, Q, q, qa, qb);
+  const int ncol = qb - qa;
+  const int c = tid & (HS - 1), g = tid >> 5;
+  constexpr int JU = 13;
+  // independent loads first: this slice's W3 columns (first output group) and h2 mask
+  f32x4 w[JU];
+  auto load_w = [&](int j0) {
+#pragma unroll
+    for (int j = 0; j < JU; ++j) {
+      const int o = 8 * (j0 + j) + g;
+      w[j] = (o < C && c < ncol) ? *reinterpret_cast<const f32x4*>(W3 + (int64_t)o * ldw3 + 4 * (qa + c))
+                                 : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  load_w(0);
+  f32x4 hh = {0.f, 0.f, 0.f, 0.f};
+  if (tid < ncol) hh = reinterpret_cast<const f32x4*>(h2 + (int64_t)m * N2)[qa + tid];
   for (int o = tid; o < C; o += 256) {
     float v = b3 ? b3[o] : 0.f;
+#pragma unroll 8
     for (int s = 0; s < Q; ++s) v += plog[((int64_t)s * M + m) * C + o];
     lg[o] = v;
   }
@@ -134,21 +159,10 @@ head_bwd_kernel(const float* __restrict__ plog, const float* __restrict__ b3, co
   }
   __syncthreads();
   if (q == 0)
-    for (int c = tid; c < C; c += 256) dlog[(int64_t)m * C + c] = lg[c];
-  int qa, qb;
-  head_slice(N2 >> 2, Q, q, qa, qb);
-  const int ncol = qb - qa;
-  const int c = tid & (HS - 1), g = tid >> 5;
+    for (int cc = tid; cc < C; cc += 256) dlog[(int64_t)m * C + cc] = lg[cc];
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  constexpr int JU = 13;
   for (int j0 = 0; j0 * 8 < C; j0 += JU) {
-    f32x4 w[JU];
-#pragma unroll
-    for (int j = 0; j < JU; ++j) {
-      const int o = 8 * (j0 + j) + g;
-      w[j] = (o < C && c < ncol) ? *reinterpret_cast<const f32x4*>(W3 + (int64_t)o * ldw3 + 4 * (qa + c))
-                                 : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
+    if (j0) load_w(j0);
 #pragma unroll
     for (int j = 0; j < JU; ++j) {
       const int o = 8 * (j0 + j) + g;
@@ -161,7 +175,6 @@ head_bwd_kernel(const float* __restrict__ plog, const float* __restrict__ b3, co
     f32x4 v = part[0][tid];
 #pragma unroll
     for (int gg = 1; gg < 8; ++gg) v += part[gg][tid];
-    const f32x4 hh = reinterpret_cast<const f32x4*>(h2 + (int64_t)m * N2)[qa + tid];
     f32x4 out;
 #pragma unroll
     for (int i = 0; i < 4; ++i) out[i] = hh[i] > 0.f ? v[i] * dscale : 0.f;

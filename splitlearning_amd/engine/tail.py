@@ -199,7 +199,12 @@ class TailEngine:
             self._pre = None
             h1 = ops.linear_fwd(x, L1.W, L1.b, True, p1, seeds[0], L1.col_off, **ds(0))
         if L2.style == "row":
-            P2 = ops.linear_fwd(h1, L2.W, None, False, 0.0, 0, 0)
+            if L2.W.shape[1] <= 1280:
+                # small K shard (TP >= 4): one unsplit product, all-reduced as is — no
+                # split-K reduce launch before the collective
+                P2 = ops.linear_fwd_partial(h1, L2.W, max_split=1)
+            else:
+                P2 = ops.linear_fwd(h1, L2.W, None, False, 0.0, 0, 0)
             self.allreduce(P2)
         else:
             P2 = ops.linear_fwd_partial(h1, L2.W)

@@ -95,17 +95,30 @@ def test_graphed_tp_tail_with_native_allreduce(cuda):
         assert torch.equal(L1.W, L2.W) and torch.equal(L1.b, L2.b)
 
 
+@pytest.mark.parametrize("tp", [1, 8])
 @pytest.mark.parametrize("need_dx", [False, True])
 @pytest.mark.parametrize("kind", ["adam", "sgd"])
-def test_fused_server_step_matches_generic(cuda, need_dx, kind):
+def test_fused_server_step_matches_generic(cuda, need_dx, kind, tp):
+    """Fused 3-layer step == the generic per-layer step; tp=8 runs rank 0's shard of a
+    tensor-parallel tail (1-rank all-reduce): the row-parallel fc2 takes its unsplit path."""
     from splitlearning_amd.engine import sgd_momentum
     g = torch.Generator().manual_seed(2)
     B, steps = 16, 4
     acts = (torch.rand(B * steps, 5408, generator=g) * 30).to(cuda)
     labels = torch.randint(0, 10, (B * steps,), generator=g).to(cuda)
     mk_slot = (lambda: OptSlot(adam(1e-3, 1e-5))) if kind == "adam" else (lambda: OptSlot(sgd_momentum(1e-2)))
-    ta, sa = _tail(cuda), mk_slot()
-    tb, sb = _tail(cuda), mk_slot()
+    if tp == 1:
+        mk = lambda: _tail(cuda)  # noqa: E731
+    else:
+        from splitlearning_amd.parallel.rccl import native_allreduce, self_comm
+        ar = native_allreduce(self_comm())
+
+        def mk():
+            torch.manual_seed(0)
+            return TailEngine(ServerTailSisa(), sisa_server_spec(), cuda, tp_rank=0, tp_size=tp, allreduce=ar,
+                              seed_base=42)
+    ta, sa = mk(), mk_slot()
+    tb, sb = mk(), mk_slot()
     assert tb.fused3_ok()
     for s in range(0, B * steps, B):
         x, y = acts[s:s + B], labels[s:s + B]
