@@ -25,7 +25,11 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--tp", type=int, default=1, help="simulate a TP shard (rank 0 of tp, 1-rank all-reduce)")
     ap.add_argument("--time", action="store_true", help="print wall-clock us/step (second half of the run)")
+    ap.add_argument("--variant", action="append", default=[], help="slot=value kernel variant (A/B)")
     a = ap.parse_args()
+    for kv in a.variant:
+        slot, val = (int(v) for v in kv.split("="))
+        H.C().set_variant(slot, val)
     dev = torch.device("cuda", 0)
     ops.set_backend("hip")
     torch.manual_seed(0)

@@ -580,7 +580,9 @@ hipError_t linear_dgrad(const float* dZ, int ldz, const float* W, int ldw, const
   const int kt = (K + 63) / 64, mt = (M + 15) / 16;
   int S = 1;
   // aim for >= ~256 workgroups on the 256-CU part; split N when there are few K tiles
-  while (S < 16 && kt * mt * S < 768 && N / (S * 2) >= 64) S *= 2;
+  // (variant 5 = max split, for A/B: 1 = never split)
+  const int smax = g_variant[5] > 0 ? g_variant[5] : 16;
+  while (S < smax && kt * mt * S < 768 && N / (S * 2) >= 64) S *= 2;
   const int64_t slab = (int64_t)M * K;
   if (S > 1 && (ws == nullptr || ws_elems < slab * S)) S = 1;
   dim3 grid(kt, mt, S);
