@@ -104,6 +104,17 @@ def main():
     cases.append(("conv_fwd", lambda: H.conv_front_fwd(shard, idx, cw, cb), 0))
     cases.append(("conv_local_step(2 kernels)", lambda: H.conv_local_step_(shard, ylab, idx, cw, cb, cfg, scw,
                                                                             scb, 2), 0))
+    n_ep = min(2048, shard.shape[0] // 16 * 16)
+    order = torch.randperm(shard.shape[0], device=dev)[:n_ep]
+
+    def _epoch(v):
+        def run():
+            C.set_variant(6, v)
+            H.conv_local_epoch_(shard, ylab, order, 16, cw, cb, cfg, scw, scb, 2)
+            C.set_variant(6, 0)
+        return run
+    cases.append((f"conv_local_epoch[{n_ep // 16} steps, fused opt]", _epoch(0), 0))
+    cases.append((f"conv_local_epoch[{n_ep // 16} steps, 2 launches, 8 lanes/ch]", _epoch(1), 0))
     y, am = H.conv_front_fwd(shard, idx, cw, cb)
     dy = torch.randn(M, 5408, device=dev)
     cases.append(("conv_bwd_step(2 kernels)", lambda: H.conv_front_bwd_step_(dy, y, am, shard, idx, cw, cb, cfg,

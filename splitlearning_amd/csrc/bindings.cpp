@@ -23,6 +23,10 @@ hipError_t conv_fwd(const void* x, bool x_u8, const int64_t* idx, int64_t row0, 
 hipError_t conv_local_step(const void* x, bool x_u8, const int64_t* idx, const int64_t* labels, int B, float* w,
                            float* b, float* slab, float* loss_rows, float* s0w, float* s1w, float* s0b, float* s1b,
                            SlOpt o, hipStream_t st);
+hipError_t conv_local_epoch(const void* x, bool x_u8, const int64_t* order, int64_t n, int B, const int64_t* labels,
+                            float* w, float* b, float* s0w, float* s1w, float* s0b, float* s1b, float* ws,
+                            int64_t ws_elems, float* loss_rows, SlOpt (*opt)(void*, int64_t), void* optctx,
+                            int64_t t0, hipStream_t st);
 hipError_t conv_bwd_step(const float* dy, const float* y, const uint8_t* am, const void* x, bool x_u8,
                          const int64_t* idx, int B, float* w, float* b, float* slab, float* s0w, float* s1w,
                          float* s0b, float* s1b, SlOpt o, hipStream_t st);
@@ -166,13 +170,23 @@ void conv_local_step(const at::Tensor& x, const at::Tensor& idx, const at::Tenso
         "conv_local_step");
 }
 
+struct EpochOpt {
+  int64_t kind;
+  double lr, beta1, beta2, eps, wd, momentum;
+};
+SlOpt epoch_opt(void* ctx, int64_t t) {
+  const EpochOpt& e = *static_cast<const EpochOpt*>(ctx);
+  return make_opt(e.kind, e.lr, e.beta1, e.beta2, e.eps, e.wd, e.momentum, t, 0);
+}
+
 // A whole SISA local epoch: ceil(n/B) client steps over `order` (the last one partial, like
-// DataLoader(drop_last=False)), launched from C++ back to back (2 kernels per step, the
-// optimizer step count advancing from t0) so the host never throttles the ~18 us steps.
+// DataLoader(drop_last=False)), optimizer steps t0, t0+1, ...  One launch per step: each
+// step's kernel applies the previous step's optimizer update in its prologue
+// (conv.hip: conv_local_epoch); variant 6 = 1 runs the two-launch step instead (A/B).
 void conv_local_epoch(const at::Tensor& x, const at::Tensor& order, const at::Tensor& labels, int64_t B,
                       at::Tensor& w, at::Tensor& b, at::Tensor& slab, at::Tensor& loss_rows, at::Tensor& s0w,
                       const OptT& s1w, at::Tensor& s0b, const OptT& s1b, int64_t kind, double lr, double beta1,
-                      double beta2, double eps, double wd, double momentum, int64_t t0) {
+                      double beta2, double eps, double wd, double momentum, int64_t t0, at::Tensor& ws) {
   check_x(x);
   check_params(w, b);
   need_cuda(order, "order");
@@ -185,16 +199,28 @@ void conv_local_epoch(const at::Tensor& x, const at::Tensor& order, const at::Te
   need_f32(loss_rows, "loss_rows");
   TORCH_CHECK(loss_rows.is_contiguous() && loss_rows.numel() >= n, "loss_rows [n]");
   TORCH_CHECK(s0w.numel() == 288 && s0b.numel() == 32, "optimizer state");
+  need_f32(ws, "ws");
+  TORCH_CHECK(ws.is_contiguous(), "ws contiguous");
+  TORCH_CHECK(kind == 1 || kind == 2, "local epoch: SGD-momentum or Adam");
   const hipStream_t st = cur_stream();
-  for (int64_t s = 0, t = t0; s < n; s += B, ++t) {
-    const int bs = (int)std::min<int64_t>(B, n - s);
-    check(sl::conv_local_step(x.data_ptr(), x.scalar_type() == at::kByte, order.data_ptr<int64_t>() + s,
-                              labels.data_ptr<int64_t>(), bs, w.data_ptr<float>(), b.data_ptr<float>(),
-                              slab.data_ptr<float>(), loss_rows.data_ptr<float>() + s, s0w.data_ptr<float>(),
-                              fptr(s1w), s0b.data_ptr<float>(), fptr(s1b),
-                              make_opt(kind, lr, beta1, beta2, eps, wd, momentum, t, 0), st),
-          "conv_local_epoch");
+  if (sl::g_variant[6] == 1) {
+    for (int64_t s = 0, t = t0; s < n; s += B, ++t) {
+      const int bs = (int)std::min<int64_t>(B, n - s);
+      check(sl::conv_local_step(x.data_ptr(), x.scalar_type() == at::kByte, order.data_ptr<int64_t>() + s,
+                                labels.data_ptr<int64_t>(), bs, w.data_ptr<float>(), b.data_ptr<float>(),
+                                slab.data_ptr<float>(), loss_rows.data_ptr<float>() + s, s0w.data_ptr<float>(),
+                                fptr(s1w), s0b.data_ptr<float>(), fptr(s1b),
+                                make_opt(kind, lr, beta1, beta2, eps, wd, momentum, t, 0), st),
+            "conv_local_epoch");
+    }
+    return;
   }
+  EpochOpt ctx{kind, lr, beta1, beta2, eps, wd, momentum};
+  check(sl::conv_local_epoch(x.data_ptr(), x.scalar_type() == at::kByte, order.data_ptr<int64_t>(), n, (int)B,
+                             labels.data_ptr<int64_t>(), w.data_ptr<float>(), b.data_ptr<float>(),
+                             s0w.data_ptr<float>(), fptr(s1w), s0b.data_ptr<float>(), fptr(s1b), ws.data_ptr<float>(),
+                             ws.numel(), loss_rows.data_ptr<float>(), &epoch_opt, &ctx, t0, st),
+        "conv_local_epoch");
 }
 
 // Split-mode client backward: dW partials from the cut gradient, then reduce+optimizer.

@@ -12,6 +12,8 @@
 // pooled, NCHW-flattened [5408] activation plus a 2-bit argmax for backward.
 #include "common.h"
 
+#include <algorithm>
+
 namespace sl {
 
 template <typename XT>
@@ -109,13 +111,14 @@ __device__ __forceinline__ void conv_acc_grad(const float* img, int ph, int pw, 
   acc[9] += g;
 }
 
-__device__ __forceinline__ void slab_write8(float* acc, float* dst, int sub) {
+// Sum the 10 per-thread partials over the SUB consecutive lanes that share a channel.
+template <int SUB>
+__device__ __forceinline__ void slab_write(float* acc, float* dst, int sub) {
 #pragma unroll
   for (int j = 0; j < 10; ++j) {
     float v = acc[j];
-    v += __shfl_xor(v, 1, 64);
-    v += __shfl_xor(v, 2, 64);
-    v += __shfl_xor(v, 4, 64);
+#pragma unroll
+    for (int off = 1; off < SUB; off <<= 1) v += __shfl_xor(v, off, 64);
     acc[j] = v;
   }
   if (sub == 0) {
@@ -124,40 +127,79 @@ __device__ __forceinline__ void slab_write8(float* acc, float* dst, int sub) {
   }
 }
 
+__device__ __forceinline__ void slab_write8(float* acc, float* dst, int sub) { slab_write<8>(acc, dst, sub); }
+
 template <typename XT>
 __device__ __forceinline__ void stage_sample(const XT* x, int64_t src, const float* w, const float* b, float* img,
                                              float* sw, float* sb) {
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, nt = blockDim.x;
   const XT* xr = x + src * 784;
-  for (int i = tid; i < 784; i += 256) img[i] = (float)xr[i];
-  for (int i = tid; i < 288; i += 256) sw[i] = w[i];
+  for (int i = tid; i < 784; i += nt) img[i] = (float)xr[i];
+  for (int i = tid; i < 288; i += nt) sw[i] = w[i];
   if (tid < 32) sb[tid] = b[tid];
   __syncthreads();
 }
 
-// SISA local step, stage 1: forward + softmax-CE over the 5408-wide activation + dW/db partials.
-template <typename XT>
-__global__ void __launch_bounds__(256)
+// SISA local step, stage 1: forward + softmax-CE over the 5408-wide activation + dW/db
+// partials, one workgroup per sample.  SUB lanes share an output channel (channel =
+// tid / SUB), each owning every SUB-th of its 169 pooled positions.  At batch 16 only 16
+// workgroups run, so the step is latency-bound: SUB = 32 (1024 threads, 6 positions per
+// thread) cuts each thread's serial conv/CE/grad chain ~4x against SUB = 8 (22 per thread).
+//
+// FUSE (the epoch loop): the previous step's optimizer update is folded into this step's
+// prologue instead of a separate 1-workgroup launch per step.  Every workgroup sums the
+// previous step's B slabs and applies SGD-m / Adam to the 320 parameters of buffer `pin`
+// (identical arithmetic to conv_opt_reduce_kernel), keeps the result in LDS for its own
+// forward, and workgroup 0 also stores it to `pout` (ping-pong: no workgroup reads what
+// another is writing).  Param buffer layout: [w 288 | b 32 | s0 320 | s1 320].
+template <typename XT, int SUB, bool FUSE>
+__global__ void __launch_bounds__(32 * SUB)
 conv_fwd_ce_wgrad_kernel(const XT* __restrict__ x, const int64_t* __restrict__ idx,
                          const int64_t* __restrict__ labels, const float* __restrict__ w,
                          const float* __restrict__ b, float scale, float* __restrict__ slab,
-                         float* __restrict__ loss_rows) {
+                         float* __restrict__ loss_rows, const float* __restrict__ prev_slab = nullptr,
+                         int Bprev = 0, float* __restrict__ pout = nullptr, SlOpt o = SlOpt{}) {
+  constexpr int NJ = (169 + SUB - 1) / SUB;
+  constexpr int NW = 32 * SUB / 64;
   __shared__ float img[28 * 28];
   __shared__ float sw[32 * 9];
   __shared__ float sb[32];
-  __shared__ float red[8];
+  __shared__ float red[2 * NW];
   const int s = blockIdx.x, tid = threadIdx.x;
   const int64_t src = idx[s];
-  stage_sample(x, src, w, b, img, sw, sb);
-  const int oc = tid >> 3, sub = tid & 7;
+  if (FUSE) {
+    const float* pin = w;      // [w | b | s0 | s1] of the previous step
+    for (int p = tid; p < 320; p += 32 * SUB) {
+      const int oc = p / 10, j = p - (p / 10) * 10;
+      const int k = j < 9 ? oc * 9 + j : 288 + oc;
+      float pp = pin[k], a0 = pin[320 + k], a1 = pin[640 + k];
+      if (prev_slab) {
+        float g = 0.f;
+        for (int z = 0; z < Bprev; ++z) g += prev_slab[(int64_t)z * 320 + p];
+        sl_opt_update(o, pp, g, a0, a1);
+        if (blockIdx.x == 0) {
+          pout[k] = pp;
+          pout[320 + k] = a0;
+          pout[640 + k] = a1;
+        }
+      }
+      if (k < 288) sw[k] = pp; else sb[k - 288] = pp;
+    }
+    const XT* xr = x + src * 784;
+    for (int i = tid; i < 784; i += 32 * SUB) img[i] = (float)xr[i];
+    __syncthreads();
+  } else {
+    stage_sample(x, src, w, b, img, sw, sb);
+  }
+  const int oc = tid / SUB, sub = tid % SUB;
   const float* wk = sw + oc * 9;
   const float bias = sb[oc];
-  float yv[22];
-  int av[22];
+  float yv[NJ];
+  int av[NJ];
   float mx = 0.f;   // activations are >= 0 after ReLU
 #pragma unroll
-  for (int j = 0; j < 22; ++j) {
-    const int r = sub + 8 * j;
+  for (int j = 0; j < NJ; ++j) {
+    const int r = sub + SUB * j;
     yv[j] = -1.f;
     av[j] = 0;
     if (r < 169) {
@@ -170,23 +212,27 @@ conv_fwd_ce_wgrad_kernel(const XT* __restrict__ x, const int64_t* __restrict__ i
   mx = sl_wave_max(mx);
   if (lane == 0) red[wv] = mx;
   __syncthreads();
-  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  mx = red[0];
+#pragma unroll
+  for (int i = 1; i < NW; ++i) mx = fmaxf(mx, red[i]);
   float se = 0.f;
 #pragma unroll
-  for (int j = 0; j < 22; ++j)
-    if (sub + 8 * j < 169) se += expf(yv[j] - mx);
+  for (int j = 0; j < NJ; ++j)
+    if (sub + SUB * j < 169) se += expf(yv[j] - mx);
   se = sl_wave_sum(se);
-  if (lane == 0) red[4 + wv] = se;
+  if (lane == 0) red[NW + wv] = se;
   __syncthreads();
-  se = red[4] + red[5] + red[6] + red[7];
+  se = red[NW];
+#pragma unroll
+  for (int i = 1; i < NW; ++i) se += red[NW + i];
   const float inv = 1.f / se;
   const int64_t lab = labels[src];
   float acc[10];
 #pragma unroll
   for (int j = 0; j < 10; ++j) acc[j] = 0.f;
 #pragma unroll
-  for (int j = 0; j < 22; ++j) {
-    const int r = sub + 8 * j;
+  for (int j = 0; j < NJ; ++j) {
+    const int r = sub + SUB * j;
     if (r < 169) {
       const int o = oc * 169 + r;
       float g = expf(yv[j] - mx) * inv;
@@ -198,7 +244,7 @@ conv_fwd_ce_wgrad_kernel(const XT* __restrict__ x, const int64_t* __restrict__ i
       if (yv[j] > 0.f) conv_acc_grad(img, r / 13, r - (r / 13) * 13, av[j], g, acc);
     }
   }
-  slab_write8(acc, slab + (int64_t)s * 320 + oc * 10, sub);
+  slab_write<SUB>(acc, slab + (int64_t)s * 320 + oc * 10, sub);
 }
 
 // Split-mode stage 1: dW/db partials of one sample from the cut-layer gradient dy.
@@ -253,11 +299,92 @@ hipError_t conv_local_step(const void* x, bool x_u8, const int64_t* idx, const i
                            SlOpt o, hipStream_t st) {
   if (B <= 0) return hipSuccess;
   const float scale = 1.f / (float)B;
-  if (x_u8)
-    conv_fwd_ce_wgrad_kernel<uint8_t><<<B, 256, 0, st>>>((const uint8_t*)x, idx, labels, w, b, scale, slab, loss_rows);
-  else
-    conv_fwd_ce_wgrad_kernel<float><<<B, 256, 0, st>>>((const float*)x, idx, labels, w, b, scale, slab, loss_rows);
+  if (g_variant[6] == 1) {   // 8 lanes per channel (256 threads): A/B reference
+    if (x_u8)
+      conv_fwd_ce_wgrad_kernel<uint8_t, 8, false><<<B, 256, 0, st>>>((const uint8_t*)x, idx, labels, w, b, scale, slab,
+                                                              loss_rows);
+    else
+      conv_fwd_ce_wgrad_kernel<float, 8, false><<<B, 256, 0, st>>>((const float*)x, idx, labels, w, b, scale, slab,
+                                                            loss_rows);
+  } else {
+    if (x_u8)
+      conv_fwd_ce_wgrad_kernel<uint8_t, 32, false><<<B, 1024, 0, st>>>((const uint8_t*)x, idx, labels, w, b, scale, slab,
+                                                                loss_rows);
+    else
+      conv_fwd_ce_wgrad_kernel<float, 32, false><<<B, 1024, 0, st>>>((const float*)x, idx, labels, w, b, scale, slab,
+                                                              loss_rows);
+  }
   conv_opt_reduce_kernel<<<1, 320, 0, st>>>(slab, B, w, b, s0w, s1w, s0b, s1b, o);
+  return hipGetLastError();
+}
+
+// Epoch finaliser: the last step's update from param buffer `pin` into the real tensors.
+__global__ void __launch_bounds__(320)
+conv_opt_finalize_kernel(const float* __restrict__ slab, int B, const float* __restrict__ pin,
+                         float* __restrict__ w, float* __restrict__ b, float* __restrict__ s0w,
+                         float* __restrict__ s1w, float* __restrict__ s0b, float* __restrict__ s1b, SlOpt o) {
+  const int p = threadIdx.x;
+  const int oc = p / 10, j = p - (p / 10) * 10;
+  const int k = j < 9 ? oc * 9 + j : 288 + oc;
+  float g = 0.f;
+  for (int z = 0; z < B; ++z) g += slab[(int64_t)z * 320 + p];
+  float pp = pin[k], a0 = pin[320 + k], a1 = pin[640 + k];
+  sl_opt_update(o, pp, g, a0, a1);
+  if (k < 288) {
+    if (o.kind != 0) w[k] = pp;
+    s0w[k] = a0;
+    if (s1w) s1w[k] = a1;
+  } else {
+    if (o.kind != 0) b[k - 288] = pp;
+    s0b[k - 288] = a0;
+    if (s1b) s1b[k - 288] = a1;
+  }
+}
+
+__global__ void conv_params_pack_kernel(const float* __restrict__ w, const float* __restrict__ b,
+                                        const float* __restrict__ s0w, const float* __restrict__ s1w,
+                                        const float* __restrict__ s0b, const float* __restrict__ s1b,
+                                        float* __restrict__ P) {
+  const int k = threadIdx.x;   // 320
+  const bool isw = k < 288;
+  P[k] = isw ? w[k] : b[k - 288];
+  P[320 + k] = isw ? s0w[k] : s0b[k - 288];
+  P[640 + k] = isw ? (s1w ? s1w[k] : 0.f) : (s1b ? s1b[k - 288] : 0.f);
+}
+
+// A whole SISA local epoch (ceil(n/B) steps) with the per-step optimizer folded into the
+// next step's kernel: 1 launch per step + 2 for the epoch.  `ws` >= 2*B*320 + 2*960 floats.
+// opt(t) gives the SlOpt of optimizer step t (host-side bias corrections).
+hipError_t conv_local_epoch(const void* x, bool x_u8, const int64_t* order, int64_t n, int B, const int64_t* labels,
+                            float* w, float* b, float* s0w, float* s1w, float* s0b, float* s1b, float* ws,
+                            int64_t ws_elems, float* loss_rows, SlOpt (*opt)(void*, int64_t), void* optctx,
+                            int64_t t0, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  if (ws_elems < 2LL * B * 320 + 2 * 960) return hipErrorInvalidValue;
+  float* slabs[2] = {ws, ws + (int64_t)B * 320};
+  float* P[2] = {ws + 2LL * B * 320, ws + 2LL * B * 320 + 960};
+  conv_params_pack_kernel<<<1, 320, 0, st>>>(w, b, s0w, s1w, s0b, s1b, P[0]);
+  int cur = 0;
+  int64_t i = 0, prevB = 0;
+  for (int64_t s = 0; s < n; s += B, ++i) {
+    const int bs = (int)std::min<int64_t>(B, n - s);
+    const float scale = 1.f / (float)bs;
+    const float* prev = i ? slabs[(i - 1) & 1] : nullptr;
+    const SlOpt o = i ? opt(optctx, t0 + i - 1) : SlOpt{};
+    float* pout = P[1 - cur];
+    if (x_u8)
+      conv_fwd_ce_wgrad_kernel<uint8_t, 32, true><<<bs, 1024, 0, st>>>((const uint8_t*)x, order + s, labels, P[cur],
+                                                                       nullptr, scale, slabs[i & 1], loss_rows + s,
+                                                                       prev, (int)prevB, pout, o);
+    else
+      conv_fwd_ce_wgrad_kernel<float, 32, true><<<bs, 1024, 0, st>>>((const float*)x, order + s, labels, P[cur],
+                                                                     nullptr, scale, slabs[i & 1], loss_rows + s,
+                                                                     prev, (int)prevB, pout, o);
+    if (i) cur = 1 - cur;
+    prevB = bs;
+  }
+  conv_opt_finalize_kernel<<<1, 320, 0, st>>>(slabs[(i - 1) & 1], (int)prevB, P[cur], w, b, s0w, s1w, s0b, s1b,
+                                             opt(optctx, t0 + i - 1));
   return hipGetLastError();
 }
 

@@ -98,8 +98,9 @@ def conv_local_epoch_(x_u8, y_all, order, B: int, w, b, cfg, st_w, st_b, t0: int
     if n == 0:
         return loss_rows
     args = _opt_args(cfg, t0)
+    ws = _workspace(x_u8.device, 2 * B * 320 + 2 * 960, "convepoch")
     C().conv_local_epoch(x_u8, order, y_all, int(B), w.detach(), b.detach(), _slab(x_u8.device, B), loss_rows,
-                         _s0(st_w), _s1(st_w), _s0(st_b), _s1(st_b), *args[:7], int(t0))
+                         _s0(st_w), _s1(st_w), _s0(st_b), _s1(st_b), *args[:7], int(t0), ws)
     return loss_rows
 
 

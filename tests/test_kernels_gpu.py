@@ -256,8 +256,9 @@ def test_wgrad_group(cuda, variant, kind, M, shapes, mn):
         _close(kw["p_next"].sum(0), kw["x_next"] @ layers[0][5].t(), rtol=1e-4, atol=2e-3)
 
 
+@pytest.mark.parametrize("variant", [0, 1])   # 0: optimizer folded into the next step, 1: 2 launches/step
 @pytest.mark.parametrize("kind", ["sgd", "adam"])
-def test_conv_local_epoch_matches_steps(cuda, kind):
+def test_conv_local_epoch_matches_steps(cuda, kind, variant):
     """The C++-looped epoch == the per-step calls (bitwise), incl. a partial last batch."""
     x = _shard(300, cuda)
     y_all = torch.randint(0, 10, (300,), device=cuda)
@@ -270,8 +271,15 @@ def test_conv_local_epoch_matches_steps(cuda, kind):
             {"buf": torch.zeros_like(p)}
     w1, b1, w2, b2 = w.clone(), b.clone(), w.clone(), b.clone()
     s = [st(w), st(b), st(w), st(b)]
-    l1 = hip_ops.conv_local_epoch_(x, y_all, order, 16, w1, b1, cfg, s[0], s[1], 3)
-    l2 = torch.cat([hip_ops.conv_local_step_(x, y_all, order[i:i + 16], w2, b2, cfg, s[2], s[3], 3 + j)
-                    for j, i in enumerate(range(0, 109, 16))])
+    C = hip_ops.C()
+    C.set_variant(6, variant)      # also selects the per-step kernel's lane layout
+    try:
+        l1 = hip_ops.conv_local_epoch_(x, y_all, order, 16, w1, b1, cfg, s[0], s[1], 3)
+        l2 = torch.cat([hip_ops.conv_local_step_(x, y_all, order[i:i + 16], w2, b2, cfg, s[2], s[3], 3 + j)
+                        for j, i in enumerate(range(0, 109, 16))])
+    finally:
+        C.set_variant(6, 0)
     torch.cuda.synchronize()
     assert torch.equal(l1, l2) and torch.equal(w1, w2) and torch.equal(b1, b2)
+    for k in s[0]:
+        assert torch.equal(s[0][k], s[2][k]) and torch.equal(s[1][k], s[3][k])
