@@ -59,36 +59,17 @@ def main():
         res.setdefault(name, []).append(us)
 
     cases = []
-    for v in (0, 7, 8, 9, 1, 3):
-        def f(v=v):
-            C.set_variant(0, v)
-            H.linear_fwd(x, W1, b1, True, 0.5, 7, 0, out=out)
-            C.set_variant(0, 0)
-        cases.append((f"fc1_fwd[v{v}]", f, W1.numel() * 4))
-    for v in (0, 2):
-        def g(v=v):
-            C.set_variant(1, v)
-            H.linear_wgrad_step_(dz1, x, W1, b1, cfg, sW1, sb1, 3)
-            C.set_variant(1, 0)
-        cases.append((f"fc1_wgrad_adam[v{v}]", g, W1.numel() * 24))
+    cases.append(("fc1_fwd", lambda: H.linear_fwd(x, W1, b1, True, 0.5, 7, 0, out=out), W1.numel() * 4))
+    cases.append(("fc1_wgrad_adam", lambda: H.linear_wgrad_step_(dz1, x, W1, b1, cfg, sW1, sb1, 3),
+                  W1.numel() * 24))
     sW2 = {"m": torch.zeros_like(W2), "v": torch.zeros_like(W2)}
     b2 = torch.zeros(N2, device=dev)
     sb2 = {"m": torch.zeros_like(b2), "v": torch.zeros_like(b2)}
-    for v in (0, 2):
-        def g2(v=v):
-            C.set_variant(1, v)
-            H.linear_wgrad_step_(dz2, h1, W2, b2, cfg, sW2, sb2, 3)
-            C.set_variant(1, 0)
-        cases.append((f"fc2_wgrad_adam[v{v}]", g2, W2.numel() * 24))
+    cases.append(("fc2_wgrad_adam", lambda: H.linear_wgrad_step_(dz2, h1, W2, b2, cfg, sW2, sb2, 3),
+                  W2.numel() * 24))
     cases.append(("fc1_dgrad", lambda: H.linear_dgrad(dz1, W1, None, 1.0), W1.numel() * 4))
     cases.append(("fc2_dgrad", lambda: H.linear_dgrad(dz2, W2, h1, 2.0), W2.numel() * 4))
     cases.append(("fc2_fwd", lambda: H.linear_fwd(h1, W2, None, True, 0.5, 7, 0), W2.numel() * 4))
-    for v in (7, 8, 9):
-        def f2(v=v):
-            C.set_variant(0, v)
-            H.linear_fwd(h1, W2, None, True, 0.5, 7, 0)
-            C.set_variant(0, 0)
-        cases.append((f"fc2_fwd[v{v}]", f2, W2.numel() * 4))
     logits = torch.randn(M, 100, device=dev)
     yl = torch.randint(0, 10, (M,), device=dev)
     cases.append(("ce_100", lambda: H.softmax_ce(logits, yl, 1 / 16), 0))
@@ -205,8 +186,8 @@ def main():
     for _ in range(a.rounds):
         for name, fn, nb in cases:
             rec(name, timeit(fn, a.iters), nb)
-    C.set_variant(0, 0)
-    C.set_variant(1, 0)
+    for slot in range(8):
+        C.set_variant(slot, 0)
     table = []
     for name, ts in res.items():
         ts = sorted(ts)

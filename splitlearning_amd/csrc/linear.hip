@@ -14,10 +14,12 @@
 //   * dgrad    dX = dZ W: same MFMA, a 64-column K tile per workgroup, waves split
 //     N, optional split-N across workgroups, ReLU/dropout backward of the *previous*
 //     layer fused into the store;
-//   * wgrad + optimizer: dW is never materialised.  Each thread owns 4 adjacent
-//     weights of R rows, recomputes g = sum_m dZ[m,n] X[m,k] from registers, and
-//     applies SGD-momentum / Adam in place: 24 B of HBM traffic per parameter
-//     (p, m, v read + write) instead of 36 B for wgrad-then-optimizer.
+//   * wgrad + optimizer: dW is never materialised.  A 1024-thread workgroup owns a
+//     16-row x 256-column tile, each thread one float4 of a row; g = sum_m dZ[m,n] X[m,k]
+//     from LDS-staged operands, then SGD-momentum / Adam in place: 24 B of HBM traffic
+//     per parameter (p, m, v read + write) instead of 36 B for wgrad-then-optimizer.
+//   Variants that measured slower (non-temporal loads, software-pipelined forward,
+//   row-blocked and loads-first wgrad) were removed after measurement (docs/PERF.md).
 #include "common.h"
 
 namespace sl {
@@ -110,77 +112,6 @@ skinny_fwd_kernel(const float* __restrict__ X, int ldx, const float* __restrict_
           Y[(int64_t)m * ldy + n] = apply_epi(e, s[r], m, n);
         else
           P[(int64_t)blockIdx.z * slab + (int64_t)m * N + n] = s[r];
-      }
-    }
-  }
-}
-
-// Software-pipelined forward: two register buffers, the next chunk's loads are issued
-// before the current chunk's MFMAs so a wave always has U float4 pairs in flight.
-template <int NW, int U>
-__global__ void __launch_bounds__(NW * 64)
-skinny_fwd_pipe_kernel(const float* __restrict__ X, int ldx, const float* __restrict__ W, int ldw,
-                       float* __restrict__ Y, int ldy, int M, int N, int K, Epi e) {
-  __shared__ f32x4 red[NW][64];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int n0 = blockIdx.x * 16, m0 = blockIdx.y * 16;
-  const int kper = ((K + 16 * NW - 1) / (16 * NW)) * 16;
-  const int kb = wv * kper;
-  const int ke = min(K, kb + kper);
-  const int ra = m0 + (lane & 15), rb = n0 + (lane & 15);
-  const int kq = (lane >> 4) * 4;
-  const bool va = ra < M, vb = rb < N;
-  const float* pa = X + (int64_t)(va ? ra : 0) * ldx + kq;
-  const float* pb = W + (int64_t)(vb ? rb : 0) * ldw + kq;
-  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-  const f32x4 zv = {0.f, 0.f, 0.f, 0.f};
-  constexpr int CH = 16 * U;
-  const int nfull = ke > kb ? (ke - kb) / CH : 0;
-  f32x4 a0[U], w0[U], a1[U], w1[U];
-#define SL_LD(A_, W_, K0_)                                                           \
-  _Pragma("unroll") for (int u = 0; u < U; ++u) {                                    \
-    A_[u] = va ? *reinterpret_cast<const f32x4*>(pa + (K0_) + 16 * u) : zv;          \
-    W_[u] = vb ? *reinterpret_cast<const f32x4*>(pb + (K0_) + 16 * u) : zv;          \
-  }
-#define SL_MM(A_, W_)                                                                \
-  _Pragma("unroll") for (int u = 0; u < U; ++u) {                                    \
-    acc0 = mfma4(A_[u][0], W_[u][0], acc0);                                          \
-    acc1 = mfma4(A_[u][1], W_[u][1], acc1);                                          \
-    acc0 = mfma4(A_[u][2], W_[u][2], acc0);                                          \
-    acc1 = mfma4(A_[u][3], W_[u][3], acc1);                                          \
-  }
-  if (nfull > 0) { SL_LD(a0, w0, kb); }
-  int c = 0;
-  for (; c + 1 < nfull; c += 2) {
-    SL_LD(a1, w1, kb + (c + 1) * CH);
-    SL_MM(a0, w0);
-    if (c + 2 < nfull) { SL_LD(a0, w0, kb + (c + 2) * CH); }
-    SL_MM(a1, w1);
-  }
-  if (c < nfull) { SL_MM(a0, w0); }
-#undef SL_LD
-#undef SL_MM
-  for (int k = kb + nfull * CH; k < ke; k += 16) {
-    const bool in = k + kq < ke;
-    const f32x4 a = (va && in) ? *reinterpret_cast<const f32x4*>(pa + k) : zv;
-    const f32x4 w = (vb && in) ? *reinterpret_cast<const f32x4*>(pb + k) : zv;
-    acc0 = mfma4(a[0], w[0], acc0);
-    acc1 = mfma4(a[1], w[1], acc1);
-    acc0 = mfma4(a[2], w[2], acc0);
-    acc1 = mfma4(a[3], w[3], acc1);
-  }
-  red[wv][lane] = acc0 + acc1;
-  __syncthreads();
-  if (wv == 0) {
-    f32x4 s = red[0][lane];
-#pragma unroll
-    for (int i = 1; i < NW; ++i) s += red[i][lane];
-    const int n = n0 + (lane & 15);
-    if (n < N) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + (lane >> 4) * 4 + r;
-        if (m < M) Y[(int64_t)m * ldy + n] = apply_epi(e, s[r], m, n);
       }
     }
   }
@@ -304,155 +235,6 @@ __global__ void epilogue_kernel(const float* __restrict__ P, int ldp, float* __r
 }
 
 // ---------------------------------------------------------------------------- wgrad + optimizer
-// For rows n in [blockIdx.y*R, +R) and 4 columns per thread starting at
-// (blockIdx.x*256 + tid)*4:  g = sum_m dZ[m,n] A[m,k];  p <- opt(p, g).
-// Bias rows handled by blockIdx.x == 0.  Requires K % 4 == 0, ld % 4 == 0.
-template <int R>
-__global__ void __launch_bounds__(256)
-wgrad_opt_kernel(const float* __restrict__ dZ, int ldz, const float* __restrict__ A, int lda,
-                 float* __restrict__ W, int ldw, float* __restrict__ s0, float* __restrict__ s1,
-                 float* __restrict__ bias, float* __restrict__ sb0, float* __restrict__ sb1,
-                 int M, int N, int K, SlOpt o) {
-  const int tid = threadIdx.x;
-  const int kq = (blockIdx.x * 256 + tid) * 4;
-  const int n0 = blockIdx.y * R;
-  const int nr = min(R, N - n0);
-  if (kq < K) {
-    float4 g[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) g[r] = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int mc = 0; mc < M; mc += 16) {
-      float4 a[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j)
-        a[j] = (mc + j < M) ? ld4(A + (int64_t)(mc + j) * lda + kq) : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        if (r < nr) {
-#pragma unroll
-          for (int j = 0; j < 16; ++j) {
-            const float d = (mc + j < M) ? dZ[(int64_t)(mc + j) * ldz + n0 + r] : 0.f;
-            g[r].x = fmaf(d, a[j].x, g[r].x);
-            g[r].y = fmaf(d, a[j].y, g[r].y);
-            g[r].z = fmaf(d, a[j].z, g[r].z);
-            g[r].w = fmaf(d, a[j].w, g[r].w);
-          }
-        }
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      if (r >= nr) break;
-      const int64_t off = (int64_t)(n0 + r) * ldw + kq;
-      float4 p = ld4(W + off);
-      float4 m0 = ld4(s0 + off);
-      float4 m1 = s1 ? ld4(s1 + off) : make_float4(0.f, 0.f, 0.f, 0.f);
-      sl_opt_update(o, p.x, g[r].x, m0.x, m1.x);
-      sl_opt_update(o, p.y, g[r].y, m0.y, m1.y);
-      sl_opt_update(o, p.z, g[r].z, m0.z, m1.z);
-      sl_opt_update(o, p.w, g[r].w, m0.w, m1.w);
-      if (o.kind != 0) *reinterpret_cast<float4*>(W + off) = p;
-      *reinterpret_cast<float4*>(s0 + off) = m0;
-      if (s1) *reinterpret_cast<float4*>(s1 + off) = m1;
-    }
-  }
-  if (bias && blockIdx.x == 0 && tid < nr) {
-    const int n = n0 + tid;
-    float g = 0.f;
-    for (int m = 0; m < M; ++m) g += dZ[(int64_t)m * ldz + n];
-    float p = bias[n], b0 = sb0[n], b1 = sb1 ? sb1[n] : 0.f;
-    sl_opt_update(o, p, g, b0, b1);
-    if (o.kind != 0) bias[n] = p;
-    sb0[n] = b0;
-    if (sb1) sb1[n] = b1;
-  }
-}
-
-// v2: all R rows' parameter/state loads are issued first (non-temporal, 3R float4 in
-// flight per lane), the block's dZ slice sits in LDS (broadcast reads), the batch rows
-// of A stream from L2 four at a time while the state loads are in flight.
-template <int R, bool ADAM, bool NT>
-__global__ void __launch_bounds__(256)
-wgrad_opt_v2_kernel(const float* __restrict__ dZ, int ldz, const float* __restrict__ A, int lda,
-                    float* __restrict__ W, int ldw, float* __restrict__ s0, float* __restrict__ s1,
-                    float* __restrict__ bias, float* __restrict__ sb0, float* __restrict__ sb1,
-                    int M, int N, int K, SlOpt o) {
-  __shared__ float sdz[16 * R];
-  const int tid = threadIdx.x;
-  const int kq = (blockIdx.x * 256 + tid) * 4;
-  const int n0 = blockIdx.y * R;
-  const int nr = min(R, N - n0);
-  const bool act = kq < K;
-  const f32x4 zv = {0.f, 0.f, 0.f, 0.f};
-  f32x4 p[R], q0[R], q1[R], g[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    g[r] = zv;
-    p[r] = q0[r] = q1[r] = zv;
-    if (act && r < nr) {
-      const int64_t off = (int64_t)(n0 + r) * ldw + kq;
-      if (NT) {
-        p[r] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(W + off));
-        q0[r] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(s0 + off));
-        if (ADAM) q1[r] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(s1 + off));
-      } else {
-        p[r] = *reinterpret_cast<const f32x4*>(W + off);
-        q0[r] = *reinterpret_cast<const f32x4*>(s0 + off);
-        if (ADAM) q1[r] = *reinterpret_cast<const f32x4*>(s1 + off);
-      }
-    }
-  }
-  for (int mc = 0; mc < M; mc += 16) {
-    __syncthreads();
-    if (tid < 16 * R) {
-      const int j = tid / R, r = tid - (tid / R) * R;
-      sdz[tid] = (mc + j < M && r < nr) ? dZ[(int64_t)(mc + j) * ldz + n0 + r] : 0.f;
-    }
-    __syncthreads();
-    if (act) {
-#pragma unroll
-      for (int j = 0; j < 16; j += 4) {
-        f32x4 a[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-          a[u] = (mc + j + u < M) ? *reinterpret_cast<const f32x4*>(A + (int64_t)(mc + j + u) * lda + kq) : zv;
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-          for (int r = 0; r < R; ++r) g[r] += sdz[(j + u) * R + r] * a[u];
-      }
-    }
-  }
-  if (act) {
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      if (r < nr) {
-        const int64_t off = (int64_t)(n0 + r) * ldw + kq;
-        sl_opt_update4<ADAM>(o, p[r], g[r], q0[r], q1[r]);
-        if (NT) {
-          if (o.kind != 0) __builtin_nontemporal_store(p[r], reinterpret_cast<f32x4*>(W + off));
-          __builtin_nontemporal_store(q0[r], reinterpret_cast<f32x4*>(s0 + off));
-          if (ADAM) __builtin_nontemporal_store(q1[r], reinterpret_cast<f32x4*>(s1 + off));
-        } else {
-          if (o.kind != 0) *reinterpret_cast<f32x4*>(W + off) = p[r];
-          *reinterpret_cast<f32x4*>(s0 + off) = q0[r];
-          if (ADAM) *reinterpret_cast<f32x4*>(s1 + off) = q1[r];
-        }
-      }
-    }
-  }
-  if (bias && blockIdx.x == 0 && tid < nr) {
-    const int n = n0 + tid;
-    float gb = 0.f;
-    for (int m = 0; m < M; ++m) gb += dZ[(int64_t)m * ldz + n];
-    float pb = bias[n], b0 = sb0[n], b1 = sb1 ? sb1[n] : 0.f;
-    sl_opt_update(o, pb, gb, b0, b1);
-    if (o.kind != 0) bias[n] = pb;
-    sb0[n] = b0;
-    if (sb1) sb1[n] = b1;
-  }
-}
-
 // v3: memory-level parallelism first.  A 1024-thread workgroup owns a 16-row x 256-column
 // tile; every wave covers one row's 256 contiguous weights (1 KB per instruction), so each
 // thread holds exactly one float4 of p/m/v, issues those loads before anything else, and
@@ -532,43 +314,26 @@ hipError_t linear_fwd(const float* X, int ldx, const float* W, int ldw, float* Y
                       int K, Epi e, float* ws, int64_t ws_elems, hipStream_t st) {
   if (M <= 0 || N <= 0) return hipSuccess;
   dim3 grid((N + 15) / 16, (M + 15) / 16);
-  const int v = g_variant[0];
-  if (v == 0 || v >= 7) {
-    // split K until there are ~4 workgroups per CU, keeping >= 256 k per workgroup
-    const int tiles = grid.x * grid.y;
-    int S = 1;
-    const int target = (v == 8) ? 2048 : (v == 9 ? 512 : 1024);
-    while (S < 16 && tiles * S * 2 <= target && K / (S * 2) >= 256) S *= 2;
-    const int64_t slab = (int64_t)M * N;
-    if (S > 1 && (ws == nullptr || ws_elems < slab * S)) S = 1;
-    const int kz = (K + S - 1) / S;
-    const int nw = kz >= 1024 ? 8 : (kz >= 512 ? 4 : 2);
-    dim3 g3(grid.x, grid.y, S);
-    float* P = S > 1 ? ws : nullptr;
-    if (nw == 8)
-      skinny_fwd_kernel<8, 4, false><<<g3, 512, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e, P, slab);
-    else if (nw == 4)
-      skinny_fwd_kernel<4, 4, false><<<g3, 256, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e, P, slab);
-    else
-      skinny_fwd_kernel<2, 4, false><<<g3, 128, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e, P, slab);
-    if (S > 1) {
-      const int64_t tot = (int64_t)M * N;
-      epilogue_kernel<<<(unsigned)((tot + 255) / 256), 256, 0, st>>>(ws, N, Y, ldy, M, N, e, S, slab);
-    }
-    return hipGetLastError();
-  }
-  if (K >= 2048) {
-    switch (v) {
-      case 1: skinny_fwd_kernel<8, 4, true><<<grid, 512, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e); break;
-      case 2: skinny_fwd_kernel<8, 8, false><<<grid, 512, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e); break;
-      case 3: skinny_fwd_pipe_kernel<8, 4><<<grid, 512, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e); break;
-      case 4: skinny_fwd_pipe_kernel<8, 8><<<grid, 512, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e); break;
-      case 5: skinny_fwd_pipe_kernel<16, 4><<<grid, 1024, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e); break;
-      case 6: skinny_fwd_pipe_kernel<4, 8><<<grid, 256, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e); break;
-      default: skinny_fwd_kernel<8, 4, false><<<grid, 512, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e); break;
-    }
-  } else {
-    skinny_fwd_kernel<4, 4, false><<<grid, 256, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e);
+  // split K until there are ~8 workgroups per CU, keeping >= 256 k per workgroup: fc1
+  // (313 column tiles) runs S = 4 (30.6 us vs 35.2 us at S = 2; profiles/r1_kbench_call17)
+  const int tiles = grid.x * grid.y;
+  int S = 1;
+  while (S < 16 && tiles * S * 2 <= 2048 && K / (S * 2) >= 256) S *= 2;
+  const int64_t slab = (int64_t)M * N;
+  if (S > 1 && (ws == nullptr || ws_elems < slab * S)) S = 1;
+  const int kz = (K + S - 1) / S;
+  const int nw = kz >= 1024 ? 8 : (kz >= 512 ? 4 : 2);
+  dim3 g3(grid.x, grid.y, S);
+  float* P = S > 1 ? ws : nullptr;
+  if (nw == 8)
+    skinny_fwd_kernel<8, 4, false><<<g3, 512, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e, P, slab);
+  else if (nw == 4)
+    skinny_fwd_kernel<4, 4, false><<<g3, 256, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e, P, slab);
+  else
+    skinny_fwd_kernel<2, 4, false><<<g3, 128, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e, P, slab);
+  if (S > 1) {
+    const int64_t tot = (int64_t)M * N;
+    epilogue_kernel<<<(unsigned)((tot + 255) / 256), 256, 0, st>>>(ws, N, Y, ldy, M, N, e, S, slab);
   }
   return hipGetLastError();
 }
@@ -657,26 +422,12 @@ hipError_t linear_wgrad_opt(const float* dZ, int ldz, const float* A, int lda, f
                             float* s1, float* bias, float* sb0, float* sb1, int M, int N, int K, SlOpt o,
                             hipStream_t st) {
   if (N <= 0 || K <= 0) return hipSuccess;
-  constexpr int R = 8;
-  dim3 grid((K / 4 + 255) / 256, (N + R - 1) / R);
-  // default (0) = v3 (5.8 TB/s effective on fc1 at M = 16); 3 = v1, 1/2 = v2 variants
-  const int v = g_variant[1];
-  if (v == 3) {
-    wgrad_opt_kernel<R><<<grid, 256, 0, st>>>(dZ, ldz, A, lda, W, ldw, s0, s1, bias, sb0, sb1, M, N, K, o);
-  } else if (v == 1) {
-    if (o.kind == 2)
-      wgrad_opt_v2_kernel<R, true, false><<<grid, 256, 0, st>>>(dZ, ldz, A, lda, W, ldw, s0, s1, bias, sb0, sb1, M,
-                                                                N, K, o);
-    else
-      wgrad_opt_v2_kernel<R, false, false><<<grid, 256, 0, st>>>(dZ, ldz, A, lda, W, ldw, s0, s1, bias, sb0, sb1, M,
-                                                                 N, K, o);
-  } else {
-    dim3 g3((K + 255) / 256, (N + 15) / 16);
-    if (o.kind == 2)
-      wgrad_opt_v3_kernel<true><<<g3, 1024, 0, st>>>(dZ, ldz, A, lda, W, ldw, s0, s1, bias, sb0, sb1, M, N, K, o);
-    else
-      wgrad_opt_v3_kernel<false><<<g3, 1024, 0, st>>>(dZ, ldz, A, lda, W, ldw, s0, s1, bias, sb0, sb1, M, N, K, o);
-  }
+  // v3 layout (5.8 TB/s effective on fc1 at M = 16)
+  dim3 g3((K + 255) / 256, (N + 15) / 16);
+  if (o.kind == 2)
+    wgrad_opt_v3_kernel<true><<<g3, 1024, 0, st>>>(dZ, ldz, A, lda, W, ldw, s0, s1, bias, sb0, sb1, M, N, K, o);
+  else
+    wgrad_opt_v3_kernel<false><<<g3, 1024, 0, st>>>(dZ, ldz, A, lda, W, ldw, s0, s1, bias, sb0, sb1, M, N, K, o);
   return hipGetLastError();
 }
 

@@ -181,41 +181,6 @@ def test_conv_local_step(cuda, kind, B):
     _close(b1, b2, rtol=1e-3, atol=3e-4 if kind == "adam" else 1e-6)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6])
-def test_linear_fwd_variants(cuda, variant):
-    C = hip_ops.C()
-    x = torch.randn(16, 5408, device=cuda)
-    w = torch.randn(5000, 5408, device=cuda) / 70
-    b = torch.randn(5000, device=cuda)
-    yr = torch_ops.linear_fwd(x, w, b, True, 0.5, 99, 0)
-    try:
-        C.set_variant(0, variant)
-        y = hip_ops.linear_fwd(x, w, b, True, 0.5, 99, 0)
-    finally:
-        C.set_variant(0, 0)
-    _close(y, yr, rtol=1e-4, atol=1e-4)
-
-
-def test_wgrad_v1_matches_v2(cuda):
-    C = hip_ops.C()
-    dz = torch.randn(16, 1000, device=cuda)
-    a = torch.randn(16, 5000, device=cuda)
-    cfg = OptimCfg("adam", 1e-3, weight_decay=1e-5)
-    outs = []
-    for v in (0, 1, 3):
-        w = torch.ones(1000, 5000, device=cuda)
-        b = torch.ones(1000, device=cuda)
-        sw = {"m": torch.zeros_like(w), "v": torch.zeros_like(w)}
-        sb = {"m": torch.zeros_like(b), "v": torch.zeros_like(b)}
-        C.set_variant(1, v)
-        hip_ops.linear_wgrad_step_(dz, a, w, b, cfg, sw, sb, 1)
-        outs.append((w, b, sw["m"], sw["v"]))
-    C.set_variant(1, 0)
-    for other in outs[1:]:
-        for p, q in zip(outs[0], other):
-            _close(p, q, rtol=1e-6, atol=1e-7)
-
-
 @pytest.mark.parametrize("variant", [0, 1])          # 0 = LDS-staged (default), 1 = all-MFMA
 @pytest.mark.parametrize("kind", ["sgd", "adam"])
 @pytest.mark.parametrize("M,shapes,mn", [(16, [(5000, 5408), (1000, 5000)], 16), (20, [(100, 1000), (33, 20)], 5),
