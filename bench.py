@@ -48,7 +48,8 @@ def _session_args(a, world_size, log_dir):
         batch_size=a.batch_size, partition_alpha=0.5, datapath="", lr=1e-3, server_epochs=a.server_epochs,
         vanilla=False, sisa=True, concat=False, control=False, mode="sisa", seed=a.seed, log_dir=log_dir,
         no_tqdm=True, true_reset=False, eval_dropout_fix=False, concat_unlearn=False, omit_label=9,
-        unlearn_client_ids=[1], save_dir="", resume_dir="", kernels=a.kernels, graphs=a.graphs)
+        unlearn_client_ids=[1], save_dir="", resume_dir="", kernels=a.kernels, graphs=a.graphs,
+        act_dtype=a.act_dtype)
 
 
 def main(argv=None):
@@ -65,6 +66,8 @@ def main(argv=None):
     ap.add_argument("--bob_tp", type=int, default=0, help="0 = all ranks")
     ap.add_argument("--json_out", type=str, default="")
     ap.add_argument("--graphs", choices=("auto", "on", "off"), default="auto")
+    ap.add_argument("--act_dtype", choices=("fp32", "bf16"), default="fp32",
+                    help="SISA activation-cache storage dtype (compute stays fp32)")
     a = ap.parse_args(argv)
 
     from splitlearning_amd import ops
@@ -143,7 +146,8 @@ def main(argv=None):
                        "mode": "sisa", "world_size": ws, "global_batch": a.batch_size,
                        "samples_per_client": S, "seq_len": None,
                        "parallelism": f"alices{k}_one_per_gpu+bob_tp{pl.bob_tp}",
-                       "device": "MI355X" if use_gpu else "cpu", "kernels": kern},
+                       "device": "MI355X" if use_gpu else "cpu", "kernels": kern,
+                       "act_cache_dtype": a.act_dtype},
         }
         line = json.dumps(rec)
         print(line, flush=True)

@@ -58,6 +58,9 @@ def build_parser() -> argparse.ArgumentParser:
     g.add_argument("--bob_tp", type=int, default=0,
                    help="tensor-parallel degree of Bob's server tail (0 = all processes on GPU, 1 on CPU)")
     g.add_argument("--backend", choices=("auto", "nccl", "gloo"), default="auto")
+    g.add_argument("--act_dtype", choices=("fp32", "bf16"), default="fp32",
+                   help="storage/transfer dtype of SISA's cached cut activations (compute stays fp32; "
+                        "bf16 halves the dump traffic and the cache, rounding the activations)")
     g.add_argument("--kernels", choices=("auto", "hip", "torch"), default="auto",
                    help="compute path: hand-written HIP kernels (GPU) or torch ops")
     g.add_argument("--seed", type=int, default=None, help="seed everything (reference is unseeded)")

@@ -201,9 +201,10 @@ class Session:
 
     @staticmethod
     def pack(act: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
-        """One message per batch: [B*5408 activation | B labels as fp32] (labels < 2^24)."""
+        """One message per batch: [B*5408 activation | B labels] in the activation's dtype
+        (labels are small integers, exact in fp32 below 2^24 and in bf16 below 256)."""
         B = act.shape[0]
-        buf = torch.empty(B * CUT_FEATURES + B, device=act.device, dtype=torch.float32)
+        buf = torch.empty(B * CUT_FEATURES + B, device=act.device, dtype=act.dtype)
         buf[:B * CUT_FEATURES].view(B, CUT_FEATURES).copy_(act)
         buf[B * CUT_FEATURES:].copy_(labels)
         return buf

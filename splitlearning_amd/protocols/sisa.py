@@ -125,7 +125,15 @@ class SisaSession(Session):
             order = a.unlearn_order
         else:
             order = a.train.shuffled_order(a.gen)
-        return a.front.forward_chunked(a.train, order), a.train.y[order]
+        acts = a.front.forward_chunked(a.train, order)
+        if self.act_dtype != torch.float32:
+            acts = acts.to(self.act_dtype)
+        return acts, a.train.y[order]
+
+    @property
+    def act_dtype(self):
+        """Storage / transfer dtype of the cached cut activations (`--act_dtype`)."""
+        return torch.bfloat16 if getattr(self.args, "act_dtype", "fp32") == "bf16" else torch.float32
 
     def get_activation_and_labels(self, client_id: int, unlearned: bool = False, unlearn_id=None):
         key = (client_id, unlearned, unlearn_id)
@@ -139,7 +147,7 @@ class SisaSession(Session):
         acts = labels = None
         if self.hosts(client_id):
             acts, labels = self.give_activation_and_labels(client_id, unlearned)
-        acts = self.to_bob_var(client_id, acts, (CUT_FEATURES,), torch.float32)
+        acts = self.to_bob_var(client_id, acts, (CUT_FEATURES,), self.act_dtype)
         labels = self.to_bob_var(client_id, labels, (), torch.int64)
         self._cache_keys.add(key)
         if self.is_bob:
@@ -184,7 +192,7 @@ class SisaSession(Session):
                 sends += [(local[cid], b) for b in self.bob_ranks if b != h]
                 got[cid] = local[cid]
             elif self.is_bob:
-                got[cid] = torch.empty(n * CUT_FEATURES + n, device=self.device, dtype=torch.float32)
+                got[cid] = torch.empty(n * CUT_FEATURES + n, device=self.device, dtype=self.act_dtype)
                 recvs.append((got[cid], h))
         self.comm.exchange(sends, recvs)
         for key in keys:
@@ -230,6 +238,8 @@ class SisaSession(Session):
         """One pass of Bob's optimizer over one client's cached activations (batch order as
         cached).  Full batches run as HIP-graph chunks of GRAPH_STEPS steps when possible."""
         n, B = labels.numel(), self.B
+        if acts.dtype != torch.float32:          # --act_dtype bf16: the kernels compute in fp32
+            acts = acts.float()
         s = 0
         G = self.GRAPH_STEPS
         la = self.tail.lookahead_ok(B)

@@ -97,6 +97,7 @@ def _run(tmp_path, mode_flags, world_size, nprocs, bob_tp=1, extra=()):
     (["--vanilla"], 3, 2, 2),          # MI355X placement: Alices co-located, Bob TP=2
     ([], 3, 2, 2),                     # U-shape
     (["--sisa"], 3, 2, 2),
+    (["--sisa", "--act_dtype", "bf16"], 3, 3, 2),   # bf16 activation cache over p2p
     (["--control"], 3, 3, 1),
     (["--sisa", "--concat", "--concat_unlearn"], 3, 2, 2),
 ])
