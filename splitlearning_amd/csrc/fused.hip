@@ -14,9 +14,13 @@
 //                all of W3 with dependent loads; this split measures in profiles/.)
 //
 //  wgrad_group_kernel   the fused wgrad+optimizer (v3 layout) for up to 3 layers in one
-//                launch; a layer's dZ may be given as un-reduced split-N partial slabs plus
-//                a ReLU/dropout mask, reduced while staging into LDS (replaces the dgrad
-//                reduce kernel).
+//                launch, plus (FWDN) fc1's look-ahead forward for the next batch.  A layer's
+//                dZ may also be given as un-reduced split-N slabs plus a ReLU/dropout mask
+//                (PART), reduced while staging into LDS; measured slower than a separate
+//                reduce launch at fc1's size, so the server step passes a plain dZ.
+//
+// The look-ahead SISA step is 7 launches: slab epilogue (h1), fc2 forward (split-K),
+// head_fwd, head_bwd, fc2 dgrad (split-N) + reduce, wgrad_group.
 #include "fused.h"
 
 #include <algorithm>

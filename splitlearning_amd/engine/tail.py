@@ -153,7 +153,7 @@ class TailEngine:
     # ------------------------------------------------------------------ fused 3-layer step
     def fused3_ok(self) -> bool:
         """The SISA/vanilla server tail (fc1 ReLU+Dropout, fc2 ReLU+Dropout, fc3 -> CE) on the
-        HIP kernels: 6 launches per step instead of 13 (csrc/fused.hip)."""
+        fused HIP kernels: 7-8 launches per step instead of 13 (csrc/fused.hip)."""
         if not hasattr(self.ops, "server_head3") or len(self.layers) != 3:
             return False
         s = [L.spec for L in self.layers]
