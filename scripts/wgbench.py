@@ -1,0 +1,95 @@
+"""wgrad+optimizer microbenchmark at Bob's tensor-parallel shard sizes (MI355X).
+
+For each TP degree T the fc1 shard is [ceil(5000/T), 5408], fc2's [1000, ceil(5000/T)], fc3
+replicated.  Prints device us/call (CUDA events over back-to-back calls, so the shard's
+state is as cache-warm as in the real step loop) for:
+  stream      opt_flat over the fc1 shard (p, g, m, v read; p, m, v written: 28 B/param) —
+              a plain streaming roofline for the same parameter count;
+  fc1         wgrad_group over fc1 alone (24 B/param);
+  fc1+la      the same plus the look-ahead forward of the next batch;
+  group+la    fc1 + fc2 + fc3 + look-ahead (what the server step launches).
+
+    python scripts/wgbench.py [--tps 1 2 4 8] [--iters 100] [--variant 3=1]
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from splitlearning_amd.config import OptimCfg  # noqa: E402
+from splitlearning_amd.ops import hip_ops as H  # noqa: E402
+
+
+def timeit(fn, iters):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) * 1000.0 / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tps", type=int, nargs="+", default=[1, 2, 4, 8])
+    ap.add_argument("--iters", type=int, default=100)
+    ap.add_argument("--variant", action="append", default=[])
+    a = ap.parse_args()
+    C = H.C()
+    for kv in a.variant:
+        slot, val = (int(v) for v in kv.split("="))
+        C.set_variant(slot, val)
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    M, K1, N2, N3 = 16, 5408, 1000, 100
+    cfg = OptimCfg("adam", 1e-3, weight_decay=1e-5)
+
+    def layer(n, k):
+        W = torch.randn(n, k, device=dev) * 0.01
+        b = torch.zeros(n, device=dev)
+        return W, {"m": torch.zeros_like(W), "v": torch.zeros_like(W)}, b, {"m": torch.zeros_like(b),
+                                                                           "v": torch.zeros_like(b)}
+
+    for T in a.tps:
+        n1 = -(-5000 // T)
+        n1 = -(-n1 // 4) * 4
+        x = torch.rand(M, K1, device=dev)
+        xn = torch.rand(M, K1, device=dev)
+        h1 = torch.rand(M, n1, device=dev)
+        h2 = torch.rand(M, N2, device=dev)
+        dz1 = torch.randn(M, n1, device=dev)
+        dz2 = torch.randn(M, N2, device=dev)
+        dz3 = torch.randn(M, N3, device=dev)
+        W1, s1, b1, sb1 = layer(n1, K1)
+        W2, s2, b2, sb2 = layer(N2, n1)
+        W3, s3, b3, sb3 = layer(N3, N2)
+        g1 = torch.randn_like(W1)
+        pn = H.lookahead_slabs(dev, K1, M, n1)
+        L1 = (dz1, None, None, 1.0, x, W1, s1, b1, sb1)
+        L2 = (dz2, None, None, 1.0, h1, W2, s2, b2, sb2)
+        L3 = (dz3, None, None, 1.0, h2, W3, s3, b3, sb3)
+        st = {"m": s1["m"], "v": s1["v"]}
+        n_par = W1.numel()
+        res = {
+            "stream": timeit(lambda: H.apply_update_(W1.view(-1), g1.view(-1), {"m": st["m"].view(-1),
+                                                                               "v": st["v"].view(-1)}, cfg, 5),
+                             a.iters),
+            "fc1": timeit(lambda: H.wgrad_group_([L1], M, cfg, 5), a.iters),
+            "fc1+la": timeit(lambda: H.wgrad_group_([L1], M, cfg, 5, x_next=xn, p_next=pn), a.iters),
+            "group+la": timeit(lambda: H.wgrad_group_([L1, L2, L3], M, cfg, 5, x_next=xn, p_next=pn), a.iters),
+        }
+        gb = {"stream": 28 * n_par, "fc1": 24 * n_par, "fc1+la": 24 * n_par,
+              "group+la": 24 * (n_par + W2.numel() + W3.numel())}
+        for k, us in res.items():
+            print(f"tp={T} {k:9s} {us:8.2f} us  {gb[k] / us / 1e3:7.0f} GB/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()

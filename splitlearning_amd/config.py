@@ -68,6 +68,9 @@ def build_parser() -> argparse.ArgumentParser:
                    help="synthetic MNIST-shaped dataset size (no network: fetch_openml unavailable)")
     g.add_argument("--mnist_npz", type=str, default="",
                    help="optional local MNIST .npz (x uint8 [N,28,28], y [N]) used instead of synthetic")
+    g.add_argument("--data_layout", choices=("image", "flat"), default="image",
+                   help="shard rows as [1,28,28] images (load_mnist_image) or flat 784-vectors "
+                        "(load_mnist_flat); the client front reads either")
     g.add_argument("--reuse_data", action="store_true",
                    help="reuse existing shards instead of regenerating (reference regenerates, Q12)")
     g.add_argument("--log_dir", type=str, default="logs")

@@ -11,7 +11,10 @@
 //                ReLU/dropout backward (-> dz2).  Replaces fc2-epilogue, fc3-forward,
 //                CE and fc3-dgrad.  (A one-workgroup-per-row version that recomputed the
 //                logits per slice measured 59 us under rocprofv3: each workgroup streamed
-//                all of W3 with dependent loads; this split measures in profiles/.)
+//                all of W3 with dependent loads.  A one-workgroup-per-row version holding
+//                its W3 share in registers, used for both the logits and dz2, measured
+//                16.6 us against 14.4 us for these two kernels (TP = 1): one CU cannot pull
+//                400 KB fast enough, W3 has to be spread over many CUs.)
 //
 //  wgrad_group_kernel   the fused wgrad+optimizer (v3 layout) for up to 3 layers in one
 //                launch, plus (FWDN) fc1's look-ahead forward for the next batch.  A layer's
@@ -387,8 +390,9 @@ hipError_t server_head3(const float* P2, int S2, int64_t slab2, Epi e2, const fl
                         const int64_t* y, int64_t ignore, float scale, float* h2, float* dlog, float* dz2,
                         float* loss_rows, float* ws, int64_t ws_elems, int M, int N2, int C, hipStream_t st) {
   if (M <= 0) return hipSuccess;
+  if ((N2 & 3) || (ldw3 & 3)) return hipErrorInvalidValue;
   const int Q = head3_slices(N2);
-  if (ws_elems < (int64_t)Q * M * C || (N2 & 3) || (ldw3 & 3)) return hipErrorInvalidValue;
+  if (ws_elems < (int64_t)Q * M * C) return hipErrorInvalidValue;
   head_fwd_kernel<<<dim3(M, Q), 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C);
   head_bwd_kernel<<<dim3(M, Q), 256, (size_t)C * sizeof(float), st>>>(ws, b3, W3, ldw3, y, ignore, scale, e2.dscale,
                                                                       h2, dlog, dz2, loss_rows, M, N2, C);

@@ -201,14 +201,30 @@ skinny_dgrad_kernel(const float* __restrict__ dZ, int ldz, const float* __restri
   }
 }
 
+// Sum of S split-K / split-N partials p[0], p[slab], ...: up to 32 slabs are loaded with
+// every load issued before the first add (one memory round trip instead of S / 4), in
+// slab order so the result is bit-identical to the sequential sum.
+__device__ __forceinline__ float sum_slabs(const float* __restrict__ p, int S, int64_t slab) {
+  constexpr int U = 32;
+  float v = 0.f;
+  int s0 = 0;
+  for (; s0 < S; s0 += U) {
+    float r[U];
+#pragma unroll
+    for (int i = 0; i < U; ++i) r[i] = (s0 + i < S) ? p[(int64_t)(s0 + i) * slab] : 0.f;
+#pragma unroll
+    for (int i = 0; i < U; ++i) v += r[i];
+  }
+  return v;
+}
+
 __global__ void dgrad_reduce_kernel(const float* __restrict__ P, int S, int64_t slab,
                                     const float* __restrict__ hprev, int ldh, float scale,
                                     float* __restrict__ out, int ldo, int M, int K) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (int64_t)M * K) return;
   const int m = (int)(t / K), k = (int)(t - (int64_t)m * K);
-  float v = 0.f;
-  for (int s = 0; s < S; ++s) v += P[s * slab + t];
+  float v = sum_slabs(P + t, S, slab);
   if (hprev) v = (hprev[(int64_t)m * ldh + k] > 0.f) ? v * scale : 0.f;
   out[(int64_t)m * ldo + k] = v;
 }
@@ -219,18 +235,7 @@ __global__ void epilogue_kernel(const float* __restrict__ P, int ldp, float* __r
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (int64_t)M * N) return;
   const int m = (int)(t / N), n = (int)(t - (int64_t)m * N);
-  const float* src = P + (int64_t)m * ldp + n;
-  float v = src[0];
-  // independent slab loads in flight together (the look-ahead hands over ~22 slabs)
-  int s = 1;
-  for (; s + 4 <= S; s += 4) {
-    const float a = src[s * slab], b = src[(s + 1) * slab], c = src[(s + 2) * slab], d = src[(s + 3) * slab];
-    v += a;
-    v += b;
-    v += c;
-    v += d;
-  }
-  for (; s < S; ++s) v += src[s * slab];
+  const float v = sum_slabs(P + (int64_t)m * ldp + n, S, slab);
   Y[(int64_t)m * ldy + n] = apply_epi(e, v, m, n);
 }
 

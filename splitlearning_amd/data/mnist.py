@@ -94,14 +94,19 @@ def make_client_shards(x: np.ndarray, y: np.ndarray, client_num: int, alpha: flo
     return out
 
 
-def write_shards(args, verbose: bool = True) -> dict[int, tuple[int, int]]:
-    """Generate and save every client shard (reference `load_mnist_image`)."""
+def write_shards(args, verbose: bool = True, layout: str = "image") -> dict[int, tuple[int, int]]:
+    """Generate and save every client shard (reference `load_mnist_image`; `layout="flat"`
+    = `load_mnist_flat`, rows of 784 pixels)."""
+    if layout not in ("image", "flat"):
+        raise ValueError(f"unknown shard layout {layout!r}")
     os.makedirs(args.datapath, exist_ok=True)
     x, y = load_source(args)
     shards = make_client_shards(x, y, args.client_num_in_total, args.partition_alpha,
                                 seed=getattr(args, "seed", None))
     sizes = {}
     for cid, (xtr, ytr, xte, yte) in shards.items():
+        if layout == "flat":
+            xtr, xte = xtr.reshape(len(xtr), 784), xte.reshape(len(xte), 784)
         ptr, pte = shard_paths(args.datapath, cid)
         torch.save({"x": torch.from_numpy(np.ascontiguousarray(xtr)),
                     "y": torch.from_numpy(np.ascontiguousarray(ytr))}, ptr)

@@ -124,7 +124,7 @@ def prepare_data(args, verbose=True):
     from ..data.mnist import shards_exist, write_shards
     if args.reuse_data and shards_exist(args.datapath, args.client_num_in_total):
         return
-    write_shards(args, verbose=verbose)
+    write_shards(args, verbose=verbose, layout=getattr(args, "data_layout", "image"))
 
 
 def main(argv=None):

@@ -124,3 +124,51 @@ def test_model_forward_shapes():
     assert model2_sisa_concat(3)(torch.zeros(2, 5408 * 3)).shape == (2, 300)
     assert model2()(torch.zeros(2, 32, 13, 13)).shape == (2, 100)
     assert model3()(torch.zeros(2, 100)).shape == (2, 10)
+
+
+# ---------------------------------------------------------------- reference-named data API
+def test_reference_data_api(tmp_path):
+    from types import SimpleNamespace
+
+    import numpy as np
+
+    from splitlearning_amd.data import (DeviceLoader, image_preprocess_dl, load_mnist_flat, load_mnist_image,
+                                        load_shard, non_iid_partition_with_dirichlet_distribution,
+                                        partition_class_samples_with_dirichlet_distribution,
+                                        record_data_stats, relational_table_preprocess_dl)
+    from splitlearning_amd.data.device_dataset import DeviceShard
+    from splitlearning_amd.data.mnist import synthetic_mnist
+
+    x, y = synthetic_mnist(600, seed=1)
+    rng = np.random.default_rng(0)
+    idx_map = non_iid_partition_with_dirichlet_distribution(y, 3, 10, 0.5, rng=rng)
+    allidx = sorted(i for v in idx_map.values() for i in v)
+    assert allidx == list(range(600)) and min(len(v) for v in idx_map.values()) >= 10
+    stats = record_data_stats(y, idx_map)
+    assert sum(sum(c.values()) for c in stats.values()) == 600
+    buckets = [[], []]
+    _, mn = partition_class_samples_with_dirichlet_distribution(600, 0.5, 2, buckets, np.arange(50),
+                                                                 rng=np.random.default_rng(1))
+    assert sum(len(b) for b in buckets) == 50 and mn == min(len(b) for b in buckets)
+
+    args = SimpleNamespace(client_num_in_total=3, partition_alpha=0.5, batch_size=16, class_num=10, seed=0)
+    out = image_preprocess_dl(args, x.astype(np.float32), y)
+    train_num, test_num, tg, teg, tln, tl, tel, cn = out
+    assert train_num + test_num == 600 and cn == 10 and set(tl) == {0, 1, 2}
+    assert sum(tln.values()) == train_num and len(tg.dataset[1]) == train_num
+    xb, yb = next(iter(tl[0]))
+    assert xb.shape[1:] == (1, 28, 28) and xb.shape[0] == yb.shape[0] <= 16
+    assert sum(b[1].numel() for b in tl[1]) == tln[1]          # one epoch covers the shard
+    tab = relational_table_preprocess_dl(args, x.reshape(600, -1).astype(np.float32), y)
+    assert next(iter(tab[5][0]))[0].shape[1] == 784
+    ld = DeviceLoader(torch.arange(10.0).view(10, 1), torch.arange(10), 4)
+    assert len(ld) == 3 and [b[1].tolist() for b in ld] == [[0, 1, 2, 3], [4, 5, 6, 7], [8, 9]]
+
+    for fn, shape in ((load_mnist_image, (1, 28, 28)), (load_mnist_flat, (784,))):
+        d = tmp_path / fn.__name__
+        a = SimpleNamespace(datapath=str(d), client_num_in_total=2, partition_alpha=0.5, seed=0, num_samples=500,
+                            mnist_npz="")
+        sizes = fn(a, verbose=False)
+        tr, te = load_shard(str(d), 1)
+        assert tuple(tr["x"].shape[1:]) == shape and len(tr["y"]) == sizes[1][0]
+        assert DeviceShard(tr["x"], tr["y"], torch.device("cpu")).x.shape[1] == 784

@@ -132,3 +132,27 @@ def test_checkpoint_roundtrip(tmp_path):
     assert set(a1) == {"conv_layers.0.weight", "conv_layers.0.bias"}
     # resume into a fresh run: loads without error and trains on
     _run(tmp_path, ["--vanilla"], 3, 2, 2, extra=["--resume_dir", str(ck)])
+
+
+@pytest.mark.slow
+def test_bench_two_ranks_gloo(tmp_path):
+    """bench.py under torch.distributed.run with 2 CPU ranks (gloo): one JSON line from rank 0
+    with the driver's contract fields (the GPU path is the same code over RCCL)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = tmp_path / "b.json"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
+           "--gpus", "2", "--steps", "1", "--warmup", "1", "--samples_per_client", "48", "--json_out", str(out)]
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    rec = json.loads(lines[0])
+    assert rec == json.loads(out.read_text())
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in rec, k
+    assert rec["n_gpus"] == 2 and rec["value"] > 0 and rec["config"]["world_size"] == 3

@@ -248,3 +248,27 @@ def test_conv_local_epoch_matches_steps(cuda, kind, variant):
     assert torch.equal(l1, l2) and torch.equal(w1, w2) and torch.equal(b1, b2)
     for k in s[0]:
         assert torch.equal(s[0][k], s[2][k]) and torch.equal(s[1][k], s[3][k])
+
+
+@pytest.mark.parametrize("M,S2,N2,C", [(16, 4, 1000, 100), (7, 1, 1000, 100), (16, 8, 1000, 10),
+                                       (3, 2, 512, 97), (16, 1, 1000, 300)])
+def test_server_head3(cuda, M, S2, N2, C):
+    """fc2 slab reduce + epilogue, fc3, softmax-CE, fc3 dgrad, fc2 ReLU/dropout backward
+    against the eager composition of the same ops."""
+    g = torch.Generator().manual_seed(7)
+    P2 = (torch.randn(S2, M, N2, generator=g) * 0.5).to(cuda)
+    b2 = (torch.randn(N2, generator=g) * 0.1).to(cuda)
+    W3 = (torch.randn(C, N2, generator=g) * 0.05).to(cuda)
+    b3 = (torch.randn(C, generator=g) * 0.1).to(cuda)
+    y = torch.randint(0, min(C, 10), (M,), generator=g).to(cuda)
+    y[0] = -100                                        # ignored row
+    seed = 1234567
+    h2, dlog, dz2, loss = hip_ops.server_head3(P2, b2, True, 0.5, seed, W3, b3, y, 1.0 / M)
+    h2r = torch_ops.linear_epilogue(P2.sum(0).cpu(), b2.cpu(), True, 0.5, seed)
+    logits = h2r @ W3.cpu().t() + b3.cpu()
+    lossr, dlogr = torch_ops.softmax_ce(logits, y.cpu(), 1.0 / M)
+    dz2r = (dlogr @ W3.cpu()) * (h2r > 0) * 2.0
+    _close(h2, h2r)
+    _close(loss, lossr, rtol=1e-4, atol=1e-5)
+    _close(dlog, dlogr, rtol=1e-4, atol=1e-6)
+    _close(dz2, dz2r, rtol=1e-4, atol=1e-6)
