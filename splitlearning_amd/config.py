@@ -91,6 +91,17 @@ def build_parser() -> argparse.ArgumentParser:
                    help="extend the concat schedule with unlearning + retrain (BASELINE config 5)")
     g.add_argument("--timeout_s", type=float, default=1800.0,
                    help="bounded wait for every collective / control message")
+    g.add_argument("--watchdog", choices=("abort", "report", "off"), default="abort",
+                   help="failure detection over the rendezvous store: a dead peer or (with "
+                        "--stall_after_s) a job-wide stall is reported and, with 'abort', ends the job")
+    g.add_argument("--dead_after_s", type=float, default=60.0,
+                   help="a peer with no heartbeat for this long is declared dead")
+    g.add_argument("--stall_after_s", type=float, default=0.0,
+                   help="report a stall when no rank passes a phase boundary for this long (0 = off)")
+    g.add_argument("--watchdog_interval", type=float, default=1.0)
+    g.add_argument("--fault_inject", type=str, default="",
+                   help="RANK:PHASE[:crash|hang|silent] - make RANK fail at the phase beacon PHASE "
+                        "(tests the failure paths)")
     g.add_argument("--no_tqdm", action="store_true")
     g.add_argument("--graphs", choices=("auto", "on", "off"), default="auto",
                    help="capture Bob's fixed-shape server steps in HIP graphs (auto: single-GPU "

@@ -31,6 +31,10 @@ import torch
 import torch.distributed as dist
 
 
+def _noop():
+    pass
+
+
 @dataclass
 class Placement:
     world_size: int          # roles: 1 Bob + k Alices (reference --world_size)
@@ -78,6 +82,7 @@ class Comm:
         self.tp_group = tp_group
         self.bytes_sent = 0
         self.msgs_sent = 0
+        self.progress = _noop        # watchdog tick (runtime/watchdog.py), called per data-plane op
 
     @property
     def distributed(self) -> bool:
@@ -87,6 +92,7 @@ class Comm:
     def multicast(self, t: torch.Tensor | None, src: int, dsts, shape=None, dtype=None) -> torch.Tensor | None:
         """`src` sends `t` to every rank in `dsts` (concurrent p2p).  Returns the tensor on
         src and on each dst (freshly received), None elsewhere."""
+        self.progress()
         dsts = [d for d in dict.fromkeys(dsts) if d != src]
         if self.rank == src:
             if dsts:
@@ -108,6 +114,7 @@ class Comm:
         `recvs` = [(buffer, src)] (this rank's side of every pair).  All transfers are
         posted together (RCCL groups them), so distinct peers' xGMI links run
         concurrently instead of one message after another."""
+        self.progress()
         ops = [dist.P2POp(dist.isend, t.contiguous(), d) for t, d in sends if d != self.rank]
         ops += [dist.P2POp(dist.irecv, b, s) for b, s in recvs if s != self.rank]
         if not ops:
@@ -124,6 +131,7 @@ class Comm:
         and return a `finish()` callable giving the sum on dst (None elsewhere).  Work the
         caller enqueues between post and finish (Bob's wgrad + optimizer) overlaps the
         transfer of the cut-layer gradient."""
+        self.progress()
         srcs = list(dict.fromkeys(srcs))
         others = [s for s in srcs if s != dst]
         if self.rank == dst:
@@ -157,6 +165,7 @@ class Comm:
         return self.reduce_to_async(t, dst, srcs, shape, dtype)()
 
     def send_recv(self, t: torch.Tensor | None, src: int, dst: int, shape=None, dtype=None):
+        self.progress()
         if src == dst:
             return t
         if self.rank == src:
@@ -192,6 +201,7 @@ class Comm:
         return [o[:int(s.item())] for o, s in zip(outs, sizes)]
 
     def allreduce_sum_(self, t: torch.Tensor):
+        self.progress()
         if self.distributed:
             dist.all_reduce(t)
         return t
@@ -211,6 +221,7 @@ class Comm:
         return out
 
     def barrier(self):
+        self.progress()
         if self.distributed:
             if self.device.type == "cuda":
                 dist.barrier(device_ids=[self.device.index])

@@ -92,6 +92,7 @@ class ConcatSession(SisaSession):
                 T = max(-(-c[1].numel() // self.B) for c in caches)
                 for t in range(T):
                     samples += self.concat_step(caches, t)
+                    self.comm.progress()
         self.bob_log.info("Global training completed.")
         self.comm.barrier()
         return samples

@@ -64,6 +64,7 @@ class SisaSession(Session):
         for _ in _progress(range(self.args.epochs), self.show, desc="Epochs", ascii=" >="):
             order = fixed_order if fixed_order is not None else a.train.shuffled_order(a.gen)
             a.front.local_epoch(a.train, order, self.B, a.slot)
+            self.comm.progress()
 
     def train(self, cid: int):
         a = self.alices[cid]
@@ -254,6 +255,7 @@ class SisaSession(Session):
                 gs = self._graphed[key] = GraphedServerSteps(self.tail, self.bob_slot, B, G, acts.shape[1])
             ng = (n // B // G) * G
             pre = gs.run(acts, labels, ng)
+            self.comm.progress()
             s = ng * B
         elif la and n >= B:
             self.tail.lookahead_prologue(acts[:B])
@@ -262,6 +264,7 @@ class SisaSession(Session):
             # look ahead only to a full batch (the prologue / slabs are sized for B rows)
             nxt = acts[s + B:s + 2 * B] if la and s + 2 * B <= n else None
             self.server_step(acts[s:s + B], labels[s:s + B], pre=pre, x_next=nxt)
+            self.comm.progress()
             pre = nxt is not None
 
     def train_and_backward(self, unlearn_request_from_alices, unlearn_id):

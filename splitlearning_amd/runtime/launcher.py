@@ -72,11 +72,19 @@ def worker(rank: int, nprocs: int, args, result_q=None):
         init_process(rank, nprocs, args.backend, args.master_addr, args.master_port, args.timeout_s, dev)
         tp_group = make_tp_group(pl, args.backend)
     comm = Comm(rank, nprocs, dev, pl, tp_group)
+    from .watchdog import make_watchdog
+    wd = make_watchdog(args, comm)
+    if wd is not None:
+        comm.progress = wd.tick
     if getattr(args, "prep_in_worker", False):
         if rank == 0:
             prepare_data(args)
         comm.barrier()
     sess = make_session(args, comm, dev)
+    if wd is not None:
+        wd.logger = sess.bob_log if rank == 0 else None
+        sess.timer.beacon = wd.beat
+        wd.beat("session_ready")
     if args.resume_dir:
         sess.load_checkpoints(args.resume_dir)
     out = run_schedule(sess, args)
@@ -90,6 +98,8 @@ def worker(rank: int, nprocs: int, args, result_q=None):
         if result_q is not None:
             result_q.put({"phases": out["phases"], **extra})
     sess.close()
+    if wd is not None:
+        wd.stop()
     if nprocs > 1:
         import torch.distributed as dist
         comm.barrier()

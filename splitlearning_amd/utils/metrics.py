@@ -21,14 +21,17 @@ def sync(device):
 
 
 class PhaseTimer:
-    def __init__(self, device, logger=None, barrier=None):
+    def __init__(self, device, logger=None, barrier=None, beacon=None):
         self.device = device
         self.logger = logger
         self.barrier = barrier
+        self.beacon = beacon          # progress callback (runtime/watchdog.py): beacon(tag)
         self.records: list[dict] = []
 
     @contextmanager
     def phase(self, name: str, samples: int = 0):
+        if self.beacon is not None:
+            self.beacon(name)
         sync(self.device)
         t0 = time.perf_counter()
         box = {"samples": samples}
@@ -43,6 +46,8 @@ class PhaseTimer:
             rec = {"phase": name, "seconds": dt, "samples": n,
                    "samples_per_s": (n / dt) if (n and dt > 0) else None}
             self.records.append(rec)
+            if self.beacon is not None:
+                self.beacon(f"{name}:done")
             if self.logger is not None:
                 if n:
                     self.logger.info(f"[perf] {name}: {n} samples in {dt:.4f} s = {n / dt:.1f} samples/s")
