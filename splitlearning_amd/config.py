@@ -102,6 +102,9 @@ def build_parser() -> argparse.ArgumentParser:
     g.add_argument("--fault_inject", type=str, default="",
                    help="RANK:PHASE[:crash|hang|silent] - make RANK fail at the phase beacon PHASE "
                         "(tests the failure paths)")
+    g.add_argument("--trace_dir", type=str, default="",
+                   help="write a Chrome-trace timeline per rank (phases, data-plane ops with bytes, "
+                        "device time of server / local epochs) to DIR/trace_rank<r>.json")
     g.add_argument("--no_tqdm", action="store_true")
     g.add_argument("--graphs", choices=("auto", "on", "off"), default="auto",
                    help="capture Bob's fixed-shape server steps in HIP graphs (auto: single-GPU "

@@ -24,15 +24,37 @@ All waits are bounded by the process-group timeout (`--timeout_s`).
 from __future__ import annotations
 
 import datetime
+import functools
 import os
 from dataclasses import dataclass, field
 
 import torch
 import torch.distributed as dist
 
+from ..utils.trace import NULL_TRACER
+
 
 def _noop():
     pass
+
+
+def _dataplane(fn):
+    """Data-plane op: tick the watchdog's progress counter and, when tracing, record a
+    "comm" span with the bytes this rank sent."""
+    name = fn.__name__
+
+    @functools.wraps(fn)
+    def op(self, *a, **k):
+        self.progress()
+        if not self.tracer.on:
+            return fn(self, *a, **k)
+        b0, m0 = self.bytes_sent, self.msgs_sent
+        with self.tracer.span(name, "comm") as info:
+            out = fn(self, *a, **k)
+            info["bytes_sent"] = self.bytes_sent - b0
+            info["msgs_sent"] = self.msgs_sent - m0
+        return out
+    return op
 
 
 @dataclass
@@ -83,16 +105,17 @@ class Comm:
         self.bytes_sent = 0
         self.msgs_sent = 0
         self.progress = _noop        # watchdog tick (runtime/watchdog.py), called per data-plane op
+        self.tracer = NULL_TRACER    # utils/trace.py: one "comm" span per data-plane op
 
     @property
     def distributed(self) -> bool:
         return self.world > 1
 
     # ---------------------------------------------------------------- p2p
+    @_dataplane
     def multicast(self, t: torch.Tensor | None, src: int, dsts, shape=None, dtype=None) -> torch.Tensor | None:
         """`src` sends `t` to every rank in `dsts` (concurrent p2p).  Returns the tensor on
         src and on each dst (freshly received), None elsewhere."""
-        self.progress()
         dsts = [d for d in dict.fromkeys(dsts) if d != src]
         if self.rank == src:
             if dsts:
@@ -109,12 +132,12 @@ class Comm:
             return buf
         return None
 
+    @_dataplane
     def exchange(self, sends, recvs):
         """One batched round of point-to-point transfers: `sends` = [(tensor, dst)],
         `recvs` = [(buffer, src)] (this rank's side of every pair).  All transfers are
         posted together (RCCL groups them), so distinct peers' xGMI links run
         concurrently instead of one message after another."""
-        self.progress()
         ops = [dist.P2POp(dist.isend, t.contiguous(), d) for t, d in sends if d != self.rank]
         ops += [dist.P2POp(dist.irecv, b, s) for b, s in recvs if s != self.rank]
         if not ops:
@@ -126,12 +149,12 @@ class Comm:
                 self.bytes_sent += t.numel() * t.element_size()
                 self.msgs_sent += 1
 
+    @_dataplane
     def reduce_to_async(self, t: torch.Tensor | None, dst: int, srcs, shape=None, dtype=None):
         """Post the sum-to-`dst` of `t` over `srcs` (each src sends its partial, dst adds)
         and return a `finish()` callable giving the sum on dst (None elsewhere).  Work the
         caller enqueues between post and finish (Bob's wgrad + optimizer) overlaps the
         transfer of the cut-layer gradient."""
-        self.progress()
         srcs = list(dict.fromkeys(srcs))
         others = [s for s in srcs if s != dst]
         if self.rank == dst:
@@ -164,8 +187,8 @@ class Comm:
     def reduce_to(self, t: torch.Tensor | None, dst: int, srcs, shape=None, dtype=None):
         return self.reduce_to_async(t, dst, srcs, shape, dtype)()
 
+    @_dataplane
     def send_recv(self, t: torch.Tensor | None, src: int, dst: int, shape=None, dtype=None):
-        self.progress()
         if src == dst:
             return t
         if self.rank == src:
@@ -185,6 +208,7 @@ class Comm:
             dist.all_reduce(t, group=self.tp_group)
         return t
 
+    @_dataplane
     def tp_allgather(self, t: torch.Tensor) -> list[torch.Tensor]:
         if self.tp_group is None:
             return [t]
@@ -200,8 +224,8 @@ class Comm:
         dist.all_gather(outs, pad, group=self.tp_group)
         return [o[:int(s.item())] for o, s in zip(outs, sizes)]
 
+    @_dataplane
     def allreduce_sum_(self, t: torch.Tensor):
-        self.progress()
         if self.distributed:
             dist.all_reduce(t)
         return t
@@ -220,8 +244,8 @@ class Comm:
         dist.gather_object(obj, out, dst=dst)
         return out
 
+    @_dataplane
     def barrier(self):
-        self.progress()
         if self.distributed:
             if self.device.type == "cuda":
                 dist.barrier(device_ids=[self.device.index])

@@ -26,6 +26,7 @@ from ..engine.tail import TailEngine
 from ..parallel.dist import Comm, Placement
 from ..utils.logging import NULL, role_logger
 from ..utils.metrics import PhaseTimer
+from ..utils.trace import make_tracer
 
 
 def _progress(it, enabled, **kw):
@@ -69,6 +70,8 @@ class Session:
         self.seed = int(comm.broadcast_obj(seed, 0))
         self.bob_log = role_logger("bob", args.log_dir, self.rank == 0)
         self.timer = PhaseTimer(device, self.bob_log if self.rank == 0 else None, comm.barrier)
+        self.tracer = make_tracer(args, self.rank, device)
+        self.timer.tracer = comm.tracer = self.tracer
         self.alices: dict[int, AliceState] = {}
         self._build_alices()
         self._exchange_meta()

@@ -63,7 +63,8 @@ class SisaSession(Session):
         filtered, shuffle=False) order is given."""
         for _ in _progress(range(self.args.epochs), self.show, desc="Epochs", ascii=" >="):
             order = fixed_order if fixed_order is not None else a.train.shuffled_order(a.gen)
-            a.front.local_epoch(a.train, order, self.B, a.slot)
+            with self.tracer.gpu_span(f"local_epoch[alice{a.cid}]", samples=int(order.numel())):
+                a.front.local_epoch(a.train, order, self.B, a.slot)
             self.comm.progress()
 
     def train(self, cid: int):
@@ -281,7 +282,8 @@ class SisaSession(Session):
                     got = self.get_activation_and_labels(cid, unlearned=False)
                 if self.is_bob:
                     acts, labels = got
-                    self.server_epoch(acts, labels)
+                    with self.tracer.gpu_span(f"server_epoch[alice{cid}]", samples=int(labels.numel())):
+                        self.server_epoch(acts, labels)
                     samples += labels.numel()
         self.bob_log.info("Global training completed.")
         self.comm.barrier()

@@ -97,6 +97,7 @@ def worker(rank: int, nprocs: int, args, result_q=None):
         sess.timer.dump(os.path.join(args.log_dir, "metrics.json"), extra)
         if result_q is not None:
             result_q.put({"phases": out["phases"], **extra})
+    sess.tracer.dump()
     sess.close()
     if wd is not None:
         wd.stop()

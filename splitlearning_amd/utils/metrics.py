@@ -14,6 +14,8 @@ from contextlib import contextmanager
 
 import torch
 
+from .trace import NULL_TRACER
+
 
 def sync(device):
     if device is not None and torch.device(device).type == "cuda":
@@ -26,6 +28,7 @@ class PhaseTimer:
         self.logger = logger
         self.barrier = barrier
         self.beacon = beacon          # progress callback (runtime/watchdog.py): beacon(tag)
+        self.tracer = NULL_TRACER     # utils/trace.py: one "phase" span per phase
         self.records: list[dict] = []
 
     @contextmanager
@@ -35,9 +38,13 @@ class PhaseTimer:
         sync(self.device)
         t0 = time.perf_counter()
         box = {"samples": samples}
+        span = self.tracer.span(name, "phase")
+        info = span.__enter__()
         try:
             yield box
         finally:
+            info["samples"] = box["samples"]
+            span.__exit__(None, None, None)
             sync(self.device)
             if self.barrier is not None:
                 self.barrier()

@@ -37,3 +37,13 @@ def test_modes_on_gpu(cuda, tmp_path, flags):
     m, bob = _run(tmp_path, flags)
     assert "Bob Started Getting Tipsy" in bob and "Accuracy over all data" in bob
     assert m["world_size"] == 2 and m["nprocs"] == 1
+
+
+def test_trace_has_device_spans(cuda, tmp_path):
+    """--trace_dir on the GPU: server/local epochs appear as HIP-event timed spans."""
+    _run(tmp_path, ["--sisa"], extra=["--trace_dir", str(tmp_path / "tr")])
+    ev = json.loads((tmp_path / "tr" / "trace_rank0.json").read_text())["traceEvents"]
+    gpu = [e for e in ev if e.get("tid") == "gpu"]
+    assert any(e["name"] == "server_epoch[alice1]" for e in gpu)
+    assert any(e["name"] == "local_epoch[alice1]" for e in gpu)
+    assert all(e["dur"] > 0 for e in gpu)

@@ -123,3 +123,21 @@ def test_watchdog_quiet_on_healthy_run(tmp_path):
     m = _cli(tmp_path, ["--stall_after_s", "60"])
     assert m is not None and m["mode"] == "sisa"
     assert not os.path.exists(tmp_path / "logs" / "watchdog_rank0.json")
+
+
+@pytest.mark.slow
+def test_trace_timeline(tmp_path):
+    """--trace_dir: one Chrome-trace file per rank with phase spans, data-plane spans
+    carrying byte counts, and the marked epoch regions."""
+    _cli(tmp_path, ["--trace_dir", str(tmp_path / "tr")])
+    for r in range(3):
+        ev = json.loads((tmp_path / "tr" / f"trace_rank{r}.json").read_text())["traceEvents"]
+        names = {e["name"] for e in ev}
+        assert "server_training" in names and "eval_breakdown" in names
+        comm = [e for e in ev if e.get("cat") == "comm"]
+        assert comm and all("bytes_sent" in e["args"] for e in comm)
+        assert all(e["dur"] >= 0 for e in ev if e.get("ph") == "X")
+    ev0 = json.loads((tmp_path / "tr" / "trace_rank0.json").read_text())["traceEvents"]
+    assert any(e["name"].startswith("server_epoch[alice") for e in ev0)
+    assert any(e.get("cat") == "comm" and e["args"]["bytes_sent"] > 0
+               for r in range(3) for e in json.loads((tmp_path / "tr" / f"trace_rank{r}.json").read_text())["traceEvents"])
