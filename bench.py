@@ -39,14 +39,24 @@ import torch
 import torch.distributed as dist
 
 BASELINE_SAMPLES_PER_S = 5600.0 / (10.536 + 71.264)
+# per-mode reference numbers (CPU): vanilla ws=2 train phase 5,600 / 32.126 s;
+# the reference's U-shape and concat modes crash, so they have none
+BASELINES = {"sisa": BASELINE_SAMPLES_PER_S, "vanilla": 5600.0 / 32.126, "ushape": None, "concat": None}
 METRIC = "samples/sec (whole node) split-NN MNIST, world_size=2/3/5/9 on 1/2/4/8 MI355X"
+MODELS = {
+    "sisa": "model1_sisa (Alice) + model2_sisa (Bob), SISA round (split_nn.py --sisa)",
+    "concat": "model1_sisa (Alices) + model2_sisa_concat(k) (Bob), SISA-concat round (--sisa --concat)",
+    "vanilla": "model1_sisa (Alice) + model2_sisa (Bob), SGD-m, round-robin iteration (--vanilla)",
+    "ushape": "model1 + model3 (Alice) + model2 (Bob), Adam, round-robin iteration (U-shape default)",
+}
 
 
 def _session_args(a, world_size, log_dir):
     return SimpleNamespace(
         world_size=world_size, client_num_in_total=world_size - 1, epochs=a.epochs, iterations=1,
         batch_size=a.batch_size, partition_alpha=0.5, datapath="", lr=1e-3, server_epochs=a.server_epochs,
-        vanilla=False, sisa=True, concat=False, control=False, mode="sisa", seed=a.seed, log_dir=log_dir,
+        vanilla=a.mode == "vanilla", sisa=a.mode in ("sisa", "concat"), concat=a.mode == "concat", control=False,
+        mode=a.mode, seed=a.seed, log_dir=log_dir,
         no_tqdm=True, true_reset=False, eval_dropout_fix=False, concat_unlearn=False, omit_label=9,
         unlearn_client_ids=[1], save_dir="", resume_dir="", kernels=a.kernels, graphs=a.graphs,
         act_dtype=a.act_dtype)
@@ -68,12 +78,16 @@ def main(argv=None):
     ap.add_argument("--graphs", choices=("auto", "on", "off"), default="auto")
     ap.add_argument("--act_dtype", choices=("fp32", "bf16"), default="fp32",
                     help="SISA activation-cache storage dtype (compute stays fp32)")
+    ap.add_argument("--mode", choices=("sisa", "vanilla", "ushape", "concat"), default="sisa",
+                    help="sisa (headline): one SISA round; vanilla / ushape: one round-robin "
+                         "iteration (every Alice one epoch of split training, weight relay); "
+                         "concat: one SISA-concat round")
     a = ap.parse_args(argv)
 
     from splitlearning_amd import ops
     from splitlearning_amd.data.mnist import synthetic_mnist
     from splitlearning_amd.parallel.dist import Comm, Placement, make_tp_group
-    from splitlearning_amd.protocols.sisa import SisaSession
+    from splitlearning_amd.protocols import SESSIONS
 
     if a.kernels == "torch":
         ops.set_backend("torch")
@@ -97,7 +111,7 @@ def main(argv=None):
     comm = Comm(rank, N, dev, pl, make_tp_group(pl, "nccl" if use_gpu else "gloo") if N > 1 else None)
     S = a.samples_per_client
 
-    class BenchSession(SisaSession):
+    class BenchSession(SESSIONS[a.mode]):
         def _load_client_shard(self, cid):
             x, y = synthetic_mnist(S + 256, seed=1000 + cid)
             return ({"x": torch.from_numpy(x[:S]), "y": torch.from_numpy(y[:S])},
@@ -109,6 +123,10 @@ def main(argv=None):
     all_alices = range(1, k + 1)
 
     def step():
+        if a.mode in ("vanilla", "ushape"):
+            for cid in all_alices:             # split_nn.py:49-52, one iteration
+                sess.train_request(cid)
+            return
         sess.train_request_parallel()
         sess.freeze_alice_weights(all_alices)
         sess.reset_activation_cache()          # the fronts changed: rebuild the cut-layer cache
@@ -140,10 +158,9 @@ def main(argv=None):
             "metric": METRIC, "value": round(value, 2), "unit": "samples/s", "n_gpus": N,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(1000 * dt / a.steps, 3),
             "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": round(value / BASELINE_SAMPLES_PER_S, 2),
+            "vs_baseline": round(value / BASELINES[a.mode], 2) if BASELINES[a.mode] else None,
             "dtype": "fp32", "data": "synthetic",
-            "config": {"model": "model1_sisa (Alice) + model2_sisa (Bob), SISA round (split_nn.py --sisa)",
-                       "mode": "sisa", "world_size": ws, "global_batch": a.batch_size,
+            "config": {"model": MODELS[a.mode], "mode": a.mode, "world_size": ws, "global_batch": a.batch_size,
                        "samples_per_client": S, "seq_len": None,
                        "parallelism": f"alices{k}_one_per_gpu+bob_tp{pl.bob_tp}",
                        "device": "MI355X" if use_gpu else "cpu", "kernels": kern,

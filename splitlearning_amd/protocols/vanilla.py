@@ -73,6 +73,60 @@ class VanillaSession(Session):
         if a is not None:
             a.front.backward_step(dx, act, am, a.train, idx, a.slot)
 
+    def split_epoch(self, cid: int, order, n: int):
+        """Split training of Alice_cid over `order` (n samples), pipelined so Bob never
+        re-reads fc1 for a forward: per batch i, Bob's forward + CE + data gradients, the
+        cut gradient to Alice, Alice's backward + step, Alice's forward of batch i+1 (sent
+        to Bob), and only then Bob's wgrad + optimizer, whose kernel also forms batch i+1's
+        fc1 product with the freshly updated weights (look-ahead, TailEngine.fused_step).
+        Same math and update order as `split_step` per batch (both sides step on batch i
+        before either runs batch i+1); on one GPU the reordering is free because the
+        launches were serial anyway."""
+        B = self.B
+        a = self.alices.get(cid)
+        host = self.host(cid)
+        spans = [(s, min(s + B, n)) for s in range(0, n, B)]
+        if not spans:
+            return
+        la = self.is_bob and self.tail.fused3_ok() and self.tail.lookahead_ok(B)
+
+        def alice_fwd(span):
+            s, e = span
+            idx = order[s:e] if order is not None else None
+            act = am = labels = None
+            if a is not None:
+                act, am = a.front.forward(a.train, idx)
+                labels = a.train.y[idx]
+            act_b, lab_b = self.send_act_labels(cid, act, labels, e - s)
+            return idx, act, am, act_b, lab_b
+
+        cur = alice_fwd(spans[0])
+        pre = False
+        for i, (s, e) in enumerate(spans):
+            idx, act, am, act_b, lab_b = cur
+            M = e - s
+            dxp = None
+            fused = self.is_bob and self.tail.fused3_ok()
+            if self.is_bob:
+                if fused:
+                    _, dxp = self.tail.train_fwd_bwd3(act_b, lab_b, need_dx=True, pre=pre)
+                else:
+                    out = self.tail.forward(act_b, train=True)
+                    _, dout = self.ops.softmax_ce(out, lab_b, 1.0 / M)
+                    dxp = self.tail.backward_dgrad(dout, need_dx=True)
+            dx = self.comm.reduce_to(dxp, host, self.bob_ranks, (M, CUT_FEATURES), torch.float32)
+            if a is not None:
+                a.front.backward_step(dx, act, am, a.train, idx, a.slot)
+            nxt = alice_fwd(spans[i + 1]) if i + 1 < len(spans) else None
+            if self.is_bob:
+                if fused:
+                    x_next = nxt[3] if (la and nxt is not None and nxt[3].shape[0] <= 16) else None
+                    self.tail.fused_step(self.bob_slot(cid), x_next=x_next)
+                    pre = x_next is not None
+                else:
+                    self.tail.backward_step(self.bob_slot(cid))
+            cur = nxt
+
     def _order_len(self, cid, order):
         n = torch.tensor([order.numel() if order is not None else 0], dtype=torch.int64, device=self.device)
         n = self.comm.multicast(n if self.hosts(cid) else None, self.host(cid),
@@ -98,10 +152,7 @@ class VanillaSession(Session):
         for _ in _progress(range(self.args.epochs), self.show, desc="Epochs", ascii=" >="):
             a = self.alices.get(cid)
             order = a.train.shuffled_order(a.gen) if a is not None else None
-            n = self.n_train[cid]
-            for s in range(0, n, self.B):
-                e = min(s + self.B, n)
-                self.split_step(cid, order[s:e] if order is not None else None, e - s)
+            self.split_epoch(cid, order, self.n_train[cid])
 
     def unlearn_request(self, client_id: int, omit_label: int):
         self.bob_log.info(f"Unlearn Request for Alice-{client_id}")
@@ -118,9 +169,7 @@ class VanillaSession(Session):
         self.bob_slots[client_id] = OptSlot(self.bob_optim())  # ... with a fresh Bob-side state
         n = self._order_len(client_id, order)
         for _ in _progress(range(self.args.epochs), self.show, desc="Epochs", ascii=" >="):
-            for s in range(0, n, self.B):
-                e = min(s + self.B, n)
-                self.split_step(client_id, order[s:e] if order is not None else None, e - s)
+            self.split_epoch(client_id, order, n)
 
     def inference(self, x):
         return self.tail.forward(x)

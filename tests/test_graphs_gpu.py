@@ -180,3 +180,38 @@ def test_wgrad_group_lookahead_kernel(cuda):
     W_new = Wref - 1e-2 * (dz.t() @ A)          # first SGD-momentum step: buf = g
     torch.testing.assert_close(W, W_new, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(pn.sum(0), xn @ W.t(), rtol=1e-4, atol=1e-3)
+
+
+def _vanilla_session(cuda, tmp_path):
+    from splitlearning_amd.config import parse_args
+    from splitlearning_amd.data.mnist import write_shards
+    from splitlearning_amd.parallel.dist import Comm, Placement
+    from splitlearning_amd.protocols import VanillaSession
+    args = parse_args(["--vanilla", "--world_size", "2", "--seed", "5", "--num_samples", "1500", "--no_tqdm",
+                       "--datapath", str(tmp_path / "d"), "--log_dir", str(tmp_path / "logs")])
+    if not (tmp_path / "d").exists():
+        write_shards(args, verbose=False)
+    comm = Comm(0, 1, cuda, Placement.make(2, 1, 1))
+    return VanillaSession(args, comm, cuda)
+
+
+def test_vanilla_pipelined_epoch_matches_per_batch_steps(cuda, tmp_path):
+    """split_epoch (Alice's next forward before Bob's update, fc1 look-ahead in Bob's
+    wgrad kernel) follows the same trajectory as one split_step per batch."""
+    sa = _vanilla_session(cuda, tmp_path)
+    sb = _vanilla_session(cuda, tmp_path)
+    assert sb.tail.lookahead_ok(16)
+    a = sa.alices[1]
+    order = a.train.shuffled_order(torch.Generator().manual_seed(9))[:16 * 6 + 5]   # a partial last batch
+    n = order.numel()
+    for s in range(0, n, 16):
+        sa.split_step(1, order[s:s + 16], min(16, n - s))
+    sb.split_epoch(1, order, n)
+    torch.cuda.synchronize()
+    for L1, L2 in zip(sa.tail.layers, sb.tail.layers):
+        d = (L1.W - L2.W).abs()
+        assert d.max().item() < 1e-2 and (d > 1e-4).float().mean().item() < 1e-4
+    wa = sa.alices[1].front.module.state_dict()
+    wb = sb.alices[1].front.module.state_dict()
+    for k in wa:
+        torch.testing.assert_close(wa[k], wb[k], rtol=1e-3, atol=1e-4)
