@@ -19,7 +19,8 @@
 
 namespace sl {
 hipError_t conv_fwd(const void* x, bool x_u8, const int64_t* idx, int64_t row0, int B, const float* w,
-                    const float* b, float* y, uint8_t* am, hipStream_t st);
+                    const float* b, float* y, uint8_t* am, hipStream_t st, const int64_t* lab_in,
+                    int64_t* lab_out);
 hipError_t conv_local_step(const void* x, bool x_u8, const int64_t* idx, const int64_t* labels, int B, float* w,
                            float* b, float* slab, float* loss_rows, float* s0w, float* s1w, float* s0b, float* s1b,
                            SlOpt o, hipStream_t st);
@@ -45,6 +46,7 @@ hipError_t linear_wgrad_opt(const float* dZ, int ldz, const float* A, int lda, f
                             float* s1, float* bias, float* sb0, float* sb1, int M, int N, int K, SlOpt o,
                             hipStream_t st);
 hipError_t opt_flat(float* p, const float* g, float* s0, float* s1, int64_t n, SlOpt o, hipStream_t st);
+hipError_t relu_mask(const float* d, const float* h, float scale, float* out, int64_t n, hipStream_t st);
 hipError_t softmax_ce(const float* x, int ldx, const int64_t* y, int64_t ignore, float scale, float* loss_rows,
                       float* d, int ldd, int M, int C, hipStream_t st);
 hipError_t eval_counters(const float* x, int ldx, const int64_t* y, int64_t omit, unsigned long long* counters,
@@ -136,17 +138,32 @@ void check_slab(const at::Tensor& slab, int64_t B) {
   TORCH_CHECK(slab.is_contiguous() && slab.numel() >= B * 320, "slab workspace [B,320]");
 }
 
+// lab_in / lab_out (optional, together): the shard's labels [N] and the batch's gathered
+// labels [B], written by the forward kernel (no separate index launch).
 void conv_fwd(const at::Tensor& x, const at::Tensor& idx, int64_t B, const at::Tensor& w, const at::Tensor& b,
-              at::Tensor& y, at::Tensor& am) {
+              at::Tensor& y, at::Tensor& am, const OptT& lab_in, const OptT& lab_out) {
   check_x(x);
   check_params(w, b);
   check_idx(idx, B);
   need_f32(y, "y");
   TORCH_CHECK(y.is_contiguous() && y.numel() >= B * 5408, "y too small");
   TORCH_CHECK(am.scalar_type() == at::kByte && am.is_contiguous() && am.numel() >= B * 5408, "am too small");
+  TORCH_CHECK(lab_in.has_value() == lab_out.has_value(), "lab_in and lab_out go together");
+  const int64_t* li = nullptr;
+  int64_t* lo = nullptr;
+  if (lab_in.has_value()) {
+    need_cuda(*lab_in, "lab_in");
+    need_cuda(*lab_out, "lab_out");
+    TORCH_CHECK(lab_in->scalar_type() == at::kLong && lab_in->is_contiguous() && lab_in->numel() == x.numel() / 784,
+                "lab_in int64 [N]");
+    TORCH_CHECK(lab_out->scalar_type() == at::kLong && lab_out->is_contiguous() && lab_out->numel() >= B,
+                "lab_out int64 [B]");
+    li = lab_in->data_ptr<int64_t>();
+    lo = lab_out->data_ptr<int64_t>();
+  }
   check(sl::conv_fwd(x.data_ptr(), x.scalar_type() == at::kByte, idx.data_ptr<int64_t>(), 0, (int)B,
                      w.data_ptr<float>(), b.data_ptr<float>(), y.data_ptr<float>(), am.data_ptr<uint8_t>(),
-                     cur_stream()),
+                     cur_stream(), li, lo),
         "conv_fwd");
 }
 
@@ -371,6 +388,18 @@ void softmax_ce(const at::Tensor& x, const at::Tensor& y, int64_t ignore, double
         "softmax_ce");
 }
 
+void relu_mask(const at::Tensor& d, const at::Tensor& h, double scale, at::Tensor& out) {
+  need_f32(d, "d");
+  need_f32(h, "h");
+  need_f32(out, "out");
+  TORCH_CHECK(d.is_contiguous() && h.is_contiguous() && out.is_contiguous() && d.numel() == h.numel() &&
+                  out.numel() == d.numel(),
+              "relu_mask: contiguous tensors of one size");
+  check(sl::relu_mask(d.data_ptr<float>(), h.data_ptr<float>(), (float)scale, out.data_ptr<float>(), d.numel(),
+                      cur_stream()),
+        "relu_mask");
+}
+
 void eval_counters(const at::Tensor& x, const at::Tensor& y, int64_t omit, at::Tensor& counters) {
   need_2d(x, "logits");
   TORCH_CHECK(y.scalar_type() == at::kLong && y.numel() == x.size(0) && y.is_contiguous(), "labels");
@@ -532,6 +561,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("opt_flat", &opt_flat);
   m.def("softmax_ce", &softmax_ce);
   m.def("eval_counters", &eval_counters);
+  m.def("relu_mask", &relu_mask);
   m.def("server_head3", &server_head3);
   m.def("head3_slices", [](int64_t n2) { return (int64_t)sl::head3_slices((int)n2); });
   m.def("linear_fwd_partial", &linear_fwd_partial);

@@ -121,6 +121,22 @@ eval_counters_kernel(const float* __restrict__ x, int ldx, const int64_t* __rest
   if (threadIdx.x < 6 && part[threadIdx.x]) atomicAdd(&counters[threadIdx.x], (unsigned long long)part[threadIdx.x]);
 }
 
+// ReLU / dropout backward of a layer's own output: out = dout * scale * [h > 0] (the last
+// layer of the U-shape middle, model2's fc2 + ReLU).  One launch instead of three eager
+// elementwise ops (compare, multiply, multiply).
+__global__ void __launch_bounds__(256)
+relu_mask_kernel(const float* __restrict__ d, const float* __restrict__ h, float scale, float* __restrict__ out,
+                 int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = h[i] > 0.f ? d[i] * scale : 0.f;
+}
+
+hipError_t relu_mask(const float* d, const float* h, float scale, float* out, int64_t n, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  relu_mask_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(d, h, scale, out, n);
+  return hipGetLastError();
+}
+
 hipError_t softmax_ce(const float* x, int ldx, const int64_t* y, int64_t ignore, float scale, float* loss_rows,
                       float* d, int ldd, int M, int C, hipStream_t st) {
   if (M <= 0) return hipSuccess;

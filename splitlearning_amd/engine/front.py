@@ -31,8 +31,11 @@ class FrontEngine:
         w, b = self.module.conv_params()
         return w.data, b.data
 
-    def forward(self, shard: DeviceShard, idx: torch.Tensor):
+    def forward(self, shard: DeviceShard, idx: torch.Tensor, with_labels: bool = False):
+        """(activation, argmax); with_labels: (activation, argmax, shard.y[idx]) from one launch."""
         w, b = self.params
+        if with_labels:
+            return self.ops.conv_front_fwd(shard.x, idx, w, b, labels=shard.y)
         return self.ops.conv_front_fwd(shard.x, idx, w, b)
 
     def forward_chunked(self, shard: DeviceShard, idx: torch.Tensor, chunk: int = 8192) -> torch.Tensor:

@@ -122,7 +122,7 @@ class TailEngine:
         dz = dout
         if last.relu or (last.dropout and self._train_fwd):
             scale = 1.0 / (1.0 - last.dropout) if (last.dropout and self._train_fwd) else 1.0
-            dz = dout * (self.acts[-1] > 0) * scale
+            dz = self.ops.relu_mask(dout, self.acts[-1], scale)
         dzs = [None] * n
         dzs[n - 1] = dz
         dx = None

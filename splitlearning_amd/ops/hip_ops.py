@@ -52,14 +52,17 @@ def _slab(device, B):
 
 
 # ---------------------------------------------------------------- conv front
-def conv_front_fwd(x_u8, idx, w, b, y=None, am=None):
+def conv_front_fwd(x_u8, idx, w, b, y=None, am=None, labels=None):
+    """(y, am); with `labels` (the shard's [N] labels) also the batch's labels, gathered by
+    the same kernel: (y, am, labels[idx])."""
     B = int(idx.numel())
     if y is None:
         y = torch.empty(B, CUT, device=x_u8.device, dtype=torch.float32)
     if am is None:
         am = torch.empty(B, CUT, device=x_u8.device, dtype=torch.uint8)
-    C().conv_fwd(x_u8, idx, B, w.detach(), b.detach(), y, am)
-    return y, am
+    lab = None if labels is None else torch.empty(B, device=x_u8.device, dtype=torch.int64)
+    C().conv_fwd(x_u8, idx, B, w.detach(), b.detach(), y, am, labels, lab)
+    return (y, am) if labels is None else (y, am, lab)
 
 
 def conv_front_bwd(dy, y, am, x_u8, idx, w, b):
@@ -242,6 +245,13 @@ def softmax_ce(logits, labels, scale: float, ignore_index: int = -100, d_out=Non
     d = torch.empty_like(logits) if d_out is None else d_out
     C().softmax_ce(logits, labels, int(ignore_index), float(scale), loss, d)
     return loss, d
+
+
+def relu_mask(d, h, scale: float = 1.0):
+    """d * scale * [h > 0] (a layer's own ReLU/dropout backward)."""
+    out = torch.empty_like(d)
+    C().relu_mask(d.contiguous(), h.contiguous(), float(scale), out)
+    return out
 
 
 def eval_counters(logits, labels, omit_label: int, counters=None):

@@ -18,11 +18,14 @@ CUT = 5408
 
 
 # ---------------------------------------------------------------- conv front
-def conv_front_fwd(x_u8: torch.Tensor, idx: torch.Tensor, w: torch.Tensor, b: torch.Tensor):
+def conv_front_fwd(x_u8: torch.Tensor, idx: torch.Tensor, w: torch.Tensor, b: torch.Tensor, labels=None):
     """Gather rows `idx` of the uint8 shard, conv3x3(1->32)+bias, ReLU, maxpool2x2.
 
-    Returns (y [B,5408] fp32 NCHW-flattened, am uint8 [B,5408] argmax-in-window 0..3).
+    Returns (y [B,5408] fp32 NCHW-flattened, am uint8 [B,5408] argmax-in-window 0..3),
+    plus `labels[idx]` when the shard's labels are given.
     """
+    if labels is not None:
+        return conv_front_fwd(x_u8, idx, w, b) + (labels.index_select(0, idx),)
     x = x_u8.index_select(0, idx).to(torch.float32).reshape(-1, 1, 28, 28)
     z = F.relu(F.conv2d(x, w, b))
     y, ind = F.max_pool2d(z, 2, 2, return_indices=True)
@@ -168,6 +171,11 @@ def softmax_ce(logits, labels, scale: float, ignore_index: int = -100):
     p.scatter_add_(1, safe.view(-1, 1), -torch.ones_like(picked).view(-1, 1))
     d = p * scale * valid.view(-1, 1)
     return loss, d
+
+
+def relu_mask(d, h, scale: float = 1.0):
+    """d * scale * [h > 0] (a layer's own ReLU/dropout backward)."""
+    return d * (h > 0) * scale
 
 
 def eval_counters(logits, labels, omit_label: int):

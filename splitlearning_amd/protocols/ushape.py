@@ -84,9 +84,9 @@ class UShapeSession(Session):
     def split_step(self, cid: int, idx, B: int):
         host = self.host(cid)
         a = self.alices.get(cid)
-        act = am = None
+        act = am = labels = None
         if a is not None:
-            act, am = a.front.forward(a.train, idx)
+            act, am, labels = a.front.forward(a.train, idx, with_labels=True)
         act_b = self.to_bob(cid, act, (B, CUT_FEATURES))
         out = self.tail.forward(act_b, train=True) if self.is_bob else None
         mid = self.from_bob(cid, out, (B, 100))
@@ -94,7 +94,7 @@ class UShapeSession(Session):
         t = None
         if a is not None:
             logits = a.head.forward(mid, train=True)
-            _, dlog = self.ops.softmax_ce(logits, a.train.y[idx], 1.0 / B)
+            _, dlog = self.ops.softmax_ce(logits, labels, 1.0 / B)
             dmid = a.head.backward_dgrad(dlog, need_dx=True)
             t = a.slot.tick()
             a.head.backward_step(a.slot, t, prefix="head.")

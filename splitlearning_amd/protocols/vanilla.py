@@ -51,8 +51,7 @@ class VanillaSession(Session):
         a = self.alices.get(cid)
         act = am = labels = None
         if a is not None:
-            act, am = a.front.forward(a.train, idx)
-            labels = a.train.y[idx]
+            act, am, labels = a.front.forward(a.train, idx, with_labels=True)
         act_b, lab_b = self.send_act_labels(cid, act, labels, B)
         dxp = None
         fused = self.is_bob and self.tail.fused3_ok()
@@ -95,8 +94,7 @@ class VanillaSession(Session):
             idx = order[s:e] if order is not None else None
             act = am = labels = None
             if a is not None:
-                act, am = a.front.forward(a.train, idx)
-                labels = a.train.y[idx]
+                act, am, labels = a.front.forward(a.train, idx, with_labels=True)
             act_b, lab_b = self.send_act_labels(cid, act, labels, e - s)
             return idx, act, am, act_b, lab_b
 

@@ -37,6 +37,9 @@ def test_conv_fwd(cuda, B):
     # argmax agrees except on near-ties, where fp summation order may pick the other window cell
     mism = (am[pos] != amr[pos]).float().mean().item()
     assert mism < 1e-4
+    labels = torch.randint(0, 10, (1000,), device=cuda)
+    y2, am2, lab = hip_ops.conv_front_fwd(x, idx, w, b, labels=labels)     # labels gathered in passing
+    assert torch.equal(lab, labels[idx]) and torch.equal(y2, y) and torch.equal(am2, am)
 
 
 @pytest.mark.parametrize("kind", ["grad", "sgd", "adam"])
@@ -272,3 +275,9 @@ def test_server_head3(cuda, M, S2, N2, C):
     _close(loss, lossr, rtol=1e-4, atol=1e-5)
     _close(dlog, dlogr, rtol=1e-4, atol=1e-6)
     _close(dz2, dz2r, rtol=1e-4, atol=1e-6)
+
+
+def test_relu_mask(cuda):
+    g = torch.Generator().manual_seed(11)
+    d, h = torch.randn(16, 100, generator=g).to(cuda), torch.randn(16, 100, generator=g).to(cuda)
+    torch.testing.assert_close(hip_ops.relu_mask(d, h, 2.0), torch_ops.relu_mask(d, h, 2.0))
