@@ -37,6 +37,24 @@ __device__ __forceinline__ float sl_wave_max(float v) {
   return v;
 }
 
+// ------------------------------------------------------------------ partial-sum slabs
+// Sum of S split-K / split-N partials p[0], p[slab], ...: up to 32 slabs are loaded with
+// every load issued before the first add (one memory round trip instead of S / 4), in
+// slab order so the result is bit-identical to the sequential sum.
+__device__ __forceinline__ float sum_slabs(const float* __restrict__ p, int S, int64_t slab) {
+  constexpr int U = 32;
+  float v = 0.f;
+  int s0 = 0;
+  for (; s0 < S; s0 += U) {
+    float r[U];
+#pragma unroll
+    for (int i = 0; i < U; ++i) r[i] = (s0 + i < S) ? p[(int64_t)(s0 + i) * slab] : 0.f;
+#pragma unroll
+    for (int i = 0; i < U; ++i) v += r[i];
+  }
+  return v;
+}
+
 // ------------------------------------------------------------------ optimizer
 // kind: 0 = write gradient only (p untouched, grad -> s0), 1 = SGD(momentum), 2 = Adam (L2 wd).
 struct SlOpt {

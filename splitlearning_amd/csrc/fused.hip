@@ -233,8 +233,11 @@ wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
         float v = 0.f;
         if (mr < M && nn < L.N) {
           if (PART && L.dzp) {
-            for (int s = 0; s < L.S; ++s) v += L.dzp[s * L.slab + (int64_t)mr * L.N + nn];
-            if (L.hmask) v = L.hmask[(int64_t)mr * L.N + nn] > 0.f ? v * L.mscale : 0.f;
+            // every slab load (and the mask load) in flight at once: bit-identical to
+            // dgrad_reduce_kernel's sum, one round trip instead of S dependent ones
+            const float hm = L.hmask ? L.hmask[(int64_t)mr * L.N + nn] : 1.f;
+            v = sum_slabs(L.dzp + (int64_t)mr * L.N + nn, L.S, L.slab);
+            if (L.hmask) v = hm > 0.f ? v * L.mscale : 0.f;
           } else {
             v = L.dz[(int64_t)mr * L.ldz + nn];
           }

@@ -212,8 +212,10 @@ class TailEngine:
         s1 = 1.0 / (1.0 - p1) if p1 else 1.0
         dx = None
         # dz1 is materialised (split-N dgrad + reduce/mask kernel): reducing the split-N
-        # slabs inside the wgrad staging put ~9 dependent L2 loads per element on every
-        # workgroup's critical path (measured 166 vs 120 us on fc1), a net loss.
+        # slabs inside the wgrad staging (every slab load issued at once) measured 250 vs
+        # 185 us per step at TP = 1 and 62 vs 56 at TP = 8: all ~8000 workgroups re-read
+        # the slabs of their 16 columns, ~9x the L2 traffic of reading dz1, on every
+        # workgroup's critical path.
         dz1 = ops.linear_dgrad(dz2, L2.W, h1, s1)
         if need_dx:
             dx = ops.linear_dgrad(dz1, L1.W, None, 1.0)
