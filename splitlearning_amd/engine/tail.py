@@ -87,19 +87,27 @@ class TailEngine:
         self._pre = None          # pending look-ahead fc1 partial slabs (see fused_step)
 
     # ------------------------------------------------------------------ forward
-    def forward(self, x: torch.Tensor, train: bool | None = None, dseeds=None) -> torch.Tensor:
-        """`dseeds[i]` (graph replay only): device int32[2] holding layer i's dropout seed."""
+    def forward(self, x: torch.Tensor, train: bool | None = None, dseeds=None, pre: bool = False) -> torch.Tensor:
+        """`dseeds[i]` (graph replay only): device int32[2] holding layer i's dropout seed.
+        `pre`: layer 0's product for `x` was formed by the previous `group_step(x_next=x)`;
+        only its epilogue runs here."""
         train = self.training if train is None else train
         self.fwd_count += 1
         step = self.fwd_count
         acts = [x]
         h = x
+        P0 = None
+        if pre:
+            P0, self._pre = self._pre, None
+            assert P0 is not None and P0.shape[1] == x.shape[0], "no pending look-ahead for this batch"
         for i, L in enumerate(self.layers):
             ls = L.spec
             drop = ls.dropout if train else 0.0
             seed = step_seed(self.seed_base, i, step)
             kw = {} if dseeds is None else {"dseed": dseeds[i]}
-            if L.style == "row":
+            if i == 0 and pre:
+                h = self.ops.linear_epilogue(P0, L.b, ls.relu, drop, seed, L.col_off, **kw)
+            elif L.style == "row":
                 part = self.ops.linear_fwd(h, L.W, None, False, 0.0, 0, 0)
                 self.allreduce(part)
                 h = self.ops.linear_epilogue(part, L.b, ls.relu, drop, seed, 0, **kw)
@@ -148,6 +156,29 @@ class TailEngine:
             self.ops.linear_wgrad_step_(self.dz[i], self.acts[i], L.W, L.b, slot.cfg,
                                         slot.state(f"{prefix}{L.spec.name}.weight", L.W),
                                         slot.state(f"{prefix}{L.spec.name}.bias", L.b), t, **kw)
+        self.dz = []
+
+    def grouped_ok(self, m: int = 0) -> bool:
+        """Whether `group_step` can run (HIP backend, <= 3 layers); with `m`, also whether it
+        can form the next batch's layer-0 product for m rows (look-ahead)."""
+        ok = hasattr(self.ops, "wgrad_group_") and 0 < len(self.layers) <= 3
+        if m:
+            ok = ok and hasattr(self.ops, "lookahead_slabs") and 0 < m <= 16
+        return ok
+
+    def group_step(self, slot: OptSlot, t: int | None = None, prefix: str = "", x_next=None):
+        """`backward_step` in ONE launch (every layer's wgrad + optimizer, wgrad_group_), after
+        `backward_dgrad`.  `x_next`: also form the next batch's layer-0 product with the updated
+        weights, consumed by `forward(x_next, pre=True)` (no separate read of W0)."""
+        t = slot.tick() if t is None else t
+        layers = [(self.dz[i], None, None, 1.0, self.acts[i], L.W, slot.state(f"{prefix}{L.spec.name}.weight", L.W),
+                   L.b, slot.state(f"{prefix}{L.spec.name}.bias", L.b)) for i, L in enumerate(self.layers)]
+        pn = None
+        if x_next is not None:
+            assert self.grouped_ok(x_next.shape[0])
+            pn = self.lookahead_slabs(x_next.shape[0])
+        self.ops.wgrad_group_(layers, self.acts[0].shape[0], slot.cfg, t, None, x_next=x_next, p_next=pn)
+        self._pre = pn
         self.dz = []
 
     # ------------------------------------------------------------------ fused 3-layer step

@@ -107,13 +107,64 @@ class UShapeSession(Session):
         if a is not None:
             a.front.backward_step(dx, act, am, a.train, idx, a.slot, t=t, prefix="front.")
 
+    def split_epoch(self, cid: int, order, n: int):
+        """U-shape training of Alice_cid over `order` (n samples), pipelined like
+        VanillaSession.split_epoch: per batch i, Bob's forward, the head + CE + head step on
+        Alice, Bob's data gradients, Alice's conv backward + step and her forward of batch
+        i+1 (sent to Bob) — and only then Bob's wgrad + Adam of both layers in one launch,
+        which also forms batch i+1's fc1 product with the updated weights (no separate fc1
+        forward read).  Same per-batch math and update order as `split_step`."""
+        B = self.B
+        a = self.alices.get(cid)
+        host = self.host(cid)
+        spans = [(s, min(s + B, n)) for s in range(0, n, B)]
+        if not spans:
+            return
+        grouped = self.is_bob and self.tail.grouped_ok()
+
+        def alice_fwd(span):
+            s, e = span
+            idx = order[s:e] if order is not None else None
+            act = am = labels = None
+            if a is not None:
+                act, am, labels = a.front.forward(a.train, idx, with_labels=True)
+            return idx, act, am, labels, self.to_bob(cid, act, (e - s, CUT_FEATURES))
+
+        cur = alice_fwd(spans[0])
+        pre = False
+        for i, (s, e) in enumerate(spans):
+            idx, act, am, labels, act_b = cur
+            M = e - s
+            out = self.tail.forward(act_b, train=True, pre=pre) if self.is_bob else None
+            mid = self.from_bob(cid, out, (M, 100))
+            dmid = t = None
+            if a is not None:
+                logits = a.head.forward(mid, train=True)
+                _, dlog = self.ops.softmax_ce(logits, labels, 1.0 / M)
+                dmid = a.head.backward_dgrad(dlog, need_dx=True)
+                t = a.slot.tick()
+                a.head.backward_step(a.slot, t, prefix="head.")
+            dmid_b = self.to_bob(cid, dmid, (M, 100))
+            dxp = self.tail.backward_dgrad(dmid_b, need_dx=True) if self.is_bob else None
+            dx = self.comm.reduce_to(dxp, host, self.bob_ranks, (M, CUT_FEATURES), torch.float32)
+            if a is not None:
+                a.front.backward_step(dx, act, am, a.train, idx, a.slot, t=t, prefix="front.")
+            nxt = alice_fwd(spans[i + 1]) if i + 1 < len(spans) else None
+            pre = False
+            if self.is_bob:
+                if grouped:
+                    x_next = nxt[4] if (nxt is not None and self.tail.grouped_ok(nxt[4].shape[0])) else None
+                    self.tail.group_step(self.bob_slot(cid), x_next=x_next)
+                    pre = x_next is not None
+                else:
+                    self.tail.backward_step(self.bob_slot(cid))
+            cur = nxt
+
     def _run_epochs(self, cid: int, order_fn, n: int):
         for _ in _progress(range(self.args.epochs), self.show, desc="Epochs", ascii=" >="):
             a = self.alices.get(cid)
             order = order_fn(a) if a is not None else None
-            for s in range(0, n, self.B):
-                e = min(s + self.B, n)
-                self.split_step(cid, order[s:e] if order is not None else None, e - s)
+            self.split_epoch(cid, order, n)
 
     # ------------------------------------------------------------------ Bob API
     def train_request(self, client_id: int):

@@ -215,3 +215,30 @@ def test_vanilla_pipelined_epoch_matches_per_batch_steps(cuda, tmp_path):
     wb = sb.alices[1].front.module.state_dict()
     for k in wa:
         torch.testing.assert_close(wa[k], wb[k], rtol=1e-3, atol=1e-4)
+
+
+def test_ushape_pipelined_epoch_matches_per_batch_steps(cuda, tmp_path):
+    """U-shape split_epoch (grouped Bob step with the fc1 look-ahead) == per-batch split_step."""
+    from splitlearning_amd.config import parse_args
+    from splitlearning_amd.data.mnist import write_shards
+    from splitlearning_amd.parallel.dist import Comm, Placement
+    from splitlearning_amd.protocols import UShapeSession
+    args = parse_args(["--world_size", "2", "--seed", "6", "--num_samples", "1500", "--no_tqdm",
+                       "--datapath", str(tmp_path / "d"), "--log_dir", str(tmp_path / "logs")])
+    write_shards(args, verbose=False)
+    mk = lambda: UShapeSession(args, Comm(0, 1, cuda, Placement.make(2, 1, 1)), cuda)  # noqa: E731
+    sa, sb = mk(), mk()
+    assert sb.tail.grouped_ok(16)
+    order = sa.alices[1].train.shuffled_order(torch.Generator().manual_seed(3))[:16 * 6 + 7]
+    n = order.numel()
+    for s in range(0, n, 16):
+        sa.split_step(1, order[s:s + 16], min(16, n - s))
+    sb.split_epoch(1, order, n)
+    torch.cuda.synchronize()
+    for L1, L2 in zip(sa.tail.layers, sb.tail.layers):
+        d = (L1.W - L2.W).abs()
+        assert d.max().item() < 1e-2 and (d > 1e-4).float().mean().item() < 1e-4
+    for ma, mb in ((sa.alices[1].front.module, sb.alices[1].front.module),
+                   (sa.alices[1].head.module, sb.alices[1].head.module)):
+        for (k, va), vb in zip(ma.state_dict().items(), mb.state_dict().values()):
+            torch.testing.assert_close(va, vb, rtol=1e-3, atol=1e-4, msg=k)
