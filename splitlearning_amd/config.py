@@ -59,8 +59,9 @@ def build_parser() -> argparse.ArgumentParser:
                    help="tensor-parallel degree of Bob's server tail (0 = all processes on GPU, 1 on CPU)")
     g.add_argument("--backend", choices=("auto", "nccl", "gloo"), default="auto")
     g.add_argument("--act_dtype", choices=("fp32", "bf16"), default="fp32",
-                   help="storage/transfer dtype of SISA's cached cut activations (compute stays fp32; "
-                        "bf16 halves the dump traffic and the cache, rounding the activations)")
+                   help="wire dtype of every cut-layer activation transfer (per-batch vanilla / U-shape "
+                        "messages, eval, SISA's dump and cache); compute stays fp32; bf16 halves the "
+                        "traffic, rounding the activations")
     g.add_argument("--kernels", choices=("auto", "hip", "torch"), default="auto",
                    help="compute path: hand-written HIP kernels (GPU) or torch ops")
     g.add_argument("--seed", type=int, default=None, help="seed everything (reference is unseeded)")

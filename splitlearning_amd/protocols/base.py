@@ -193,6 +193,22 @@ class Session:
             return t
         return out
 
+    @property
+    def act_dtype(self):
+        """Wire / cache dtype of cut-layer activations (`--act_dtype`): bf16 halves every
+        activation transfer (and SISA's cache); compute stays fp32."""
+        return torch.bfloat16 if getattr(self.args, "act_dtype", "fp32") == "bf16" else torch.float32
+
+    def act_to_bob(self, cid: int, act, B: int):
+        """Cut activation [B, cut] Alice_cid -> every Bob rank in the wire dtype, fp32 on arrival.
+        With a bf16 wire the host rounds its own copy too, so every Bob rank (and every
+        placement of the roles) sees the same input."""
+        wire = self.act_dtype
+        if wire != torch.float32 and act is not None:
+            act = act.to(wire)
+        got = self.to_bob(cid, act, (B, self.cut_width_in()), wire)
+        return got.float() if (got is not None and wire != torch.float32) else got
+
     def to_bob_var(self, cid: int, t, inner_shape, dtype):
         """Variable-length Alice -> Bob transfer (length header first)."""
         n = torch.tensor([t.shape[0] if t is not None else 0], dtype=torch.int64, device=self.device)
@@ -221,16 +237,20 @@ class Session:
     def send_act_labels(self, cid, act, labels, B):
         """Cut activation + labels Alice -> Bob, packed into one message when remote."""
         host = self.host(cid)
+        wire = self.act_dtype
+        if wire != torch.float32 and act is not None:
+            act = act.to(wire).float()             # every Bob rank sees the rounded input
         remote = [r for r in self.bob_ranks if r != host]
         if not remote:
             return (act, labels) if self.is_bob else (None, None)
-        pkt = self.pack(act, labels) if self.rank == host else None
-        got = self.comm.multicast(pkt, host, self.bob_ranks, (B * CUT_FEATURES + B,), torch.float32)
+        pkt = self.pack(act.to(wire), labels) if self.rank == host else None
+        got = self.comm.multicast(pkt, host, self.bob_ranks, (B * CUT_FEATURES + B,), wire)
         if not self.is_bob:
             return None, None
         if self.rank == host:
             return act, labels
-        return self.unpack(got, B)
+        a, lab = self.unpack(got, B)
+        return a.float(), lab
 
     # ------------------------------------------------------------------ shared Alice API
     def give_weights(self, cid: int) -> dict:
@@ -295,7 +315,7 @@ class Session:
     def _bob_logits_for(self, cid: int, act):
         """Bob's inference on Alice_cid's activations; logits delivered to Alice_cid."""
         n = self.n_test[cid]
-        act_b = self.to_bob(cid, act, (n, self.cut_width_in()), torch.float32)
+        act_b = self.act_to_bob(cid, act, n)
         out = None
         if self.is_bob:
             out = self.bob_infer(act_b, cid)

@@ -132,11 +132,6 @@ class SisaSession(Session):
             acts = acts.to(self.act_dtype)
         return acts, a.train.y[order]
 
-    @property
-    def act_dtype(self):
-        """Storage / transfer dtype of the cached cut activations (`--act_dtype`)."""
-        return torch.bfloat16 if getattr(self.args, "act_dtype", "fp32") == "bf16" else torch.float32
-
     def get_activation_and_labels(self, client_id: int, unlearned: bool = False, unlearn_id=None):
         key = (client_id, unlearned, unlearn_id)
         hit = self.activation_and_labels_cache.get(key) if self.is_bob else None

@@ -87,7 +87,7 @@ class UShapeSession(Session):
         act = am = labels = None
         if a is not None:
             act, am, labels = a.front.forward(a.train, idx, with_labels=True)
-        act_b = self.to_bob(cid, act, (B, CUT_FEATURES))
+        act_b = self.act_to_bob(cid, act, B)
         out = self.tail.forward(act_b, train=True) if self.is_bob else None
         mid = self.from_bob(cid, out, (B, 100))
         dmid = None
@@ -128,7 +128,7 @@ class UShapeSession(Session):
             act = am = labels = None
             if a is not None:
                 act, am, labels = a.front.forward(a.train, idx, with_labels=True)
-            return idx, act, am, labels, self.to_bob(cid, act, (e - s, CUT_FEATURES))
+            return idx, act, am, labels, self.act_to_bob(cid, act, e - s)
 
         cur = alice_fwd(spans[0])
         pre = False

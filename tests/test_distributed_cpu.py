@@ -98,6 +98,8 @@ def _run(tmp_path, mode_flags, world_size, nprocs, bob_tp=1, extra=()):
     ([], 3, 2, 2),                     # U-shape
     (["--sisa"], 3, 2, 2),
     (["--sisa", "--act_dtype", "bf16"], 3, 3, 2),   # bf16 activation cache over p2p
+    (["--vanilla", "--act_dtype", "bf16"], 3, 3, 2),  # bf16 cut activations on the wire
+    (["--act_dtype", "bf16"], 3, 2, 2),              # U-shape, bf16 wire
     (["--control"], 3, 3, 1),
     (["--sisa", "--concat", "--concat_unlearn"], 3, 2, 2),
 ])
