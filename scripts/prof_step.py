@@ -3,7 +3,7 @@
     rocprofv3 --kernel-trace --stats --output-format csv -d OUT -o step -- \
         python3 scripts/prof_step.py --path fused --steps 200
 
---path generic|fused|lookahead|graph|local (local = the SISA client step).
+--path generic|fused|lookahead|graph|native|local (local = the SISA client step).
 """
 import argparse
 import os
@@ -71,6 +71,20 @@ def main():
         if a.time:
             dt = time.perf_counter() - t0
             print(f"path=graph tp={a.tp} us_per_step={dt / ((reps - reps // 2) * per) * 1e6:.2f}")
+    elif a.path == "native":
+        import time
+        per = n // 16
+        reps = max(1, a.steps // per)
+        for i in range(reps):
+            if i == reps // 2:
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+            tail.lookahead_prologue(acts[:16])
+            tail.run_native_epoch(acts, labels, slot, 16, True)
+        torch.cuda.synchronize()
+        if a.time:
+            dt = time.perf_counter() - t0
+            print(f"path=native tp={a.tp} us_per_step={dt / ((reps - reps // 2) * per) * 1e6:.2f}")
     else:
         if a.path == "lookahead":
             tail.lookahead_prologue(acts[:16])

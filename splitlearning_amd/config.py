@@ -103,6 +103,9 @@ def build_parser() -> argparse.ArgumentParser:
     g.add_argument("--fault_inject", type=str, default="",
                    help="RANK:PHASE[:crash|hang|silent] - make RANK fail at the phase beacon PHASE "
                         "(tests the failure paths)")
+    g.add_argument("--python_epoch", dest="native_epoch", action="store_false",
+                   help="issue Bob's eager server steps from Python instead of the native "
+                        "executor (_C.ServerEpoch); numerics are identical")
     g.add_argument("--trace_dir", type=str, default="",
                    help="write a Chrome-trace timeline per rank (phases, data-plane ops with bytes, "
                         "device time of server / local epochs) to DIR/trace_rank<r>.json")

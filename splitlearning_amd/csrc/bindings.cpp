@@ -16,6 +16,7 @@
 
 #include "common.h"
 #include "fused.h"
+#include "host.h"
 
 namespace sl {
 hipError_t conv_fwd(const void* x, bool x_u8, const int64_t* idx, int64_t row0, int B, const float* w,
@@ -82,36 +83,12 @@ float* fptr(const OptT& t) { return t.has_value() && t->defined() ? t->data_ptr<
 
 SlOpt make_opt(int64_t kind, double lr, double beta1, double beta2, double eps, double wd, double momentum,
                int64_t t, int64_t dyn) {
-  SlOpt o{};
-  o.kind = (int)kind;
-  o.lr = (float)lr;
-  o.beta1 = (float)beta1;
-  o.beta2 = (float)beta2;
-  o.eps = (float)eps;
-  o.wd = (float)wd;
-  o.momentum = (float)momentum;
-  o.dyn = reinterpret_cast<const float*>(dyn);
-  if (kind == 2 && !dyn) {
-    TORCH_CHECK(t >= 1, "Adam step count must be >= 1");
-    const double bc1 = 1.0 - std::pow(beta1, (double)t);
-    const double bc2 = 1.0 - std::pow(beta2, (double)t);
-    o.step_size = (float)(lr / bc1);
-    o.inv_bc2_sqrt = (float)(1.0 / std::sqrt(bc2));
-  }
-  return o;
+  if (kind == 2 && !dyn) TORCH_CHECK(t >= 1, "Adam step count must be >= 1");
+  return sl::make_opt_raw((int)kind, lr, beta1, beta2, eps, wd, momentum, t, reinterpret_cast<const float*>(dyn));
 }
 
 Epi make_epi(const OptT& bias, bool relu, double drop_p, uint64_t seed, int64_t col_off, int64_t dseed) {
-  Epi e{};
-  e.bias = fptr(bias);
-  e.relu = relu ? 1 : 0;
-  e.thresh = drop_p > 0 ? (uint32_t)(drop_p * 4294967296.0) : 0u;
-  e.dscale = drop_p > 0 ? (float)(1.0 / (1.0 - drop_p)) : 1.f;
-  e.seed_lo = (uint32_t)(seed & 0xffffffffull);
-  e.seed_hi = (uint32_t)(seed >> 32);
-  e.col_off = (int)col_off;
-  e.dseed = reinterpret_cast<const uint32_t*>(dseed);
-  return e;
+  return sl::make_epi_raw(fptr(bias), relu, drop_p, seed, (int)col_off, reinterpret_cast<const uint32_t*>(dseed));
 }
 
 #define OPT_ARGS int64_t kind, double lr, double beta1, double beta2, double eps, double wd, double momentum, \
@@ -546,10 +523,12 @@ void wgrad_group(const std::vector<py::tuple>& layers, int64_t M, const OptT& xn
 }  // namespace
 
 void sl_register_comm(pybind11::module& m);
+void sl_register_engine(pybind11::module& m);
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "splitlearning_amd gfx950 (MI355X) HIP kernels";
   sl_register_comm(m);
+  sl_register_engine(m);
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_local_step", &conv_local_step);
   m.def("conv_bwd_step", &conv_bwd_step);

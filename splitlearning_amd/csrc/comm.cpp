@@ -14,15 +14,36 @@
 #include <cstring>
 #include <string>
 
-namespace py = pybind11;
+#include "comm.h"
 
-namespace {
+namespace py = pybind11;
 
 #define SL_NCCL(cmd)                                                                        \
   do {                                                                                      \
     ncclResult_t r_ = (cmd);                                                                \
     TORCH_CHECK(r_ == ncclSuccess, "RCCL error '", ncclGetErrorString(r_), "' in " #cmd); \
   } while (0)
+
+namespace sl {
+
+TpComm::TpComm(const std::string& uid, int nranks, int rank) : nranks_(nranks), rank_(rank) {
+  TORCH_CHECK(uid.size() == NCCL_UNIQUE_ID_BYTES, "bad RCCL unique id size");
+  ncclUniqueId id;
+  std::memcpy(id.internal, uid.data(), NCCL_UNIQUE_ID_BYTES);
+  SL_NCCL(ncclCommInitRank(&comm_, nranks, id, rank));
+}
+
+TpComm::~TpComm() {
+  if (comm_) ncclCommDestroy(comm_);
+}
+
+void TpComm::allreduce_sum_f32(float* p, size_t n, hipStream_t st) {
+  SL_NCCL(ncclAllReduce(p, p, n, ncclFloat32, ncclSum, comm_, st));
+}
+
+}  // namespace sl
+
+namespace {
 
 hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
@@ -42,49 +63,29 @@ void need(const at::Tensor& t) {
   TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "RCCL tensors must be contiguous GPU tensors");
 }
 
-class TpComm {
- public:
-  TpComm(const py::bytes& uid, int nranks, int rank) : nranks_(nranks), rank_(rank) {
-    std::string s = uid;
-    TORCH_CHECK(s.size() == NCCL_UNIQUE_ID_BYTES, "bad RCCL unique id size");
-    ncclUniqueId id;
-    std::memcpy(id.internal, s.data(), NCCL_UNIQUE_ID_BYTES);
-    SL_NCCL(ncclCommInitRank(&comm_, nranks, id, rank));
-  }
-  ~TpComm() {
-    if (comm_) ncclCommDestroy(comm_);
-  }
-  void allreduce_sum(at::Tensor& t) {
-    need(t);
-    SL_NCCL(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), dtype_of(t), ncclSum, comm_, stream()));
-  }
-  void broadcast(at::Tensor& t, int root) {
-    need(t);
-    SL_NCCL(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), dtype_of(t), root, comm_, stream()));
-  }
-  void all_gather(at::Tensor& out, const at::Tensor& in) {
-    need(out);
-    need(in);
-    TORCH_CHECK(out.numel() == in.numel() * nranks_ && out.scalar_type() == in.scalar_type(), "all_gather sizes");
-    SL_NCCL(ncclAllGather(in.data_ptr(), out.data_ptr(), in.numel(), dtype_of(in), comm_, stream()));
-  }
-  void send(const at::Tensor& t, int peer) {
-    need(t);
-    SL_NCCL(ncclSend(t.data_ptr(), t.numel(), dtype_of(t), peer, comm_, stream()));
-  }
-  void recv(at::Tensor& t, int peer) {
-    need(t);
-    SL_NCCL(ncclRecv(t.data_ptr(), t.numel(), dtype_of(t), peer, comm_, stream()));
-  }
-  void group_start() { SL_NCCL(ncclGroupStart()); }
-  void group_end() { SL_NCCL(ncclGroupEnd()); }
-  int rank() const { return rank_; }
-  int size() const { return nranks_; }
-
- private:
-  ncclComm_t comm_ = nullptr;
-  int nranks_, rank_;
-};
+// Python-facing methods on tensors (the class itself is sl::TpComm, comm.h)
+void allreduce_sum(sl::TpComm& c, at::Tensor& t) {
+  need(t);
+  SL_NCCL(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), dtype_of(t), ncclSum, c.get(), stream()));
+}
+void broadcast(sl::TpComm& c, at::Tensor& t, int root) {
+  need(t);
+  SL_NCCL(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), dtype_of(t), root, c.get(), stream()));
+}
+void all_gather(sl::TpComm& c, at::Tensor& out, const at::Tensor& in) {
+  need(out);
+  need(in);
+  TORCH_CHECK(out.numel() == in.numel() * c.size() && out.scalar_type() == in.scalar_type(), "all_gather sizes");
+  SL_NCCL(ncclAllGather(in.data_ptr(), out.data_ptr(), in.numel(), dtype_of(in), c.get(), stream()));
+}
+void send(sl::TpComm& c, const at::Tensor& t, int peer) {
+  need(t);
+  SL_NCCL(ncclSend(t.data_ptr(), t.numel(), dtype_of(t), peer, c.get(), stream()));
+}
+void recv(sl::TpComm& c, at::Tensor& t, int peer) {
+  need(t);
+  SL_NCCL(ncclRecv(t.data_ptr(), t.numel(), dtype_of(t), peer, c.get(), stream()));
+}
 
 py::bytes unique_id() {
   ncclUniqueId id;
@@ -95,17 +96,19 @@ py::bytes unique_id() {
 }  // namespace
 
 void sl_register_comm(py::module& m) {
-  py::class_<TpComm>(m, "TpComm")
-      .def(py::init<const py::bytes&, int, int>())
-      .def("allreduce_sum", &TpComm::allreduce_sum)
-      .def("broadcast", &TpComm::broadcast)
-      .def("all_gather", &TpComm::all_gather)
-      .def("send", &TpComm::send)
-      .def("recv", &TpComm::recv)
-      .def("group_start", &TpComm::group_start)
-      .def("group_end", &TpComm::group_end)
-      .def_property_readonly("rank", &TpComm::rank)
-      .def_property_readonly("size", &TpComm::size);
+  py::class_<sl::TpComm>(m, "TpComm")
+      .def(py::init([](const py::bytes& uid, int nranks, int rank) {
+        return new sl::TpComm(std::string(uid), nranks, rank);
+      }))
+      .def("allreduce_sum", &allreduce_sum)
+      .def("broadcast", &broadcast)
+      .def("all_gather", &all_gather)
+      .def("send", &send)
+      .def("recv", &recv)
+      .def("group_start", [](sl::TpComm&) { SL_NCCL(ncclGroupStart()); })
+      .def("group_end", [](sl::TpComm&) { SL_NCCL(ncclGroupEnd()); })
+      .def_property_readonly("rank", &sl::TpComm::rank)
+      .def_property_readonly("size", &sl::TpComm::size);
   m.def("nccl_unique_id", &unique_id);
   int v = 0;
   ncclGetVersion(&v);

@@ -1,0 +1,248 @@
+// Native executor of Bob's SISA server epoch (`_C.ServerEpoch`).
+//
+// Reference: bob.train_and_backward's inner loop (data_entities_vanilla_sisa.py:298-313):
+// per cached batch `zero_grad; CE(model2_sisa(act), y).backward(); Adam.step()`.
+// The Python engine issues each step as ~8 launches (TailEngine.train_fwd_bwd3 +
+// fused_step) plus, tensor-parallel, one RCCL all-reduce; at a TP = 8 shard the GPU
+// finishes a step in ~55 us and Python's issue cost is of the same order, so every
+// rank's host jitter lands on the all-reduce.  This executor issues the same launch
+// sequence for a whole epoch from C++:
+//
+//   [fc1 epilogue of the look-ahead slabs | fc1 forward]  -> h1
+//   fc2 forward (split-K slabs; row-parallel: unsplit product + native all-reduce)
+//   head_fwd + head_bwd  (fc2 epilogue, fc3, softmax-CE, fc3 dgrad, fc2 ReLU/dropout bwd)
+//   fc2 dgrad (+ fc1 ReLU/dropout mask)                     -> dz1
+//   wgrad_group: fc1/fc2/fc3 dW fused into Adam/SGD, plus fc1's product for the next
+//   full batch with the updated weights (look-ahead)
+//
+// Same kernels, arguments, dropout seeds (host.h step_seed == ops/rng.py) and Adam step
+// counts as the Python path, so results are bit-identical to it
+// (tests/test_graphs_gpu.py::test_native_server_epoch_matches_python).
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+
+#include <algorithm>
+#include <string>
+
+#include "comm.h"
+#include "common.h"
+#include "fused.h"
+#include "host.h"
+
+namespace sl {
+hipError_t linear_fwd(const float* X, int ldx, const float* W, int ldw, float* Y, int ldy, int M, int N, int K,
+                      Epi e, float* ws, int64_t ws_elems, hipStream_t st);
+hipError_t linear_dgrad(const float* dZ, int ldz, const float* W, int ldw, const float* hprev, int ldh,
+                        float scale, float* dX, int ldx, float* ws, int64_t ws_elems, int M, int N, int K,
+                        hipStream_t st);
+hipError_t linear_epilogue(const float* P, int ldp, float* Y, int ldy, int M, int N, Epi e, int S, int64_t slab,
+                           hipStream_t st);
+hipError_t linear_fwd_partial(const float* X, int ldx, const float* W, int ldw, int M, int N, int K, float* ws,
+                              int64_t ws_elems, int max_split, int* S_out, hipStream_t st);
+}  // namespace sl
+
+namespace py = pybind11;
+
+namespace {
+
+void ck(hipError_t e, const char* what) { TORCH_CHECK(e == hipSuccess, what, ": ", hipGetErrorString(e)); }
+
+at::Tensor get(const py::dict& d, const char* k) {
+  TORCH_CHECK(d.contains(k), "ServerEpoch: missing '", k, "'");
+  return d[k].cast<at::Tensor>();
+}
+
+struct Layer {
+  at::Tensor W, b, s0, s1, sb0, sb1;   // s1 / sb1 undefined for SGD
+  int N = 0, K = 0;
+};
+
+class ServerEpoch {
+ public:
+  // cfg: layers = [3 dicts {W, b, s0, s1, sb0, sb1}], kind/lr/beta1/beta2/eps/wd/momentum,
+  // p1, p2 (dropout), col_off1, row2 (fc2 row-parallel), comm (TpComm | None),
+  // workspaces: pn, p2ws, fwdws, dgws, headws, h1, h2, dz1, dz2, dlog (each for B rows).
+  explicit ServerEpoch(const py::dict& cfg) {
+    auto layers = cfg["layers"].cast<std::vector<py::dict>>();
+    TORCH_CHECK(layers.size() == 3, "ServerEpoch drives the 3-layer server tail");
+    for (int i = 0; i < 3; ++i) {
+      Layer& L = L_[i];
+      const py::dict& d = layers[i];
+      L.W = get(d, "W");
+      L.b = get(d, "b");
+      L.s0 = get(d, "s0");
+      L.sb0 = get(d, "sb0");
+      if (d.contains("s1") && !d["s1"].is_none()) L.s1 = get(d, "s1");
+      if (d.contains("sb1") && !d["sb1"].is_none()) L.sb1 = get(d, "sb1");
+      for (const at::Tensor* t : {&L.W, &L.b, &L.s0, &L.sb0}) {
+        TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous(), "layer tensors: f32 GPU");
+      }
+      TORCH_CHECK(L.W.dim() == 2 && L.W.size(1) % 4 == 0, "W [N, K] with K % 4 == 0");
+      L.N = (int)L.W.size(0);
+      L.K = (int)L.W.size(1);
+      TORCH_CHECK(L.b.numel() == L.N && L.s0.sizes() == L.W.sizes() && L.sb0.numel() == L.N, "layer state shapes");
+    }
+    TORCH_CHECK(L_[1].K == L_[0].N && L_[2].K == L_[1].N, "layer chain shapes");
+    TORCH_CHECK(L_[1].N % 4 == 0, "fc2 width % 4");
+    kind_ = cfg["kind"].cast<int>();
+    TORCH_CHECK(kind_ == 1 || kind_ == 2, "SGD-momentum or Adam");
+    if (kind_ == 2)
+      for (auto& L : L_) TORCH_CHECK(L.s1.defined() && L.sb1.defined() && L.s1.sizes() == L.W.sizes(), "Adam v");
+    lr_ = cfg["lr"].cast<double>();
+    beta1_ = cfg["beta1"].cast<double>();
+    beta2_ = cfg["beta2"].cast<double>();
+    eps_ = cfg["eps"].cast<double>();
+    wd_ = cfg["wd"].cast<double>();
+    mom_ = cfg["momentum"].cast<double>();
+    p1_ = cfg["p1"].cast<double>();
+    p2_ = cfg["p2"].cast<double>();
+    col_off1_ = cfg["col_off1"].cast<int>();
+    row2_ = cfg["row2"].cast<bool>();
+    if (!cfg["comm"].is_none()) comm_ = cfg["comm"].cast<sl::TpComm*>();
+    TORCH_CHECK(!row2_ || comm_ != nullptr, "a row-parallel fc2 needs the native communicator");
+    B_ = cfg["B"].cast<int>();
+    TORCH_CHECK(B_ >= 1 && B_ <= 16, "batch 1..16 (look-ahead slabs, head kernels)");
+    pn_ = get(cfg, "pn");
+    p2ws_ = get(cfg, "p2ws");
+    fwdws_ = get(cfg, "fwdws");
+    dgws_ = get(cfg, "dgws");
+    headws_ = get(cfg, "headws");
+    h1_ = get(cfg, "h1");
+    h2_ = get(cfg, "h2");
+    dz1_ = get(cfg, "dz1");
+    dz2_ = get(cfg, "dz2");
+    dlog_ = get(cfg, "dlog");
+    const int64_t S1 = (L_[0].K + 255) / 256;
+    TORCH_CHECK(pn_.numel() >= S1 * B_ * L_[0].N, "pn workspace");
+    TORCH_CHECK(h1_.numel() >= (int64_t)B_ * L_[0].N && dz1_.numel() >= (int64_t)B_ * L_[0].N, "h1 / dz1");
+    TORCH_CHECK(h2_.numel() >= (int64_t)B_ * L_[1].N && dz2_.numel() >= (int64_t)B_ * L_[1].N, "h2 / dz2");
+    TORCH_CHECK(dlog_.numel() >= (int64_t)B_ * L_[2].N, "dlog");
+    TORCH_CHECK(p2ws_.numel() >= 16LL * B_ * L_[1].N, "fc2 slab workspace");
+    TORCH_CHECK(headws_.numel() >= (int64_t)sl::head3_slices(L_[1].N) * B_ * L_[2].N, "head workspace");
+  }
+
+  // One epoch over acts [n, K1] / labels [n] in batches of B.  `pre`: fc1's product for the
+  // first batch is pending in pn (look-ahead prologue / previous step).  Returns the
+  // updated (fwd_count, t, pre).
+  py::tuple run(const at::Tensor& acts, const at::Tensor& labels, at::Tensor& loss_rows, int64_t seed_base,
+                int64_t fwd_count, int64_t t, bool pre, bool lookahead) {
+    TORCH_CHECK(acts.is_cuda() && acts.scalar_type() == at::kFloat && acts.dim() == 2 && acts.is_contiguous() &&
+                    acts.size(1) == L_[0].K,
+                "acts [n, K1] contiguous f32");
+    const int64_t n = acts.size(0);
+    TORCH_CHECK(labels.is_cuda() && labels.scalar_type() == at::kLong && labels.is_contiguous() && labels.numel() == n,
+                "labels int64 [n]");
+    TORCH_CHECK(loss_rows.is_cuda() && loss_rows.scalar_type() == at::kFloat && loss_rows.numel() >= n, "loss [n]");
+    const int B = B_;
+    const int K1 = L_[0].K, N1 = L_[0].N, N2 = L_[1].N, C = L_[2].N;
+    const int64_t S1 = (K1 + 255) / 256;
+    const hipStream_t st = c10::hip::getCurrentHIPStream().stream();
+    const float* X = acts.data_ptr<float>();
+    float* pn = pn_.data_ptr<float>();
+    float* h1 = h1_.data_ptr<float>();
+    float* h2 = h2_.data_ptr<float>();
+    float* dz1 = dz1_.data_ptr<float>();
+    float* dz2 = dz2_.data_ptr<float>();
+    float* dlog = dlog_.data_ptr<float>();
+    float* P2 = p2ws_.data_ptr<float>();
+    const double s1 = p1_ > 0 ? 1.0 / (1.0 - p1_) : 1.0;
+    for (int64_t s = 0; s < n; s += B) {
+      const int M = (int)std::min<int64_t>(B, n - s);
+      const float* x = X + s * K1;
+      ++fwd_count;
+      const uint64_t sd0 = sl::step_seed((uint64_t)seed_base, 0, (uint64_t)fwd_count);
+      const uint64_t sd1 = sl::step_seed((uint64_t)seed_base, 1, (uint64_t)fwd_count);
+      const Epi e1 = sl::make_epi_raw(L_[0].b.data_ptr<float>(), true, p1_, sd0, col_off1_, nullptr);
+      // fc1 -> h1
+      if (pre)
+        ck(sl::linear_epilogue(pn, N1, h1, N1, M, N1, e1, (int)S1, (int64_t)M * N1, st), "fc1 epilogue");
+      else
+        ck(sl::linear_fwd(x, K1, L_[0].W.data_ptr<float>(), K1, h1, N1, M, N1, K1, e1, fwdws_.data_ptr<float>(),
+                          fwdws_.numel(), st),
+           "fc1 forward");
+      // fc2 -> P2 (split-K slabs, or the all-reduced product when row-parallel)
+      int S2 = 1;
+      if (row2_) {
+        if (N1 <= 1280) {
+          ck(sl::linear_fwd_partial(h1, N1, L_[1].W.data_ptr<float>(), N1, M, N2, N1, P2, p2ws_.numel(), 1, &S2, st),
+             "fc2 forward");
+        } else {
+          Epi plain{};
+          plain.dscale = 1.f;
+          ck(sl::linear_fwd(h1, N1, L_[1].W.data_ptr<float>(), N1, P2, N2, M, N2, N1, plain, fwdws_.data_ptr<float>(),
+                            fwdws_.numel(), st),
+             "fc2 forward");
+          S2 = 1;
+        }
+        comm_->allreduce_sum_f32(P2, (size_t)M * N2, st);
+      } else {
+        ck(sl::linear_fwd_partial(h1, N1, L_[1].W.data_ptr<float>(), N1, M, N2, N1, P2, p2ws_.numel(), 16, &S2, st),
+           "fc2 forward");
+      }
+      // head: h2, dlogits, dz2, loss
+      const Epi e2 = sl::make_epi_raw(L_[1].b.data_ptr<float>(), true, p2_, sd1, 0, nullptr);
+      ck(sl::server_head3(P2, S2, (int64_t)M * N2, e2, L_[2].W.data_ptr<float>(), N2, L_[2].b.data_ptr<float>(),
+                          labels.data_ptr<int64_t>() + s, -100, (float)(1.0 / M), h2, dlog, dz2,
+                          loss_rows.data_ptr<float>() + s, headws_.data_ptr<float>(), headws_.numel(), M, N2, C, st),
+         "server head");
+      // fc1's dZ
+      ck(sl::linear_dgrad(dz2, N2, L_[1].W.data_ptr<float>(), N1, h1, N1, (float)s1, dz1, N1, dgws_.data_ptr<float>(),
+                          dgws_.numel(), M, N2, N1, st),
+         "fc2 dgrad");
+      // optimizer step of all three layers (+ look-ahead of the next full batch)
+      ++t;
+      sl::WgGroup g{};
+      g.n = 3;
+      const float* dzs[3] = {dz1, dz2, dlog};
+      const float* As[3] = {x, h1, h2};
+      const int lds[3] = {N1, N2, C}, ldas[3] = {K1, N1, N2};
+      for (int i = 0; i < 3; ++i) {
+        sl::WgDesc& d = g.d[i];
+        Layer& L = L_[i];
+        d.dz = dzs[i];
+        d.ldz = lds[i];
+        d.A = As[i];
+        d.lda = ldas[i];
+        d.W = L.W.data_ptr<float>();
+        d.ldw = L.K;
+        d.s0 = L.s0.data_ptr<float>();
+        d.s1 = L.s1.defined() ? L.s1.data_ptr<float>() : nullptr;
+        d.bias = L.b.data_ptr<float>();
+        d.sb0 = L.sb0.data_ptr<float>();
+        d.sb1 = L.sb1.defined() ? L.sb1.data_ptr<float>() : nullptr;
+        d.N = L.N;
+        d.K = L.K;
+      }
+      const bool next_full = lookahead && s + 2LL * B <= n;
+      if (next_full) {
+        g.xn = X + (s + B) * K1;
+        g.ldxn = K1;
+        g.mn = B;
+        g.pn = pn;
+      }
+      const SlOpt o = sl::make_opt_raw(kind_, lr_, beta1_, beta2_, eps_, wd_, mom_, t, nullptr);
+      ck(sl::wgrad_group(g, M, o, st), "wgrad_group");
+      pre = next_full;
+    }
+    return py::make_tuple(fwd_count, t, pre);
+  }
+
+ private:
+  Layer L_[3];
+  int kind_ = 2;
+  double lr_ = 0, beta1_ = 0, beta2_ = 0, eps_ = 0, wd_ = 0, mom_ = 0, p1_ = 0, p2_ = 0;
+  int col_off1_ = 0;
+  bool row2_ = false;
+  sl::TpComm* comm_ = nullptr;
+  int B_ = 16;
+  at::Tensor pn_, p2ws_, fwdws_, dgws_, headws_, h1_, h2_, dz1_, dz2_, dlog_;
+};
+
+}  // namespace
+
+void sl_register_engine(py::module& m) {
+  py::class_<ServerEpoch>(m, "ServerEpoch")
+      .def(py::init<const py::dict&>())
+      .def("run", &ServerEpoch::run, py::arg("acts"), py::arg("labels"), py::arg("loss_rows"), py::arg("seed_base"),
+           py::arg("fwd_count"), py::arg("t"), py::arg("pre"), py::arg("lookahead"));
+}

@@ -274,6 +274,59 @@ class TailEngine:
         self._pre = pn
         self._wg = []
 
+    # ------------------------------------------------------------------ native epoch executor
+    def native_epoch_ok(self, B: int) -> bool:
+        """Whether `run_native_epoch` can drive this tail: the fused 3-layer HIP path with
+        the look-ahead, and (tensor-parallel) the native RCCL communicator."""
+        if self.device.type != "cuda" or not self.lookahead_ok(B) or not hasattr(self.ops, "C"):
+            return False
+        if self.layers[1].style == "row":
+            return getattr(self.allreduce, "comm", None) is not None
+        return self.tp_size == 1
+
+    def run_native_epoch(self, acts: torch.Tensor, labels: torch.Tensor, slot: OptSlot, B: int, pre: bool,
+                         lookahead: bool = True) -> torch.Tensor:
+        """One epoch of fused server steps over `acts`/`labels` (batches of B, last one
+        partial) issued from C++ (`_C.ServerEpoch`, csrc/engine.cpp): the same launches,
+        seeds and step counts as looping `train_fwd_bwd3` + `fused_step`, without a
+        Python round trip per step.  `pre`: the first batch's fc1 product is pending
+        (`lookahead_prologue`).  Returns the per-row losses."""
+        ex = self._native_executor(slot, B)
+        loss = torch.empty(acts.shape[0], device=self.device)
+        fc, t, pre = ex.run(acts, labels, loss, self.seed_base, self.fwd_count, slot.t, pre, lookahead)
+        self.fwd_count, slot.t = int(fc), int(t)
+        self._pre = self.lookahead_slabs(B) if pre else None
+        return loss
+
+    def _native_executor(self, slot: OptSlot, B: int):
+        cached = getattr(self, "_native", None)
+        if cached is not None and cached[0] is slot and cached[1] == B:
+            return cached[2]
+        ops, dev = self.ops, self.device
+        L1, L2, L3 = self.layers
+        N1, N2, C = L1.W.shape[0], L2.W.shape[0], L3.W.shape[0]
+        layers = []
+        for L in self.layers:
+            sw, sb = slot.state(f"{L.spec.name}.weight", L.W), slot.state(f"{L.spec.name}.bias", L.b)
+            layers.append({"W": L.W, "b": L.b, "s0": sw.get("m", sw.get("buf")), "s1": sw.get("v"),
+                           "sb0": sb.get("m", sb.get("buf")), "sb1": sb.get("v")})
+        cfg = slot.cfg
+        kmax = max(L.W.shape[1] for L in self.layers)
+        nmax = max(L.W.shape[0] for L in self.layers)
+        d = {"layers": layers, "kind": {"sgd": 1, "adam": 2}[cfg.kind], "lr": cfg.lr, "beta1": cfg.beta1,
+             "beta2": cfg.beta2, "eps": cfg.eps, "wd": cfg.weight_decay, "momentum": cfg.momentum,
+             "p1": L1.spec.dropout, "p2": L2.spec.dropout, "col_off1": L1.col_off, "row2": L2.style == "row",
+             "comm": getattr(self.allreduce, "comm", None) if L2.style == "row" else None, "B": B,
+             "pn": self.lookahead_slabs(B), "p2ws": ops._workspace(dev, 16 * B * N2, "fc2p"),
+             "fwdws": ops._workspace(dev, 16 * B * nmax, "fwd"), "dgws": ops._workspace(dev, 16 * B * kmax, "dgrad"),
+             "headws": ops._workspace(dev, ops.C().head3_slices(N2) * B * C, "head"),
+             "h1": torch.empty(B, N1, device=dev), "h2": torch.empty(B, N2, device=dev),
+             "dz1": torch.empty(B, N1, device=dev), "dz2": torch.empty(B, N2, device=dev),
+             "dlog": torch.empty(B, C, device=dev)}
+        ex = ops.C().ServerEpoch(d)
+        self._native = (slot, B, ex, d)      # d keeps the workspaces alive
+        return ex
+
     # ------------------------------------------------------------------ state
     def local_state(self) -> dict:
         out = {}

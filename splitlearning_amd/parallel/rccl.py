@@ -35,4 +35,5 @@ def native_allreduce(tpc):
         tpc.allreduce_sum(t)
         return t
     _ar.capturable = True
+    _ar.comm = tpc            # the native executor (engine.ServerEpoch) issues it from C++
     return _ar

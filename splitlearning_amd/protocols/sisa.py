@@ -256,6 +256,11 @@ class SisaSession(Session):
         elif la and n >= B:
             self.tail.lookahead_prologue(acts[:B])
             pre = True
+            if getattr(self.args, "native_epoch", True) and self.tail.native_epoch_ok(B):
+                # the whole epoch's steps issued from C++ (csrc/engine.cpp), same numerics
+                self.tail.run_native_epoch(acts.contiguous(), labels.contiguous(), self.bob_slot, B, pre)
+                self.comm.progress()
+                return
         for s in range(s, n, B):
             # look ahead only to a full batch (the prologue / slabs are sized for B rows)
             nxt = acts[s + B:s + 2 * B] if la and s + 2 * B <= n else None

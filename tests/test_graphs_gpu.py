@@ -242,3 +242,47 @@ def test_ushape_pipelined_epoch_matches_per_batch_steps(cuda, tmp_path):
                    (sa.alices[1].head.module, sb.alices[1].head.module)):
         for (k, va), vb in zip(ma.state_dict().items(), mb.state_dict().values()):
             torch.testing.assert_close(va, vb, rtol=1e-3, atol=1e-4, msg=k)
+
+
+@pytest.mark.parametrize("tp", [1, 8])
+@pytest.mark.parametrize("kind", ["adam", "sgd"])
+def test_native_server_epoch_matches_python(cuda, tp, kind):
+    """_C.ServerEpoch (csrc/engine.cpp) issues the same launches, seeds and step counts as the
+    Python look-ahead loop: bit-identical weights, optimizer state and losses (tp = 8: rank
+    0's shard, row-parallel fc2 through the native 1-rank communicator)."""
+    from splitlearning_amd.engine import sgd_momentum
+    from splitlearning_amd.parallel.rccl import native_allreduce, self_comm
+    g = torch.Generator().manual_seed(8)
+    B = 16
+    n = B * 9 + 5                                       # full batches + a partial last one
+    acts = (torch.rand(n, 5408, generator=g) * 30).to(cuda)
+    labels = torch.randint(0, 10, (n,), generator=g).to(cuda)
+    ar = native_allreduce(self_comm()) if tp > 1 else None
+    mk_slot = (lambda: OptSlot(adam(1e-3, 1e-5))) if kind == "adam" else (lambda: OptSlot(sgd_momentum(1e-2)))
+
+    def mk():
+        torch.manual_seed(0)
+        return TailEngine(ServerTailSisa(), sisa_server_spec(), cuda, tp_rank=0, tp_size=tp, allreduce=ar,
+                          seed_base=1234567)
+    ta, sa = mk(), mk_slot()
+    tb, sb = mk(), mk_slot()
+    assert tb.native_epoch_ok(B)
+    losses = []
+    ta.lookahead_prologue(acts[:B])
+    pre = True
+    for s in range(0, n, B):
+        nxt = acts[s + B:s + 2 * B] if s + 2 * B <= n else None
+        loss, _ = ta.train_fwd_bwd3(acts[s:s + B], labels[s:s + B], need_dx=False, pre=pre)
+        losses.append(loss)
+        ta.fused_step(sa, x_next=nxt)
+        pre = nxt is not None
+    tb.lookahead_prologue(acts[:B])
+    loss_b = tb.run_native_epoch(acts, labels, sb, B, True)
+    torch.cuda.synchronize()
+    assert torch.equal(torch.cat(losses), loss_b)
+    assert (ta.fwd_count, sa.t) == (tb.fwd_count, sb.t)
+    for L1, L2 in zip(ta.layers, tb.layers):
+        assert torch.equal(L1.W, L2.W) and torch.equal(L1.b, L2.b)
+    for name, st in sa.states.items():
+        for k, v in st.items():
+            assert torch.equal(v, sb.states[name][k]), (name, k)
