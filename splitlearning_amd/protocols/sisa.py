@@ -222,6 +222,11 @@ class SisaSession(Session):
         mode = getattr(self.args, "graphs", "auto")
         if mode == "off" or self.device.type != "cuda":
             return False
+        if mode == "auto" and getattr(self.args, "native_epoch", True) and self.tail.native_epoch_ok(self.B):
+            # the native executor issues the same steps from C++ at ~17-25 us of host time
+            # per step, and skips the graph's per-chunk staging copies (187.9 vs 190.0 us per
+            # step at TP = 1, 54.4 vs 56.1 at TP = 8)
+            return False
         if self.tail.tp_size != 1:
             # A TP shard step is GPU-bound even eagerly (measured 58 us eager vs 59 us
             # replayed at TP=8, docs/PERF.md), so "auto" keeps the collective out of the
