@@ -286,3 +286,35 @@ def test_native_server_epoch_matches_python(cuda, tp, kind):
     for name, st in sa.states.items():
         for k, v in st.items():
             assert torch.equal(v, sb.states[name][k]), (name, k)
+
+
+def test_concat_pipelined_epoch_matches_per_step(cuda, tmp_path):
+    """ConcatSession.concat_epoch (epoch-wide layout, grouped step + fc1 look-ahead) ==
+    one concat_step per t, with clients of different sizes (exhausted / partial batches)."""
+    from splitlearning_amd.config import parse_args
+    from splitlearning_amd.parallel.dist import Comm, Placement
+    from splitlearning_amd.protocols import ConcatSession
+
+    class S(ConcatSession):
+        def _load_client_shard(self, cid):
+            from splitlearning_amd.data.mnist import synthetic_mnist
+            n = 90 + 37 * cid
+            x, y = synthetic_mnist(n + 20, seed=cid)
+            return ({"x": torch.from_numpy(x[:n]), "y": torch.from_numpy(y[:n])},
+                    {"x": torch.from_numpy(x[n:]), "y": torch.from_numpy(y[n:])})
+    args = parse_args(["--sisa", "--concat", "--world_size", "3", "--seed", "4", "--no_tqdm",
+                       "--log_dir", str(tmp_path / "logs")])
+    mk = lambda: S(args, Comm(0, 1, cuda, Placement.make(3, 1, 1)), cuda)  # noqa: E731
+    sa, sb = mk(), mk()
+    caches = [sa.get_activation_and_labels(c) for c in (1, 2)]
+    caches_b = [sb.get_activation_and_labels(c) for c in (1, 2)]
+    for (a1, l1), (a2, l2) in zip(caches, caches_b):
+        assert torch.equal(a1, a2) and torch.equal(l1, l2)
+    T = max(-(-c[1].numel() // sa.B) for c in caches)
+    na = sum(sa.concat_step(caches, t) for t in range(T))
+    nb = sb.concat_epoch(caches_b)
+    torch.cuda.synchronize()
+    assert na == nb == sum(c[1].numel() for c in caches)
+    for L1, L2 in zip(sa.tail.layers, sb.tail.layers):
+        d = (L1.W - L2.W).abs()
+        assert d.max().item() < 1e-2 and (d > 1e-4).float().mean().item() < 1e-4
