@@ -168,15 +168,39 @@ conv_fwd_ce_wgrad_kernel(const XT* __restrict__ x, const int64_t* __restrict__ i
   __shared__ float red[2 * NW];
   const int s = blockIdx.x, tid = threadIdx.x;
   const int64_t src = idx[s];
-  if (FUSE) {
+  // every load that does not depend on another goes out before anything is consumed: the
+  // sample's label and pixels, and (FUSE) the previous step's B slabs and parameters —
+  // one memory round trip after the index instead of one per slab
+  const int64_t lab = labels[src];
+  if (FUSE && 32 * SUB >= 784) {
+    const XT* xr = x + src * 784;
+    const float px = tid < 784 ? (float)xr[tid] : 0.f;
     const float* pin = w;      // [w | b | s0 | s1] of the previous step
+    if (tid < 320) {
+      const int p = tid, oc = p / 10, j = p - (p / 10) * 10;
+      const int k = j < 9 ? oc * 9 + j : 288 + oc;
+      float pp = pin[k], a0 = pin[320 + k], a1 = pin[640 + k];
+      if (prev_slab) {
+        const float g = sum_slabs(prev_slab + p, Bprev, 320);
+        sl_opt_update(o, pp, g, a0, a1);
+        if (blockIdx.x == 0) {
+          pout[k] = pp;
+          pout[320 + k] = a0;
+          pout[640 + k] = a1;
+        }
+      }
+      if (k < 288) sw[k] = pp; else sb[k - 288] = pp;
+    }
+    if (tid < 784) img[tid] = px;
+    __syncthreads();
+  } else if (FUSE) {
+    const float* pin = w;
     for (int p = tid; p < 320; p += 32 * SUB) {
       const int oc = p / 10, j = p - (p / 10) * 10;
       const int k = j < 9 ? oc * 9 + j : 288 + oc;
       float pp = pin[k], a0 = pin[320 + k], a1 = pin[640 + k];
       if (prev_slab) {
-        float g = 0.f;
-        for (int z = 0; z < Bprev; ++z) g += prev_slab[(int64_t)z * 320 + p];
+        const float g = sum_slabs(prev_slab + p, Bprev, 320);
         sl_opt_update(o, pp, g, a0, a1);
         if (blockIdx.x == 0) {
           pout[k] = pp;
@@ -227,7 +251,6 @@ conv_fwd_ce_wgrad_kernel(const XT* __restrict__ x, const int64_t* __restrict__ i
 #pragma unroll
   for (int i = 1; i < NW; ++i) se += red[NW + i];
   const float inv = 1.f / se;
-  const int64_t lab = labels[src];
   float acc[10];
 #pragma unroll
   for (int j = 0; j < 10; ++j) acc[j] = 0.f;
