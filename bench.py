@@ -82,6 +82,8 @@ def main(argv=None):
                     help="sisa (headline): one SISA round; vanilla / ushape: one round-robin "
                          "iteration (every Alice one epoch of split training, weight relay); "
                          "concat: one SISA-concat round")
+    ap.add_argument("--kernel_variant", action="append", default=[], metavar="SLOT=VALUE",
+                    help="A/B hook: select a measured-alternative kernel form (_C.set_variant)")
     a = ap.parse_args(argv)
 
     from splitlearning_amd import ops
@@ -91,6 +93,10 @@ def main(argv=None):
 
     if a.kernels == "torch":
         ops.set_backend("torch")
+    for kv in a.kernel_variant:
+        from splitlearning_amd.ops import hip_ops
+        slot, val = (int(v) for v in kv.split("="))
+        hip_ops.C().set_variant(slot, val)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))

@@ -34,6 +34,8 @@ struct WgGroup {
   int ldxn;
   int mn;
   float* pn;            // [ceil(K0/256)][mn][N0]
+  int rev0;             // walk layer 0's tiles last-to-first (set by wgrad_group)
+  int wt;               // write-through (sc1) W/m/v stores (set by wgrad_group)
 };
 
 int head3_slices(int N2);

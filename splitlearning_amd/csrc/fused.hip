@@ -189,6 +189,35 @@ head_bwd_kernel(const float* __restrict__ plog, const float* __restrict__ b3, co
   }
 }
 
+// Traversal order.  Workgroups are dispatched in linear (x fastest) order, so the tile
+// order is the order in which fc1's W/m/v stream through the 256 MiB Infinity Cache.
+// With grp.rev0 set, layer 0's tiles are walked last-to-first (the other layers keep
+// their place at the end).  Alternating the direction every step makes the tiles one step
+// touched last the ones the next step touches first: their lines are still resident
+// (LRU reuse distance = the state streamed after them, not all 385 MB of it), so that
+// part of the read+write stream is served on-die instead of by HBM.
+// Reversing the linear id within layer 0's block rows is reversing both coordinates, so
+// the tile stays a pure function of blockIdx (scalar: no VALU division, and the layer
+// picked from it stays provably wave-uniform).
+__device__ __forceinline__ void wg_tile(const WgGroup& g, int& bx, int& by) {
+  bx = (int)blockIdx.x;
+  by = (int)blockIdx.y;
+  const int y0 = g.n > 1 ? g.d[1].yb0 : (int)gridDim.y;   // layer 0's block rows
+  if (g.rev0 && by < y0) {
+    bx = (int)gridDim.x - 1 - bx;
+    by = y0 - 1 - by;
+  }
+}
+
+// Write-through (sc1) 16-B store: the line leaves the XCD's L2 with the store, so the
+// kernel does not end with up to 32 MB of dirty L2 lines for the next launch boundary to
+// write back (default; variant 4 = 1: plain stores).  `boff` is the byte offset from `base` ([N, ld] floats).
+__device__ __forceinline__ void st_wt(float* base, int N, int ld, int boff, f32x4 v) {
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, N * ld * 4, 0x00020000);
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), rs, boff, 0, 16);
+}
+
 template <bool ADAM, bool FWDN, bool PART>
 __global__ void __launch_bounds__(1024)
 wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
@@ -197,14 +226,15 @@ wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
   __shared__ f32x4 sw[FWDN ? 16 : 1][64];    // look-ahead: the updated W tile
   __shared__ f32x4 red[FWDN ? 16 : 1][64];   // look-ahead: per-wave 16x16 partials
   // pick the layer with selects (no runtime-indexed access to the by-value argument)
-  const int by = (int)blockIdx.y;
+  int bx, by;
+  wg_tile(grp, bx, by);
   const bool l0 = !(grp.n > 1 && by >= grp.d[1].yb0);
   const WgDesc L = (grp.n > 2 && by >= grp.d[2].yb0) ? grp.d[2] : (l0 ? grp.d[0] : grp.d[1]);
-  const int kb = blockIdx.x * 256;
+  const int kb = bx * 256;
   if (kb >= L.K) return;                 // uniform per workgroup
   const int tid = threadIdx.x;
   const int r = tid >> 6, lane = tid & 63;
-  const int n0 = ((int)blockIdx.y - L.yb0) * 16;
+  const int n0 = (by - L.yb0) * 16;
   const int n = n0 + r;
   const int k = kb + lane * 4;
   const bool act = (n < L.N) && (k < L.K);
@@ -255,9 +285,16 @@ wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
   }
   if (act) {
     sl_opt_update4<ADAM>(o, p, g, q0, q1);
-    if (o.kind != 0) *reinterpret_cast<f32x4*>(L.W + off) = p;
-    *reinterpret_cast<f32x4*>(L.s0 + off) = q0;
-    if (ADAM) *reinterpret_cast<f32x4*>(L.s1 + off) = q1;
+    if (grp.wt) {
+      const int boff = (int)(off * 4);
+      if (o.kind != 0) st_wt(L.W, L.N, L.ldw, boff, p);
+      st_wt(L.s0, L.N, L.ldw, boff, q0);
+      if (ADAM) st_wt(L.s1, L.N, L.ldw, boff, q1);
+    } else {
+      if (o.kind != 0) *reinterpret_cast<f32x4*>(L.W + off) = p;
+      *reinterpret_cast<f32x4*>(L.s0 + off) = q0;
+      if (ADAM) *reinterpret_cast<f32x4*>(L.s1 + off) = q1;
+    }
   }
   if (FWDN && l0) {
     // next batch's partial pre-activations with the updated tile: stage W_new through LDS
@@ -276,10 +313,10 @@ wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
       float v = 0.f;
 #pragma unroll
       for (int w = 0; w < 16; ++w) v += red[w][16 * (m >> 2) + nn][m & 3];
-      if (m < grp.mn && n0 + nn < L.N) grp.pn[((int64_t)blockIdx.x * grp.mn + m) * L.N + n0 + nn] = v;
+      if (m < grp.mn && n0 + nn < L.N) grp.pn[((int64_t)bx * grp.mn + m) * L.N + n0 + nn] = v;
     }
   }
-  if (L.bias && blockIdx.x == 0 && lane == 0 && n < L.N) {
+  if (L.bias && bx == 0 && lane == 0 && n < L.N) {
     float pb = L.bias[n], b0 = L.sb0[n], b1 = L.sb1 ? L.sb1[n] : 0.f;
     sl_opt_update(o, pb, gb, b0, b1);
     if (o.kind != 0) L.bias[n] = pb;
@@ -402,9 +439,27 @@ hipError_t server_head3(const float* P2, int S2, int64_t slab2, Epi e2, const fl
   return hipGetLastError();
 }
 
+// Per-launch traversal / store form.  The direction of layer 0's walk alternates from one
+// launch to the next (graph capture bakes the pattern in; every captured chunk has an even
+// number of steps).  Variant 7 (A/B and tests): 1 = always forward, 2 = always reversed.
+// W/m/v are stored write-through (32-bit byte offsets: layers under 2 GB only); variant
+// 4 = 1 selects plain stores.  Measured (scripts/cache_ab.py, one process, interleaved
+// rounds, us per look-ahead server step at TP = 1 / 2 / 4 / 8): always-forward 183.4 /
+// 102.2 / 70.2 / 59.7, alternating 172.6 / 100.9 / 69.6 / 59.8, alternating +
+// write-through 171.8 / 100.9 / 68.7 / 59.5 (profiles/r1_cache_ab.txt).
+static void set_traversal(WgGroup& gg) {
+  static unsigned flip = 0;
+  const int v7 = g_variant[7];
+  gg.rev0 = v7 == 1 ? 0 : (v7 == 2 ? 1 : (int)(flip++ & 1u));
+  gg.wt = g_variant[4] == 1 ? 0 : 1;
+  for (int i = 0; i < gg.n; ++i)
+    if ((int64_t)gg.d[i].N * gg.d[i].ldw * 4 > 2147483647LL) gg.wt = 0;
+}
+
 hipError_t wgrad_group(const WgGroup& g, int M, SlOpt o, hipStream_t st) {
   int kmax = 0, yb = 0;
   WgGroup gg = g;
+  set_traversal(gg);
   for (int i = 0; i < gg.n; ++i) {
     gg.d[i].yb0 = yb;
     yb += (gg.d[i].N + 15) / 16;

@@ -224,6 +224,43 @@ def test_wgrad_group(cuda, variant, kind, M, shapes, mn):
         _close(kw["p_next"].sum(0), kw["x_next"] @ layers[0][5].t(), rtol=1e-4, atol=2e-3)
 
 
+@pytest.mark.parametrize("kind", ["sgd", "adam"])
+def test_wgrad_group_traversal_and_store_form_are_bit_identical(cuda, kind):
+    """The tile walk direction (variant 7: forward / reversed / alternating) and the store
+    form (variant 4: plain / write-through) only change where bytes are cached: every
+    output, the look-ahead slabs included, is bitwise the same."""
+    C = hip_ops.C()
+    cfg = OptimCfg("adam", 1e-3, weight_decay=1e-5) if kind == "adam" else OptimCfg("sgd", 1e-2, momentum=0.9)
+    g = torch.Generator().manual_seed(3)
+    M, shapes = 16, [(1000, 5408), (200, 1000), (100, 200)]
+    base = [(torch.randn(M, N, generator=g), torch.randn(M, K, generator=g), torch.randn(N, K, generator=g),
+             torch.randn(N, generator=g)) for N, K in shapes]
+    xn = torch.randn(M, shapes[0][1], generator=g).to(cuda)
+    outs = []
+    try:
+        for v7, v4 in ((1, 0), (2, 0), (0, 0), (0, 0), (1, 1), (2, 1)):
+            layers = []
+            for dz, a, w, b in base:
+                w, b = w.to(cuda), b.to(cuda)
+                sw = {"m": torch.full_like(w, 0.01), "v": torch.full_like(w, 0.02)} if kind == "adam" else \
+                    {"buf": torch.full_like(w, 0.01)}
+                sb = {k: torch.full_like(b, 0.01) for k in sw}
+                layers.append((dz.to(cuda), None, None, 1.0, a.to(cuda), w, sw, b, sb))
+            pn = hip_ops.lookahead_slabs(cuda, shapes[0][1], M, shapes[0][0])
+            C.set_variant(7, v7)
+            C.set_variant(4, v4)
+            hip_ops.wgrad_group_(layers, M, cfg, 3, x_next=xn, p_next=pn)
+            torch.cuda.synchronize()
+            outs.append([t.clone() for L in layers for t in (L[5], L[7], *L[6].values(), *L[8].values())]
+                        + [pn.clone()])
+    finally:
+        C.set_variant(7, 0)
+        C.set_variant(4, 0)
+    for o in outs[1:]:
+        for x, y in zip(outs[0], o):
+            assert torch.equal(x, y)
+
+
 @pytest.mark.parametrize("variant", [0, 1])   # 0: optimizer folded into the next step, 1: 2 launches/step
 @pytest.mark.parametrize("kind", ["sgd", "adam"])
 def test_conv_local_epoch_matches_steps(cuda, kind, variant):
