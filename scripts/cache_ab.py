@@ -5,6 +5,9 @@ Variants (csrc/fused.hip `set_traversal`):
   zigzag  variant 7 = 0, 4 = 1: direction alternates every step, so the tiles a step touched
           last are the next step's first (still resident in the 256 MiB Infinity Cache)
   zz+wt   variant 7 = 0, 4 = 0 (the default): zig-zag plus write-through (sc1) W/m/v stores
+  zz+wt2d / zz+wt1d   the same, forcing the 2-D grid (empty workgroups where a layer is
+          narrower than the widest) / the 1-D grid over the real tiles; by default the
+          launcher picks 2-D only when < 10 % of its workgroups would be empty
 
 All variants run in ONE process, in interleaved rounds (rule: cross-process variance is
 larger than the effect), each round `--steps` timed steps after `--settle` untimed ones
@@ -27,7 +30,8 @@ from splitlearning_amd.engine import OptSlot, TailEngine, adam  # noqa: E402
 from splitlearning_amd.models import ServerTailSisa, sisa_server_spec  # noqa: E402
 from splitlearning_amd.ops import hip_ops as H  # noqa: E402
 
-VARIANTS = {"fwd": {7: 1, 4: 1}, "zigzag": {7: 0, 4: 1}, "zz+wt": {7: 0, 4: 0}}
+VARIANTS = {"fwd": {7: 1, 4: 1, 2: 0}, "zigzag": {7: 0, 4: 1, 2: 0}, "zz+wt": {7: 0, 4: 0, 2: 0},
+            "zz+wt2d": {7: 0, 4: 0, 2: 1}, "zz+wt1d": {7: 0, 4: 0, 2: 2}}
 
 
 def main():
@@ -75,7 +79,7 @@ def main():
                 steps(a.steps)
                 torch.cuda.synchronize()
                 res[v].append((time.perf_counter() - t0) / a.steps * 1e6)
-        for slot_id in (4, 7):
+        for slot_id in (2, 4, 7):
             C.set_variant(slot_id, 0)       # back to the defaults
         for v, xs in res.items():
             print(f"tp={tp} {v:7s} median {statistics.median(xs):7.2f} us/step  min {min(xs):7.2f}  "

@@ -8,7 +8,7 @@ timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 
 tail -1 gpurun_out/t_wg.log
 timeout -k 10 400 python -u scripts/cache_ab.py --tp 1 2 4 8 ${AB_ARGS} > gpurun_out/cache_ab.txt 2>&1 || { echo AB_FAIL; tail -20 gpurun_out/cache_ab.txt; exit 1; }
 cat gpurun_out/cache_ab.txt
-for v in "7=1" "7=0" "4=1"; do
+for v in ${WGB_VARIANTS:-"7=1" "7=0" "4=1"}; do
   echo "== wgbench variant $v" >> gpurun_out/cache_ab.txt
   timeout -k 10 200 python -u scripts/wgbench.py --iters 100 --variant $v >> gpurun_out/cache_ab.txt 2>&1 || { echo WGB_FAIL; exit 1; }
 done

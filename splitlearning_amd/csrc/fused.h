@@ -22,7 +22,8 @@ struct WgDesc {
   float* sb0;
   float* sb1;
   int N, K;
-  int yb0;              // first blockIdx.y of this layer
+  int yb0;              // first blockIdx.y of this layer (2-D grid: all-MFMA variant)
+  int wb0;              // first block of this layer (1-D grid: default kernel)
 };
 struct WgGroup {
   WgDesc d[3];
@@ -35,6 +36,8 @@ struct WgGroup {
   int mn;
   float* pn;            // [ceil(K0/256)][mn][N0]
   int rev0;             // walk layer 0's tiles last-to-first (set by wgrad_group)
+  int nt0;              // layer 0's tile count (set by wgrad_group)
+  int grid2d;           // 2-D grid (set by wgrad_group: when few of its workgroups are empty)
   int wt;               // write-through (sc1) W/m/v stores (set by wgrad_group)
 };
 

@@ -196,17 +196,36 @@ head_bwd_kernel(const float* __restrict__ plog, const float* __restrict__ b3, co
 // touched last the ones the next step touches first: their lines are still resident
 // (LRU reuse distance = the state streamed after them, not all 385 MB of it), so that
 // part of the read+write stream is served on-die instead of by HBM.
-// Reversing the linear id within layer 0's block rows is reversing both coordinates, so
-// the tile stays a pure function of blockIdx (scalar: no VALU division, and the layer
-// picked from it stays provably wave-uniform).
-__device__ __forceinline__ void wg_tile(const WgGroup& g, int& bx, int& by) {
-  bx = (int)blockIdx.x;
-  by = (int)blockIdx.y;
-  const int y0 = g.n > 1 ? g.d[1].yb0 : (int)gridDim.y;   // layer 0's block rows
-  if (g.rev0 && by < y0) {
-    bx = (int)gridDim.x - 1 - bx;
-    by = y0 - 1 - by;
+// Tile mapping.  Either a 2-D grid (K blocks of the widest layer) x (row tiles of every
+// layer), or a 1-D grid over the layers' real tiles, layer i owning blocks [wb0_i, wb0_i +
+// ceil(N_i/16) * ceil(K_i/256)) in row-major tile order: the 2-D form leaves 55 % of its
+// workgroups empty at a TP = 8 shard, where fc2's and fc3's K is 628 / 1000 against fc1's
+// 5408 (the launcher picks the form, set_traversal's caller).  Layer 0's local index is
+// reversed when grp.rev0 is set.  Every quantity is wave-uniform (readfirstlane on the
+// quotient: the division itself is emitted on the VALU), so the layer descriptor stays in
+// scalar registers.
+__device__ __forceinline__ int wg_tile(const WgGroup& g, int& bx, int& by) {
+  if (g.grid2d) {   // 2-D grid: (K blocks of the widest layer) x (row tiles of all layers)
+    const int y = (int)blockIdx.y;
+    const int layer = (g.n > 2 && y >= g.d[2].yb0) ? 2 : ((g.n > 1 && y >= g.d[1].yb0) ? 1 : 0);
+    bx = (int)blockIdx.x;
+    by = y - (layer == 2 ? g.d[2].yb0 : (layer == 1 ? g.d[1].yb0 : 0));
+    if (layer == 0 && g.rev0) {
+      bx = (int)gridDim.x - 1 - bx;
+      by = (g.n > 1 ? g.d[1].yb0 : (int)gridDim.y) - 1 - by;
+    }
+    return layer;
   }
+  const int lin = (int)blockIdx.x;
+  const int li = (g.n > 2 && lin >= g.d[2].wb0) ? 2 : ((g.n > 1 && lin >= g.d[1].wb0) ? 1 : 0);
+  const int wb0 = li == 2 ? g.d[2].wb0 : (li == 1 ? g.d[1].wb0 : 0);
+  const int K = li == 2 ? g.d[2].K : (li == 1 ? g.d[1].K : g.d[0].K);
+  const int kx = (K + 255) >> 8;
+  int local = lin - wb0;
+  if (li == 0 && g.rev0) local = g.nt0 - 1 - local;
+  by = __builtin_amdgcn_readfirstlane(local / kx);
+  bx = local - by * kx;
+  return li;
 }
 
 // Write-through (sc1) 16-B store: the line leaves the XCD's L2 with the store, so the
@@ -227,14 +246,14 @@ wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
   __shared__ f32x4 red[FWDN ? 16 : 1][64];   // look-ahead: per-wave 16x16 partials
   // pick the layer with selects (no runtime-indexed access to the by-value argument)
   int bx, by;
-  wg_tile(grp, bx, by);
-  const bool l0 = !(grp.n > 1 && by >= grp.d[1].yb0);
-  const WgDesc L = (grp.n > 2 && by >= grp.d[2].yb0) ? grp.d[2] : (l0 ? grp.d[0] : grp.d[1]);
+  const int layer = wg_tile(grp, bx, by);
+  const bool l0 = layer == 0;
+  const WgDesc L = layer == 2 ? grp.d[2] : (l0 ? grp.d[0] : grp.d[1]);
   const int kb = bx * 256;
-  if (kb >= L.K) return;                 // uniform per workgroup
+  if (kb >= L.K) return;                 // 2-D grid only; uniform per workgroup
   const int tid = threadIdx.x;
   const int r = tid >> 6, lane = tid & 63;
-  const int n0 = (by - L.yb0) * 16;
+  const int n0 = by * 16;
   const int n = n0 + r;
   const int k = kb + lane * 4;
   const bool act = (n < L.N) && (k < L.K);
@@ -457,22 +476,31 @@ static void set_traversal(WgGroup& gg) {
 }
 
 hipError_t wgrad_group(const WgGroup& g, int M, SlOpt o, hipStream_t st) {
-  int kmax = 0, yb = 0;
+  int kmax = 0, yb = 0, wb = 0;
   WgGroup gg = g;
   set_traversal(gg);
   for (int i = 0; i < gg.n; ++i) {
     gg.d[i].yb0 = yb;
+    gg.d[i].wb0 = wb;
     yb += (gg.d[i].N + 15) / 16;
+    wb += ((gg.d[i].N + 15) / 16) * ((gg.d[i].K + 255) / 256);
     kmax = max(kmax, gg.d[i].K);
   }
   if (yb == 0 || kmax == 0) return hipSuccess;
-  dim3 grid((kmax + 255) / 256, yb);
+  gg.nt0 = ((gg.d[0].N + 15) / 16) * ((gg.d[0].K + 255) / 256);
+  dim3 grid((kmax + 255) / 256, yb);     // 2-D grid of the all-MFMA variant
+  const dim3 grid1(wb);                  // 1-D grid over the real tiles (default kernel)
   if (gg.xn && (gg.mn <= 0 || gg.mn > 16 || !gg.pn)) return hipErrorInvalidValue;
   const bool fw = gg.xn != nullptr;
   bool part = false;
   for (int i = 0; i < gg.n; ++i) part = part || gg.d[i].dzp != nullptr;
   if (g_variant[3] != 1) {   // default: LDS-staged VALU dW (row-contiguous W streams)
-#define SL_WG(A, F, P) wgrad_group_kernel<A, F, P><<<grid, 1024, 0, st>>>(gg, M, o)
+  // 2-D grid when it wastes < 10 % of its workgroups (TP = 1: 3 %, measured 1.4 us per step
+  // faster there), else the 1-D grid (TP = 2 / 4 / 8: 18-55 % empty, 0.3-1.2 us faster);
+  // variant 2: 1 = always 2-D, 2 = always 1-D (profiles/r1_cache_ab_grid.txt)
+  const int64_t g2 = (int64_t)grid.x * grid.y;
+  gg.grid2d = g_variant[2] == 1 ? 1 : (g_variant[2] == 2 ? 0 : ((g2 - wb) * 10 < g2 ? 1 : 0));
+#define SL_WG(A, F, P) wgrad_group_kernel<A, F, P><<<gg.grid2d ? grid : grid1, 1024, 0, st>>>(gg, M, o)
     if (part) {
       if (o.kind == 2) { if (fw) SL_WG(true, true, true); else SL_WG(true, false, true); }
       else { if (fw) SL_WG(false, true, true); else SL_WG(false, false, true); }

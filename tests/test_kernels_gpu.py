@@ -226,9 +226,10 @@ def test_wgrad_group(cuda, variant, kind, M, shapes, mn):
 
 @pytest.mark.parametrize("kind", ["sgd", "adam"])
 def test_wgrad_group_traversal_and_store_form_are_bit_identical(cuda, kind):
-    """The tile walk direction (variant 7: forward / reversed / alternating) and the store
-    form (variant 4: plain / write-through) only change where bytes are cached: every
-    output, the look-ahead slabs included, is bitwise the same."""
+    """The tile walk direction (variant 7: forward / reversed / alternating), the store form
+    (variant 4: write-through / plain) and the grid form (variant 2: auto / 2-D / 1-D) only
+    change where and when bytes move: every output, the look-ahead slabs included, is
+    bitwise the same."""
     C = hip_ops.C()
     cfg = OptimCfg("adam", 1e-3, weight_decay=1e-5) if kind == "adam" else OptimCfg("sgd", 1e-2, momentum=0.9)
     g = torch.Generator().manual_seed(3)
@@ -238,7 +239,8 @@ def test_wgrad_group_traversal_and_store_form_are_bit_identical(cuda, kind):
     xn = torch.randn(M, shapes[0][1], generator=g).to(cuda)
     outs = []
     try:
-        for v7, v4 in ((1, 0), (2, 0), (0, 0), (0, 0), (1, 1), (2, 1)):
+        for v7, v4, v2 in ((1, 0, 0), (2, 0, 0), (0, 0, 0), (0, 0, 0), (1, 1, 0), (2, 1, 0), (2, 0, 1),
+                           (1, 0, 2), (2, 1, 1), (2, 1, 2)):
             layers = []
             for dz, a, w, b in base:
                 w, b = w.to(cuda), b.to(cuda)
@@ -249,13 +251,14 @@ def test_wgrad_group_traversal_and_store_form_are_bit_identical(cuda, kind):
             pn = hip_ops.lookahead_slabs(cuda, shapes[0][1], M, shapes[0][0])
             C.set_variant(7, v7)
             C.set_variant(4, v4)
+            C.set_variant(2, v2)
             hip_ops.wgrad_group_(layers, M, cfg, 3, x_next=xn, p_next=pn)
             torch.cuda.synchronize()
             outs.append([t.clone() for L in layers for t in (L[5], L[7], *L[6].values(), *L[8].values())]
                         + [pn.clone()])
     finally:
-        C.set_variant(7, 0)
-        C.set_variant(4, 0)
+        for slot in (2, 4, 7):
+            C.set_variant(slot, 0)
     for o in outs[1:]:
         for x, y in zip(outs[0], o):
             assert torch.equal(x, y)
