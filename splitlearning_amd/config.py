@@ -79,6 +79,13 @@ def build_parser() -> argparse.ArgumentParser:
                    help="write checkpoints (reference state_dict key names) at the end of the run")
     g.add_argument("--resume_dir", type=str, default="",
                    help="load checkpoints written by --save_dir before the schedule starts")
+    g.add_argument("--ckpt_dir", type=str, default="",
+                   help="write a full snapshot (weights, optimizer slots, step counters, RNG states, "
+                        "SISA activation cache) after every schedule step, one file per rank")
+    g.add_argument("--resume", action="store_true",
+                   help="resume from the latest complete snapshot in --ckpt_dir: completed schedule "
+                        "steps are skipped and the run continues exactly where it stopped")
+    g.add_argument("--ckpt_keep", type=int, default=2, help="snapshots kept in --ckpt_dir")
     g.add_argument("--master_addr", type=str, default="127.0.0.1")
     g.add_argument("--master_port", type=int, default=5689)
     g.add_argument("--omit_label", type=int, default=DEFAULT_OMIT_LABEL)
@@ -136,6 +143,8 @@ def validate(args: argparse.Namespace) -> argparse.Namespace:
         if not 1 <= i <= args.client_num_in_total:
             raise ValueError(f"unlearn client {i} is not an Alice id in 1..{args.client_num_in_total}")
     args.unlearn_client_ids = ids
+    if getattr(args, "resume", False) and not getattr(args, "ckpt_dir", ""):
+        raise ValueError("--resume needs --ckpt_dir")
     return args
 
 

@@ -47,3 +47,24 @@ def test_trace_has_device_spans(cuda, tmp_path):
     assert any(e["name"] == "server_epoch[alice1]" for e in gpu)
     assert any(e["name"] == "local_epoch[alice1]" for e in gpu)
     assert all(e["dur"] > 0 for e in gpu)
+
+
+@pytest.mark.parametrize("flags", [["--sisa"], ["--vanilla"]])
+def test_resume_from_mid_schedule_snapshot_on_gpu(cuda, tmp_path, flags):
+    """Snapshots taken on the HIP path restore exactly: resuming from the snapshot after
+    step 3 (weights, optimizer slots, RNG and step counters, SISA activation cache)
+    finishes with Bob's and the Alices' weights bitwise equal to the uninterrupted run."""
+    import torch
+    ck = tmp_path / "ck"
+    full, _ = _run(tmp_path / "a", flags, ws=3,
+                   extra=["--ckpt_dir", str(ck), "--ckpt_keep", "100", "--save_dir", str(tmp_path / "full")])
+    (ck / "latest").write_text("3")
+    res, bob = _run(tmp_path / "b", flags, ws=3,
+                    extra=["--ckpt_dir", str(ck), "--resume", "--save_dir", str(tmp_path / "res")])
+    assert "[resume] 3 of" in bob
+    assert res["last_eval"] == full["last_eval"]
+    for f in ["bob.pt", "alice1.pt", "alice2.pt"]:
+        a = torch.load(tmp_path / "full" / f, weights_only=True)
+        b = torch.load(tmp_path / "res" / f, weights_only=True)
+        for k in a:
+            assert torch.equal(a[k], b[k]), (f, k)
