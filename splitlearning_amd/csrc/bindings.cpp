@@ -21,7 +21,7 @@
 namespace sl {
 hipError_t conv_fwd(const void* x, bool x_u8, const int64_t* idx, int64_t row0, int B, const float* w,
                     const float* b, float* y, uint8_t* am, hipStream_t st, const int64_t* lab_in,
-                    int64_t* lab_out);
+                    int64_t* lab_out, const ConvPending* pend);
 hipError_t conv_local_step(const void* x, bool x_u8, const int64_t* idx, const int64_t* labels, int B, float* w,
                            float* b, float* slab, float* loss_rows, float* s0w, float* s1w, float* s0b, float* s1b,
                            SlOpt o, hipStream_t st);
@@ -31,7 +31,8 @@ hipError_t conv_local_epoch(const void* x, bool x_u8, const int64_t* order, int6
                             int64_t t0, hipStream_t st);
 hipError_t conv_bwd_step(const float* dy, const float* y, const uint8_t* am, const void* x, bool x_u8,
                          const int64_t* idx, int B, float* w, float* b, float* slab, float* s0w, float* s1w,
-                         float* s0b, float* s1b, SlOpt o, hipStream_t st);
+                         float* s0b, float* s1b, SlOpt o, hipStream_t st, bool defer, const ConvPending* pend);
+hipError_t conv_apply(const ConvPending& p, float* w, float* b, hipStream_t st);
 hipError_t linear_fwd(const float* X, int ldx, const float* W, int ldw, float* Y, int ldy, int M, int N, int K,
                       Epi e, float* ws, int64_t ws_elems, hipStream_t st);
 hipError_t linear_dgrad(const float* dZ, int ldz, const float* W, int ldw, const float* hprev, int ldh,
@@ -140,8 +141,42 @@ void conv_fwd(const at::Tensor& x, const at::Tensor& idx, int64_t B, const at::T
   }
   check(sl::conv_fwd(x.data_ptr(), x.scalar_type() == at::kByte, idx.data_ptr<int64_t>(), 0, (int)B,
                      w.data_ptr<float>(), b.data_ptr<float>(), y.data_ptr<float>(), am.data_ptr<uint8_t>(),
-                     cur_stream(), li, lo),
+                     cur_stream(), li, lo, nullptr),
         "conv_fwd");
+}
+
+ConvPending make_pending(const at::Tensor& slab, int64_t pB, at::Tensor& s0w, const OptT& s1w, at::Tensor& s0b,
+                             const OptT& s1b, SlOpt o) {
+  check_slab(slab, pB);
+  TORCH_CHECK(pB >= 1, "pending batch");
+  TORCH_CHECK(s0w.numel() == 288 && s0b.numel() == 32, "optimizer state");
+  return ConvPending{slab.data_ptr<float>(), (int)pB, s0w.data_ptr<float>(), fptr(s1w), s0b.data_ptr<float>(),
+                         fptr(s1b), o};
+}
+
+// Forward with a deferred optimizer step applied in-kernel (FrontEngine, split modes):
+// (pslab, pB, states, opt of that step) is the last backward's update, not yet stored.
+void conv_fwd_pending(const at::Tensor& x, const at::Tensor& idx, int64_t B, const at::Tensor& w, const at::Tensor& b,
+                      at::Tensor& y, at::Tensor& am, const at::Tensor& lab_in, at::Tensor& lab_out,
+                      const at::Tensor& pslab, int64_t pB, at::Tensor& s0w, const OptT& s1w, at::Tensor& s0b,
+                      const OptT& s1b, OPT_ARGS) {
+  check_x(x);
+  check_params(w, b);
+  check_idx(idx, B);
+  need_f32(y, "y");
+  TORCH_CHECK(y.is_contiguous() && y.numel() >= B * 5408, "y too small");
+  TORCH_CHECK(am.scalar_type() == at::kByte && am.is_contiguous() && am.numel() >= B * 5408, "am too small");
+  need_cuda(lab_in, "lab_in");
+  need_cuda(lab_out, "lab_out");
+  TORCH_CHECK(lab_in.scalar_type() == at::kLong && lab_in.is_contiguous() && lab_in.numel() == x.numel() / 784,
+              "lab_in int64 [N]");
+  TORCH_CHECK(lab_out.scalar_type() == at::kLong && lab_out.is_contiguous() && lab_out.numel() >= B,
+              "lab_out int64 [B]");
+  const ConvPending p = make_pending(pslab, pB, s0w, s1w, s0b, s1b, OPT_PASS);
+  check(sl::conv_fwd(x.data_ptr(), x.scalar_type() == at::kByte, idx.data_ptr<int64_t>(), 0, (int)B,
+                     w.data_ptr<float>(), b.data_ptr<float>(), y.data_ptr<float>(), am.data_ptr<uint8_t>(),
+                     cur_stream(), lab_in.data_ptr<int64_t>(), lab_out.data_ptr<int64_t>(), &p),
+        "conv_fwd_pending");
 }
 
 // SISA local step: fused gather+conv+pool+softmax-CE(5408)+dW partials, then reduce+optimizer.
@@ -233,8 +268,43 @@ void conv_bwd_step(const at::Tensor& dy, const at::Tensor& y, const at::Tensor& 
   check(sl::conv_bwd_step(dy.data_ptr<float>(), y.data_ptr<float>(), am.data_ptr<uint8_t>(), x.data_ptr(),
                           x.scalar_type() == at::kByte, idx.data_ptr<int64_t>(), (int)B, w.data_ptr<float>(),
                           b.data_ptr<float>(), slab.data_ptr<float>(), s0w.data_ptr<float>(), fptr(s1w),
-                          s0b.data_ptr<float>(), fptr(s1b), OPT_PASS, cur_stream()),
+                          s0b.data_ptr<float>(), fptr(s1b), OPT_PASS, cur_stream(), false, nullptr),
         "conv_bwd_step");
+}
+
+// Deferred-update backward: this step's dW/db partials into `slab` (no update launch);
+// workgroup 0 stores the pending update of the previous step (pslab / pB / its opt), if any.
+void conv_bwd_defer(const at::Tensor& dy, const at::Tensor& y, const at::Tensor& am, const at::Tensor& x,
+                    const at::Tensor& idx, int64_t B, at::Tensor& w, at::Tensor& b, at::Tensor& slab, const OptT& pslab,
+                    int64_t pB, at::Tensor& s0w, const OptT& s1w, at::Tensor& s0b, const OptT& s1b, OPT_ARGS) {
+  check_x(x);
+  check_params(w, b);
+  check_idx(idx, B);
+  check_slab(slab, B);
+  need_f32(dy, "dy");
+  need_f32(y, "y");
+  TORCH_CHECK(dy.is_contiguous() && y.is_contiguous() && dy.numel() >= B * 5408 && y.numel() >= B * 5408, "dy/y");
+  TORCH_CHECK(am.scalar_type() == at::kByte && am.is_contiguous() && am.numel() >= B * 5408, "am");
+  TORCH_CHECK(s0w.numel() == 288 && s0b.numel() == 32, "optimizer state");
+  const bool has = pslab.has_value() && pslab->defined();
+  ConvPending p{};
+  if (has) {
+    TORCH_CHECK(pslab->data_ptr<float>() != slab.data_ptr<float>(), "pending and new slabs must differ");
+    p = make_pending(*pslab, pB, s0w, s1w, s0b, s1b, OPT_PASS);
+  }
+  check(sl::conv_bwd_step(dy.data_ptr<float>(), y.data_ptr<float>(), am.data_ptr<uint8_t>(), x.data_ptr(),
+                          x.scalar_type() == at::kByte, idx.data_ptr<int64_t>(), (int)B, w.data_ptr<float>(),
+                          b.data_ptr<float>(), slab.data_ptr<float>(), s0w.data_ptr<float>(), fptr(s1w),
+                          s0b.data_ptr<float>(), fptr(s1b), SlOpt{}, cur_stream(), true, has ? &p : nullptr),
+        "conv_bwd_defer");
+}
+
+// Store a deferred update (FrontEngine.flush).
+void conv_apply(const at::Tensor& pslab, int64_t pB, at::Tensor& w, at::Tensor& b, at::Tensor& s0w, const OptT& s1w,
+                at::Tensor& s0b, const OptT& s1b, OPT_ARGS) {
+  check_params(w, b);
+  const ConvPending p = make_pending(pslab, pB, s0w, s1w, s0b, s1b, OPT_PASS);
+  check(sl::conv_apply(p, w.data_ptr<float>(), b.data_ptr<float>(), cur_stream()), "conv_apply");
 }
 
 // ---------------------------------------------------------------- linear
@@ -532,6 +602,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_local_step", &conv_local_step);
   m.def("conv_bwd_step", &conv_bwd_step);
+  m.def("conv_bwd_defer", &conv_bwd_defer);
+  m.def("conv_fwd_pending", &conv_fwd_pending);
+  m.def("conv_apply", &conv_apply);
   m.def("conv_local_epoch", &conv_local_epoch);
   m.def("linear_fwd", &linear_fwd);
   m.def("linear_epilogue", &linear_epilogue);

@@ -87,6 +87,18 @@ __device__ __forceinline__ void sl_opt_update(const SlOpt& o, float& p, float g,
   }
 }
 
+// A client optimizer step not yet stored (split modes, conv.hip): the B partial dW/db slabs
+// of the last backward and that step's optimizer scalars.  The next forward applies it for
+// its own use and the next backward stores it (FrontEngine's deferred update).
+struct ConvPending {
+  const float* slab;
+  int B;
+  float* s0w;
+  float* s1w;
+  float* s0b;
+  float* s1b;
+  SlOpt o;
+};
 
 // Fused GEMM epilogue: bias, ReLU, counter-hash dropout (global column index).
 struct Epi {

@@ -6,78 +6,18 @@
 // DistributedOptimizer (data_entities_vanilla.py:37-42).  SURVEY §2.7 K1-K3, K13.
 //
 // The conv has K = 9 (one input channel), far too small for MFMA, so it is a
-// direct LDS-tiled convolution: one 256-thread workgroup per sample stages the
-// 28x28 image (converted from the uint8 shard row it gathers itself, so there
-// is no separate collate/convert kernel) and 32x9 weights in LDS and writes the
-// pooled, NCHW-flattened [5408] activation plus a 2-bit argmax for backward.
+// direct LDS-tiled convolution: a 256-thread workgroup per (sample, 8 output channels)
+// stages the 28x28 image (converted from the uint8 shard row it gathers itself, so there
+// is no separate collate/convert kernel) and its 8x9 weights in LDS and writes its part of
+// the pooled, NCHW-flattened [5408] activation plus a 2-bit argmax for backward.
 #include "common.h"
 
 #include <algorithm>
 
 namespace sl {
 
-template <typename XT>
-__global__ void __launch_bounds__(256)
-conv_relu_pool_fwd_kernel(const XT* __restrict__ x, const int64_t* __restrict__ idx, int64_t row0,
-                          const float* __restrict__ w, const float* __restrict__ b,
-                          float* __restrict__ y, uint8_t* __restrict__ am,
-                          const int64_t* __restrict__ lab_in = nullptr, int64_t* __restrict__ lab_out = nullptr) {
-  __shared__ float img[28 * 28];
-  __shared__ float sw[32 * 9];
-  __shared__ float sb[32];
-  const int s = blockIdx.x;
-  const int tid = threadIdx.x;
-  const int64_t src = idx ? idx[s] : row0 + s;
-  if (lab_in && tid == 0) lab_out[s] = lab_in[src];     // the batch's labels, gathered in passing
-  const XT* xr = x + src * 784;
-  for (int i = tid; i < 784; i += 256) img[i] = (float)xr[i];
-  for (int i = tid; i < 288; i += 256) sw[i] = w[i];
-  if (tid < 32) sb[tid] = b[tid];
-  __syncthreads();
-  float* yo = y + (int64_t)s * 5408;
-  uint8_t* ao = am + (int64_t)s * 5408;
-  for (int o = tid; o < 5408; o += 256) {
-    const int oc = o / 169;
-    const int r = o - oc * 169;
-    const int ph = r / 13;
-    const int pw = r - ph * 13;
-    const float* wk = sw + oc * 9;
-    const float* base = img + (2 * ph) * 28 + 2 * pw;
-    float patch[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) patch[i][j] = base[i * 28 + j];
-    float best = 0.f;
-    int arg = 0;
-#pragma unroll
-    for (int dy = 0; dy < 2; ++dy)
-#pragma unroll
-      for (int dx = 0; dx < 2; ++dx) {
-        float acc = 0.f;
-#pragma unroll
-        for (int kh = 0; kh < 3; ++kh)
-#pragma unroll
-          for (int kw = 0; kw < 3; ++kw) acc = fmaf(wk[kh * 3 + kw], patch[dy + kh][dx + kw], acc);
-        acc += sb[oc];
-        const int pos = dy * 2 + dx;
-        if (pos == 0 || acc > best) { best = acc; arg = pos; }   // first max (torch order)
-      }
-    yo[o] = fmaxf(best, 0.f);
-    ao[o] = (uint8_t)arg;
-  }
-}
-
-// ---------------------------------------------------------------------------------------
-// Two-stage backward + optimizer (a first single-kernel version, 32 workgroups each reducing
-// one channel over the whole batch, left most of the GPU idle):
-//   stage 1, one workgroup per sample: thread t owns output channel t>>3 and every 8th
-//   pooled position of it, so its dW/db contributions all go to ONE channel and are
-//   reduced by three xor-shuffles inside 8-lane groups -> slab[s][oc*10 + j];
-//   stage 2, one workgroup: sum the B slabs and apply SGD-m / Adam to the 320 params.
-// The SISA local step fuses stage 1 with the forward and the 5408-way softmax-CE of the
-// activation (Q5): the activation never leaves registers.
-
+// One pooled output: 4x4 input patch -> 2x2 conv outputs -> bias, max (first max, torch
+// order), ReLU; `arg` is the 2-bit position of the max for the backward.
 __device__ __forceinline__ void conv_pool_at(const float* img, const float* wk, float bias, int ph, int pw,
                                              float& y, int& arg) {
   const float* base = img + (2 * ph) * 28 + 2 * pw;
@@ -103,6 +43,98 @@ __device__ __forceinline__ void conv_pool_at(const float* img, const float* wk, 
     }
   y = fmaxf(best, 0.f);
 }
+
+// Deferred client optimizer step (split modes, FrontEngine): parameter slot p (slab layout
+// oc*10 + j; j = 9 is the bias) updated from the previous backward's pB partial slabs with
+// exactly conv_opt_reduce_kernel's arithmetic.  Returns the new value, a0/a1 the new states.
+__device__ __forceinline__ float conv_pending_param(const float* w, const float* b, const float* s0w,
+                                                   const float* s1w, const float* s0b, const float* s1b,
+                                                   const float* pslab, int pB, int p, const SlOpt& o,
+                                                   float& a0, float& a1) {
+  const int oc = p / 10, j = p - oc * 10;
+  const bool isw = j < 9;
+  const int k = isw ? oc * 9 + j : oc;
+  float pp = isw ? w[k] : b[k];
+  a0 = isw ? s0w[k] : s0b[k];
+  a1 = isw ? (s1w ? s1w[k] : 0.f) : (s1b ? s1b[k] : 0.f);
+  const float g = sum_slabs(pslab + p, pB, 320);
+  sl_opt_update(o, pp, g, a0, a1);
+  return pp;
+}
+
+// Grid (B, 4): workgroup (s, q) computes channels [8q, 8q + 8) of sample s (1352 pooled
+// outputs, 5-6 per thread), so a batch of 16 runs 64 workgroups instead of 16 and each
+// thread's serial chain is a quarter as long (the per-sample 256-thread form measured
+// 11 us per batch of 16 in the split modes, where this kernel is on the critical path).
+template <typename XT>
+__global__ void __launch_bounds__(256)
+conv_relu_pool_fwd_kernel(const XT* __restrict__ x, const int64_t* __restrict__ idx, int64_t row0,
+                          const float* __restrict__ w, const float* __restrict__ b,
+                          float* __restrict__ y, uint8_t* __restrict__ am,
+                          const int64_t* __restrict__ lab_in = nullptr, int64_t* __restrict__ lab_out = nullptr,
+                          const float* __restrict__ pslab = nullptr, int pB = 0, const float* __restrict__ s0w = nullptr,
+                          const float* __restrict__ s1w = nullptr, const float* __restrict__ s0b = nullptr,
+                          const float* __restrict__ s1b = nullptr, SlOpt o = SlOpt{}) {
+  constexpr int CH = 8, NO = CH * 169, PER = (NO + 255) / 256;
+  __shared__ float img[28 * 28];
+  __shared__ float sw[CH * 9];
+  __shared__ float sb[CH];
+  const int s = blockIdx.x, q = blockIdx.y;
+  const int tid = threadIdx.x;
+  const int64_t src = idx ? idx[s] : row0 + s;
+  // every independent load goes out before anything is consumed
+  const XT* xr = x + src * 784;
+  const float p0 = (float)xr[tid], p1 = (float)xr[256 + tid], p2 = (float)xr[512 + tid];
+  const float p3 = tid < 784 - 768 ? (float)xr[768 + tid] : 0.f;
+  if (lab_in && q == 0 && tid == 0) lab_out[s] = lab_in[src];     // the batch's labels, gathered in passing
+  if (pslab) {
+    // the previous backward's optimizer step, applied here for this group's 8 channels
+    // (80 parameters); FrontEngine's next backward stores the same values
+    if (tid < CH * 10) {
+      float a0, a1;
+      const float pp = conv_pending_param(w, b, s0w, s1w, s0b, s1b, pslab, pB, q * CH * 10 + tid, o, a0, a1);
+      const int c = tid / 10, j = tid - c * 10;
+      if (j < 9) sw[c * 9 + j] = pp; else sb[c] = pp;
+    }
+  } else {
+    const float wv = tid < CH * 9 ? w[q * CH * 9 + tid] : 0.f;
+    const float bv = tid < CH ? b[q * CH + tid] : 0.f;
+    if (tid < CH * 9) sw[tid] = wv;
+    if (tid < CH) sb[tid] = bv;
+  }
+  img[tid] = p0;
+  img[256 + tid] = p1;
+  img[512 + tid] = p2;
+  if (tid < 784 - 768) img[768 + tid] = p3;
+  __syncthreads();
+  float* yo = y + (int64_t)s * 5408 + q * NO;
+  uint8_t* ao = am + (int64_t)s * 5408 + q * NO;
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int o = tid + 256 * u;
+    if (o < NO) {
+      const int oc = o / 169;
+      const int r = o - oc * 169;
+      const int ph = r / 13;
+      const int pw = r - ph * 13;
+      float yv;
+      int arg;
+      conv_pool_at(img, sw + oc * 9, sb[oc], ph, pw, yv, arg);
+      yo[o] = yv;
+      ao[o] = (uint8_t)arg;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Two-stage backward + optimizer (a first single-kernel version, 32 workgroups each reducing
+// one channel over the whole batch, left most of the GPU idle):
+//   stage 1, one workgroup per sample: thread t owns output channel t>>3 and every 8th
+//   pooled position of it, so its dW/db contributions all go to ONE channel and are
+//   reduced by three xor-shuffles inside 8-lane groups -> slab[s][oc*10 + j];
+//   stage 2, one workgroup: sum the B slabs and apply SGD-m / Adam to the 320 params.
+// The SISA local step fuses stage 1 with the forward and the 5408-way softmax-CE of the
+// activation (Q5): the activation never leaves registers.
 
 __device__ __forceinline__ void conv_acc_grad(const float* img, int ph, int pw, int a, float g, float* acc) {
   const float* xr = img + (2 * ph + (a >> 1)) * 28 + 2 * pw + (a & 1);
@@ -280,10 +312,31 @@ template <typename XT>
 __global__ void __launch_bounds__(1024)
 conv_wgrad_partial_kernel(const float* __restrict__ dy, const float* __restrict__ y,
                           const uint8_t* __restrict__ am, const XT* __restrict__ x,
-                          const int64_t* __restrict__ idx, float* __restrict__ slab) {
+                          const int64_t* __restrict__ idx, float* __restrict__ slab,
+                          const float* __restrict__ pslab = nullptr, int pB = 0, float* __restrict__ w = nullptr,
+                          float* __restrict__ b = nullptr, float* __restrict__ s0w = nullptr,
+                          float* __restrict__ s1w = nullptr, float* __restrict__ s0b = nullptr,
+                          float* __restrict__ s1b = nullptr, SlOpt o = SlOpt{}) {
   __shared__ float img[28 * 28];
   constexpr int SUB = 32, P = (169 + SUB - 1) / SUB;
   const int s = blockIdx.x, tid = threadIdx.x;
+  if (pslab && s == 0 && tid < 320) {
+    // deferred mode: store the previous step's update (the values this step's forward
+    // already used); nothing in this launch reads w/b or the states, and this launch's
+    // own partials go to the other slab buffer
+    float a0, a1;
+    const float pp = conv_pending_param(w, b, s0w, s1w, s0b, s1b, pslab, pB, tid, o, a0, a1);
+    const int c = tid / 10, j = tid - c * 10;
+    if (j < 9) {
+      if (o.kind != 0) w[c * 9 + j] = pp;
+      s0w[c * 9 + j] = a0;
+      if (s1w) s1w[c * 9 + j] = a1;
+    } else {
+      if (o.kind != 0) b[c] = pp;
+      s0b[c] = a0;
+      if (s1b) s1b[c] = a1;
+    }
+  }
   const int oc = tid / SUB, sub = tid % SUB;
   const int64_t row = (int64_t)s * 5408 + oc * 169;
   float g[P], yv[P];
@@ -429,26 +482,45 @@ hipError_t conv_local_epoch(const void* x, bool x_u8, const int64_t* order, int6
   return hipGetLastError();
 }
 
+// Split-mode backward + optimizer.  Immediate (defer = false): partials, then the reduce +
+// update launch.  Deferred (defer = true): partials only, with `pend` (the step before,
+// if any) stored by workgroup 0; this step's update is left to the next forward / backward
+// or to conv_apply.  Both give bitwise the same parameters.
 hipError_t conv_bwd_step(const float* dy, const float* y, const uint8_t* am, const void* x, bool x_u8,
                          const int64_t* idx, int B, float* w, float* b, float* slab, float* s0w, float* s1w,
-                         float* s0b, float* s1b, SlOpt o, hipStream_t st) {
+                         float* s0b, float* s1b, SlOpt o, hipStream_t st, bool defer, const ConvPending* pend) {
   if (B <= 0) return hipSuccess;
+  const ConvPending p = pend ? *pend : ConvPending{nullptr, 0, nullptr, nullptr, nullptr, nullptr, SlOpt{}};
   if (x_u8)
-    conv_wgrad_partial_kernel<uint8_t><<<B, 1024, 0, st>>>(dy, y, am, (const uint8_t*)x, idx, slab);
+    conv_wgrad_partial_kernel<uint8_t><<<B, 1024, 0, st>>>(dy, y, am, (const uint8_t*)x, idx, slab, p.slab, p.B, w, b,
+                                                           p.s0w, p.s1w, p.s0b, p.s1b, p.o);
   else
-    conv_wgrad_partial_kernel<float><<<B, 1024, 0, st>>>(dy, y, am, (const float*)x, idx, slab);
-  conv_opt_reduce_kernel<<<1, 320, 0, st>>>(slab, B, w, b, s0w, s1w, s0b, s1b, o);
+    conv_wgrad_partial_kernel<float><<<B, 1024, 0, st>>>(dy, y, am, (const float*)x, idx, slab, p.slab, p.B, w, b,
+                                                         p.s0w, p.s1w, p.s0b, p.s1b, p.o);
+  if (!defer) conv_opt_reduce_kernel<<<1, 320, 0, st>>>(slab, B, w, b, s0w, s1w, s0b, s1b, o);
+  return hipGetLastError();
+}
+
+// Store a deferred update (end of a deferred run, or before the weights are read).
+hipError_t conv_apply(const ConvPending& p, float* w, float* b, hipStream_t st) {
+  if (!p.slab || p.B <= 0) return hipSuccess;
+  conv_opt_reduce_kernel<<<1, 320, 0, st>>>(p.slab, p.B, w, b, p.s0w, p.s1w, p.s0b, p.s1b, p.o);
   return hipGetLastError();
 }
 
 hipError_t conv_fwd(const void* x, bool x_u8, const int64_t* idx, int64_t row0, int B,
                     const float* w, const float* b, float* y, uint8_t* am, hipStream_t st,
-                    const int64_t* lab_in, int64_t* lab_out) {
+                    const int64_t* lab_in, int64_t* lab_out, const ConvPending* pend) {
   if (B <= 0) return hipSuccess;
+  const ConvPending p = pend ? *pend : ConvPending{nullptr, 0, nullptr, nullptr, nullptr, nullptr, SlOpt{}};
   if (x_u8)
-    conv_relu_pool_fwd_kernel<uint8_t><<<B, 256, 0, st>>>((const uint8_t*)x, idx, row0, w, b, y, am, lab_in, lab_out);
+    conv_relu_pool_fwd_kernel<uint8_t><<<dim3(B, 4), 256, 0, st>>>((const uint8_t*)x, idx, row0, w, b, y, am, lab_in,
+                                                                   lab_out, p.slab, p.B, p.s0w, p.s1w, p.s0b, p.s1b,
+                                                                   p.o);
   else
-    conv_relu_pool_fwd_kernel<float><<<B, 256, 0, st>>>((const float*)x, idx, row0, w, b, y, am, lab_in, lab_out);
+    conv_relu_pool_fwd_kernel<float><<<dim3(B, 4), 256, 0, st>>>((const float*)x, idx, row0, w, b, y, am, lab_in,
+                                                                 lab_out, p.slab, p.B, p.s0w, p.s1w, p.s0b, p.s1b,
+                                                                 p.o);
   return hipGetLastError();
 }
 

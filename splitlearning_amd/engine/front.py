@@ -25,14 +25,44 @@ class FrontEngine:
         self.device = device
         self.ops = ops.impl(device)
         self.frozen = False
+        # deferred optimizer step (split-mode epochs): (slab, B, cfg, st_w, st_b, t) of the last
+        # backward, applied by the next forward in-kernel and stored by the next backward, so
+        # a training batch is 2 client launches instead of 3; `flush` stores it
+        self._pending = None
+        self._slabs = None
+        self._defer_i = 0
 
-    @property
-    def params(self):
+    def _raw_params(self):
         w, b = self.module.conv_params()
         return w.data, b.data
 
+    @property
+    def params(self):
+        self.flush()
+        return self._raw_params()
+
+    def _slab_buf(self, B: int) -> torch.Tensor:
+        """Ping-pong partial-slab buffers: a pending step's slabs stay intact while the next
+        backward writes its own."""
+        if self._slabs is None or self._slabs[0].numel() < B * 320:
+            self.flush()                      # a pending step may point into the old buffers
+            self._slabs = [torch.empty(max(B, 64) * 320, device=self.device) for _ in range(2)]
+        buf = self._slabs[self._defer_i][:B * 320]
+        self._defer_i ^= 1
+        return buf
+
+    def flush(self):
+        """Store a deferred optimizer step (before anything else reads the weights)."""
+        p, self._pending = self._pending, None
+        if p is not None:
+            w, b = self._raw_params()
+            self.ops.conv_apply_(p, w, b)
+
     def forward(self, shard: DeviceShard, idx: torch.Tensor, with_labels: bool = False):
         """(activation, argmax); with_labels: (activation, argmax, shard.y[idx]) from one launch."""
+        if self._pending is not None and with_labels:
+            w, b = self._raw_params()
+            return self.ops.conv_front_fwd_pending(shard.x, idx, w, b, shard.y, self._pending)
         w, b = self.params
         if with_labels:
             return self.ops.conv_front_fwd(shard.x, idx, w, b, labels=shard.y)
@@ -46,11 +76,22 @@ class FrontEngine:
         return outs[0] if len(outs) == 1 else torch.cat(outs, 0)
 
     def backward_step(self, dy, y, am, shard: DeviceShard, idx, slot: OptSlot, t: int | None = None,
-                      prefix: str = ""):
+                      prefix: str = "", defer: bool = False):
+        """Backward + optimizer step.  `defer` (split-mode epochs, HIP path): launch only the
+        dW/db partials and leave the update pending for the next forward/backward (call
+        `flush` when the run of steps ends); bitwise the same parameters."""
         if self.frozen:
             # reference: loss.backward() on frozen params raises (Q18)
             raise RuntimeError("element 0 of tensors does not require grad and does not have a grad_fn "
                                "(client front is frozen: call unfreeze_weights first)")
+        if defer and hasattr(self.ops, "conv_front_bwd_defer_"):
+            w, b = self._raw_params()
+            t = slot.tick() if t is None else t
+            st_w, st_b = slot.state(prefix + "conv.weight", w), slot.state(prefix + "conv.bias", b)
+            slab = self._slab_buf(int(idx.numel()))
+            self.ops.conv_front_bwd_defer_(dy, y, am, shard.x, idx, w, b, slab, self._pending, st_w, st_b)
+            self._pending = (slab, int(idx.numel()), slot.cfg, st_w, st_b, t)
+            return
         w, b = self.params
         t = slot.tick() if t is None else t
         self.ops.conv_front_bwd_step_(dy, y, am, shard.x, idx, w, b, slot.cfg,
@@ -87,6 +128,7 @@ class FrontEngine:
         """Reference `reset_model` (data_entities_vanilla.py:204-207): reset the direct
         children that have `reset_parameters`.  For model1_sisa that is nothing (Q4) unless
         `true_reset` asks for the evident intent."""
+        self.flush()
         with torch.no_grad():
             if true_reset:
                 for m in self.module.modules():

@@ -82,6 +82,40 @@ def conv_front_bwd_step_(dy, y, am, x_u8, idx, w, b, cfg, st_w, st_b, t, dyn=Non
                       _s0(st_b), _s1(st_b), *_opt_args(cfg, t, dyn))
 
 
+def conv_front_fwd_pending(x_u8, idx, w, b, labels, pend):
+    """(y, am, labels[idx]) with the deferred optimizer step `pend` = (slab, B, cfg, st_w,
+    st_b, t) applied inside the kernel (not stored)."""
+    B = int(idx.numel())
+    dev = x_u8.device
+    y = torch.empty(B, CUT, device=dev, dtype=torch.float32)
+    am = torch.empty(B, CUT, device=dev, dtype=torch.uint8)
+    lab = torch.empty(B, device=dev, dtype=torch.int64)
+    slab, pB, cfg, st_w, st_b, t = pend
+    C().conv_fwd_pending(x_u8, idx, B, w.detach(), b.detach(), y, am, labels, lab, slab, int(pB), _s0(st_w),
+                         _s1(st_w), _s0(st_b), _s1(st_b), *_opt_args(cfg, t))
+    return y, am, lab
+
+
+def conv_front_bwd_defer_(dy, y, am, x_u8, idx, w, b, slab, pend, st_w, st_b):
+    """This step's dW/db partials into `slab`, no update launch; the pending step `pend`
+    (or None) is stored by the same launch."""
+    B = int(idx.numel())
+    if pend is None:
+        C().conv_bwd_defer(dy, y, am, x_u8, idx, B, w.detach(), b.detach(), slab, None, 0, _s0(st_w), _s1(st_w),
+                           _s0(st_b), _s1(st_b), *_opt_args(None, 0))
+        return
+    pslab, pB, cfg, pw, pb, t = pend
+    C().conv_bwd_defer(dy, y, am, x_u8, idx, B, w.detach(), b.detach(), slab, pslab, int(pB), _s0(pw), _s1(pw),
+                       _s0(pb), _s1(pb), *_opt_args(cfg, t))
+
+
+def conv_apply_(pend, w, b):
+    """Store a deferred client optimizer step."""
+    slab, pB, cfg, st_w, st_b, t = pend
+    C().conv_apply(slab, int(pB), w.detach(), b.detach(), _s0(st_w), _s1(st_w), _s0(st_b), _s1(st_b),
+                   *_opt_args(cfg, t))
+
+
 def conv_local_step_(x_u8, y_all, idx, w, b, cfg, st_w, st_b, t, loss_rows=None, dyn=None):
     """SISA client step in two kernels: gather+conv+pool+softmax-CE(5408)+dW partials,
     then reduce+optimizer.  Returns per-sample losses."""

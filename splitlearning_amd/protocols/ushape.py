@@ -148,7 +148,7 @@ class UShapeSession(Session):
             dxp = self.tail.backward_dgrad(dmid_b, need_dx=True) if self.is_bob else None
             dx = self.comm.reduce_to(dxp, host, self.bob_ranks, (M, CUT_FEATURES), torch.float32)
             if a is not None:
-                a.front.backward_step(dx, act, am, a.train, idx, a.slot, t=t, prefix="front.")
+                a.front.backward_step(dx, act, am, a.train, idx, a.slot, t=t, prefix="front.", defer=True)
             nxt = alice_fwd(spans[i + 1]) if i + 1 < len(spans) else None
             pre = False
             if self.is_bob:
@@ -159,6 +159,8 @@ class UShapeSession(Session):
                 else:
                     self.tail.backward_step(self.bob_slot(cid))
             cur = nxt
+        if a is not None:
+            a.front.flush()          # the last step's deferred client update
 
     def _run_epochs(self, cid: int, order_fn, n: int):
         for _ in _progress(range(self.args.epochs), self.show, desc="Epochs", ascii=" >="):

@@ -114,7 +114,7 @@ class VanillaSession(Session):
                     dxp = self.tail.backward_dgrad(dout, need_dx=True)
             dx = self.comm.reduce_to(dxp, host, self.bob_ranks, (M, CUT_FEATURES), torch.float32)
             if a is not None:
-                a.front.backward_step(dx, act, am, a.train, idx, a.slot)
+                a.front.backward_step(dx, act, am, a.train, idx, a.slot, defer=True)
             nxt = alice_fwd(spans[i + 1]) if i + 1 < len(spans) else None
             if self.is_bob:
                 if fused:
@@ -124,6 +124,8 @@ class VanillaSession(Session):
                 else:
                     self.tail.backward_step(self.bob_slot(cid))
             cur = nxt
+        if a is not None:
+            a.front.flush()          # the last step's deferred client update
 
     def _order_len(self, cid, order):
         n = torch.tensor([order.numel() if order is not None else 0], dtype=torch.int64, device=self.device)

@@ -321,3 +321,40 @@ def test_relu_mask(cuda):
     g = torch.Generator().manual_seed(11)
     d, h = torch.randn(16, 100, generator=g).to(cuda), torch.randn(16, 100, generator=g).to(cuda)
     torch.testing.assert_close(hip_ops.relu_mask(d, h, 2.0), torch_ops.relu_mask(d, h, 2.0))
+
+
+@pytest.mark.parametrize("kind", ["sgd", "adam"])
+def test_front_deferred_update_is_bitwise_immediate(cuda, kind):
+    """FrontEngine's deferred client step (the update applied by the next forward in-kernel
+    and stored by the next backward; 2 launches per batch instead of 3) gives bitwise the
+    same activations, parameters and optimizer states as the immediate form."""
+    from splitlearning_amd.data.device_dataset import DeviceShard
+    from splitlearning_amd.engine import FrontEngine, OptSlot
+    from splitlearning_amd.models import ClientFrontSisa
+    cfg = OptimCfg("adam", 1e-3, weight_decay=1e-5) if kind == "adam" else OptimCfg("sgd", 1e-2, momentum=0.9)
+    g = torch.Generator().manual_seed(5)
+    shard = DeviceShard(torch.randint(0, 256, (300, 784), dtype=torch.uint8, generator=g),
+                        torch.randint(0, 10, (300,), generator=g), cuda)
+    engines = []
+    for _ in range(2):
+        torch.manual_seed(11)
+        engines.append((FrontEngine(ClientFrontSisa(), cuda), OptSlot(cfg)))
+    batches = [torch.randperm(300, generator=g)[:bs].to(cuda) for bs in (16, 16, 16, 7, 16)]
+    dys = [torch.randn(idx.numel(), 5408, generator=g).to(cuda) * 1e-2 for idx in batches]
+    acts = [[], []]
+    for e, (fe, slot) in enumerate(engines):
+        for idx, dy in zip(batches, dys):
+            y, am, lab = fe.forward(shard, idx, with_labels=True)
+            acts[e].append((y.clone(), am.clone(), lab.clone()))
+            fe.backward_step(dy, y, am, shard, idx, slot, defer=(e == 1))
+        fe.flush()
+    torch.cuda.synchronize()
+    for (ya, aa, la), (yb, ab, lb) in zip(*acts):
+        assert torch.equal(ya, yb) and torch.equal(aa, ab) and torch.equal(la, lb)
+    (fa, sa), (fb, sb) = engines
+    for ta, tb in zip(fa.params, fb.params):
+        assert torch.equal(ta, tb)
+    assert sa.t == sb.t == len(batches)
+    for name in sa.states:
+        for k in sa.states[name]:
+            assert torch.equal(sa.states[name][k], sb.states[name][k]), (name, k)
