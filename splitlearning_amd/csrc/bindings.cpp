@@ -33,6 +33,9 @@ hipError_t conv_bwd_step(const float* dy, const float* y, const uint8_t* am, con
                          const int64_t* idx, int B, float* w, float* b, float* slab, float* s0w, float* s1w,
                          float* s0b, float* s1b, SlOpt o, hipStream_t st, bool defer, const ConvPending* pend);
 hipError_t conv_apply(const ConvPending& p, float* w, float* b, hipStream_t st);
+hipError_t head_step(const float* X, float* W, float* b, const int64_t* y, int64_t ignore, float scale,
+                     float* loss_rows, float* dX, float* s0w, float* s1w, float* s0b, float* s1b, int M, int K, int C,
+                     SlOpt o, hipStream_t st);
 hipError_t linear_fwd(const float* X, int ldx, const float* W, int ldw, float* Y, int ldy, int M, int N, int K,
                       Epi e, float* ws, int64_t ws_elems, hipStream_t st);
 hipError_t linear_dgrad(const float* dZ, int ldz, const float* W, int ldw, const float* hprev, int ldh,
@@ -297,6 +300,28 @@ void conv_bwd_defer(const at::Tensor& dy, const at::Tensor& y, const at::Tensor&
                           b.data_ptr<float>(), slab.data_ptr<float>(), s0w.data_ptr<float>(), fptr(s1w),
                           s0b.data_ptr<float>(), fptr(s1b), SlOpt{}, cur_stream(), true, has ? &p : nullptr),
         "conv_bwd_defer");
+}
+
+// U-shape head (Linear + CE) forward, data gradient and optimizer step in one launch.
+void head_step(const at::Tensor& X, at::Tensor& W, const OptT& b, const at::Tensor& y, int64_t ignore, double scale,
+               at::Tensor& loss_rows, at::Tensor& dX, at::Tensor& s0w, const OptT& s1w, const OptT& s0b,
+               const OptT& s1b, OPT_ARGS) {
+  need_rows(X, "X");
+  need_rows(W, "W");
+  const int64_t M = X.size(0), K = X.size(1), C = W.size(0);
+  TORCH_CHECK(X.is_contiguous() && W.is_contiguous() && W.size(1) == K, "X [M,K], W [C,K] contiguous");
+  TORCH_CHECK(M * K <= 4096 && C * K <= 4096 && M * C <= 1024, "head_step: layer too large for one workgroup");
+  need_cuda(y, "y");
+  TORCH_CHECK(y.scalar_type() == at::kLong && y.numel() == M, "labels int64 [M]");
+  need_f32(loss_rows, "loss_rows");
+  need_f32(dX, "dX");
+  TORCH_CHECK(loss_rows.numel() >= M && dX.is_contiguous() && dX.numel() == M * K, "outputs");
+  TORCH_CHECK(s0w.numel() == C * K && s0w.is_contiguous(), "state");
+  if (b.has_value() && b->defined()) TORCH_CHECK(b->numel() == C && s0b.has_value(), "bias state");
+  check(sl::head_step(X.data_ptr<float>(), W.data_ptr<float>(), fptr(b), y.data_ptr<int64_t>(), ignore, (float)scale,
+                      loss_rows.data_ptr<float>(), dX.data_ptr<float>(), s0w.data_ptr<float>(), fptr(s1w), fptr(s0b),
+                      fptr(s1b), (int)M, (int)K, (int)C, OPT_PASS, cur_stream()),
+        "head_step");
 }
 
 // Store a deferred update (FrontEngine.flush).
@@ -605,6 +630,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_bwd_defer", &conv_bwd_defer);
   m.def("conv_fwd_pending", &conv_fwd_pending);
   m.def("conv_apply", &conv_apply);
+  m.def("head_step", &head_step);
   m.def("conv_local_epoch", &conv_local_epoch);
   m.def("linear_fwd", &linear_fwd);
   m.def("linear_epilogue", &linear_epilogue);

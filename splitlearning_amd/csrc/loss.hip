@@ -154,4 +154,90 @@ hipError_t eval_counters(const float* x, int ldx, const int64_t* y, int64_t omit
   return hipGetLastError();
 }
 
+
+// U-shape head (reference model3 = Linear(100, 10) + CrossEntropyLoss on Alice,
+// data_entities.py:74-81): forward, softmax-CE, data gradient and the optimizer step of
+// the whole layer in ONE workgroup (the separate path is four launches of a few us each
+// for 1,010 parameters).  dX uses the weights before the update.  Sizes: M*K, C*K <= 4096.
+__global__ void __launch_bounds__(256)
+head_step_kernel(const float* __restrict__ X, const float* __restrict__ W, const float* __restrict__ bias,
+                 const int64_t* __restrict__ y, int64_t ignore, float scale, float* __restrict__ loss_rows,
+                 float* __restrict__ dX, float* __restrict__ Wout, float* __restrict__ bout, float* __restrict__ s0w,
+                 float* __restrict__ s1w, float* __restrict__ s0b, float* __restrict__ s1b, int M, int K, int C,
+                 SlOpt o) {
+  __shared__ float sx[4096];
+  __shared__ float sw[4096];
+  __shared__ float sd[1024];     // dlogits [M][C]
+  const int tid = threadIdx.x;
+  for (int i = tid; i < M * K; i += 256) sx[i] = X[i];
+  for (int i = tid; i < C * K; i += 256) sw[i] = W[i];
+  __syncthreads();
+  // logits (into sd), one (m, c) per thread
+  for (int i = tid; i < M * C; i += 256) {
+    const int m = i / C, c = i - m * C;
+    float v = 0.f;
+    for (int k = 0; k < K; ++k) v = fmaf(sx[m * K + k], sw[c * K + k], v);
+    sd[i] = v + (bias ? bias[c] : 0.f);
+  }
+  __syncthreads();
+  // softmax-CE per row
+  if (tid < M) {
+    float* r = sd + tid * C;
+    const int64_t lab = y[tid];
+    if (lab == ignore) {
+      loss_rows[tid] = 0.f;
+      for (int c = 0; c < C; ++c) r[c] = 0.f;
+    } else {
+      float mx = -INFINITY;
+      for (int c = 0; c < C; ++c) mx = fmaxf(mx, r[c]);
+      float se = 0.f;
+      for (int c = 0; c < C; ++c) se += expf(r[c] - mx);
+      const float inv = 1.f / se;
+      loss_rows[tid] = mx + logf(se) - r[lab];
+      for (int c = 0; c < C; ++c) {
+        float p = expf(r[c] - mx) * inv;
+        if (c == lab) p -= 1.f;
+        r[c] = p * scale;
+      }
+    }
+  }
+  __syncthreads();
+  // data gradient with the current weights
+  for (int i = tid; i < M * K; i += 256) {
+    const int m = i / K, k = i - m * K;
+    float v = 0.f;
+    for (int c = 0; c < C; ++c) v = fmaf(sd[m * C + c], sw[c * K + k], v);
+    dX[i] = v;
+  }
+  // weight / bias gradient and the optimizer step
+  for (int i = tid; i < C * K; i += 256) {
+    const int c = i / K, k = i - c * K;
+    float g = 0.f;
+    for (int m = 0; m < M; ++m) g = fmaf(sd[m * C + c], sx[m * K + k], g);
+    float pp = sw[i], a0 = s0w[i], a1 = s1w ? s1w[i] : 0.f;
+    sl_opt_update(o, pp, g, a0, a1);
+    if (o.kind != 0) Wout[i] = pp;
+    s0w[i] = a0;
+    if (s1w) s1w[i] = a1;
+  }
+  if (bias && tid < C) {
+    float g = 0.f;
+    for (int m = 0; m < M; ++m) g += sd[m * C + tid];
+    float pp = bias[tid], a0 = s0b[tid], a1 = s1b ? s1b[tid] : 0.f;
+    sl_opt_update(o, pp, g, a0, a1);
+    if (o.kind != 0) bout[tid] = pp;
+    s0b[tid] = a0;
+    if (s1b) s1b[tid] = a1;
+  }
+}
+
+hipError_t head_step(const float* X, float* W, float* b, const int64_t* y, int64_t ignore, float scale,
+                     float* loss_rows, float* dX, float* s0w, float* s1w, float* s0b, float* s1b, int M, int K, int C,
+                     SlOpt o, hipStream_t st) {
+  if (M <= 0) return hipSuccess;
+  if (M * K > 4096 || C * K > 4096 || M * C > 1024) return hipErrorInvalidValue;
+  head_step_kernel<<<1, 256, 0, st>>>(X, W, b, y, ignore, scale, loss_rows, dX, W, b, s0w, s1w, s0b, s1b, M, K, C, o);
+  return hipGetLastError();
+}
+
 }  // namespace sl

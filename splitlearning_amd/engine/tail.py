@@ -181,6 +181,29 @@ class TailEngine:
         self._pre = pn
         self.dz = []
 
+    # ------------------------------------------------------------------ fused one-layer head step
+    def head_step_ok(self, m: int) -> bool:
+        """A single Linear layer (no ReLU / dropout) small enough for `_C.head_step`: the
+        U-shape head (reference model3, 100 -> 10)."""
+        if not hasattr(self.ops, "head_step_") or len(self.layers) != 1:
+            return False
+        L = self.layers[0]
+        n, k = L.W.shape
+        return (not L.spec.relu and L.spec.dropout == 0 and self.tp_size == 1
+                and m * k <= 4096 and n * k <= 4096 and m * n <= 1024)
+
+    def head_step(self, x, labels, slot: OptSlot, t: int, prefix: str = ""):
+        """forward + softmax-CE (mean) + dL/dx + optimizer step of the one-layer head in one
+        launch; same math as forward / softmax_ce / backward_dgrad / backward_step.
+        Returns (per-row loss, dL/dx)."""
+        L = self.layers[0]
+        self.fwd_count += 1
+        loss, dx = self.ops.head_step_(x, L.W, L.b, labels, 1.0 / x.shape[0], slot.cfg,
+                                       slot.state(f"{prefix}{L.spec.name}.weight", L.W),
+                                       slot.state(f"{prefix}{L.spec.name}.bias", L.b), t)
+        self.acts, self.dz = [], []
+        return loss, dx
+
     # ------------------------------------------------------------------ fused 3-layer step
     def fused3_ok(self) -> bool:
         """The SISA/vanilla server tail (fc1 ReLU+Dropout, fc2 ReLU+Dropout, fc3 -> CE) on the

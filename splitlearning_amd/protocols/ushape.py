@@ -81,6 +81,18 @@ class UShapeSession(Session):
             a.head.reset_parameters()
 
     # ------------------------------------------------------------------ one U-shape step
+    def head_train(self, a, mid, labels, t: int):
+        """Alice's head on Bob's output: forward, CE, dL/d(mid) and the head's optimizer step
+        (data_entities.py:74-81).  One launch when the head fits `_C.head_step`."""
+        if a.head.head_step_ok(mid.shape[0]):
+            _, dmid = a.head.head_step(mid, labels, a.slot, t, prefix="head.")
+            return dmid
+        logits = a.head.forward(mid, train=True)
+        _, dlog = self.ops.softmax_ce(logits, labels, 1.0 / mid.shape[0])
+        dmid = a.head.backward_dgrad(dlog, need_dx=True)
+        a.head.backward_step(a.slot, t, prefix="head.")
+        return dmid
+
     def split_step(self, cid: int, idx, B: int):
         host = self.host(cid)
         a = self.alices.get(cid)
@@ -93,11 +105,8 @@ class UShapeSession(Session):
         dmid = None
         t = None
         if a is not None:
-            logits = a.head.forward(mid, train=True)
-            _, dlog = self.ops.softmax_ce(logits, labels, 1.0 / B)
-            dmid = a.head.backward_dgrad(dlog, need_dx=True)
             t = a.slot.tick()
-            a.head.backward_step(a.slot, t, prefix="head.")
+            dmid = self.head_train(a, mid, labels, t)
         dmid_b = self.to_bob(cid, dmid, (B, 100))
         dxp = self.tail.backward_dgrad(dmid_b, need_dx=True) if self.is_bob else None
         fin = self.comm.reduce_to_async(dxp, host, self.bob_ranks, (B, CUT_FEATURES), torch.float32)
@@ -139,11 +148,8 @@ class UShapeSession(Session):
             mid = self.from_bob(cid, out, (M, 100))
             dmid = t = None
             if a is not None:
-                logits = a.head.forward(mid, train=True)
-                _, dlog = self.ops.softmax_ce(logits, labels, 1.0 / M)
-                dmid = a.head.backward_dgrad(dlog, need_dx=True)
                 t = a.slot.tick()
-                a.head.backward_step(a.slot, t, prefix="head.")
+                dmid = self.head_train(a, mid, labels, t)
             dmid_b = self.to_bob(cid, dmid, (M, 100))
             dxp = self.tail.backward_dgrad(dmid_b, need_dx=True) if self.is_bob else None
             dx = self.comm.reduce_to(dxp, host, self.bob_ranks, (M, CUT_FEATURES), torch.float32)

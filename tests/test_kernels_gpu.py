@@ -324,6 +324,38 @@ def test_relu_mask(cuda):
 
 
 @pytest.mark.parametrize("kind", ["sgd", "adam"])
+@pytest.mark.parametrize("M", [16, 7])
+def test_head_step_matches_torch(cuda, kind, M):
+    """_C.head_step (the U-shape head's forward + CE + dgrad + optimizer in one launch) ==
+    the fp32 torch reference of the same step."""
+    cfg = OptimCfg("adam", 1e-3) if kind == "adam" else OptimCfg("sgd", 1e-2, momentum=0.9)
+    g = torch.Generator().manual_seed(2)
+    x = torch.rand(M, 100, generator=g)
+    W, b = torch.randn(10, 100, generator=g) * 0.1, torch.randn(10, generator=g) * 0.1
+    y = torch.randint(0, 10, (M,), generator=g)
+    st = lambda p: ({"m": torch.full_like(p, 0.01), "v": torch.full_like(p, 0.02)} if kind == "adam"  # noqa: E731
+                    else {"buf": torch.full_like(p, 0.01)})
+    sw_ref, sb_ref = st(W), st(b)
+    Wr, br = W.clone().requires_grad_(), b.clone().requires_grad_()
+    xr = x.clone().requires_grad_()
+    loss_ref = torch.nn.functional.cross_entropy(xr @ Wr.t() + br, y, reduction="none")
+    loss_ref.mean().backward()
+    Wn, bn = W.clone(), b.clone()
+    torch_ops.apply_update_(Wn, Wr.grad, sw_ref, cfg, 3)
+    torch_ops.apply_update_(bn, br.grad, sb_ref, cfg, 3)
+    Wg, bg = W.to(cuda), b.to(cuda)
+    swg, sbg = {k: v.to(cuda) for k, v in st(W).items()}, {k: v.to(cuda) for k, v in st(b).items()}
+    loss, dx = hip_ops.head_step_(x.to(cuda), Wg, bg, y.to(cuda), 1.0 / M, cfg, swg, sbg, 3)
+    _close(loss, loss_ref.detach(), rtol=1e-5, atol=1e-5)
+    _close(dx, xr.grad, rtol=1e-5, atol=1e-6)
+    _close(Wg, Wn, rtol=1e-5, atol=1e-6)
+    _close(bg, bn, rtol=1e-5, atol=1e-6)
+    for k in swg:
+        _close(swg[k], sw_ref[k], rtol=1e-5, atol=1e-7)
+        _close(sbg[k], sb_ref[k], rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("kind", ["sgd", "adam"])
 def test_front_deferred_update_is_bitwise_immediate(cuda, kind):
     """FrontEngine's deferred client step (the update applied by the next forward in-kernel
     and stored by the next backward; 2 launches per batch instead of 3) gives bitwise the
