@@ -35,7 +35,7 @@ hipError_t conv_bwd_step(const float* dy, const float* y, const uint8_t* am, con
 hipError_t conv_apply(const ConvPending& p, float* w, float* b, hipStream_t st);
 hipError_t head_step(const float* X, float* W, float* b, const int64_t* y, int64_t ignore, float scale,
                      float* loss_rows, float* dX, float* s0w, float* s1w, float* s0b, float* s1b, int M, int K, int C,
-                     SlOpt o, hipStream_t st);
+                     SlOpt o, bool mask_dx, hipStream_t st);
 hipError_t linear_fwd(const float* X, int ldx, const float* W, int ldw, float* Y, int ldy, int M, int N, int K,
                       Epi e, float* ws, int64_t ws_elems, hipStream_t st);
 hipError_t linear_dgrad(const float* dZ, int ldz, const float* W, int ldw, const float* hprev, int ldh,
@@ -304,7 +304,7 @@ void conv_bwd_defer(const at::Tensor& dy, const at::Tensor& y, const at::Tensor&
 
 // U-shape head (Linear + CE) forward, data gradient and optimizer step in one launch.
 void head_step(const at::Tensor& X, at::Tensor& W, const OptT& b, const at::Tensor& y, int64_t ignore, double scale,
-               at::Tensor& loss_rows, at::Tensor& dX, at::Tensor& s0w, const OptT& s1w, const OptT& s0b,
+               bool mask_dx, at::Tensor& loss_rows, at::Tensor& dX, at::Tensor& s0w, const OptT& s1w, const OptT& s0b,
                const OptT& s1b, OPT_ARGS) {
   need_rows(X, "X");
   need_rows(W, "W");
@@ -320,7 +320,7 @@ void head_step(const at::Tensor& X, at::Tensor& W, const OptT& b, const at::Tens
   if (b.has_value() && b->defined()) TORCH_CHECK(b->numel() == C && s0b.has_value(), "bias state");
   check(sl::head_step(X.data_ptr<float>(), W.data_ptr<float>(), fptr(b), y.data_ptr<int64_t>(), ignore, (float)scale,
                       loss_rows.data_ptr<float>(), dX.data_ptr<float>(), s0w.data_ptr<float>(), fptr(s1w), fptr(s0b),
-                      fptr(s1b), (int)M, (int)K, (int)C, OPT_PASS, cur_stream()),
+                      fptr(s1b), (int)M, (int)K, (int)C, OPT_PASS, mask_dx, cur_stream()),
         "head_step");
 }
 

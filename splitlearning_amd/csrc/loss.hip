@@ -158,17 +158,35 @@ hipError_t eval_counters(const float* x, int ldx, const int64_t* y, int64_t omit
 // U-shape head (reference model3 = Linear(100, 10) + CrossEntropyLoss on Alice,
 // data_entities.py:74-81): forward, softmax-CE, data gradient and the optimizer step of
 // the whole layer in ONE workgroup (the separate path is four launches of a few us each
-// for 1,010 parameters).  dX uses the weights before the update.  Sizes: M*K, C*K <= 4096.
+// for 1,010 parameters).  dX uses the weights before the update; with mask_dx it is also
+// masked by [X > 0], the ReLU backward of the layer that produced X (Bob's model2 ends in a
+// ReLU whose output X is), so the producer skips its own mask launch.  M*K, C*K <= 4096.
 __global__ void __launch_bounds__(256)
 head_step_kernel(const float* __restrict__ X, const float* __restrict__ W, const float* __restrict__ bias,
                  const int64_t* __restrict__ y, int64_t ignore, float scale, float* __restrict__ loss_rows,
                  float* __restrict__ dX, float* __restrict__ Wout, float* __restrict__ bout, float* __restrict__ s0w,
                  float* __restrict__ s1w, float* __restrict__ s0b, float* __restrict__ s1b, int M, int K, int C,
-                 SlOpt o) {
+                 SlOpt o, int mask_dx) {
   __shared__ float sx[4096];
   __shared__ float sw[4096];
   __shared__ float sd[1024];     // dlogits [M][C]
   const int tid = threadIdx.x;
+  // the optimizer state this thread updates at the end is loaded first, so the update does
+  // not wait on dependent global loads (4 elements per thread covers C*K <= 1024)
+  constexpr int PF = 4;
+  float r0[PF], r1[PF];
+#pragma unroll
+  for (int j = 0; j < PF; ++j) {
+    const int i = tid + 256 * j;
+    r0[j] = i < C * K ? s0w[i] : 0.f;
+    r1[j] = (i < C * K && s1w) ? s1w[i] : 0.f;
+  }
+  float rb0 = 0.f, rb1 = 0.f, rbp = 0.f;
+  if (bias && tid < C) {
+    rbp = bias[tid];
+    rb0 = s0b[tid];
+    rb1 = s1b ? s1b[tid] : 0.f;
+  }
   for (int i = tid; i < M * K; i += 256) sx[i] = X[i];
   for (int i = tid; i < C * K; i += 256) sw[i] = W[i];
   __syncthreads();
@@ -207,23 +225,27 @@ head_step_kernel(const float* __restrict__ X, const float* __restrict__ W, const
     const int m = i / K, k = i - m * K;
     float v = 0.f;
     for (int c = 0; c < C; ++c) v = fmaf(sd[m * C + c], sw[c * K + k], v);
-    dX[i] = v;
+    dX[i] = (mask_dx && !(sx[i] > 0.f)) ? 0.f : v;   // mask_dx: the producer's ReLU backward too
   }
   // weight / bias gradient and the optimizer step
-  for (int i = tid; i < C * K; i += 256) {
+  auto wstep = [&](int i, float a0, float a1) {
     const int c = i / K, k = i - c * K;
     float g = 0.f;
     for (int m = 0; m < M; ++m) g = fmaf(sd[m * C + c], sx[m * K + k], g);
-    float pp = sw[i], a0 = s0w[i], a1 = s1w ? s1w[i] : 0.f;
+    float pp = sw[i];
     sl_opt_update(o, pp, g, a0, a1);
     if (o.kind != 0) Wout[i] = pp;
     s0w[i] = a0;
     if (s1w) s1w[i] = a1;
-  }
+  };
+#pragma unroll
+  for (int j = 0; j < PF; ++j)       // compile-time register index (no scratch)
+    if (tid + 256 * j < C * K) wstep(tid + 256 * j, r0[j], r1[j]);
+  for (int i = tid + 256 * PF; i < C * K; i += 256) wstep(i, s0w[i], s1w ? s1w[i] : 0.f);
   if (bias && tid < C) {
     float g = 0.f;
     for (int m = 0; m < M; ++m) g += sd[m * C + tid];
-    float pp = bias[tid], a0 = s0b[tid], a1 = s1b ? s1b[tid] : 0.f;
+    float pp = rbp, a0 = rb0, a1 = rb1;
     sl_opt_update(o, pp, g, a0, a1);
     if (o.kind != 0) bout[tid] = pp;
     s0b[tid] = a0;
@@ -233,10 +255,11 @@ head_step_kernel(const float* __restrict__ X, const float* __restrict__ W, const
 
 hipError_t head_step(const float* X, float* W, float* b, const int64_t* y, int64_t ignore, float scale,
                      float* loss_rows, float* dX, float* s0w, float* s1w, float* s0b, float* s1b, int M, int K, int C,
-                     SlOpt o, hipStream_t st) {
+                     SlOpt o, bool mask_dx, hipStream_t st) {
   if (M <= 0) return hipSuccess;
   if (M * K > 4096 || C * K > 4096 || M * C > 1024) return hipErrorInvalidValue;
-  head_step_kernel<<<1, 256, 0, st>>>(X, W, b, y, ignore, scale, loss_rows, dX, W, b, s0w, s1w, s0b, s1b, M, K, C, o);
+  head_step_kernel<<<1, 256, 0, st>>>(X, W, b, y, ignore, scale, loss_rows, dX, W, b, s0w, s1w, s0b, s1b, M, K, C, o,
+                                      mask_dx ? 1 : 0);
   return hipGetLastError();
 }
 

@@ -121,14 +121,18 @@ class TailEngine:
     __call__ = forward
 
     # ------------------------------------------------------------------ backward
-    def backward_dgrad(self, dout: torch.Tensor, need_dx: bool):
+    def backward_dgrad(self, dout: torch.Tensor, need_dx: bool, premasked: bool = False):
         """Phase 1: all data gradients.  Returns dL/dx (a *partial sum* across TP
-        ranks when fc1 is column-parallel) if `need_dx`, else None."""
+        ranks when fc1 is column-parallel) if `need_dx`, else None.  `premasked`: the
+        consumer already applied this tail's final ReLU backward (no active dropout)."""
         L = self.layers
         n = len(L)
         last = L[-1].spec
         dz = dout
-        if last.relu or (last.dropout and self._train_fwd):
+        drop_on = bool(last.dropout and self._train_fwd)
+        if premasked and not drop_on:
+            pass
+        elif last.relu or drop_on:
             scale = 1.0 / (1.0 - last.dropout) if (last.dropout and self._train_fwd) else 1.0
             dz = self.ops.relu_mask(dout, self.acts[-1], scale)
         dzs = [None] * n
@@ -192,15 +196,17 @@ class TailEngine:
         return (not L.spec.relu and L.spec.dropout == 0 and self.tp_size == 1
                 and m * k <= 4096 and n * k <= 4096 and m * n <= 1024)
 
-    def head_step(self, x, labels, slot: OptSlot, t: int, prefix: str = ""):
+    def head_step(self, x, labels, slot: OptSlot, t: int, prefix: str = "", mask_input: bool = False):
         """forward + softmax-CE (mean) + dL/dx + optimizer step of the one-layer head in one
         launch; same math as forward / softmax_ce / backward_dgrad / backward_step.
+        `mask_input`: dL/dx also gets the producer's ReLU backward ([x > 0]).
         Returns (per-row loss, dL/dx)."""
         L = self.layers[0]
         self.fwd_count += 1
         loss, dx = self.ops.head_step_(x, L.W, L.b, labels, 1.0 / x.shape[0], slot.cfg,
                                        slot.state(f"{prefix}{L.spec.name}.weight", L.W),
-                                       slot.state(f"{prefix}{L.spec.name}.bias", L.b), t)
+                                       slot.state(f"{prefix}{L.spec.name}.bias", L.b), t,
+                                       mask_by_input=mask_input)
         self.acts, self.dz = [], []
         return loss, dx
 

@@ -281,15 +281,17 @@ def softmax_ce(logits, labels, scale: float, ignore_index: int = -100, d_out=Non
     return loss, d
 
 
-def head_step_(x, W, b, labels, scale: float, cfg, st_w, st_b, t, ignore_index: int = -100):
+def head_step_(x, W, b, labels, scale: float, cfg, st_w, st_b, t, ignore_index: int = -100,
+               mask_by_input: bool = False):
     """One small Linear + CE layer's forward, softmax-CE, data gradient and optimizer step in
     one launch (the U-shape head on Alice).  Returns (loss_rows, dX); dX uses the weights
-    before the update."""
+    before the update, and with `mask_by_input` is also masked by [x > 0] (the producer's
+    ReLU backward)."""
     M = x.shape[0]
     loss = torch.empty(M, device=x.device, dtype=torch.float32)
     dx = torch.empty_like(x)
     C().head_step(x.contiguous(), W.detach(), b.detach() if b is not None else None, labels, int(ignore_index),
-                  float(scale), loss, dx, _s0(st_w), _s1(st_w), _s0(st_b) if b is not None else None,
+                  float(scale), bool(mask_by_input), loss, dx, _s0(st_w), _s1(st_w), _s0(st_b) if b is not None else None,
                   _s1(st_b) if b is not None else None, *_opt_args(cfg, t))
     return loss, dx
 

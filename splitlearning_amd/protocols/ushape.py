@@ -81,11 +81,19 @@ class UShapeSession(Session):
             a.head.reset_parameters()
 
     # ------------------------------------------------------------------ one U-shape step
+    def head_fused(self, M: int) -> bool:
+        """Whether Alice's head runs as one `_C.head_step` launch for a batch of M.  Every
+        rank evaluates this same rule (device kernels + the fixed 100 -> 10 head), so Bob
+        knows that the dL/d(mid) he receives already carries his final ReLU's backward."""
+        return hasattr(self.ops, "head_step_") and M * 100 <= 4096 and M * 10 <= 1024
+
     def head_train(self, a, mid, labels, t: int):
         """Alice's head on Bob's output: forward, CE, dL/d(mid) and the head's optimizer step
-        (data_entities.py:74-81).  One launch when the head fits `_C.head_step`."""
-        if a.head.head_step_ok(mid.shape[0]):
-            _, dmid = a.head.head_step(mid, labels, a.slot, t, prefix="head.")
+        (data_entities.py:74-81).  One launch when the head fits `_C.head_step`; that launch
+        also applies the [mid > 0] mask of Bob's final ReLU (mid is that ReLU's output)."""
+        if self.head_fused(mid.shape[0]):
+            assert a.head.head_step_ok(mid.shape[0])
+            _, dmid = a.head.head_step(mid, labels, a.slot, t, prefix="head.", mask_input=True)
             return dmid
         logits = a.head.forward(mid, train=True)
         _, dlog = self.ops.softmax_ce(logits, labels, 1.0 / mid.shape[0])
@@ -108,7 +116,7 @@ class UShapeSession(Session):
             t = a.slot.tick()
             dmid = self.head_train(a, mid, labels, t)
         dmid_b = self.to_bob(cid, dmid, (B, 100))
-        dxp = self.tail.backward_dgrad(dmid_b, need_dx=True) if self.is_bob else None
+        dxp = self.tail.backward_dgrad(dmid_b, need_dx=True, premasked=self.head_fused(B)) if self.is_bob else None
         fin = self.comm.reduce_to_async(dxp, host, self.bob_ranks, (B, CUT_FEATURES), torch.float32)
         if self.is_bob:
             self.tail.backward_step(self.bob_slot(cid))
@@ -151,7 +159,8 @@ class UShapeSession(Session):
                 t = a.slot.tick()
                 dmid = self.head_train(a, mid, labels, t)
             dmid_b = self.to_bob(cid, dmid, (M, 100))
-            dxp = self.tail.backward_dgrad(dmid_b, need_dx=True) if self.is_bob else None
+            dxp = (self.tail.backward_dgrad(dmid_b, need_dx=True, premasked=self.head_fused(M))
+                   if self.is_bob else None)
             dx = self.comm.reduce_to(dxp, host, self.bob_ranks, (M, CUT_FEATURES), torch.float32)
             if a is not None:
                 a.front.backward_step(dx, act, am, a.train, idx, a.slot, t=t, prefix="front.", defer=True)

@@ -353,6 +353,15 @@ def test_head_step_matches_torch(cuda, kind, M):
     for k in swg:
         _close(swg[k], sw_ref[k], rtol=1e-5, atol=1e-7)
         _close(sbg[k], sb_ref[k], rtol=1e-5, atol=1e-7)
+    # mask_by_input: dX also carries the producer's ReLU backward, [x > 0]
+    xs = torch.randn(M, 100, generator=g)
+    outs = []
+    for mask in (False, True):
+        W2, b2 = W.to(cuda), b.to(cuda)
+        s2w, s2b = {k: v.to(cuda) for k, v in st(W).items()}, {k: v.to(cuda) for k, v in st(b).items()}
+        outs.append(hip_ops.head_step_(xs.to(cuda), W2, b2, y.to(cuda), 1.0 / M, cfg, s2w, s2b, 3,
+                                       mask_by_input=mask)[1])
+    assert torch.equal(outs[1], torch.where(xs.to(cuda) > 0, outs[0], torch.zeros_like(outs[0])))
 
 
 @pytest.mark.parametrize("kind", ["sgd", "adam"])
