@@ -68,3 +68,22 @@ def test_resume_from_mid_schedule_snapshot_on_gpu(cuda, tmp_path, flags):
         b = torch.load(tmp_path / "res" / f, weights_only=True)
         for k in a:
             assert torch.equal(a[k], b[k]), (f, k)
+
+
+@pytest.mark.parametrize("flags", [[], ["--sisa", "--concat", "--concat_unlearn"], ["--control"]])
+def test_runs_are_bitwise_deterministic_on_gpu(cuda, tmp_path, flags):
+    """Race screen for the kernels: the same seeded run twice gives bitwise equal weights.
+    Every cross-workgroup reduction in csrc/ is a fixed-order slab sum (no float atomics),
+    so a difference here means an inter-workgroup race or an uninitialised read."""
+    import torch
+    outs = []
+    for r in ("a", "b"):
+        _run(tmp_path / r, flags, ws=3, extra=["--save_dir", str(tmp_path / r / "out")])
+        outs.append(tmp_path / r / "out")
+    for f in ["bob.pt", "alice1.pt", "alice2.pt"]:
+        a = torch.load(outs[0] / f, weights_only=True)
+        b = torch.load(outs[1] / f, weights_only=True)
+        fa = a if "model1" not in a else {**a["model1"], **a["model3"]}
+        fb = b if "model1" not in b else {**b["model1"], **b["model3"]}
+        for k in fa:
+            assert torch.equal(fa[k], fb[k]), (f, k)
