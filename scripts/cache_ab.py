@@ -31,7 +31,10 @@ from splitlearning_amd.models import ServerTailSisa, sisa_server_spec  # noqa: E
 from splitlearning_amd.ops import hip_ops as H  # noqa: E402
 
 VARIANTS = {"fwd": {7: 1, 4: 1, 2: 0}, "zigzag": {7: 0, 4: 1, 2: 0}, "zz+wt": {7: 0, 4: 0, 2: 0},
-            "zz+wt2d": {7: 0, 4: 0, 2: 1}, "zz+wt1d": {7: 0, 4: 0, 2: 2}}
+            "zz+wt2d": {7: 0, 4: 0, 2: 1}, "zz+wt1d": {7: 0, 4: 0, 2: 2},
+            # fc2 dgrad split-N cap (csrc/linear.hip linear_dgrad, variant 5): max S, 16-row slices
+            "dgS16": {5: 16}, "dgS32": {5: 32}, "dgS64": {5: 64}}
+SLOTS = (2, 4, 5, 7)
 
 
 def main():
@@ -71,6 +74,8 @@ def main():
         res = {v: [] for v in a.variants}
         for _ in range(a.rounds):
             for v in a.variants:
+                for slot_id in SLOTS:
+                    C.set_variant(slot_id, 0)
                 for slot_id, val in VARIANTS[v].items():
                     C.set_variant(slot_id, val)
                 steps(a.settle)
@@ -79,7 +84,7 @@ def main():
                 steps(a.steps)
                 torch.cuda.synchronize()
                 res[v].append((time.perf_counter() - t0) / a.steps * 1e6)
-        for slot_id in (2, 4, 7):
+        for slot_id in SLOTS:
             C.set_variant(slot_id, 0)       # back to the defaults
         for v, xs in res.items():
             print(f"tp={tp} {v:7s} median {statistics.median(xs):7.2f} us/step  min {min(xs):7.2f}  "

@@ -334,10 +334,14 @@ hipError_t linear_dgrad(const float* dZ, int ldz, const float* W, int ldw, const
   int S = 1;
   // aim for >= ~256 workgroups on the 256-CU part; split N when there are few K tiles
   // (variant 5 = max split, for A/B: 1 = never split)
+  // (variant 5 = max split, for A/B: 1 = never split; >1 also lets a workgroup's N slice
+  //  shrink to 16 rows, so TP shards with few K tiles can still fill the chip)
   const int smax = g_variant[5] > 0 ? g_variant[5] : 16;
-  while (S < smax && kt * mt * S < 768 && N / (S * 2) >= 64) S *= 2;
+  const int rmin = g_variant[5] > 1 ? 16 : 64;
+  while (S < smax && kt * mt * S < 768 && N / (S * 2) >= rmin) S *= 2;
   const int64_t slab = (int64_t)M * K;
-  if (S > 1 && (ws == nullptr || ws_elems < slab * S)) S = 1;
+  if (ws == nullptr) S = 1;
+  while (S > 1 && ws_elems < slab * S) S >>= 1;
   dim3 grid(kt, mt, S);
   if (S == 1) {
     skinny_dgrad_kernel<8><<<grid, 512, 0, st>>>(dZ, ldz, W, ldw, hprev, ldh, scale, dX, ldx, 0, M, N, K);
