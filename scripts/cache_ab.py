@@ -33,7 +33,7 @@ from splitlearning_amd.ops import hip_ops as H  # noqa: E402
 VARIANTS = {"fwd": {7: 1, 4: 1, 2: 0}, "zigzag": {7: 0, 4: 1, 2: 0}, "zz+wt": {7: 0, 4: 0, 2: 0},
             "zz+wt2d": {7: 0, 4: 0, 2: 1}, "zz+wt1d": {7: 0, 4: 0, 2: 2},
             # fc2 dgrad split-N cap (csrc/linear.hip linear_dgrad, variant 5): max S, 16-row slices
-            "dgS16": {5: 16}, "dgS32": {5: 32}, "dgS64": {5: 64}}
+            "dgS1": {5: 1}, "dgS2": {5: 2}, "dgS16": {5: 16}, "dgS32": {5: 32}, "dgS64": {5: 64}}
 SLOTS = (2, 4, 5, 7)
 
 

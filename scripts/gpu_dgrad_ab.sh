@@ -24,5 +24,5 @@ C.set_variant(5, 0)
 print("dgrad check ok")
 PY
 tail -1 gpurun_out/dgrad_check.txt
-timeout -k 10 500 python -u scripts/cache_ab.py --tp 1 2 4 8 --variants zz+wt dgS16 dgS32 dgS64 ${AB_ARGS} > gpurun_out/dgrad_ab.txt 2>&1 || { echo AB_FAIL; tail -20 gpurun_out/dgrad_ab.txt; exit 1; }
+timeout -k 10 500 python -u scripts/cache_ab.py --tp 1 2 4 8 --variants ${AB_VARIANTS:-zz+wt dgS16 dgS32 dgS64} ${AB_ARGS} > gpurun_out/dgrad_ab.txt 2>&1 || { echo AB_FAIL; tail -20 gpurun_out/dgrad_ab.txt; exit 1; }
 cat gpurun_out/dgrad_ab.txt

@@ -332,12 +332,13 @@ hipError_t linear_dgrad(const float* dZ, int ldz, const float* W, int ldw, const
   if (M <= 0 || K <= 0) return hipSuccess;
   const int kt = (K + 63) / 64, mt = (M + 15) / 16;
   int S = 1;
-  // aim for >= ~256 workgroups on the 256-CU part; split N when there are few K tiles
-  // (variant 5 = max split, for A/B: 1 = never split)
-  // (variant 5 = max split, for A/B: 1 = never split; >1 also lets a workgroup's N slice
-  //  shrink to 16 rows, so TP shards with few K tiles can still fill the chip)
-  const int smax = g_variant[5] > 0 ? g_variant[5] : 16;
-  const int rmin = g_variant[5] > 1 ? 16 : 64;
+  // aim for >= ~256 workgroups on the 256-CU part; split N when there are few K tiles.
+  // Variant 5, for A/B: 1 = never split, >1 = max split with N slices down to 16 rows.
+  // Both measured slower or equal at every TP shard (at TP = 8: 57.6 us per native-executor
+  // server step unsplit vs 51.8 us split; profiles/r1_dgrad_split_ab.txt).
+  const int v5 = g_variant[5];
+  const int smax = v5 > 0 ? v5 : 16;
+  const int rmin = v5 > 1 ? 16 : 64;
   while (S < smax && kt * mt * S < 768 && N / (S * 2) >= rmin) S *= 2;
   const int64_t slab = (int64_t)M * K;
   if (ws == nullptr) S = 1;
