@@ -39,7 +39,7 @@ struct WgGroup {
   int nt0;              // layer 0's tile count (set by wgrad_group)
   int grid2d;           // 2-D grid (set by wgrad_group: when few of its workgroups are empty)
   int wt;               // write-through (sc1) W/m/v stores (set by wgrad_group)
-  int sws;              // look-ahead LDS tile row stride in float4 (set by wgrad_group)
+  int swz;              // look-ahead LDS tile layout: 0 padded, 1 plain, 2 XOR (set by wgrad_group)
 };
 
 int head3_slices(int N2);

@@ -242,7 +242,8 @@ __global__ void __launch_bounds__(1024)
 wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
   __shared__ f32x4 sa[16][64];
   __shared__ float sdz[16][16];
-  // look-ahead: the updated W tile, rows padded to grp.sws = 65 float4 (variant 1 = 1: 64).
+  // look-ahead: the updated W tile, rows padded to 65 float4 (variant 1 = 1: plain 64-float4
+  // rows; 2: XOR-swizzled columns, conflict-free for both the row write and the column read).
   // The MFMA B-layout read below takes 16 rows of one column: with a 1 KB row stride all
   // 16 hit the same LDS banks (rocprofv3 SQ_LDS_BANK_CONFLICT 3.96 M cycles per TP = 1
   // step, 0 without the look-ahead); one float4 of padding spreads them over all banks.
@@ -323,9 +324,13 @@ wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
     // next batch's partial pre-activations with the updated tile: stage W_new through LDS
     // into MFMA B layout; wave w covers columns [16w, 16w+16) with 4 exact-fp32 MFMAs
     // (B[k][n] = W_new[n][k]: lane (n = li, k-group lq) reads one float4 of the tile)
-    sw[r * grp.sws + lane] = act ? p : zv;
+    // layout: grp.swz 0 = rows padded to 65 float4, 1 = plain 64, 2 = column XOR (row & 15)
+    const int wcol = grp.swz == 2 ? (lane ^ r) : lane;
+    const int rcol = grp.swz == 2 ? ((4 * r + lq) ^ li) : 4 * r + lq;
+    const int rs = grp.swz == 0 ? 65 : 64;
+    sw[r * rs + wcol] = act ? p : zv;
     __syncthreads();
-    const f32x4 wv4 = sw[li * grp.sws + 4 * r + lq];
+    const f32x4 wv4 = sw[li * rs + rcol];
     f32x4 z = zv;
 #pragma unroll
     for (int i = 0; i < 4; ++i) z = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[i], wv4[i], z, 0, 0, 0);
@@ -475,7 +480,7 @@ static void set_traversal(WgGroup& gg) {
   const int v7 = g_variant[7];
   gg.rev0 = v7 == 1 ? 0 : (v7 == 2 ? 1 : (int)(flip++ & 1u));
   gg.wt = g_variant[4] == 1 ? 0 : 1;
-  gg.sws = g_variant[1] == 1 ? 64 : 65;
+  gg.swz = g_variant[1];
   for (int i = 0; i < gg.n; ++i)
     if ((int64_t)gg.d[i].N * gg.d[i].ldw * 4 > 2147483647LL) gg.wt = 0;
 }
