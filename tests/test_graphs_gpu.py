@@ -318,3 +318,34 @@ def test_concat_pipelined_epoch_matches_per_step(cuda, tmp_path):
     for L1, L2 in zip(sa.tail.layers, sb.tail.layers):
         d = (L1.W - L2.W).abs()
         assert d.max().item() < 1e-2 and (d > 1e-4).float().mean().item() < 1e-4
+
+
+@pytest.mark.parametrize("tp", [1, 8])
+def test_lookahead_lds_layouts_bitwise_equal(cuda, tp):
+    """The look-ahead's LDS staging layouts (kernel variant 1: 0 padded rows, 1 plain, 2 XOR
+    swizzle) only move data: a native server epoch gives bit-identical weights and losses."""
+    C = hip_ops.C()
+
+    def run(variant):
+        C.set_variant(1, variant)
+        try:
+            torch.manual_seed(0)
+            acts = torch.rand(16 * 6, 5408, device=cuda) * 20
+            labels = torch.randint(0, 10, (16 * 6,), device=cuda)
+            ar = None
+            if tp > 1:
+                from splitlearning_amd.parallel.rccl import native_allreduce, self_comm
+                ar = native_allreduce(self_comm())
+            torch.manual_seed(1)
+            tail = TailEngine(ServerTailSisa(), sisa_server_spec(), cuda, tp_rank=0, tp_size=tp, allreduce=ar)
+            slot = OptSlot(adam(1e-3, 1e-5))
+            tail.lookahead_prologue(acts[:16])
+            loss = tail.run_native_epoch(acts, labels, slot, 16, True)
+            torch.cuda.synchronize()
+            return [loss.clone()] + [L.W.detach().clone() for L in tail.layers]
+        finally:
+            C.set_variant(1, 0)
+
+    ref = run(0)
+    for v in (1, 2):
+        assert all(torch.equal(a, b) for a, b in zip(ref, run(v))), f"layout {v} differs"
