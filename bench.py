@@ -1,29 +1,35 @@
-"""Headline benchmark: whole-node samples/s of the SISA split-learning pipeline.
+"""Headline benchmark: whole-node samples/s of the reference's SISA job on MNIST-scale data.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...      (N > 1; one rank per GPU)
 
-Metric (BASELINE.json): "samples/sec (whole node) split-NN MNIST, world_size=2/3/5/9
-on 1/2/4/8 MI355X".  With N GPUs the job has world_size = N + 1 roles: N Alices
-(one per GPU) and Bob, whose server tail is tensor-parallel over all N GPUs.
+Metric (BASELINE.json): "samples/sec (whole node) split-NN MNIST, world_size=2/3/5/9 on
+1/2/4/8 MI355X".  Config (BASELINE.json configs[3]): `split_nn.py --sisa
+--server_epochs=5`, world_size = N + 1 on N GPUs: N Alices (one per GPU) and Bob, whose
+server tail is tensor-parallel over all N GPUs.
 
-One timed step = one full SISA round with the reference's semantics
-(split_nn.py:74-95, data_entities_vanilla_sisa.py): every Alice trains her conv
-front for one local epoch over her shard (all Alices concurrently, Adam), the
-fronts are frozen, the activation cache is rebuilt (each Alice's shard through the
-frozen front, multicast to every Bob rank), and Bob trains one server epoch over
-all cached activations (Adam wd=1e-5, batch 16, one optimizer step per batch).
-Every training sample therefore passes one Alice-local step and one Bob step;
-value = (N * samples_per_client) / seconds per round, summed over the node.
-Per-Alice work is fixed as N grows ("weak" scaling).  Data: synthetic
-MNIST-shaped uint8 images (learnable class prototypes), random-init weights of
-the reference architectures (model1_sisa + model2_sisa), fp32 parameters and
-optimizer state, fp32 MFMA compute (higher precision than bf16; the step is
-HBM-bound, so fp32 costs no time).
+Data: the reference's data volume through the reference's data path — 70,000 synthetic
+MNIST-shaped uint8 images (no network for fetch_openml), Dirichlet(alpha=0.5) non-IID
+partition over the N Alices and the per-client 80/20 train/test split
+(`data.mnist.partition_and_split`, the same code `split_nn.py` uses), random-init weights
+of the reference architectures (model1_sisa + model2_sisa), fp32 parameters, optimizer
+state and compute.  The whole dataset is fixed as N grows ("strong" scaling).
 
-vs_baseline divides by the reference's own CPU number for the same pipeline at
-world_size 2 (5,600 samples through the SISA local + server phases
-in 10.536 s + 71.264 s = 68.46 samples/s).
+One timed step = one run of the reference's whole Bob schedule for the mode
+(`protocols/schedule.py` = split_nn.py:74-117 for SISA): every Alice's local epoch (all
+concurrently), freeze, the activation dump into Bob's cache, `--server_epochs` Bob epochs
+over all clients' cached activations, the breakdown evaluation, Alice_1's unlearning
+(label 9 removed, local retrain), Bob's retraining (`--server_epochs` epochs, reusing the
+other clients' cached activations) and the final evaluation.  Nothing is skipped: the
+eval and unlearn phases are inside the timed region.
+
+value = training samples processed per second: every sample counted once per training
+epoch it passes through (Alice-local or Bob-server), eval samples not counted (their time
+is).  The reference publishes no number; BASELINE.md measured its phase rates on CPU
+(SISA ws=2: Alice local 531.5, Bob server 78.6, Bob retrain 90.5 samples/s).
+vs_baseline divides by those rates composed over THIS schedule's sample counts
+(reference eval time counted as zero, in its favour); config.baseline_samples_per_s
+records the composed number.
 """
 from __future__ import annotations
 
@@ -32,64 +38,80 @@ import json
 import os
 import sys
 import time
-from types import SimpleNamespace
 
-import numpy as np
 import torch
 import torch.distributed as dist
 
-BASELINE_SAMPLES_PER_S = 5600.0 / (10.536 + 71.264)
-# per-mode reference numbers (CPU): vanilla ws=2 train phase 5,600 / 32.126 s;
-# the reference's U-shape and concat modes crash, so they have none
-BASELINES = {"sisa": BASELINE_SAMPLES_PER_S, "vanilla": 5600.0 / 32.126, "ushape": None, "concat": None}
 METRIC = "samples/sec (whole node) split-NN MNIST, world_size=2/3/5/9 on 1/2/4/8 MI355X"
-MODELS = {
-    "sisa": "model1_sisa (Alice) + model2_sisa (Bob), SISA round (split_nn.py --sisa)",
-    "concat": "model1_sisa (Alices) + model2_sisa_concat(k) (Bob), SISA-concat round (--sisa --concat)",
-    "vanilla": "model1_sisa (Alice) + model2_sisa (Bob), SGD-m, round-robin iteration (--vanilla)",
-    "ushape": "model1 + model3 (Alice) + model2 (Bob), Adam, round-robin iteration (U-shape default)",
+# reference CPU phase rates, samples/s, by schedule phase kind
+REF_RATES = {
+    "sisa": {"local": 531.5, "server": 78.6, "retrain": 90.5},
+    "control": {"local": 531.5, "server": 78.6, "retrain": 90.5},
+    "vanilla": {"train": 5600.0 / 32.126},
+    "ushape": None,          # the reference's U-shape crashes (Q1)
+    "concat": None,          # the reference's concat crashes (Q3)
 }
+MODELS = {
+    "sisa": "model1_sisa (Alice) + model2_sisa (Bob), split_nn.py --sisa",
+    "control": "model1_sisa (Alice) + model2_sisa (Bob), split_nn.py --control",
+    "concat": "model1_sisa (Alices) + model2_sisa_concat(k) (Bob), split_nn.py --sisa --concat",
+    "vanilla": "model1_sisa (Alice) + model2_sisa (Bob), SGD-m, split_nn.py --vanilla",
+    "ushape": "model1 + model3 (Alice) + model2 (Bob), Adam, split_nn.py (U-shape default)",
+}
+MODE_FLAGS = {"sisa": ["--sisa"], "control": ["--control"], "concat": ["--sisa", "--concat"],
+              "vanilla": ["--vanilla"], "ushape": []}
 
 
-def _session_args(a, world_size, log_dir):
-    return SimpleNamespace(
-        world_size=world_size, client_num_in_total=world_size - 1, epochs=a.epochs, iterations=1,
-        batch_size=a.batch_size, partition_alpha=0.5, datapath="", lr=1e-3, server_epochs=a.server_epochs,
-        vanilla=a.mode == "vanilla", sisa=a.mode in ("sisa", "concat"), concat=a.mode == "concat", control=False,
-        mode=a.mode, seed=a.seed, log_dir=log_dir,
-        no_tqdm=True, true_reset=False, eval_dropout_fix=False, concat_unlearn=False, omit_label=9,
-        unlearn_client_ids=[1], save_dir="", resume_dir="", kernels=a.kernels, graphs=a.graphs,
-        act_dtype=a.act_dtype)
+def _phase_kind(mode: str, name: str):
+    """Map a schedule phase to the reference rate that prices it (None = not a training phase)."""
+    if mode in ("sisa", "control", "concat"):
+        if name.startswith("server_retraining"):
+            return "retrain"
+        if name.startswith("server_training"):
+            return "server"
+        if name.startswith(("local_training", "unlearn_local", "control_local")):
+            return "local"
+        return None
+    if name.startswith(("train_request", "unlearn_request")):
+        return "train"
+    return None
 
 
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--samples_per_client", type=int, default=2048)
-    ap.add_argument("--batch_size", type=int, default=16)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--mode", choices=tuple(MODE_FLAGS), default="sisa")
+    ap.add_argument("--schedule", choices=("full", "round"), default="full",
+                    help="full: the mode's whole split_nn.py schedule; round (SISA modes): local "
+                         "training + the server epochs only")
+    ap.add_argument("--world_size", type=int, default=0, help="0 = gpus + 1 (BASELINE configs)")
+    ap.add_argument("--server_epochs", type=int, default=5, help="BASELINE config 4: --server_epochs=5")
     ap.add_argument("--epochs", type=int, default=1)
-    ap.add_argument("--server_epochs", type=int, default=1)
-    ap.add_argument("--kernels", choices=("auto", "hip", "torch"), default="auto")
+    ap.add_argument("--iterations", type=int, default=1, help="round-robin rounds (vanilla / U-shape)")
+    ap.add_argument("--batch_size", type=int, default=16)
+    ap.add_argument("--num_samples", type=int, default=70000, help="MNIST size (train + test)")
+    ap.add_argument("--partition_alpha", type=float, default=0.5)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--kernels", choices=("auto", "hip", "torch"), default="auto")
     ap.add_argument("--bob_tp", type=int, default=0, help="0 = all ranks")
-    ap.add_argument("--json_out", type=str, default="")
     ap.add_argument("--graphs", choices=("auto", "on", "off"), default="auto")
-    ap.add_argument("--act_dtype", choices=("fp32", "bf16"), default="fp32",
-                    help="SISA activation-cache storage dtype (compute stays fp32)")
-    ap.add_argument("--mode", choices=("sisa", "vanilla", "ushape", "concat"), default="sisa",
-                    help="sisa (headline): one SISA round; vanilla / ushape: one round-robin "
-                         "iteration (every Alice one epoch of split training, weight relay); "
-                         "concat: one SISA-concat round")
+    ap.add_argument("--act_dtype", choices=("fp32", "bf16"), default="fp32")
+    ap.add_argument("--dtype", choices=("fp32", "bf16"), default="fp32", help="compute dtype")
+    ap.add_argument("--concat_unlearn", action="store_true", default=True,
+                    help="concat: add the unlearning retrain (BASELINE config 5)")
+    ap.add_argument("--json_out", type=str, default="")
     ap.add_argument("--kernel_variant", action="append", default=[], metavar="SLOT=VALUE",
                     help="A/B hook: select a measured-alternative kernel form (_C.set_variant)")
     a = ap.parse_args(argv)
 
     from splitlearning_amd import ops
-    from splitlearning_amd.data.mnist import synthetic_mnist
+    from splitlearning_amd.config import parse_args
+    from splitlearning_amd.data.mnist import make_client_shards, synthetic_mnist
     from splitlearning_amd.parallel.dist import Comm, Placement, make_tp_group
     from splitlearning_amd.protocols import SESSIONS
+    from splitlearning_amd.protocols.schedule import build_steps
 
     if a.kernels == "torch":
         ops.set_backend("torch")
@@ -112,32 +134,49 @@ def main(argv=None):
         dist.init_process_group("nccl" if use_gpu else "gloo", rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=900), **kw)
     N = world
-    ws = N + 1
+    ws = a.world_size if a.world_size > 0 else N + 1
+    log_dir = os.path.join("/tmp", f"sl_bench_logs_{os.getpid()}")
+    argv_s = MODE_FLAGS[a.mode] + [
+        "--world_size", str(ws), "--epochs", str(a.epochs), "--iterations", str(a.iterations),
+        "--batch_size", str(a.batch_size), "--partition_alpha", str(a.partition_alpha),
+        "--server_epochs", str(a.server_epochs), "--seed", str(a.seed), "--num_samples", str(a.num_samples),
+        "--kernels", a.kernels, "--graphs", a.graphs, "--act_dtype", a.act_dtype, "--no_tqdm",
+        "--log_dir", log_dir, "--watchdog", "off"]
+    if a.mode == "concat" and a.concat_unlearn:
+        argv_s.append("--concat_unlearn")
+    sargs = parse_args(argv_s)
+    sargs.dtype = a.dtype
     pl = Placement.make(ws, N, a.bob_tp if a.bob_tp > 0 else N)
     comm = Comm(rank, N, dev, pl, make_tp_group(pl, "nccl" if use_gpu else "gloo") if N > 1 else None)
-    S = a.samples_per_client
-
-    class BenchSession(SESSIONS[a.mode]):
-        def _load_client_shard(self, cid):
-            x, y = synthetic_mnist(S + 256, seed=1000 + cid)
-            return ({"x": torch.from_numpy(x[:S]), "y": torch.from_numpy(y[:S])},
-                    {"x": torch.from_numpy(x[S:]), "y": torch.from_numpy(y[S:])})
-
-    log_dir = os.path.join("/tmp", f"sl_bench_logs_{os.getpid()}")
-    sess = BenchSession(_session_args(a, ws, log_dir), comm, dev)
     k = ws - 1
-    all_alices = range(1, k + 1)
+
+    # the reference's data volume and data path: one MNIST-sized set, Dirichlet-partitioned
+    x, y = synthetic_mnist(a.num_samples, seed=a.seed)
+    shards = make_client_shards(x, y, k, a.partition_alpha, seed=a.seed)
+    del x, y
+
+    class BenchSession(SESSIONS[sargs.mode]):
+        def _load_client_shard(self, cid):
+            xtr, ytr, xte, yte = shards[cid]
+            return ({"x": torch.from_numpy(xtr), "y": torch.from_numpy(ytr)},
+                    {"x": torch.from_numpy(xte), "y": torch.from_numpy(yte)})
+
+    sess = BenchSession(sargs, comm, dev)
+    sess.quiet = True                  # stdout carries the one JSON line only
+    all_alices = list(range(1, k + 1))
+    steps = build_steps(sess, sargs)
+    if a.schedule == "round":
+        if sargs.mode not in ("sisa", "concat", "control"):
+            raise SystemExit("--schedule round is a SISA-mode schedule")
+        steps = [(n, f) for n, f in steps if n in ("local_training", "server_training")]
 
     def step():
-        if a.mode in ("vanilla", "ushape"):
-            for cid in all_alices:             # split_nn.py:49-52, one iteration
-                sess.train_request(cid)
-            return
-        sess.train_request_parallel()
-        sess.freeze_alice_weights(all_alices)
-        sess.reset_activation_cache()          # the fronts changed: rebuild the cut-layer cache
-        sess.train_and_backward([], None)
+        # a fresh repetition of the schedule: fronts trainable, Bob's cut-layer cache empty
+        # (the fronts change every repetition); weights and optimizer state carry on
+        sess.reset_activation_cache()
         sess.unfreeze_alice_weights(all_alices)
+        for _, fn in steps:
+            fn()
 
     def sync():
         if use_gpu:
@@ -147,6 +186,8 @@ def main(argv=None):
     for _ in range(a.warmup):
         step()
     sync()
+    rec0 = len(sess.timer.records)
+    b0 = comm.bytes_sent
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
@@ -156,23 +197,52 @@ def main(argv=None):
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
-    samples = k * S * a.steps
+    recs = sess.timer.records[rec0:]
+    samples = 0
+    phase_s, phase_n = {}, {}
+    for r in recs:
+        key = r["phase"].split("[")[0]
+        phase_s[key] = phase_s.get(key, 0.0) + r["seconds"] / a.steps
+        if _phase_kind(sargs.mode, r["phase"]) is not None:
+            samples += r["samples"]
+            phase_n[key] = phase_n.get(key, 0) + r["samples"] // a.steps
     value = samples / dt
+    rates = REF_RATES.get(sargs.mode)
+    base = None
+    if rates is not None and samples:
+        ref_t = sum(r["samples"] / rates[_phase_kind(sargs.mode, r["phase"])] for r in recs
+                    if _phase_kind(sargs.mode, r["phase"]) is not None)
+        base = samples / ref_t
+    sent = comm.gather_obj((comm.bytes_sent - b0) // max(1, a.steps), 0)
     if rank == 0:
         kern = "torch" if (not use_gpu or ops.get_backend() == "torch") else "hip"
-        rec = {
+        tpc = getattr(sess, "tp_native_comm", None)
+        flags = " ".join(MODE_FLAGS[a.mode] + [f"--server_epochs={a.server_epochs}", f"--world_size={ws}",
+                                                f"--batch_size={a.batch_size}", f"--epochs={a.epochs}"])
+        out = {
             "metric": METRIC, "value": round(value, 2), "unit": "samples/s", "n_gpus": N,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(1000 * dt / a.steps, 3),
-            "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": round(value / BASELINES[a.mode], 2) if BASELINES[a.mode] else None,
-            "dtype": "fp32", "data": "synthetic",
-            "config": {"model": MODELS[a.mode], "mode": a.mode, "world_size": ws, "global_batch": a.batch_size,
-                       "samples_per_client": S, "seq_len": None,
-                       "parallelism": f"alices{k}_one_per_gpu+bob_tp{pl.bob_tp}",
-                       "device": "MI355X" if use_gpu else "cpu", "kernels": kern,
-                       "act_cache_dtype": a.act_dtype},
+            "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": round(value / base, 2) if base else None,
+            "dtype": a.dtype, "data": "synthetic",
+            "config": {
+                "model": MODELS[sargs.mode], "mode": sargs.mode, "flags": flags, "world_size": ws,
+                "global_batch": a.batch_size, "seq_len": None, "schedule": a.schedule,
+                "num_samples": a.num_samples, "partition": f"dirichlet(alpha={a.partition_alpha}) + 80/20 split",
+                "train_samples_per_client": {c: int(len(shards[c][1])) for c in all_alices},
+                "parallelism": f"alices{k}_on_{N}gpus+bob_tp{pl.bob_tp}",
+                "device": "MI355X" if use_gpu else "cpu", "kernels": kern, "act_cache_dtype": a.act_dtype,
+                "train_samples_per_step": samples // a.steps,
+                "phase_seconds": {p: round(v, 4) for p, v in phase_s.items()},
+                "phase_train_samples": phase_n,
+                "baseline_samples_per_s": round(base, 2) if base else None,
+                "baseline_basis": ("reference CPU phase rates from BASELINE.md composed over this schedule's "
+                                   "sample counts" if base else None),
+                "dist_world": N, "rccl_nranks": int(tpc.size) if tpc is not None else (1 if use_gpu else 0),
+                "bytes_sent_per_rank_per_step": sent,
+            },
         }
-        line = json.dumps(rec)
+        line = json.dumps(out)
         print(line, flush=True)
         if a.json_out:
             with open(a.json_out, "w") as f:
@@ -181,7 +251,6 @@ def main(argv=None):
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
-    _ = np
     return 0
 
 

@@ -78,18 +78,28 @@ def shard_paths(datapath: str, client_id: int) -> tuple[str, str]:
             os.path.join(datapath, f"data_worker{client_id}_test.pt"))
 
 
+def partition_and_split(y: np.ndarray, client_num: int, alpha: float, rng: np.random.Generator,
+                        test_partition: float = TEST_PARTITION, classes: int = NUM_CLASSES):
+    """The one partition + split used everywhere (CLI shards, the reference-named
+    `image_preprocess_dl` API, the benchmark): Dirichlet partition over the clients, then
+    per client a shuffle and the 80/20 train/test split
+    (`relational_table_preprocessor.py:62-92`).  Returns {client (0-based): (train_idx, test_idx)}."""
+    parts = dirichlet_partition(y, client_num, classes, alpha, rng=rng, min_size=MIN_SAMPLES_PER_CLIENT)
+    out = {}
+    for key, idx in parts.items():
+        idx = np.asarray(idx, dtype=np.int64).copy()
+        rng.shuffle(idx)                      # relational_table_preprocessor.py:83
+        n_train = int(len(idx) * (1 - test_partition))
+        out[key] = (idx[:n_train], idx[n_train:])
+    return out
+
+
 def make_client_shards(x: np.ndarray, y: np.ndarray, client_num: int, alpha: float,
                        seed: int | None = None, test_partition: float = TEST_PARTITION):
     """Partition + per-client 80/20 split.  Returns {client_id (1-based): (xtr, ytr, xte, yte)}."""
     rng = np.random.default_rng(seed)
-    parts = dirichlet_partition(y, client_num, NUM_CLASSES, alpha, rng=rng,
-                                min_size=MIN_SAMPLES_PER_CLIENT)
     out = {}
-    for key, idx in parts.items():
-        idx = idx.copy()
-        rng.shuffle(idx)                      # relational_table_preprocessor.py:83
-        n_train = int(len(idx) * (1 - test_partition))
-        tr, te = idx[:n_train], idx[n_train:]
+    for key, (tr, te) in partition_and_split(y, client_num, alpha, rng, test_partition).items():
         out[key + 1] = (x[tr], y[tr], x[te], y[te])
     return out
 

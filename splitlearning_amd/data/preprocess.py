@@ -115,16 +115,17 @@ def _preprocess_dl(args, data, label_list, test_partition: float, rng, device, g
         x = x.to(torch.float32)
     rng = rng if rng is not None else np.random.default_rng(getattr(args, "seed", None))
     classes = int(getattr(args, "class_num", 0) or NUM_CLASSES)
-    idx_map = non_iid_partition_with_dirichlet_distribution(labels, args.client_num_in_total, classes,
-                                                            args.partition_alpha, task="task", rng=rng)
+    # the same partition + split as the CLI's shard writer (mnist.partition_and_split)
+    from .mnist import partition_and_split
+    splits = partition_and_split(labels.numpy(), args.client_num_in_total, args.partition_alpha, rng,
+                                 test_partition, classes)
     train_num, test_num = 0, 0
     train_local_num, train_local, test_local = {}, {}, {}
     tr_x, tr_y, te_x, te_y = [], [], [], []
-    for key, idx in idx_map.items():
-        idx = np.asarray(idx, dtype=np.int64)
-        rng.shuffle(idx)                                # relational_table_preprocessor.py:83
-        n_train = int(len(idx) * (1 - test_partition))
-        tr, te = torch.from_numpy(idx[:n_train]), torch.from_numpy(idx[n_train:])
+    for key, (tr_i, te_i) in splits.items():
+        n_train = len(tr_i)
+        idx = np.concatenate([tr_i, te_i])
+        tr, te = torch.from_numpy(tr_i), torch.from_numpy(te_i)
         train_local_num[key] = n_train
         train_local[key] = DeviceLoader(x[tr], labels[tr], args.batch_size, shuffle=True, device=device,
                                         generator=generator)

@@ -54,8 +54,12 @@ class GraphedServerSteps:
         nmax = max(L.W.shape[0] for L in tail.layers)
         for key, n in (("dgrad", kmax), ("fwd", nmax), ("fc2p", nmax), ("dz1p", kmax), ("head", nmax)):
             ops._workspace(dev, 16 * B * n, key)
-        if tail.lookahead_ok(B):
-            tail.lookahead_slabs(B)
+        # the look-ahead slab buffer the graph reads: kept here and written by run()'s
+        # prologue directly, so a later growth of the shared workspace cannot leave the
+        # graph reading a buffer nobody writes any more
+        self.pn = tail.lookahead_slabs(B) if tail.lookahead_ok(B) else None
+        self._ws = [ops._workspace(dev, 16 * B * n, key) for key, n in
+                    (("dgrad", kmax), ("fwd", nmax), ("fc2p", nmax), ("dz1p", kmax), ("head", nmax))]
         torch.cuda.synchronize(dev)
         fwd0 = tail.fwd_count
         self.graph = torch.cuda.CUDAGraph()
@@ -66,7 +70,7 @@ class GraphedServerSteps:
                 fused = tail.fused3_ok()
                 self.lookahead = fused and tail.lookahead_ok(B)
                 if self.lookahead:
-                    tail._pre = tail.lookahead_slabs(B)     # filled by run()'s prologue
+                    tail._pre = self.pn                     # filled by run()'s prologue
                 for i in range(G):
                     xs = self.x[i * B:(i + 1) * B]
                     ys = self.y[i * B:(i + 1) * B]
@@ -108,7 +112,7 @@ class GraphedServerSteps:
         assert nsteps % G == 0 and nsteps * B <= n
         opt_all, seed_all = self._epoch_tables(nsteps)
         if self.lookahead:
-            self.tail.lookahead_prologue(acts[:B])
+            self.tail.lookahead_prologue(acts[:B], out=self.pn)
         for c in range(nsteps // G):
             r0 = c * G * B
             r1 = min(n, r0 + (G + 1) * B)
@@ -120,5 +124,5 @@ class GraphedServerSteps:
         self.slot.t += nsteps
         self.tail.fwd_count += nsteps
         pending = self.lookahead and nsteps * B + B <= n
-        self.tail._pre = self.tail.lookahead_slabs(B) if pending else None
+        self.tail._pre = self.pn if pending else None
         return pending

@@ -228,10 +228,11 @@ class TailEngine:
         L1 = self.layers[0]
         return self.ops.lookahead_slabs(self.device, L1.W.shape[1], m, L1.W.shape[0])
 
-    def lookahead_prologue(self, x0):
-        """Start a look-ahead chain: fc1's product for the first batch, in slab form."""
+    def lookahead_prologue(self, x0, out=None):
+        """Start a look-ahead chain: fc1's product for the first batch, in slab form (into
+        `out` when given: a captured graph's own slab buffer)."""
         L1 = self.layers[0]
-        p = self.lookahead_slabs(x0.shape[0])
+        p = self.lookahead_slabs(x0.shape[0]) if out is None else out
         p.zero_()
         p[0].copy_(self.ops.linear_fwd(x0, L1.W, None, False, 0.0, 0, 0))
         self._pre = p
@@ -321,15 +322,23 @@ class TailEngine:
         Python round trip per step.  `pre`: the first batch's fc1 product is pending
         (`lookahead_prologue`).  Returns the per-row losses."""
         ex = self._native_executor(slot, B)
+        d = self._native[3]
+        if pre:
+            assert self._pre is not None and self._pre.data_ptr() == d["pn"].data_ptr(), \
+                "pending look-ahead is not in the executor's slab buffer"
         loss = torch.empty(acts.shape[0], device=self.device)
         fc, t, pre = ex.run(acts, labels, loss, self.seed_base, self.fwd_count, slot.t, pre, lookahead)
         self.fwd_count, slot.t = int(fc), int(t)
-        self._pre = self.lookahead_slabs(B) if pre else None
+        # the executor's own slab buffer holds the pending product (not a re-fetched one)
+        self._pre = d["pn"] if pre else None
         return loss
 
     def _native_executor(self, slot: OptSlot, B: int):
         cached = getattr(self, "_native", None)
-        if cached is not None and cached[0] is slot and cached[1] == B:
+        # the executor holds raw workspace addresses: rebuild it when a workspace it uses
+        # has been replaced (grown) since it was built
+        if (cached is not None and cached[0] is slot and cached[1] == B
+                and cached[3]["pn"].data_ptr() == self.lookahead_slabs(B).data_ptr()):
             return cached[2]
         ops, dev = self.ops, self.device
         L1, L2, L3 = self.layers

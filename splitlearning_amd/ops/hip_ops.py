@@ -46,7 +46,10 @@ _SLAB: dict = {}
 def _slab(device, B):
     s = _SLAB.get(device)
     if s is None or s.numel() < B * 320:
-        s = torch.empty(max(B, 64) * 320, device=device, dtype=torch.float32)
+        if s is not None:
+            _WS_RETIRED.append(s)       # never free a handed-out buffer (see _workspace)
+        s = torch.empty(max(B, 64, 2 * (s.numel() // 320) if s is not None else 0) * 320, device=device,
+                        dtype=torch.float32)
         _SLAB[device] = s
     return s
 
@@ -172,15 +175,24 @@ def linear_epilogue(P, b, relu: bool, drop_p: float, seed: int, col_offset: int 
 
 
 _WS: dict = {}
+_WS_RETIRED: list = []
 
 
 def _workspace(device, n, key="dgrad"):
     """Split-K / split-N partial-sum slabs.  Separate buffers per producer: slabs handed to
     a later fused consumer ("fc2p" -> server_head3, "dz1p" -> wgrad_group) must not be
-    overwritten by the scratch use ("fwd", "dgrad") of the kernels launched in between."""
+    overwritten by the scratch use ("fwd", "dgrad") of the kernels launched in between.
+
+    A buffer that was ever handed out is never freed: captured HIP graphs and native
+    executors (engine/graphs.py, engine.cpp) hold its raw device address.  Growing a
+    workspace retires the old buffer (kept alive here) and doubles the size, so a
+    process retires at most a few buffers per key."""
     ws = _WS.get((device, key))
     if ws is None or ws.numel() < n:
-        ws = torch.empty(max(n, 1 << 20), device=device, dtype=torch.float32)
+        size = max(n, 1 << 20, 2 * ws.numel() if ws is not None else 0)
+        if ws is not None:
+            _WS_RETIRED.append(ws)
+        ws = torch.empty(size, device=device, dtype=torch.float32)
         _WS[(device, key)] = ws
     return ws
 

@@ -306,6 +306,15 @@ class Session:
     def reset_model(self, cid: int):
         self.alices[cid].front.reset_parameters(self.args.true_reset)
 
+    def unlearn_samples(self, cid: int) -> int:
+        """Collective: the size of Alice_cid's unlearn (label-filtered) training set, known
+        on her host rank, agreed by every rank (phase sample counts)."""
+        a = self.alices.get(cid)
+        n = int(a.unlearn_order.numel()) if (a is not None and a.unlearn_order is not None) else 0
+        if not self.comm.distributed:
+            return n
+        return int(self.comm.broadcast_obj(n, self.host(cid)))
+
     def filtered_order(self, a: AliceState, omit_label: int) -> torch.Tensor:
         """`[(x, y) for batch in train_dataloader for x, y in zip(*batch) if y != omit]`:
         one shuffled pass over the shard with the omitted label dropped."""

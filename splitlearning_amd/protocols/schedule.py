@@ -14,7 +14,7 @@ from .base import Session
 
 
 def _print(sess: Session, msg: str):
-    if sess.rank == 0:
+    if sess.rank == 0 and not getattr(sess, "quiet", False):
         print(msg, flush=True)
 
 
@@ -53,8 +53,9 @@ def build_steps(sess: Session, args) -> list:
             add(f"iter{it}.eval_breakdown", eval_breakdown)
         for it in range(args.iterations):
             def unlearn():
-                with T.phase(f"unlearn_request[{unl[0]}]"):
+                with T.phase(f"unlearn_request[{unl[0]}]") as box:
                     sess.unlearn_request(unl[0], omit)
+                    box["samples"] = sess.unlearn_samples(unl[0]) * args.epochs
             add(f"unlearn{it}.unlearn_request[{unl[0]}]", unlearn)
             add(f"unlearn{it}.eval_breakdown", eval_breakdown)
 
@@ -72,8 +73,9 @@ def build_steps(sess: Session, args) -> list:
             def unlearn_local():
                 sess.unfreeze_alice_weights(unl)
                 _print(sess, f"Retraining client {unl}")
-                with T.phase("unlearn_local"):
+                with T.phase("unlearn_local") as box:
                     sess.unlearn_request(unl[0], omit)
+                    box["samples"] = sess.unlearn_samples(unl[0]) * args.epochs
                 sess.freeze_alice_weights(unl)
                 _print(sess, "Retraining server upon the omitted labels")
             add("unlearn_local", unlearn_local)

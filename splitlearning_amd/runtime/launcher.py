@@ -53,6 +53,35 @@ def resolve(args):
     return args
 
 
+def resolve_job_seed(args):
+    """One agreed seed for a checkpointed job (`--ckpt_dir`).  The reference is unseeded
+    (Q11) and so is a plain run here, but a snapshot only resumes under the seed that
+    drew its data partition, dropout hashes and initial weights: the first run records
+    the seed it used in `<ckpt_dir>/job.json` and `--resume` reads it back, so a job
+    launched with the default flags (no `--seed`) can be resumed."""
+    ckpt = getattr(args, "ckpt_dir", "")
+    if not ckpt:
+        return args
+    path = os.path.join(ckpt, "job.json")
+    rec = None
+    if getattr(args, "resume", False) and os.path.exists(path):
+        with open(path) as f:
+            rec = json.load(f)
+    if rec is not None:
+        if args.seed is not None and int(args.seed) != int(rec["seed"]):
+            raise ValueError(f"--seed {args.seed} does not match the checkpointed job's seed {rec['seed']}")
+        args.seed = int(rec["seed"])
+        return args
+    if args.seed is None:
+        import random
+        args.seed = random.SystemRandom().randrange(1 << 31)
+    os.makedirs(ckpt, exist_ok=True)
+    with open(path + ".tmp", "w") as f:
+        json.dump({"seed": int(args.seed), "mode": args.mode, "world_size": int(args.world_size)}, f)
+    os.replace(path + ".tmp", path)
+    return args
+
+
 def worker(rank: int, nprocs: int, args, result_q=None):
     from .. import ops
     from ..parallel.dist import Comm, Placement, init_process, make_tp_group
@@ -72,6 +101,11 @@ def worker(rank: int, nprocs: int, args, result_q=None):
         init_process(rank, nprocs, args.backend, args.master_addr, args.master_port, args.timeout_s, dev)
         tp_group = make_tp_group(pl, args.backend)
     comm = Comm(rank, nprocs, dev, pl, tp_group)
+    if getattr(args, "prep_in_worker", False) and getattr(args, "ckpt_dir", ""):
+        # torchrun: every rank ran main(); rank 0's view of job.json is the agreed seed
+        if rank == 0:
+            resolve_job_seed(args)
+        args.seed = comm.broadcast_obj(args.seed, 0)
     from .watchdog import make_watchdog
     wd = make_watchdog(args, comm)
     if wd is not None:
@@ -145,6 +179,7 @@ def main(argv=None):
     if os.environ.get("RANK") is not None and os.environ.get("WORLD_SIZE"):
         args.prep_in_worker = True                       # torchrun: rank 0 writes, then a barrier
     else:
+        resolve_job_seed(args)                           # checkpointed jobs: record / reuse the seed
         prepare_data(args)                               # split_nn.py:179 (every run, Q12)
     if os.environ.get("RANK", "0") == "0":
         print("Initialize Meetup Spot", flush=True)

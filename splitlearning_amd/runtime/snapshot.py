@@ -67,7 +67,10 @@ def rank_state(sess) -> dict:
             "layers": [(_cpu(L.W), _cpu(L.b)) for L in t.layers],
             "fwd_count": int(t.fwd_count), "training": bool(t.training),
             "slots": [(k, _slot_state(s)) for k, s in sess.bob_slots.items()],
-            "cache": [(list(k), _cpu(v[0]), _cpu(v[1])) for k, v in sess.activation_and_labels_cache.items()],
+            # the SISA activation cache is identical on every Bob TP rank: only the root
+            # writes it (one copy per snapshot instead of bob_tp copies); resume multicasts it
+            "cache": ([(list(k), _cpu(v[0]), _cpu(v[1])) for k, v in sess.activation_and_labels_cache.items()]
+                      if sess.rank == sess.pl.bob_root else None),
         }
     st["cache_keys"] = [list(k) for k in sorted(getattr(sess, "_ck", set()), key=repr)]
     for cid, a in sess.alices.items():
@@ -108,8 +111,10 @@ def load_rank_state(sess, st: dict):
                 sess.bob_slots[key] = OptSlot(sess.bob_optim())
             _load_slot(sess.bob_slots[key], d, dev)
         sess.activation_and_labels_cache.clear()
-        for key, acts, labels in b["cache"]:
-            sess.activation_and_labels_cache[tuple(key)] = (acts.to(dev), labels.to(dev))
+        if b["cache"] is not None:
+            for key, acts, labels in b["cache"]:
+                sess.activation_and_labels_cache[tuple(key)] = (acts.to(dev), labels.to(dev))
+    _share_cache(sess, b)
     if st["cache_keys"] or hasattr(sess, "_ck"):
         sess._ck = {tuple(k) for k in st["cache_keys"]}
     for cid, d in st["alices"].items():
@@ -127,6 +132,28 @@ def load_rank_state(sess, st: dict):
         a.gen.set_state(d["gen"])
         a.unlearn_order = None if d["unlearn_order"] is None else d["unlearn_order"].to(dev)
         a.front.frozen = d["frozen"]
+
+
+def _share_cache(sess, b):
+    """Collective over all ranks: the Bob root sends its restored activation cache to the
+    other Bob TP ranks (every rank learns the key order and shapes from the root)."""
+    if not sess.comm.distributed or sess.pl.bob_tp <= 1:
+        return
+    root = sess.pl.bob_root
+    meta = None
+    if sess.rank == root:
+        meta = [(tuple(k), tuple(v[0].shape), str(v[0].dtype).split(".")[-1], int(v[1].numel()))
+                for k, v in sess.activation_and_labels_cache.items()]
+    meta = sess.comm.broadcast_obj(meta, root)
+    others = [r for r in sess.pl.bob_ranks if r != root]
+    for key, shape, dt, n in meta:
+        acts = labels = None
+        if sess.rank == root:
+            acts, labels = sess.activation_and_labels_cache[key]
+        acts = sess.comm.multicast(acts, root, others, shape, getattr(torch, dt))
+        labels = sess.comm.multicast(labels, root, others, (n,), torch.int64)
+        if sess.rank in others:
+            sess.activation_and_labels_cache[key] = (acts, labels)
 
 
 def _step_dir(root: str, k: int) -> str:

@@ -78,10 +78,11 @@ def test_tensor_parallel_bob_matches_single_process(tmp_path):
         assert d.max().item() < 7e-3 and (d > 1e-5).float().mean().item() < 1e-4, k
 
 
-def _run(tmp_path, mode_flags, world_size, nprocs, bob_tp=1, extra=()):
+def _run(tmp_path, mode_flags, world_size, nprocs, bob_tp=1, extra=(), seed=3):
     logs = tmp_path / "logs"
+    seed_args = [] if seed is None else ["--seed", str(seed)]
     argv = list(mode_flags) + ["--world_size", str(world_size), "--nprocs", str(nprocs), "--bob_tp", str(bob_tp),
-                               "--iterations", "1", "--server_epochs", "1", "--num_samples", "700", "--seed", "3",
+                               "--iterations", "1", "--server_epochs", "1", "--num_samples", "700"] + seed_args + [
                                "--no_tqdm", "--device", "cpu", "--datapath", str(tmp_path / "data"),
                                "--log_dir", str(logs), "--master_port", str(_free_port())] + list(extra)
     launch_main(argv)
@@ -137,27 +138,40 @@ def test_checkpoint_roundtrip(tmp_path):
 
 
 @pytest.mark.slow
-def test_bench_two_ranks_gloo(tmp_path):
-    """bench.py under torch.distributed.run with 2 CPU ranks (gloo): one JSON line from rank 0
-    with the driver's contract fields (the GPU path is the same code over RCCL)."""
+@pytest.mark.parametrize("nranks", [2, 4])
+def test_bench_multi_rank_gloo(tmp_path, nranks):
+    """bench.py under torch.distributed.run with 2 and 4 CPU ranks (gloo): one JSON line
+    from rank 0 with the driver's contract fields and the multi-rank evidence fields (the
+    GPU path is the same code over RCCL)."""
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = tmp_path / "b.json"
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nranks),
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
-           "--gpus", "2", "--steps", "1", "--warmup", "1", "--samples_per_client", "48", "--json_out", str(out)]
-    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=str(tmp_path))
+           "--gpus", str(nranks), "--steps", "1", "--warmup", "1", "--num_samples", str(300 * nranks),
+           "--server_epochs", "1", "--json_out", str(out)]
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="2")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env, cwd=str(tmp_path))
     assert r.returncode == 0, r.stderr[-3000:]
+    # gloo itself prints "[Gloo] Rank r is connected ..." lines (other processes, possibly
+    # interleaved); ours is the one JSON line
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1
+    assert len(lines) == 1, r.stdout[-2000:]
     rec = json.loads(lines[0])
     assert rec == json.loads(out.read_text())
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
               "scaling", "vs_baseline", "dtype", "data", "config"):
         assert k in rec, k
-    assert rec["n_gpus"] == 2 and rec["value"] > 0 and rec["config"]["world_size"] == 3
+    c = rec["config"]
+    assert rec["n_gpus"] == nranks and rec["value"] > 0 and c["world_size"] == nranks + 1
+    assert c["dist_world"] == nranks and len(c["bytes_sent_per_rank_per_step"]) == nranks
+    assert c["parallelism"].endswith(f"bob_tp{nranks}")
+    # the whole schedule ran: training, eval and unlearning phases are all timed
+    for p in ("local_training", "server_training", "eval_breakdown", "unlearn_local", "server_retraining"):
+        assert p in c["phase_seconds"], p
+    # the SISA dump crossed ranks (Alices on ranks 1.. multicast to every Bob TP rank)
+    assert sum(c["bytes_sent_per_rank_per_step"]) > 0
 
 
 @pytest.mark.slow
@@ -193,3 +207,27 @@ def test_crash_and_resume_matches_uninterrupted(tmp_path, flags, np_, tp, crash_
     steps = sorted(p.name for p in (run / "ck").iterdir() if p.name.startswith("step"))
     assert len(steps) <= 2
     torch.load(run / "ck" / steps[-1] / "rank0.pt", weights_only=True)
+
+
+@pytest.mark.slow
+def test_resume_without_seed_flag(tmp_path):
+    """A checkpointed job launched with the default flags (no --seed) records the seed it
+    drew in <ckpt_dir>/job.json; --resume reuses it, so the resumed job finishes bitwise
+    equal to an uninterrupted run under that seed (SISA, TP=2 Bob, co-located Alices)."""
+    ref, run = tmp_path / "ref", tmp_path / "run"
+    ref.mkdir()
+    run.mkdir()
+    flags, crash_at = ["--sisa"], "1:unlearn_local:crash"
+    with pytest.raises(mp.ProcessExitedException):
+        _run(run, flags, 3, 2, 2, extra=["--ckpt_dir", str(run / "ck"), "--fault_inject", crash_at], seed=None)
+    seed = json.loads((run / "ck" / "job.json").read_text())["seed"]
+    m_ref, _, _ = _run(ref, flags, 3, 2, 2, extra=["--save_dir", str(ref / "out")], seed=seed)
+    m_res, bob, _ = _run(run, flags, 3, 2, 2, seed=None,
+                         extra=["--ckpt_dir", str(run / "ck"), "--resume", "--save_dir", str(run / "out")])
+    assert "[resume]" in bob
+    assert m_res["last_eval"] == m_ref["last_eval"]
+    for f in ["bob.pt", "alice1.pt", "alice2.pt"]:
+        a = torch.load(ref / "out" / f, weights_only=True)
+        b = torch.load(run / "out" / f, weights_only=True)
+        for k in a:
+            assert torch.equal(a[k], b[k]), (f, k)
