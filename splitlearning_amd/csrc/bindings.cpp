@@ -646,7 +646,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("linear_dgrad_partial", &linear_dgrad_partial);
   m.def("wgrad_group", &wgrad_group);
   m.def("set_variant", [](int64_t slot, int64_t v) {
-    TORCH_CHECK(slot >= 0 && slot < 8, "variant slot");
+    TORCH_CHECK(slot >= 0 && slot < 16, "variant slot");
     sl::g_variant[slot] = (int)v;
   });
   m.def("get_variant", [](int64_t slot) { return (int64_t)sl::g_variant[slot]; });

@@ -137,7 +137,7 @@ __device__ __forceinline__ void sl_opt_update4(const SlOpt& o, f32x4& p, f32x4 g
 // Kernel-variant switches for in-process A/B measurement (set from Python via
 // _C.set_variant; 0 = the shipped default everywhere).
 namespace sl {
-extern int g_variant[8];
+extern int g_variant[16];
 }
 
 #define SL_CHECK_LAUNCH() (hipGetLastError())

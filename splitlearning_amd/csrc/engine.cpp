@@ -99,7 +99,10 @@ class ServerEpoch {
     col_off1_ = cfg["col_off1"].cast<int>();
     row2_ = cfg["row2"].cast<bool>();
     if (!cfg["comm"].is_none()) comm_ = cfg["comm"].cast<sl::TpComm*>();
-    TORCH_CHECK(!row2_ || comm_ != nullptr, "a row-parallel fc2 needs the native communicator");
+    // emulate_tp: a shard executor of a single-process tensor-parallel emulation
+    // (tp_emulate_epoch does the all-reduce); otherwise a row-parallel fc2 needs RCCL
+    emulate_ = cfg.contains("emulate_tp") && cfg["emulate_tp"].cast<bool>();
+    TORCH_CHECK(!row2_ || comm_ != nullptr || emulate_, "a row-parallel fc2 needs the native communicator");
     B_ = cfg["B"].cast<int>();
     TORCH_CHECK(B_ >= 1 && B_ <= 16, "batch 1..16 (look-ahead slabs, head kernels)");
     pn_ = get(cfg, "pn");
@@ -126,6 +129,33 @@ class ServerEpoch {
   // updated (fwd_count, t, pre).
   py::tuple run(const at::Tensor& acts, const at::Tensor& labels, at::Tensor& loss_rows, int64_t seed_base,
                 int64_t fwd_count, int64_t t, bool pre, bool lookahead) {
+    check_batch(acts, labels, loss_rows);
+    const int64_t n = acts.size(0);
+    for (int64_t s = 0; s < n; s += B_) {
+      Step st = begin(acts, labels, s, seed_base, fwd_count, t, pre, lookahead);
+      forward_product(st);
+      if (row2_) comm_->allreduce_sum_f32(p2ws_.data_ptr<float>(), (size_t)st.M * L_[1].N, stream());
+      finish(st, loss_rows);
+      fwd_count = st.fwd_count;
+      t = st.t;
+      pre = st.next_pre;
+    }
+    return py::make_tuple(fwd_count, t, pre);
+  }
+
+  // ---- step phases (public so a single-process tensor-parallel emulation can interleave
+  // T shard executors around its own all-reduce: tp_emulate_epoch below)
+  struct Step {
+    int64_t s = 0;
+    int M = 0;
+    int64_t fwd_count = 0, t = 0;
+    bool pre = false, next_pre = false, lookahead = true;
+    const at::Tensor* acts = nullptr;
+    const at::Tensor* labels = nullptr;
+    uint64_t sd0 = 0, sd1 = 0;
+  };
+
+  void check_batch(const at::Tensor& acts, const at::Tensor& labels, const at::Tensor& loss_rows) const {
     TORCH_CHECK(acts.is_cuda() && acts.scalar_type() == at::kFloat && acts.dim() == 2 && acts.is_contiguous() &&
                     acts.size(1) == L_[0].K,
                 "acts [n, K1] contiguous f32");
@@ -133,99 +163,124 @@ class ServerEpoch {
     TORCH_CHECK(labels.is_cuda() && labels.scalar_type() == at::kLong && labels.is_contiguous() && labels.numel() == n,
                 "labels int64 [n]");
     TORCH_CHECK(loss_rows.is_cuda() && loss_rows.scalar_type() == at::kFloat && loss_rows.numel() >= n, "loss [n]");
-    const int B = B_;
-    const int K1 = L_[0].K, N1 = L_[0].N, N2 = L_[1].N, C = L_[2].N;
+  }
+
+  Step begin(const at::Tensor& acts, const at::Tensor& labels, int64_t s, int64_t seed_base, int64_t fwd_count,
+             int64_t t, bool pre, bool lookahead) const {
+    Step st;
+    st.s = s;
+    st.M = (int)std::min<int64_t>(B_, acts.size(0) - s);
+    st.fwd_count = fwd_count + 1;
+    st.t = t;
+    st.pre = pre;
+    st.lookahead = lookahead;
+    st.acts = &acts;
+    st.labels = &labels;
+    st.sd0 = sl::step_seed((uint64_t)seed_base, 0, (uint64_t)st.fwd_count);
+    st.sd1 = sl::step_seed((uint64_t)seed_base, 1, (uint64_t)st.fwd_count);
+    return st;
+  }
+
+  // fc1 -> h1 (epilogue of the pending look-ahead slabs, or a plain forward), then fc2's
+  // product into p2ws: split-K slabs, or (row-parallel fc2) this shard's unsplit partial sum
+  // that the caller all-reduces before finish()
+  void forward_product(Step& st) {
+    const int M = st.M;
+    const int K1 = L_[0].K, N1 = L_[0].N, N2 = L_[1].N;
     const int64_t S1 = (K1 + 255) / 256;
-    const hipStream_t st = c10::hip::getCurrentHIPStream().stream();
-    const float* X = acts.data_ptr<float>();
-    float* pn = pn_.data_ptr<float>();
+    const hipStream_t sm = stream();
+    const float* x = st.acts->data_ptr<float>() + st.s * K1;
+    float* h1 = h1_.data_ptr<float>();
+    float* P2 = p2ws_.data_ptr<float>();
+    const Epi e1 = sl::make_epi_raw(L_[0].b.data_ptr<float>(), true, p1_, st.sd0, col_off1_, nullptr);
+    if (st.pre)
+      ck(sl::linear_epilogue(pn_.data_ptr<float>(), N1, h1, N1, M, N1, e1, (int)S1, (int64_t)M * N1, sm),
+         "fc1 epilogue");
+    else
+      ck(sl::linear_fwd(x, K1, L_[0].W.data_ptr<float>(), K1, h1, N1, M, N1, K1, e1, fwdws_.data_ptr<float>(),
+                        fwdws_.numel(), sm),
+         "fc1 forward");
+    S2_ = 1;
+    if (row2_) {
+      if (N1 <= 1280) {
+        ck(sl::linear_fwd_partial(h1, N1, L_[1].W.data_ptr<float>(), N1, M, N2, N1, P2, p2ws_.numel(), 1, &S2_, sm),
+           "fc2 forward");
+      } else {
+        Epi plain{};
+        plain.dscale = 1.f;
+        ck(sl::linear_fwd(h1, N1, L_[1].W.data_ptr<float>(), N1, P2, N2, M, N2, N1, plain, fwdws_.data_ptr<float>(),
+                          fwdws_.numel(), sm),
+           "fc2 forward");
+        S2_ = 1;
+      }
+    } else {
+      ck(sl::linear_fwd_partial(h1, N1, L_[1].W.data_ptr<float>(), N1, M, N2, N1, P2, p2ws_.numel(), 16, &S2_, sm),
+         "fc2 forward");
+    }
+  }
+
+  // head (h2, dlogits, dz2, loss), fc1's dZ, and the grouped wgrad + optimizer step with the
+  // next full batch's fc1 look-ahead
+  void finish(Step& st, at::Tensor& loss_rows) {
+    const int M = st.M;
+    const int K1 = L_[0].K, N1 = L_[0].N, N2 = L_[1].N, C = L_[2].N;
+    const hipStream_t sm = stream();
+    const int64_t n = st.acts->size(0);
+    const float* X = st.acts->data_ptr<float>();
+    const float* x = X + st.s * K1;
     float* h1 = h1_.data_ptr<float>();
     float* h2 = h2_.data_ptr<float>();
     float* dz1 = dz1_.data_ptr<float>();
     float* dz2 = dz2_.data_ptr<float>();
     float* dlog = dlog_.data_ptr<float>();
-    float* P2 = p2ws_.data_ptr<float>();
     const double s1 = p1_ > 0 ? 1.0 / (1.0 - p1_) : 1.0;
-    for (int64_t s = 0; s < n; s += B) {
-      const int M = (int)std::min<int64_t>(B, n - s);
-      const float* x = X + s * K1;
-      ++fwd_count;
-      const uint64_t sd0 = sl::step_seed((uint64_t)seed_base, 0, (uint64_t)fwd_count);
-      const uint64_t sd1 = sl::step_seed((uint64_t)seed_base, 1, (uint64_t)fwd_count);
-      const Epi e1 = sl::make_epi_raw(L_[0].b.data_ptr<float>(), true, p1_, sd0, col_off1_, nullptr);
-      // fc1 -> h1
-      if (pre)
-        ck(sl::linear_epilogue(pn, N1, h1, N1, M, N1, e1, (int)S1, (int64_t)M * N1, st), "fc1 epilogue");
-      else
-        ck(sl::linear_fwd(x, K1, L_[0].W.data_ptr<float>(), K1, h1, N1, M, N1, K1, e1, fwdws_.data_ptr<float>(),
-                          fwdws_.numel(), st),
-           "fc1 forward");
-      // fc2 -> P2 (split-K slabs, or the all-reduced product when row-parallel)
-      int S2 = 1;
-      if (row2_) {
-        if (N1 <= 1280) {
-          ck(sl::linear_fwd_partial(h1, N1, L_[1].W.data_ptr<float>(), N1, M, N2, N1, P2, p2ws_.numel(), 1, &S2, st),
-             "fc2 forward");
-        } else {
-          Epi plain{};
-          plain.dscale = 1.f;
-          ck(sl::linear_fwd(h1, N1, L_[1].W.data_ptr<float>(), N1, P2, N2, M, N2, N1, plain, fwdws_.data_ptr<float>(),
-                            fwdws_.numel(), st),
-             "fc2 forward");
-          S2 = 1;
-        }
-        comm_->allreduce_sum_f32(P2, (size_t)M * N2, st);
-      } else {
-        ck(sl::linear_fwd_partial(h1, N1, L_[1].W.data_ptr<float>(), N1, M, N2, N1, P2, p2ws_.numel(), 16, &S2, st),
-           "fc2 forward");
-      }
-      // head: h2, dlogits, dz2, loss
-      const Epi e2 = sl::make_epi_raw(L_[1].b.data_ptr<float>(), true, p2_, sd1, 0, nullptr);
-      ck(sl::server_head3(P2, S2, (int64_t)M * N2, e2, L_[2].W.data_ptr<float>(), N2, L_[2].b.data_ptr<float>(),
-                          labels.data_ptr<int64_t>() + s, -100, (float)(1.0 / M), h2, dlog, dz2,
-                          loss_rows.data_ptr<float>() + s, headws_.data_ptr<float>(), headws_.numel(), M, N2, C, st),
-         "server head");
-      // fc1's dZ
-      ck(sl::linear_dgrad(dz2, N2, L_[1].W.data_ptr<float>(), N1, h1, N1, (float)s1, dz1, N1, dgws_.data_ptr<float>(),
-                          dgws_.numel(), M, N2, N1, st),
-         "fc2 dgrad");
-      // optimizer step of all three layers (+ look-ahead of the next full batch)
-      ++t;
-      sl::WgGroup g{};
-      g.n = 3;
-      const float* dzs[3] = {dz1, dz2, dlog};
-      const float* As[3] = {x, h1, h2};
-      const int lds[3] = {N1, N2, C}, ldas[3] = {K1, N1, N2};
-      for (int i = 0; i < 3; ++i) {
-        sl::WgDesc& d = g.d[i];
-        Layer& L = L_[i];
-        d.dz = dzs[i];
-        d.ldz = lds[i];
-        d.A = As[i];
-        d.lda = ldas[i];
-        d.W = L.W.data_ptr<float>();
-        d.ldw = L.K;
-        d.s0 = L.s0.data_ptr<float>();
-        d.s1 = L.s1.defined() ? L.s1.data_ptr<float>() : nullptr;
-        d.bias = L.b.data_ptr<float>();
-        d.sb0 = L.sb0.data_ptr<float>();
-        d.sb1 = L.sb1.defined() ? L.sb1.data_ptr<float>() : nullptr;
-        d.N = L.N;
-        d.K = L.K;
-      }
-      const bool next_full = lookahead && s + 2LL * B <= n;
-      if (next_full) {
-        g.xn = X + (s + B) * K1;
-        g.ldxn = K1;
-        g.mn = B;
-        g.pn = pn;
-      }
-      const SlOpt o = sl::make_opt_raw(kind_, lr_, beta1_, beta2_, eps_, wd_, mom_, t, nullptr);
-      ck(sl::wgrad_group(g, M, o, st), "wgrad_group");
-      pre = next_full;
+    const Epi e2 = sl::make_epi_raw(L_[1].b.data_ptr<float>(), true, p2_, st.sd1, 0, nullptr);
+    ck(sl::server_head3(p2ws_.data_ptr<float>(), S2_, (int64_t)M * N2, e2, L_[2].W.data_ptr<float>(), N2,
+                        L_[2].b.data_ptr<float>(), st.labels->data_ptr<int64_t>() + st.s, -100, (float)(1.0 / M), h2,
+                        dlog, dz2, loss_rows.data_ptr<float>() + st.s, headws_.data_ptr<float>(), headws_.numel(), M,
+                        N2, C, sm),
+       "server head");
+    ck(sl::linear_dgrad(dz2, N2, L_[1].W.data_ptr<float>(), N1, h1, N1, (float)s1, dz1, N1, dgws_.data_ptr<float>(),
+                        dgws_.numel(), M, N2, N1, sm),
+       "fc2 dgrad");
+    ++st.t;
+    sl::WgGroup g{};
+    g.n = 3;
+    const float* dzs[3] = {dz1, dz2, dlog};
+    const float* As[3] = {x, h1, h2};
+    const int lds[3] = {N1, N2, C}, ldas[3] = {K1, N1, N2};
+    for (int i = 0; i < 3; ++i) {
+      sl::WgDesc& d = g.d[i];
+      Layer& L = L_[i];
+      d.dz = dzs[i];
+      d.ldz = lds[i];
+      d.A = As[i];
+      d.lda = ldas[i];
+      d.W = L.W.data_ptr<float>();
+      d.ldw = L.K;
+      d.s0 = L.s0.data_ptr<float>();
+      d.s1 = L.s1.defined() ? L.s1.data_ptr<float>() : nullptr;
+      d.bias = L.b.data_ptr<float>();
+      d.sb0 = L.sb0.data_ptr<float>();
+      d.sb1 = L.sb1.defined() ? L.sb1.data_ptr<float>() : nullptr;
+      d.N = L.N;
+      d.K = L.K;
     }
-    return py::make_tuple(fwd_count, t, pre);
+    const bool next_full = st.lookahead && st.s + 2LL * B_ <= n;
+    if (next_full) {
+      g.xn = X + (st.s + B_) * K1;
+      g.ldxn = K1;
+      g.mn = B_;
+      g.pn = pn_.data_ptr<float>();
+    }
+    const SlOpt o = sl::make_opt_raw(kind_, lr_, beta1_, beta2_, eps_, wd_, mom_, st.t, nullptr);
+    ck(sl::wgrad_group(g, M, o, sm), "wgrad_group");
+    st.next_pre = next_full;
   }
+
+  at::Tensor product_view(int M) const { return p2ws_.narrow(0, 0, (int64_t)M * L_[1].N); }
+  bool row_parallel() const { return row2_; }
+  int batch() const { return B_; }
 
  private:
   Layer L_[3];
@@ -235,12 +290,56 @@ class ServerEpoch {
   bool row2_ = false;
   sl::TpComm* comm_ = nullptr;
   int B_ = 16;
+  bool emulate_ = false;
+  int S2_ = 1;
   at::Tensor pn_, p2ws_, fwdws_, dgws_, headws_, h1_, h2_, dz1_, dz2_, dlog_;
+  static hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
 };
+
+// Single-process emulation of the tensor-parallel server epoch: T shard executors (each
+// built with emulate_tp over its own shard, optimizer state and workspaces) are stepped in
+// lock step on one GPU, and the row-parallel fc2's all-reduce is a sum of the T partial
+// products (fixed order) copied back into every shard.  Every other launch is exactly the
+// production path (ServerEpoch::run), so the shard math of the native executor is checked
+// against the single-shard run without a multi-GPU box.
+py::tuple tp_emulate_epoch(py::list exs, const at::Tensor& acts, const at::Tensor& labels, py::list loss_rows,
+                           int64_t seed_base, int64_t fwd_count, int64_t t, bool pre, bool lookahead) {
+  std::vector<ServerEpoch*> E;
+  std::vector<at::Tensor> losses;
+  for (auto h : exs) E.push_back(h.cast<ServerEpoch*>());
+  for (auto h : loss_rows) losses.push_back(h.cast<at::Tensor>());
+  TORCH_CHECK(!E.empty() && E.size() == losses.size(), "one loss buffer per shard executor");
+  const int B = E[0]->batch();
+  for (size_t i = 0; i < E.size(); ++i) {
+    TORCH_CHECK(E[i]->batch() == B, "shard executors differ in batch size");
+    E[i]->check_batch(acts, labels, losses[i]);
+  }
+  const bool row = E[0]->row_parallel();
+  const int64_t n = acts.size(0);
+  for (int64_t s = 0; s < n; s += B) {
+    std::vector<ServerEpoch::Step> st;
+    for (auto* e : E) st.push_back(e->begin(acts, labels, s, seed_base, fwd_count, t, pre, lookahead));
+    for (size_t i = 0; i < E.size(); ++i) E[i]->forward_product(st[i]);
+    if (row && E.size() > 1) {
+      const int M = st[0].M;
+      at::Tensor sum = E[0]->product_view(M).clone();
+      for (size_t i = 1; i < E.size(); ++i) sum.add_(E[i]->product_view(M));
+      for (auto* e : E) e->product_view(M).copy_(sum);
+    }
+    for (size_t i = 0; i < E.size(); ++i) E[i]->finish(st[i], losses[i]);
+    fwd_count = st[0].fwd_count;
+    t = st[0].t;
+    pre = st[0].next_pre;
+  }
+  return py::make_tuple(fwd_count, t, pre);
+}
 
 }  // namespace
 
 void sl_register_engine(py::module& m) {
+  m.def("tp_emulate_epoch", &tp_emulate_epoch, py::arg("executors"), py::arg("acts"), py::arg("labels"),
+        py::arg("loss_rows"), py::arg("seed_base"), py::arg("fwd_count"), py::arg("t"), py::arg("pre"),
+        py::arg("lookahead"));
   py::class_<ServerEpoch>(m, "ServerEpoch")
       .def(py::init<const py::dict&>())
       .def("run", &ServerEpoch::run, py::arg("acts"), py::arg("labels"), py::arg("loss_rows"), py::arg("seed_base"),

@@ -24,7 +24,7 @@
 
 namespace sl {
 
-int g_variant[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+int g_variant[16] = {0};
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -201,6 +201,92 @@ skinny_dgrad_kernel(const float* __restrict__ dZ, int ldz, const float* __restri
   }
 }
 
+// Full-N dgrad: dX[M, K] = mask(dZ[M, N] . W[N, K]) with the WHOLE reduction over N inside
+// one workgroup, so the result is stored masked and final (no split-N slabs, no reduce
+// launch).  grid (ceil(K/32), ceil(M/16)), 1024 threads = 16 waves; wave w owns an N slice.
+// MFMA v_mfma_f32_16x16x4f32 with A = dZ (16 rows m x 4 n), B = W (4 n x 16 k): the 32
+// k-columns of the workgroup are two 16-column MFMA tiles fed by one float2 load per lane
+// (16 lanes x 8 B = one 128-B row segment of W per n).  Lane (m = lane&15, q = lane>>4) takes
+// n = n0 + 4q + s at sub-step s, so its four dZ values of a 16-n group are one float4 load.
+// The 16 waves' partial tiles are summed through LDS in a fixed order (deterministic).
+// At B = 16 this reads W once (fc2: 20 MB) from 157 workgroups; the split-N form it replaces
+// needed ~630 workgroups plus a reduce launch over the slabs.
+__global__ void __launch_bounds__(1024)
+dgrad_fulln_kernel(const float* __restrict__ dZ, int ldz, const float* __restrict__ W, int ldw,
+                   const float* __restrict__ hprev, int ldh, float scale, float* __restrict__ out, int ldo,
+                   int M, int N, int K) {
+  __shared__ f32x4 red[16][2][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int k0 = blockIdx.x * 32, m0 = blockIdx.y * 16;
+  const int j = lane & 15, q = lane >> 4;
+  const int kc = k0 + 2 * j;                       // this lane's two columns kc, kc + 1
+  const bool vk = kc + 1 < K;                      // K % 4 == 0 (host check): pairs never straddle K
+  const bool vm = (m0 + j) < M;
+  // N slice of this wave: multiples of 16
+  const int nper = ((N + 16 * 16 - 1) / (16 * 16)) * 16;
+  const int nb = wv * nper, ne = min(N, nb + nper);
+  const float* za = dZ + (int64_t)(vm ? m0 + j : 0) * ldz;
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  constexpr int U = 4;                             // 16-n groups in flight per lane
+  int n = nb;
+  for (; n + 16 * U <= ne; n += 16 * U) {
+    float4 a[U];
+    float2 w[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int nq = n + 16 * u + 4 * q;
+      a[u] = vm ? *reinterpret_cast<const float4*>(za + nq) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        w[u][s] = vk ? *reinterpret_cast<const float2*>(W + (int64_t)(nq + s) * ldw + kc) : make_float2(0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float av[4] = {a[u].x, a[u].y, a[u].z, a[u].w};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        acc0 = mfma4(av[s], w[u][s].x, acc0);
+        acc1 = mfma4(av[s], w[u][s].y, acc1);
+      }
+    }
+  }
+  for (; n < ne; n += 16) {                        // tail groups (N % 16 handled per element)
+    const int nq = n + 4 * q;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int nn = nq + s;
+      const bool in = nn < ne;
+      const float av = (vm && in) ? za[nn] : 0.f;
+      const float2 wv2 = (vk && in) ? *reinterpret_cast<const float2*>(W + (int64_t)nn * ldw + kc)
+                                     : make_float2(0.f, 0.f);
+      acc0 = mfma4(av, wv2.x, acc0);
+      acc1 = mfma4(av, wv2.y, acc1);
+    }
+  }
+  red[wv][0][lane] = acc0;
+  red[wv][1][lane] = acc1;
+  __syncthreads();
+  // 512 outputs: thread t -> (half h, lane l); D_h[row][col]: row = 4*(l>>4) + r, col j = l & 15
+  const int t = threadIdx.x;
+  if (t < 128) {
+    const int h = t >> 6, l = t & 63;
+    f32x4 s = red[0][h][l];
+#pragma unroll
+    for (int v = 1; v < 16; ++v) s += red[v][h][l];
+    const int kk = k0 + 2 * (l & 15) + h;
+    if (kk < K) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + 4 * (l >> 4) + r;
+        if (m >= M) continue;
+        float v = s[r];
+        if (hprev) v = (hprev[(int64_t)m * ldh + kk] > 0.f) ? v * scale : 0.f;
+        out[(int64_t)m * ldo + kk] = v;
+      }
+    }
+  }
+}
+
 __global__ void dgrad_reduce_kernel(const float* __restrict__ P, int S, int64_t slab,
                                     const float* __restrict__ hprev, int ldh, float scale,
                                     float* __restrict__ out, int ldo, int M, int K) {
@@ -331,6 +417,14 @@ hipError_t linear_dgrad(const float* dZ, int ldz, const float* W, int ldw, const
                         hipStream_t st) {
   if (M <= 0 || K <= 0) return hipSuccess;
   const int kt = (K + 63) / 64, mt = (M + 15) / 16;
+  // default: the full-N form (reduction over N inside the workgroup, masked store, one
+  // launch) whenever the batch is a training batch; variant 8 = 1 restores the split-N +
+  // reduce pair below for A/B
+  if (g_variant[8] != 1 && M <= 64 && (K & 3) == 0 && (ldw & 1) == 0 && (ldz & 3) == 0) {
+    dim3 grid((K + 31) / 32, mt);
+    dgrad_fulln_kernel<<<grid, 1024, 0, st>>>(dZ, ldz, W, ldw, hprev, ldh, scale, dX, ldx, M, N, K);
+    return hipGetLastError();
+  }
   int S = 1;
   // aim for >= ~256 workgroups on the 256-CU part; split N when there are few K tiles.
   // Variant 5, for A/B: 1 = never split, >1 = max split with N slices down to 16 rows.

@@ -47,8 +47,11 @@ class _Layer:
 
 class TailEngine:
     def __init__(self, module: torch.nn.Module, spec: TailSpec, device: torch.device,
-                 tp_rank: int = 0, tp_size: int = 1, allreduce=None, seed_base: int = 0):
+                 tp_rank: int = 0, tp_size: int = 1, allreduce=None, seed_base: int = 0, ws_tag: str = ""):
+        """`ws_tag`: private scratch / hand-off buffers for this engine (several shards of one
+        tail living in one process: the single-process TP emulation, `emulate_tp_epoch`)."""
         self.spec = spec
+        self.ws_tag = ws_tag
         self.device = device
         self.ops = ops.impl(device)
         self.tp_rank, self.tp_size = tp_rank, tp_size
@@ -226,6 +229,8 @@ class TailEngine:
 
     def lookahead_slabs(self, m: int):
         L1 = self.layers[0]
+        if self.ws_tag:
+            return self.ops.lookahead_slabs(self.device, L1.W.shape[1], m, L1.W.shape[0], self.ws_tag)
         return self.ops.lookahead_slabs(self.device, L1.W.shape[1], m, L1.W.shape[0])
 
     def lookahead_prologue(self, x0, out=None):
@@ -351,19 +356,46 @@ class TailEngine:
         cfg = slot.cfg
         kmax = max(L.W.shape[1] for L in self.layers)
         nmax = max(L.W.shape[0] for L in self.layers)
+        tg = self.ws_tag
         d = {"layers": layers, "kind": {"sgd": 1, "adam": 2}[cfg.kind], "lr": cfg.lr, "beta1": cfg.beta1,
              "beta2": cfg.beta2, "eps": cfg.eps, "wd": cfg.weight_decay, "momentum": cfg.momentum,
              "p1": L1.spec.dropout, "p2": L2.spec.dropout, "col_off1": L1.col_off, "row2": L2.style == "row",
              "comm": getattr(self.allreduce, "comm", None) if L2.style == "row" else None, "B": B,
-             "pn": self.lookahead_slabs(B), "p2ws": ops._workspace(dev, 16 * B * N2, "fc2p"),
-             "fwdws": ops._workspace(dev, 16 * B * nmax, "fwd"), "dgws": ops._workspace(dev, 16 * B * kmax, "dgrad"),
-             "headws": ops._workspace(dev, ops.C().head3_slices(N2) * B * C, "head"),
+             "emulate_tp": L2.style == "row" and self.allreduce is None,
+             "pn": self.lookahead_slabs(B), "p2ws": ops._workspace(dev, 16 * B * N2, "fc2p" + tg),
+             "fwdws": ops._workspace(dev, 16 * B * nmax, "fwd" + tg),
+             "dgws": ops._workspace(dev, 16 * B * kmax, "dgrad" + tg),
+             "headws": ops._workspace(dev, ops.C().head3_slices(N2) * B * C, "head" + tg),
              "h1": torch.empty(B, N1, device=dev), "h2": torch.empty(B, N2, device=dev),
              "dz1": torch.empty(B, N1, device=dev), "dz2": torch.empty(B, N2, device=dev),
              "dlog": torch.empty(B, C, device=dev)}
         ex = ops.C().ServerEpoch(d)
         self._native = (slot, B, ex, d)      # d keeps the workspaces alive
         return ex
+
+    # ------------------------------------------------------------------ TP emulation
+    @staticmethod
+    def emulate_tp_epoch(shards: list, slots: list, acts: torch.Tensor, labels: torch.Tensor, B: int,
+                         lookahead: bool = True) -> torch.Tensor:
+        """One server epoch of a tensor-parallel tail emulated in ONE process: `shards` are the
+        T TailEngines of one tail (tp_rank 0..T-1, `allreduce=None`, distinct `ws_tag`s), each
+        with its own optimizer slot.  The production native executor (`_C.ServerEpoch`) runs
+        every shard; `_C.tp_emulate_epoch` steps them in lock step and stands in for RCCL's
+        all-reduce of the row-parallel fc2 products.  Returns shard 0's per-row losses."""
+        t0 = shards[0]
+        exs = [sh._native_executor(sl, B) for sh, sl in zip(shards, slots)]
+        pre = False
+        if lookahead and acts.shape[0] >= B:
+            for sh in shards:
+                sh.lookahead_prologue(acts[:B], out=sh._native[3]["pn"])
+            pre = True
+        losses = [torch.empty(acts.shape[0], device=t0.device) for _ in shards]
+        fc, t, pre = t0.ops.C().tp_emulate_epoch(exs, acts, labels, losses, t0.seed_base, t0.fwd_count,
+                                                  slots[0].t, pre, lookahead)
+        for sh, sl in zip(shards, slots):
+            sh.fwd_count, sl.t = int(fc), int(t)
+            sh._pre = None
+        return losses[0]
 
     # ------------------------------------------------------------------ state
     def local_state(self) -> dict:

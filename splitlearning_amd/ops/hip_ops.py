@@ -265,10 +265,10 @@ def server_head3(P2, b2, relu2: bool, drop2: float, seed2: int, W3, b3, labels, 
     return h2, dlog, dz2, loss
 
 
-def lookahead_slabs(device, K0: int, mn: int, N0: int):
+def lookahead_slabs(device, K0: int, mn: int, N0: int, tag: str = ""):
     """Workspace for wgrad_group_'s look-ahead forward: [ceil(K0/256), mn, N0]."""
     S = (K0 + 255) // 256
-    return _workspace(device, S * mn * N0, "fc1n")[:S * mn * N0].view(S, mn, N0)
+    return _workspace(device, S * mn * N0, "fc1n" + tag)[:S * mn * N0].view(S, mn, N0)
 
 
 def wgrad_group_(layers, M: int, cfg, t: int, dyn=None, x_next=None, p_next=None):

@@ -1,0 +1,120 @@
+"""Golden tests on the GPU: the PRODUCTION fused paths against fp32 eager PyTorch.
+
+* the native SISA server epoch (`_C.ServerEpoch`: fc1 look-ahead inside the fused
+  wgrad+Adam kernel, 128 optimizer steps) against `model2_sisa` trained by
+  `torch.optim.Adam(lr, weight_decay=1e-5)` (data_entities_vanilla_sisa.py:266,305-313);
+* the vanilla `split_epoch` (Alice's deferred in-kernel update, Bob's look-ahead) against the
+  composed `model1_sisa` + `model2_sisa` with two `torch.optim.SGD(momentum=0.9)`
+  (data_entities_vanilla.py:37-42,66-76).
+Dropout masks are the framework's counter hash (`ops/rng.keep_mask`), regenerated for the
+reference from the same (seed, layer, step).  Bounds follow the CPU golden tests'
+`assert_adam_close` form: Adam normalises each update, so an element whose gradient is ~0
+moves by up to lr per step on rounding noise; everything else must agree closely.
+"""
+import copy
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from splitlearning_amd.engine import OptSlot, TailEngine, adam
+from splitlearning_amd.models import ClientFrontSisa, ServerTailSisa, sisa_server_spec
+from splitlearning_amd.ops import rng
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref_tail_forward(mod, x, seed_base, step):
+    h = x
+    lins = mod.linears()
+    for i, lin in enumerate(lins):
+        ls = mod.spec.layers[i]
+        h = F.linear(h, lin.weight, lin.bias)
+        if ls.relu:
+            h = F.relu(h)
+        if ls.dropout:
+            keep = rng.keep_mask(rng.step_seed(seed_base, i, step), h.shape[0], h.shape[1], ls.dropout,
+                                 device=h.device)
+            h = h * keep / (1 - ls.dropout)
+    return h
+
+
+def _close_adam(a, b, lr, steps, frac=1e-3, tol=1e-4, msg=""):
+    d = (a.float() - b.float()).abs()
+    assert d.max().item() <= 2 * lr * steps + 1e-6, (msg, d.max().item())
+    assert (d > tol).float().mean().item() < frac, (msg, (d > tol).float().mean().item(), d.max().item())
+
+
+def test_native_sisa_server_epoch_matches_torch_adam(cuda):
+    torch.backends.cuda.matmul.allow_tf32 = False
+    B, steps, lr, seed_base = 16, 128, 1e-3, 99
+    g = torch.Generator().manual_seed(21)
+    n = B * steps
+    acts = (torch.rand(n, 5408, generator=g) * 30).to(cuda)
+    labels = torch.randint(0, 10, (n,), generator=g).to(cuda)
+    torch.manual_seed(4)
+    base = ServerTailSisa()
+    ref = copy.deepcopy(base).to(cuda)
+    opt = torch.optim.Adam(ref.parameters(), lr=lr, weight_decay=1e-5)
+    te = TailEngine(copy.deepcopy(base), sisa_server_spec(), cuda, seed_base=seed_base)
+    slot = OptSlot(adam(lr, 1e-5))
+    assert te.native_epoch_ok(B)
+    te.lookahead_prologue(acts[:B])
+    loss_e = te.run_native_epoch(acts, labels, slot, B, True)
+    losses_r = []
+    for i in range(steps):
+        x, y = acts[i * B:(i + 1) * B], labels[i * B:(i + 1) * B]
+        opt.zero_grad()
+        loss = F.cross_entropy(_ref_tail_forward(ref, x, seed_base, i + 1), y, reduction="none")
+        loss.mean().backward()
+        opt.step()
+        losses_r.append(loss.detach())
+    torch.cuda.synchronize()
+    loss_r = torch.cat(losses_r)
+    torch.testing.assert_close(loss_e[:B], loss_r[:B], rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(loss_e, loss_r, rtol=1e-3, atol=1e-3)
+    for (k, v), (_, v2) in zip(te.module.state_dict().items(), ref.state_dict().items()):
+        _close_adam(v, v2, lr, steps, msg=k)
+    # optimizer state too: first and second moments of fc1
+    st = opt.state[ref.fc1.weight]
+    mine = slot.states["fc1.weight"]
+    torch.testing.assert_close(mine["m"], st["exp_avg"], rtol=1e-2, atol=1e-7)
+    torch.testing.assert_close(mine["v"], st["exp_avg_sq"], rtol=1e-2, atol=1e-9)
+
+
+def test_vanilla_split_epoch_matches_composed_torch_sgd(cuda, tmp_path):
+    from splitlearning_amd.config import parse_args
+    from splitlearning_amd.data.mnist import write_shards
+    from splitlearning_amd.parallel.dist import Comm, Placement
+    from splitlearning_amd.protocols import VanillaSession
+    args = parse_args(["--vanilla", "--world_size", "2", "--seed", "5", "--num_samples", "2000", "--no_tqdm",
+                       "--datapath", str(tmp_path / "d"), "--log_dir", str(tmp_path / "logs")])
+    write_shards(args, verbose=False)
+    sess = VanillaSession(args, Comm(0, 1, cuda, Placement.make(2, 1, 1)), cuda)
+    a = sess.alices[1]
+    assert sess.tail.lookahead_ok(16)
+    front_r = copy.deepcopy(a.front.module).to(cuda)
+    tail_r = copy.deepcopy(sess.tail.module).to(cuda)
+    lr = args.lr
+    opt_a = torch.optim.SGD(front_r.parameters(), lr=lr, momentum=0.9)
+    opt_b = torch.optim.SGD(tail_r.parameters(), lr=lr, momentum=0.9)
+    order = a.train.shuffled_order(torch.Generator().manual_seed(9))[:16 * 40 + 6]   # partial last batch
+    n = order.numel()
+    fc0 = sess.tail.fwd_count
+    sess.split_epoch(1, order, n)
+    for i, s in enumerate(range(0, n, 16)):
+        idx = order[s:s + 16]
+        opt_a.zero_grad()
+        opt_b.zero_grad()
+        out = _ref_tail_forward(tail_r, front_r(a.train.x_float(idx)), sess.tail.seed_base, fc0 + i + 1)
+        F.cross_entropy(out, a.train.y[idx]).backward()
+        opt_a.step()
+        opt_b.step()
+    torch.cuda.synchronize()
+    steps = -(-n // 16)
+    for (k, v), (_, v2) in zip(sess.tail.module.state_dict().items(), tail_r.state_dict().items()):
+        # SGD-momentum: no normalisation, differences stay at rounding level
+        torch.testing.assert_close(v, v2, rtol=1e-3, atol=1e-4, msg=k)
+    for (k, v), (_, v2) in zip(a.front.module.state_dict().items(), front_r.state_dict().items()):
+        torch.testing.assert_close(v, v2, rtol=1e-3, atol=1e-3, msg=k)
+    assert steps == 41

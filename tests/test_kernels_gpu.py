@@ -87,15 +87,25 @@ def test_linear_fwd(cuda, M, N, K, relu, drop):
 
 
 @pytest.mark.parametrize("M,N,K", [(16, 5000, 5408), (16, 1000, 5000), (16, 100, 1000), (16, 10, 100),
-                                    (3, 37, 52)])
+                                    (3, 37, 52), (16, 1000, 628), (64, 1000, 5000), (40, 1000, 604),
+                                    (16, 12, 8)])
 @pytest.mark.parametrize("masked", [False, True])
-def test_linear_dgrad(cuda, M, N, K, masked):
-    dz = torch.randn(M, N, device=cuda)
-    w = torch.randn(N, K, device=cuda) / N ** 0.5
-    h = torch.relu(torch.randn(M, K, device=cuda)) if masked else None
-    dx = hip_ops.linear_dgrad(dz, w, h, 2.0)
-    dxr = torch_ops.linear_dgrad(dz, w, h, 2.0)
-    _close(dx, dxr, rtol=1e-4, atol=1e-4)
+@pytest.mark.parametrize("variant", [0, 1])
+def test_linear_dgrad(cuda, M, N, K, masked, variant):
+    """variant 0: the full-N kernel (whole reduction in one workgroup, masked store) where it
+    applies (N % 4 == 0, M <= 64); 1: the split-N + reduce pair."""
+    C = hip_ops.C()
+    old = C.get_variant(8)
+    C.set_variant(8, variant)
+    try:
+        dz = torch.randn(M, N, device=cuda)
+        w = torch.randn(N, K, device=cuda) / N ** 0.5
+        h = torch.relu(torch.randn(M, K, device=cuda)) if masked else None
+        dx = hip_ops.linear_dgrad(dz, w, h, 2.0)
+        dxr = torch_ops.linear_dgrad(dz, w, h, 2.0)
+        _close(dx, dxr, rtol=1e-4, atol=1e-4)
+    finally:
+        C.set_variant(8, old)
 
 
 @pytest.mark.parametrize("M,N,K", [(16, 5000, 5408), (16, 100, 1000), (7, 10, 100), (40, 33, 20)])
