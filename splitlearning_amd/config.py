@@ -113,6 +113,9 @@ def build_parser() -> argparse.ArgumentParser:
     g.add_argument("--python_epoch", dest="native_epoch", action="store_false",
                    help="issue Bob's eager server steps from Python instead of the native "
                         "executor (_C.ServerEpoch); numerics are identical")
+    g.add_argument("--serial_alices", dest="multi_alice", action="store_false",
+                   help="step co-located Alices' SISA local epochs one after another instead of "
+                        "together (one launch per step for all of them); numerics are identical")
     g.add_argument("--trace_dir", type=str, default="",
                    help="write a Chrome-trace timeline per rank (phases, data-plane ops with bytes, "
                         "device time of server / local epochs) to DIR/trace_rank<r>.json")

@@ -32,6 +32,9 @@ hipError_t conv_local_epoch(const void* x, bool x_u8, const int64_t* order, int6
 hipError_t conv_bwd_step(const float* dy, const float* y, const uint8_t* am, const void* x, bool x_u8,
                          const int64_t* idx, int B, float* w, float* b, float* slab, float* s0w, float* s1w,
                          float* s0b, float* s1b, SlOpt o, hipStream_t st, bool defer, const ConvPending* pend);
+hipError_t conv_local_epoch_multi(const MultiAlice* al, int k, int B, SlOpt (*opt)(void*, int64_t), void* optctx,
+                                  void* table, int64_t table_bytes, hipStream_t st);
+size_t alice_step_desc_bytes();
 hipError_t conv_apply(const ConvPending& p, float* w, float* b, hipStream_t st);
 hipError_t head_step(const float* X, float* W, float* b, const int64_t* y, int64_t ignore, float scale,
                      float* loss_rows, float* dX, float* s0w, float* s1w, float* s0b, float* s1b, int M, int K, int C,
@@ -253,6 +256,58 @@ void conv_local_epoch(const at::Tensor& x, const at::Tensor& order, const at::Te
                              s0w.data_ptr<float>(), fptr(s1w), s0b.data_ptr<float>(), fptr(s1b), ws.data_ptr<float>(),
                              ws.numel(), loss_rows.data_ptr<float>(), &epoch_opt, &ctx, t0, st),
         "conv_local_epoch");
+}
+
+// Local epochs of k co-located Alices stepped together, one launch per step for all of
+// them (conv.hip: conv_local_epoch_multi).  alices: [(x, order, labels, w, b, s0w, s1w, s0b,
+// s1b, ws, loss_rows, t0)]; every Alice shares the optimizer hyper-parameters.  `table`:
+// uint8 GPU workspace >= table_bytes(k, max steps).
+void conv_local_epoch_multi(py::list alices, int64_t B, int64_t kind, double lr, double beta1, double beta2, double eps,
+                            double wd, double momentum, at::Tensor& table) {
+  const int k = (int)alices.size();
+  TORCH_CHECK(k >= 1 && k <= 64, "1..64 co-located Alices");
+  TORCH_CHECK(B >= 1 && B <= 1024, "batch size");
+  TORCH_CHECK(kind == 1 || kind == 2, "local epoch: SGD-momentum or Adam");
+  need_cuda(table, "table");
+  TORCH_CHECK(table.scalar_type() == at::kByte && table.is_contiguous(), "table uint8 workspace");
+  std::vector<MultiAlice> al(k);
+  for (int a = 0; a < k; ++a) {
+    auto t = alices[a].cast<py::tuple>();
+    TORCH_CHECK(t.size() == 12, "alice tuple (x, order, labels, w, b, s0w, s1w, s0b, s1b, ws, loss_rows, t0)");
+    auto x = t[0].cast<at::Tensor>();
+    auto order = t[1].cast<at::Tensor>();
+    auto labels = t[2].cast<at::Tensor>();
+    auto w = t[3].cast<at::Tensor>();
+    auto b = t[4].cast<at::Tensor>();
+    auto s0w = t[5].cast<at::Tensor>();
+    auto s1w = t[6].cast<OptT>();
+    auto s0b = t[7].cast<at::Tensor>();
+    auto s1b = t[8].cast<OptT>();
+    auto ws = t[9].cast<at::Tensor>();
+    auto loss = t[10].cast<at::Tensor>();
+    check_x(x);
+    TORCH_CHECK(x.scalar_type() == at::kByte, "co-located epochs read uint8 shards");
+    check_params(w, b);
+    need_cuda(order, "order");
+    TORCH_CHECK(order.scalar_type() == at::kLong && order.is_contiguous() && order.dim() == 1, "order int64 [n]");
+    need_cuda(labels, "labels");
+    TORCH_CHECK(labels.scalar_type() == at::kLong && labels.is_contiguous() && labels.numel() == x.numel() / 784,
+                "labels int64 [N]");
+    TORCH_CHECK(s0w.numel() == 288 && s0b.numel() == 32, "optimizer state");
+    need_f32(ws, "ws");
+    TORCH_CHECK(ws.is_contiguous() && ws.numel() >= 2 * B * 320 + 2 * 960, "ws");
+    need_f32(loss, "loss_rows");
+    TORCH_CHECK(loss.is_contiguous() && loss.numel() >= order.numel(), "loss_rows [n]");
+    al[a] = MultiAlice{x.data_ptr<uint8_t>(), order.data_ptr<int64_t>(), order.numel(), labels.data_ptr<int64_t>(),
+                           w.data_ptr<float>(), b.data_ptr<float>(), s0w.data_ptr<float>(), fptr(s1w),
+                           s0b.data_ptr<float>(), fptr(s1b), ws.data_ptr<float>(), ws.numel(),
+                           loss.data_ptr<float>(), t[11].cast<int64_t>()};
+    if (kind == 2) TORCH_CHECK(al[a].s1w && al[a].s1b, "Adam second moments");
+  }
+  EpochOpt ctx{kind, lr, beta1, beta2, eps, wd, momentum};
+  check(sl::conv_local_epoch_multi(al.data(), k, (int)B, &epoch_opt, &ctx, table.data_ptr(), table.numel(),
+                                   cur_stream()),
+        "conv_local_epoch_multi");
 }
 
 // Split-mode client backward: dW partials from the cut gradient, then reduce+optimizer.
@@ -632,6 +687,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_apply", &conv_apply);
   m.def("head_step", &head_step);
   m.def("conv_local_epoch", &conv_local_epoch);
+  m.def("conv_local_epoch_multi", &conv_local_epoch_multi);
+  m.def("alice_step_desc_bytes", []() { return (int64_t)sl::alice_step_desc_bytes(); });
   m.def("linear_fwd", &linear_fwd);
   m.def("linear_epilogue", &linear_epilogue);
   m.def("linear_dgrad", &linear_dgrad);

@@ -100,6 +100,19 @@ struct ConvPending {
   SlOpt o;
 };
 
+// One co-located Alice's local epoch, for conv_local_epoch_multi (conv.hip).
+struct MultiAlice {
+  const uint8_t* x;        // shard pixels [N, 784]
+  const int64_t* order;    // this epoch's sample order [n]
+  int64_t n;
+  const int64_t* labels;   // shard labels [N]
+  float *w, *b, *s0w, *s1w, *s0b, *s1b;
+  float* ws;               // >= 2 B 320 + 2 960 floats, private to this Alice
+  int64_t ws_elems;
+  float* loss_rows;        // [n]
+  int64_t t0;              // first optimizer step of the epoch
+};
+
 // Fused GEMM epilogue: bias, ReLU, counter-hash dropout (global column index).
 struct Epi {
   const float* bias;

@@ -13,6 +13,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <vector>
 
 namespace sl {
 
@@ -186,19 +187,18 @@ __device__ __forceinline__ void stage_sample(const XT* x, int64_t src, const flo
 // forward, and workgroup 0 also stores it to `pout` (ping-pong: no workgroup reads what
 // another is writing).  Param buffer layout: [w 288 | b 32 | s0 320 | s1 320].
 template <typename XT, int SUB, bool FUSE>
-__global__ void __launch_bounds__(32 * SUB)
-conv_fwd_ce_wgrad_kernel(const XT* __restrict__ x, const int64_t* __restrict__ idx,
-                         const int64_t* __restrict__ labels, const float* __restrict__ w,
-                         const float* __restrict__ b, float scale, float* __restrict__ slab,
-                         float* __restrict__ loss_rows, const float* __restrict__ prev_slab = nullptr,
-                         int Bprev = 0, float* __restrict__ pout = nullptr, SlOpt o = SlOpt{}) {
+__device__ __forceinline__ void
+conv_step_body(const XT* __restrict__ x, const int64_t* __restrict__ idx, const int64_t* __restrict__ labels,
+               const float* __restrict__ w, const float* __restrict__ b, float scale, float* __restrict__ slab,
+               float* __restrict__ loss_rows, const float* __restrict__ prev_slab, int Bprev,
+               float* __restrict__ pout, SlOpt o, const int s) {
   constexpr int NJ = (169 + SUB - 1) / SUB;
   constexpr int NW = 32 * SUB / 64;
   __shared__ float img[28 * 28];
   __shared__ float sw[32 * 9];
   __shared__ float sb[32];
   __shared__ float red[2 * NW];
-  const int s = blockIdx.x, tid = threadIdx.x;
+  const int tid = threadIdx.x;
   const int64_t src = idx[s];
   // every load that does not depend on another goes out before anything is consumed: the
   // sample's label and pixels, and (FUSE) the previous step's B slabs and parameters —
@@ -215,7 +215,7 @@ conv_fwd_ce_wgrad_kernel(const XT* __restrict__ x, const int64_t* __restrict__ i
       if (prev_slab) {
         const float g = sum_slabs(prev_slab + p, Bprev, 320);
         sl_opt_update(o, pp, g, a0, a1);
-        if (blockIdx.x == 0) {
+        if (s == 0) {
           pout[k] = pp;
           pout[320 + k] = a0;
           pout[640 + k] = a1;
@@ -234,7 +234,7 @@ conv_fwd_ce_wgrad_kernel(const XT* __restrict__ x, const int64_t* __restrict__ i
       if (prev_slab) {
         const float g = sum_slabs(prev_slab + p, Bprev, 320);
         sl_opt_update(o, pp, g, a0, a1);
-        if (blockIdx.x == 0) {
+        if (s == 0) {
           pout[k] = pp;
           pout[320 + k] = a0;
           pout[640 + k] = a1;
@@ -301,6 +301,47 @@ conv_fwd_ce_wgrad_kernel(const XT* __restrict__ x, const int64_t* __restrict__ i
     }
   }
   slab_write<SUB>(acc, slab + (int64_t)s * 320 + oc * 10, sub);
+}
+
+template <typename XT, int SUB, bool FUSE>
+__global__ void __launch_bounds__(32 * SUB)
+conv_fwd_ce_wgrad_kernel(const XT* __restrict__ x, const int64_t* __restrict__ idx,
+                         const int64_t* __restrict__ labels, const float* __restrict__ w,
+                         const float* __restrict__ b, float scale, float* __restrict__ slab,
+                         float* __restrict__ loss_rows, const float* __restrict__ prev_slab = nullptr,
+                         int Bprev = 0, float* __restrict__ pout = nullptr, SlOpt o = SlOpt{}) {
+  conv_step_body<XT, SUB, FUSE>(x, idx, labels, w, b, scale, slab, loss_rows, prev_slab, Bprev, pout, o,
+                                (int)blockIdx.x);
+}
+
+// One SISA local step of EVERY co-located Alice in one launch: grid (B, k), workgroup (s, a)
+// runs sample s of Alice a's step with exactly conv_fwd_ce_wgrad_kernel<uint8_t, 32, true>'s
+// arithmetic (bitwise the per-Alice epochs).  The per-(step, Alice) arguments come from a
+// device table written once per epoch (row = this step's k descriptors; the index is
+// workgroup-uniform, so they are scalar loads).  At batch 16 one Alice's step is 16
+// workgroups on a 256-CU part and latency-bound; k Alices share that latency instead of
+// paying it k times.
+struct AliceStepDesc {
+  const uint8_t* x;
+  const int64_t* idx;
+  const int64_t* labels;
+  const float* pin;
+  float* slab;
+  float* loss_rows;
+  const float* prev_slab;
+  float* pout;
+  SlOpt o;
+  float scale;
+  int bs, Bprev, pad;
+};
+
+__global__ void __launch_bounds__(1024)
+conv_local_multi_kernel(const AliceStepDesc* __restrict__ row) {
+  const AliceStepDesc& d = row[blockIdx.y];
+  const int s = (int)blockIdx.x;
+  if (s >= d.bs) return;                    // this Alice's last, partial batch (uniform per workgroup)
+  conv_step_body<uint8_t, 32, true>(d.x, d.idx, d.labels, d.pin, nullptr, d.scale, d.slab, d.loss_rows,
+                                    d.prev_slab, d.Bprev, d.pout, d.o, s);
 }
 
 // Split-mode stage 1: dW/db partials of one sample from the cut-layer gradient dy.
@@ -481,6 +522,79 @@ hipError_t conv_local_epoch(const void* x, bool x_u8, const int64_t* order, int6
                                              opt(optctx, t0 + i - 1));
   return hipGetLastError();
 }
+
+// Local epochs of k co-located Alices, stepped together: step i launches ONE kernel over the
+// Alices that still have a step i (Alices sorted by descending step count, so those are a
+// prefix of the table row).  Each Alice keeps the single-Alice epoch's ping-pong param
+// buffers and slabs (in its own `ws`) and its own optimizer step counter.
+hipError_t conv_local_epoch_multi(const MultiAlice* al, int k, int B, SlOpt (*opt)(void*, int64_t), void* optctx,
+                                  void* table, int64_t table_bytes, hipStream_t st) {
+  if (k <= 0) return hipSuccess;
+  std::vector<int> ord(k);
+  int64_t nmax = 0;
+  for (int a = 0; a < k; ++a) {
+    ord[a] = a;
+    if (al[a].ws_elems < 2LL * B * 320 + 2 * 960) return hipErrorInvalidValue;
+    nmax = std::max<int64_t>(nmax, (al[a].n + B - 1) / B);
+  }
+  std::stable_sort(ord.begin(), ord.end(), [&](int p, int q) { return al[p].n > al[q].n; });
+  if (table_bytes < (int64_t)sizeof(AliceStepDesc) * nmax * k) return hipErrorInvalidValue;
+  std::vector<AliceStepDesc> host((size_t)nmax * k);
+  std::vector<int> active(nmax, 0);
+  std::vector<int> cur(k, 0), last_bs(k, 0);
+  for (int r = 0; r < k; ++r) {
+    const MultiAlice& A = al[ord[r]];
+    float* slabs[2] = {A.ws, A.ws + (int64_t)B * 320};
+    float* P[2] = {A.ws + 2LL * B * 320, A.ws + 2LL * B * 320 + 960};
+    int c = 0;
+    int64_t i = 0, prevB = 0;
+    for (int64_t s = 0; s < A.n; s += B, ++i) {
+      const int bs = (int)std::min<int64_t>(B, A.n - s);
+      AliceStepDesc& d = host[(size_t)i * k + r];
+      d.x = A.x;
+      d.idx = A.order + s;
+      d.labels = A.labels;
+      d.pin = P[c];
+      d.slab = slabs[i & 1];
+      d.loss_rows = A.loss_rows + s;
+      d.prev_slab = i ? slabs[(i - 1) & 1] : nullptr;
+      d.pout = P[1 - c];
+      d.o = i ? opt(optctx, A.t0 + i - 1) : SlOpt{};
+      d.scale = 1.f / (float)bs;
+      d.bs = bs;
+      d.Bprev = (int)prevB;
+      if (i) c = 1 - c;
+      prevB = bs;
+      active[i] = r + 1;
+    }
+    cur[ord[r]] = c;
+    last_bs[ord[r]] = (int)prevB;
+  }
+  // the table buffer is reused from epoch to epoch: wait for the stream's earlier work (a
+  // previous epoch's readers) and copy synchronously (the host table dies with this call);
+  // one sync per local phase, a phase boundary anyway
+  hipError_t e = hipStreamSynchronize(st);
+  if (e == hipSuccess) e = hipMemcpy(table, host.data(), sizeof(AliceStepDesc) * host.size(), hipMemcpyHostToDevice);
+  if (e != hipSuccess) return e;
+  for (int a = 0; a < k; ++a)
+    conv_params_pack_kernel<<<1, 320, 0, st>>>(al[a].w, al[a].b, al[a].s0w, al[a].s1w, al[a].s0b, al[a].s1b,
+                                               al[a].ws + 2LL * B * 320);
+  const AliceStepDesc* tab = static_cast<const AliceStepDesc*>(table);
+  for (int64_t i = 0; i < nmax; ++i)
+    conv_local_multi_kernel<<<dim3(B, active[i]), 1024, 0, st>>>(tab + i * k);
+  for (int a = 0; a < k; ++a) {
+    const MultiAlice& A = al[a];
+    if (A.n <= 0) continue;
+    const int64_t ns = (A.n + B - 1) / B;
+    float* slab_last = A.ws + ((ns - 1) & 1) * (int64_t)B * 320;
+    float* Pc = A.ws + 2LL * B * 320 + cur[a] * 960;
+    conv_opt_finalize_kernel<<<1, 320, 0, st>>>(slab_last, last_bs[a], Pc, A.w, A.b, A.s0w, A.s1w, A.s0b, A.s1b,
+                                               opt(optctx, A.t0 + ns - 1));
+  }
+  return hipGetLastError();
+}
+
+size_t alice_step_desc_bytes() { return sizeof(AliceStepDesc); }
 
 // Split-mode backward + optimizer.  Immediate (defer = false): partials, then the reduce +
 // update launch.  Deferred (defer = true): partials only, with `pend` (the step before,

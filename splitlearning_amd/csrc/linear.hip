@@ -417,10 +417,13 @@ hipError_t linear_dgrad(const float* dZ, int ldz, const float* W, int ldw, const
                         hipStream_t st) {
   if (M <= 0 || K <= 0) return hipSuccess;
   const int kt = (K + 63) / 64, mt = (M + 15) / 16;
-  // default: the full-N form (reduction over N inside the workgroup, masked store, one
-  // launch) whenever the batch is a training batch; variant 8 = 1 restores the split-N +
-  // reduce pair below for A/B
-  if (g_variant[8] != 1 && M <= 64 && (K & 3) == 0 && (ldw & 1) == 0 && (ldz & 3) == 0) {
+  // variant 8 = 2: the full-N form (reduction over N inside one workgroup, masked store, one
+  // launch).  Measured through the native executor it LOST to the split-N + reduce pair
+  // below at every TP shard (us per server step, TP = 1 / 2 / 4 / 8: 171.9 / 104.4 / 72.5 /
+  // 55.6 full-N vs 170.9 / 101.6 / 68.9 / 51.8 split; profiles/r2_dgrad_fulln_ab.txt): with
+  // the whole N per workgroup there are only K/32 workgroups (20 at a TP = 8 shard), each a
+  // chain of 1000-row strided reads, and the reduce launch is cheaper than that latency.
+  if (g_variant[8] == 2 && M <= 64 && (K & 3) == 0 && (ldw & 1) == 0 && (ldz & 3) == 0) {
     dim3 grid((K + 31) / 32, mt);
     dgrad_fulln_kernel<<<grid, 1024, 0, st>>>(dZ, ldz, W, ldw, hprev, ldh, scale, dX, ldx, M, N, K);
     return hipGetLastError();

@@ -124,6 +124,24 @@ class FrontEngine:
         slot.t += nsteps
         return loss
 
+    @staticmethod
+    def local_epoch_multi(fronts: list, shards: list, orders: list, B: int, slots: list):
+        """`local_epoch` of several co-located Alices at once: every step of all of them is ONE
+        launch (grid batch x Alices), bitwise the per-Alice epochs.  Falls back to one epoch
+        after another where the fused multi-Alice kernel does not apply (torch backend)."""
+        ops_ = fronts[0].ops
+        if not hasattr(ops_, "conv_local_epoch_multi_") or any(f.frozen for f in fronts) or \
+                any(sh.x.dtype != torch.uint8 for sh in shards) or len({s.cfg.kind for s in slots}) != 1:
+            return [f.local_epoch(sh, o, B, sl) for f, sh, o, sl in zip(fronts, shards, orders, slots)]
+        items = []
+        for f, sh, o, sl in zip(fronts, shards, orders, slots):
+            w, b = f.params
+            items.append((sh.x, sh.y, o, w, b, sl.state("conv.weight", w), sl.state("conv.bias", b), sl.t + 1))
+        losses = ops_.conv_local_epoch_multi_(items, B, slots[0].cfg)
+        for sl, o in zip(slots, orders):
+            sl.t += -(-int(o.numel()) // B)
+        return losses
+
     def reset_parameters(self, true_reset: bool):
         """Reference `reset_model` (data_entities_vanilla.py:204-207): reset the direct
         children that have `reset_parameters`.  For model1_sisa that is nothing (Q4) unless

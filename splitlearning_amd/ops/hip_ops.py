@@ -144,6 +144,39 @@ def conv_local_epoch_(x_u8, y_all, order, B: int, w, b, cfg, st_w, st_b, t0: int
     return loss_rows
 
 
+def conv_local_epoch_multi_(items, B: int, cfg):
+    """Local epochs of several co-located Alices stepped together: one launch per step for all
+    of them (csrc/conv.hip conv_local_epoch_multi).  items: [(x_u8, y_all, order, w, b, st_w,
+    st_b, t0)], one per Alice, each with its own parameters and optimizer state.  Returns the
+    per-sample losses of each Alice."""
+    if not items:
+        return []
+    dev = items[0][0].device
+    k = len(items)
+    per = 2 * B * 320 + 2 * 960
+    ws = _workspace(dev, k * per, "convmulti")
+    nmax = max(-(-int(it[2].numel()) // B) for it in items)
+    tb = C().alice_step_desc_bytes() * nmax * k
+    table = _TABLE.get(dev)
+    if table is None or table.numel() < tb:
+        if table is not None:
+            _WS_RETIRED.append(table)
+        table = torch.empty(max(tb, 1 << 16), device=dev, dtype=torch.uint8)
+        _TABLE[dev] = table
+    alices, losses = [], []
+    for a, (x, y_all, order, w, b, st_w, st_b, t0) in enumerate(items):
+        loss = torch.empty(int(order.numel()), device=dev, dtype=torch.float32)
+        losses.append(loss)
+        alices.append((x, order, y_all, w.detach(), b.detach(), _s0(st_w), _s1(st_w), _s0(st_b), _s1(st_b),
+                       ws[a * per:(a + 1) * per], loss, int(t0)))
+    C().conv_local_epoch_multi(alices, int(B), KIND[cfg.kind], cfg.lr, cfg.beta1, cfg.beta2, cfg.eps,
+                               cfg.weight_decay, cfg.momentum, table)
+    return losses
+
+
+_TABLE: dict = {}
+
+
 # ---------------------------------------------------------------- linear
 # eval-time inference with many rows goes through hipBLASLt (plain library GEMM)
 # plus the fused epilogue kernel; the skinny kernels cover the training batch sizes.

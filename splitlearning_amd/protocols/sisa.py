@@ -24,6 +24,7 @@ from __future__ import annotations
 import torch
 
 from ..config import ADAM_WEIGHT_DECAY, CUT_FEATURES
+from ..engine.front import FrontEngine
 from ..engine.slots import OptSlot, adam
 from ..models import ServerTailSisa, sisa_server_spec
 from .base import AliceState, Session, _progress
@@ -80,9 +81,25 @@ class SisaSession(Session):
         self.comm.barrier()
 
     def train_request_parallel(self):
+        """Reference `bob.train_request_parallel` (data_entities_vanilla_sisa.py:326-334): every
+        Alice trains at once.  Across processes they run concurrently anyway; the Alices
+        co-located on this process are stepped together (`FrontEngine.local_epoch_multi`: one
+        launch per step for all of them) instead of one epoch after another."""
         self.bob_log.info("Train all Alices in parallel")
-        for cid in sorted(self.alices):
-            self.train(cid)
+        cids = sorted(self.alices)
+        if len(cids) > 1 and getattr(self.args, "multi_alice", True):
+            als = [self.alices[c] for c in cids]
+            for a in als:
+                a.logger.info("Local Training")
+            for _ in _progress(range(self.args.epochs), self.show, desc="Epochs", ascii=" >="):
+                orders = [a.train.shuffled_order(a.gen) for a in als]
+                with self.tracer.gpu_span(f"local_epoch[alices{cids}]", samples=int(sum(o.numel() for o in orders))):
+                    FrontEngine.local_epoch_multi([a.front for a in als], [a.train for a in als], orders, self.B,
+                                                  [a.slot for a in als])
+                self.comm.progress()
+        else:
+            for cid in cids:
+                self.train(cid)
         self.comm.barrier()        # "wait for all futures"
 
     def train_request_control(self, client_id: int, omit_label: int):

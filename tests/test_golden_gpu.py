@@ -45,22 +45,40 @@ def _close_adam(a, b, lr, steps, frac=1e-3, tol=1e-4, msg=""):
     assert (d > tol).float().mean().item() < frac, (msg, (d > tol).float().mean().item(), d.max().item())
 
 
-def test_native_sisa_server_epoch_matches_torch_adam(cuda):
-    torch.backends.cuda.matmul.allow_tf32 = False
+def _gaps(loss, ref, B, steps):
+    return torch.stack([(loss[i * B:(i + 1) * B] - ref[i * B:(i + 1) * B]).abs().max() for i in range(steps)])
+
+
+@pytest.mark.parametrize("scale", [1.0, 30.0])
+def test_native_sisa_server_epoch_matches_torch_adam(cuda, scale):
+    """128 steps.  Random-label training is chaotic in fp32: any change of summation order
+    (here: the executor itself with its other fc2-dgrad form, variant 8 = 2) grows from
+    1e-6 to O(1) loss gaps over tens of steps.  The engine must match torch tightly over the
+    first steps and stay inside that rounding-noise envelope for the whole run."""
+    from splitlearning_amd.ops import hip_ops
     B, steps, lr, seed_base = 16, 128, 1e-3, 99
     g = torch.Generator().manual_seed(21)
     n = B * steps
-    acts = (torch.rand(n, 5408, generator=g) * 30).to(cuda)
+    acts = (torch.rand(n, 5408, generator=g) * scale).to(cuda)
     labels = torch.randint(0, 10, (n,), generator=g).to(cuda)
     torch.manual_seed(4)
     base = ServerTailSisa()
     ref = copy.deepcopy(base).to(cuda)
     opt = torch.optim.Adam(ref.parameters(), lr=lr, weight_decay=1e-5)
-    te = TailEngine(copy.deepcopy(base), sisa_server_spec(), cuda, seed_base=seed_base)
-    slot = OptSlot(adam(lr, 1e-5))
-    assert te.native_epoch_ok(B)
-    te.lookahead_prologue(acts[:B])
-    loss_e = te.run_native_epoch(acts, labels, slot, B, True)
+    C = hip_ops.C()
+
+    def engine(variant, tag):
+        C.set_variant(8, variant)
+        try:
+            te = TailEngine(copy.deepcopy(base), sisa_server_spec(), cuda, seed_base=seed_base, ws_tag=tag)
+            slot = OptSlot(adam(lr, 1e-5))
+            assert te.native_epoch_ok(B)
+            te.lookahead_prologue(acts[:B])
+            return te, slot, te.run_native_epoch(acts, labels, slot, B, True)
+        finally:
+            C.set_variant(8, 0)
+    te, slot, loss_e = engine(0, "")
+    alt, aslot, loss_a = engine(2, "#alt")
     losses_r = []
     for i in range(steps):
         x, y = acts[i * B:(i + 1) * B], labels[i * B:(i + 1) * B]
@@ -72,14 +90,23 @@ def test_native_sisa_server_epoch_matches_torch_adam(cuda):
     torch.cuda.synchronize()
     loss_r = torch.cat(losses_r)
     torch.testing.assert_close(loss_e[:B], loss_r[:B], rtol=1e-5, atol=1e-5)
-    torch.testing.assert_close(loss_e, loss_r, rtol=1e-3, atol=1e-3)
-    for (k, v), (_, v2) in zip(te.module.state_dict().items(), ref.state_dict().items()):
-        _close_adam(v, v2, lr, steps, msg=k)
-    # optimizer state too: first and second moments of fc1
+    torch.testing.assert_close(loss_e[:8 * B], loss_r[:8 * B], rtol=1e-3, atol=1e-3)
+    g_t, g_n = _gaps(loss_e, loss_r, B, steps), _gaps(loss_a, loss_e, B, steps)
+    assert g_t.mean().item() <= 3 * g_n.mean().item() + 1e-3, (g_t.mean().item(), g_n.mean().item())
+    sd_e, sd_a = te.module.state_dict(), alt.module.state_dict()
+    for k, v2 in ref.state_dict().items():
+        d, dn = (sd_e[k] - v2).abs(), (sd_e[k] - sd_a[k]).abs()
+        assert d.max().item() <= 2 * lr * steps + 1e-6, k
+        fd, fn = (d > 1e-4).float().mean().item(), (dn > 1e-4).float().mean().item()
+        assert fd <= 3 * fn + 1e-3, (k, fd, fn)
+    # optimizer state: fc1's first / second moments against torch's exp_avg / exp_avg_sq
     st = opt.state[ref.fc1.weight]
-    mine = slot.states["fc1.weight"]
-    torch.testing.assert_close(mine["m"], st["exp_avg"], rtol=1e-2, atol=1e-7)
-    torch.testing.assert_close(mine["v"], st["exp_avg_sq"], rtol=1e-2, atol=1e-9)
+    for mine, theirs, noise in ((slot.states["fc1.weight"]["m"], st["exp_avg"], aslot.states["fc1.weight"]["m"]),
+                                (slot.states["fc1.weight"]["v"], st["exp_avg_sq"], aslot.states["fc1.weight"]["v"])):
+        scale_t = theirs.abs().max().item() + 1e-30
+        fd = ((mine - theirs).abs() > 1e-3 * scale_t).float().mean().item()
+        fn = ((mine - noise).abs() > 1e-3 * scale_t).float().mean().item()
+        assert fd <= 3 * fn + 1e-3, (fd, fn)
 
 
 def test_vanilla_split_epoch_matches_composed_torch_sgd(cuda, tmp_path):

@@ -90,10 +90,10 @@ def test_linear_fwd(cuda, M, N, K, relu, drop):
                                     (3, 37, 52), (16, 1000, 628), (64, 1000, 5000), (40, 1000, 604),
                                     (16, 12, 8)])
 @pytest.mark.parametrize("masked", [False, True])
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0, 2])
 def test_linear_dgrad(cuda, M, N, K, masked, variant):
-    """variant 0: the full-N kernel (whole reduction in one workgroup, masked store) where it
-    applies (N % 4 == 0, M <= 64); 1: the split-N + reduce pair."""
+    """variant 0: the split-N + reduce pair (default); 2: the full-N kernel (whole reduction
+    in one workgroup, masked store) where it applies (N % 4 == 0, M <= 64)."""
     C = hip_ops.C()
     old = C.get_variant(8)
     C.set_variant(8, variant)
@@ -409,3 +409,44 @@ def test_front_deferred_update_is_bitwise_immediate(cuda, kind):
     for name in sa.states:
         for k in sa.states[name]:
             assert torch.equal(sa.states[name][k], sb.states[name][k]), (name, k)
+
+
+@pytest.mark.parametrize("kind", ["adam", "sgd"])
+def test_multi_alice_local_epoch_is_bitwise_per_alice(cuda, kind):
+    """Co-located Alices stepped together (one launch per step for all of them, Dirichlet-like
+    unequal shard sizes, partial last batches) == each Alice's own local epoch, bitwise, over
+    two epochs (the per-Alice optimizer step counters carry on)."""
+    from splitlearning_amd.data.device_dataset import DeviceShard
+    from splitlearning_amd.engine import FrontEngine, OptSlot
+    from splitlearning_amd.models import ClientFrontSisa
+    sizes = [100, 37, 64, 16, 5, 250]
+    cfg = OptimCfg("adam", 1e-3, weight_decay=1e-5) if kind == "adam" else OptimCfg("sgd", 1e-3, momentum=0.9)
+
+    def world():
+        fronts, shards, slots = [], [], []
+        for a, n in enumerate(sizes):
+            g = torch.Generator().manual_seed(100 + a)
+            x = torch.randint(0, 256, (n, 1, 28, 28), generator=g, dtype=torch.uint8)
+            y = torch.randint(0, 10, (n,), generator=g)
+            torch.manual_seed(a)
+            fronts.append(FrontEngine(ClientFrontSisa(), cuda))
+            shards.append(DeviceShard(x, y, cuda))
+            slots.append(OptSlot(cfg))
+        return fronts, shards, slots
+    fa, sa, pa = world()
+    fb, sb, pb = world()
+    for ep in range(2):
+        orders = [torch.randperm(n, generator=torch.Generator().manual_seed(7 * ep + a)).to(cuda)
+                  for a, n in enumerate(sizes)]
+        la = [f.local_epoch(s, o, 16, p) for f, s, o, p in zip(fa, sa, orders, pa)]
+        lb = FrontEngine.local_epoch_multi(fb, sb, orders, 16, pb)
+        torch.cuda.synchronize()
+        for x, y in zip(la, lb):
+            assert torch.equal(x, y)
+    for f1, f2, p1, p2 in zip(fa, fb, pa, pb):
+        for (k, v1), v2 in zip(f1.module.state_dict().items(), f2.module.state_dict().values()):
+            assert torch.equal(v1, v2), k
+        assert p1.t == p2.t
+        for name, st in p1.states.items():
+            for k, v in st.items():
+                assert torch.equal(v, p2.states[name][k]), (name, k)
