@@ -45,17 +45,28 @@ def _close_adam(a, b, lr, steps, frac=1e-3, tol=1e-4, msg=""):
     assert (d > tol).float().mean().item() < frac, (msg, (d > tol).float().mean().item(), d.max().item())
 
 
-def _gaps(loss, ref, B, steps):
-    return torch.stack([(loss[i * B:(i + 1) * B] - ref[i * B:(i + 1) * B]).abs().max() for i in range(steps)])
+def _load_adam(ref, opt, te, slot, t):
+    """torch model + Adam state := the engine's weights, moments and step count."""
+    with torch.no_grad():
+        for name, p in ref.named_parameters():
+            L = te.layers[int(name[2]) - 1]
+            p.copy_(L.W if name.endswith("weight") else L.b)
+            st = slot.states[name]
+            opt.state[p] = {"step": torch.tensor(float(t)), "exp_avg": st["m"].clone(),
+                            "exp_avg_sq": st["v"].clone()}
 
 
 @pytest.mark.parametrize("scale", [1.0, 30.0])
-def test_native_sisa_server_epoch_matches_torch_adam(cuda, scale):
-    """128 steps.  Random-label training is chaotic in fp32: any change of summation order
-    (here: the executor itself with its other fc2-dgrad form, variant 8 = 2) grows from
-    1e-6 to O(1) loss gaps over tens of steps.  The engine must match torch tightly over the
-    first steps and stay inside that rounding-noise envelope for the whole run."""
-    from splitlearning_amd.ops import hip_ops
+def test_sisa_server_epoch_matches_torch_adam_every_step(cuda, scale):
+    """The production SISA server epoch (fused fwd/dgrad kernels, fc1 look-ahead inside the
+    wgrad+Adam kernel), 128 steps, checked against `torch.optim.Adam(lr, weight_decay=1e-5)`
+    on `model2_sisa` at EVERY step: before step i torch is given the engine's weights, Adam
+    moments and step count, takes step i on the same batch with the same dropout masks, and
+    both post-step states and the step's losses must agree.  (Free-running fp32 trajectories of
+    this random-label training are chaotic — any summation-order change grows to O(1) loss
+    gaps within ~30 steps, measured — so per-step re-synchronisation is what makes a tight
+    128-step comparison possible.)  The run is also the native executor's: its free-running
+    128-step result must be bitwise the per-step Python path's."""
     B, steps, lr, seed_base = 16, 128, 1e-3, 99
     g = torch.Generator().manual_seed(21)
     n = B * steps
@@ -63,53 +74,65 @@ def test_native_sisa_server_epoch_matches_torch_adam(cuda, scale):
     labels = torch.randint(0, 10, (n,), generator=g).to(cuda)
     torch.manual_seed(4)
     base = ServerTailSisa()
+    # the native executor, free-running
+    nat = TailEngine(copy.deepcopy(base), sisa_server_spec(), cuda, seed_base=seed_base, ws_tag="#nat")
+    nslot = OptSlot(adam(lr, 1e-5))
+    nat.lookahead_prologue(acts[:B])
+    loss_nat = nat.run_native_epoch(acts, labels, nslot, B, True)
+    # the same kernels step by step, with torch re-synchronised before every step
+    te = TailEngine(copy.deepcopy(base), sisa_server_spec(), cuda, seed_base=seed_base)
+    slot = OptSlot(adam(lr, 1e-5))
+    for L in te.layers:
+        slot.state(f"{L.spec.name}.weight", L.W)
+        slot.state(f"{L.spec.name}.bias", L.b)
     ref = copy.deepcopy(base).to(cuda)
     opt = torch.optim.Adam(ref.parameters(), lr=lr, weight_decay=1e-5)
-    C = hip_ops.C()
-
-    def engine(variant, tag):
-        C.set_variant(8, variant)
-        try:
-            te = TailEngine(copy.deepcopy(base), sisa_server_spec(), cuda, seed_base=seed_base, ws_tag=tag)
-            slot = OptSlot(adam(lr, 1e-5))
-            assert te.native_epoch_ok(B)
-            te.lookahead_prologue(acts[:B])
-            return te, slot, te.run_native_epoch(acts, labels, slot, B, True)
-        finally:
-            C.set_variant(8, 0)
-    te, slot, loss_e = engine(0, "")
-    alt, aslot, loss_a = engine(2, "#alt")
-    losses_r = []
+    te.lookahead_prologue(acts[:B])
+    pre = True
+    worst = {}
+    losses = []
     for i in range(steps):
         x, y = acts[i * B:(i + 1) * B], labels[i * B:(i + 1) * B]
+        _load_adam(ref, opt, te, slot, i)
         opt.zero_grad()
-        loss = F.cross_entropy(_ref_tail_forward(ref, x, seed_base, i + 1), y, reduction="none")
-        loss.mean().backward()
+        loss_r = F.cross_entropy(_ref_tail_forward(ref, x, seed_base, i + 1), y, reduction="none")
+        loss_r.mean().backward()
         opt.step()
-        losses_r.append(loss.detach())
+        nxt = acts[(i + 1) * B:(i + 2) * B] if i + 1 < steps else None
+        loss_e, _ = te.train_fwd_bwd3(x, y, need_dx=False, pre=pre)
+        te.fused_step(slot, x_next=nxt)
+        pre = nxt is not None
+        losses.append(loss_e)
+        torch.testing.assert_close(loss_e, loss_r.detach(), rtol=2e-4, atol=1e-4)
+        for name, p in ref.named_parameters():
+            L = te.layers[int(name[2]) - 1]
+            e = L.W if name.endswith("weight") else L.b
+            d = (e - p.detach()).abs()
+            # one Adam step from the same state: rounding-level differences, except elements
+            # whose gradient is ~0, where the sign of m / sqrt(v) is rounding noise (<= 2 lr)
+            assert d.max().item() <= 2 * lr + 1e-6, (i, name, d.max().item())
+            frac = (d > 1e-6).float().mean().item()
+            worst[name] = max(worst.get(name, 0.0), frac)
+            assert frac < 1e-4, (i, name, frac)
+            st, mine = opt.state[p], slot.states[name]
+            # the moments carry the gradient's own rounding (fp32 sums over 16 rows in another
+            # order than hipBLASLt's): absolute tolerance relative to the tensor's scale
+            for k, tk in (("m", "exp_avg"), ("v", "exp_avg_sq")):
+                ref_k = st[tk]
+                torch.testing.assert_close(mine[k], ref_k, rtol=1e-3, atol=1e-5 * ref_k.abs().max().item() + 1e-30,
+                                           msg=f"step {i} {name} {k}")
     torch.cuda.synchronize()
-    loss_r = torch.cat(losses_r)
-    torch.testing.assert_close(loss_e[:B], loss_r[:B], rtol=1e-5, atol=1e-5)
-    torch.testing.assert_close(loss_e[:8 * B], loss_r[:8 * B], rtol=1e-3, atol=1e-3)
-    g_t, g_n = _gaps(loss_e, loss_r, B, steps), _gaps(loss_a, loss_e, B, steps)
-    assert g_t.mean().item() <= 3 * g_n.mean().item() + 1e-3, (g_t.mean().item(), g_n.mean().item())
-    sd_e, sd_a = te.module.state_dict(), alt.module.state_dict()
-    for k, v2 in ref.state_dict().items():
-        d, dn = (sd_e[k] - v2).abs(), (sd_e[k] - sd_a[k]).abs()
-        assert d.max().item() <= 2 * lr * steps + 1e-6, k
-        fd, fn = (d > 1e-4).float().mean().item(), (dn > 1e-4).float().mean().item()
-        assert fd <= 3 * fn + 1e-3, (k, fd, fn)
-    # optimizer state: fc1's first / second moments against torch's exp_avg / exp_avg_sq
-    st = opt.state[ref.fc1.weight]
-    for mine, theirs, noise in ((slot.states["fc1.weight"]["m"], st["exp_avg"], aslot.states["fc1.weight"]["m"]),
-                                (slot.states["fc1.weight"]["v"], st["exp_avg_sq"], aslot.states["fc1.weight"]["v"])):
-        scale_t = theirs.abs().max().item() + 1e-30
-        fd = ((mine - theirs).abs() > 1e-3 * scale_t).float().mean().item()
-        fn = ((mine - noise).abs() > 1e-3 * scale_t).float().mean().item()
-        assert fd <= 3 * fn + 1e-3, (fd, fn)
+    assert torch.equal(torch.cat(losses), loss_nat)
+    for L1, L2 in zip(te.layers, nat.layers):
+        assert torch.equal(L1.W, L2.W) and torch.equal(L1.b, L2.b)
+    assert (te.fwd_count, slot.t) == (nat.fwd_count, nslot.t) == (steps, steps)
 
 
 def test_vanilla_split_epoch_matches_composed_torch_sgd(cuda, tmp_path):
+    """The vanilla split epoch (`split_epoch`: packed act+labels, Bob's fused step, Alice's
+    deferred in-kernel update + flush) against composed `model1_sisa` + `model2_sisa` with two
+    `torch.optim.SGD(lr, momentum=0.9)`, re-synchronised before every batch (weights and
+    momentum buffers of both sides copied from the engine), 40 batches + a partial one."""
     from splitlearning_amd.config import parse_args
     from splitlearning_amd.data.mnist import write_shards
     from splitlearning_amd.parallel.dist import Comm, Placement
@@ -119,7 +142,6 @@ def test_vanilla_split_epoch_matches_composed_torch_sgd(cuda, tmp_path):
     write_shards(args, verbose=False)
     sess = VanillaSession(args, Comm(0, 1, cuda, Placement.make(2, 1, 1)), cuda)
     a = sess.alices[1]
-    assert sess.tail.lookahead_ok(16)
     front_r = copy.deepcopy(a.front.module).to(cuda)
     tail_r = copy.deepcopy(sess.tail.module).to(cuda)
     lr = args.lr
@@ -127,21 +149,36 @@ def test_vanilla_split_epoch_matches_composed_torch_sgd(cuda, tmp_path):
     opt_b = torch.optim.SGD(tail_r.parameters(), lr=lr, momentum=0.9)
     order = a.train.shuffled_order(torch.Generator().manual_seed(9))[:16 * 40 + 6]   # partial last batch
     n = order.numel()
-    fc0 = sess.tail.fwd_count
-    sess.split_epoch(1, order, n)
+    bslot = sess.bob_slot(1)
+
+    def sync_torch():
+        with torch.no_grad():
+            for (name, p), (_, e) in zip(front_r.named_parameters(), a.front.module.named_parameters()):
+                p.copy_(e)
+                st = a.slot.states.get("conv." + name.split(".")[-1])
+                opt_a.state[p] = {"momentum_buffer": st["buf"].clone().view_as(p)} if st else {}
+            for name, p in tail_r.named_parameters():
+                L = sess.tail.layers[int(name[2]) - 1]
+                p.copy_(L.W if name.endswith("weight") else L.b)
+                st = bslot.states.get(name)
+                opt_b.state[p] = {"momentum_buffer": st["buf"].clone()} if st else {}
     for i, s in enumerate(range(0, n, 16)):
         idx = order[s:s + 16]
+        sync_torch()
         opt_a.zero_grad()
         opt_b.zero_grad()
-        out = _ref_tail_forward(tail_r, front_r(a.train.x_float(idx)), sess.tail.seed_base, fc0 + i + 1)
+        step = sess.tail.fwd_count + 1
+        out = _ref_tail_forward(tail_r, front_r(a.train.x_float(idx)), sess.tail.seed_base, step)
         F.cross_entropy(out, a.train.y[idx]).backward()
         opt_a.step()
         opt_b.step()
+        sess.split_epoch(1, idx, idx.numel())         # one batch of the production split epoch
+        for name, p in tail_r.named_parameters():
+            L = sess.tail.layers[int(name[2]) - 1]
+            e = L.W if name.endswith("weight") else L.b
+            torch.testing.assert_close(e, p.detach(), rtol=1e-4, atol=1e-6, msg=f"batch {i} {name}")
+        for (name, p), (_, e) in zip(front_r.named_parameters(), a.front.module.named_parameters()):
+            # raw 0..255 pixels: conv gradients are O(1e3), summed over 16 x 676 positions
+            torch.testing.assert_close(e, p.detach(), rtol=1e-4, atol=1e-4, msg=f"batch {i} {name}")
     torch.cuda.synchronize()
-    steps = -(-n // 16)
-    for (k, v), (_, v2) in zip(sess.tail.module.state_dict().items(), tail_r.state_dict().items()):
-        # SGD-momentum: no normalisation, differences stay at rounding level
-        torch.testing.assert_close(v, v2, rtol=1e-3, atol=1e-4, msg=k)
-    for (k, v), (_, v2) in zip(a.front.module.state_dict().items(), front_r.state_dict().items()):
-        torch.testing.assert_close(v, v2, rtol=1e-3, atol=1e-3, msg=k)
-    assert steps == 41
+    assert bslot.t == -(-n // 16)

@@ -15,7 +15,6 @@ import torch
 
 from splitlearning_amd.engine import OptSlot, TailEngine, adam
 from splitlearning_amd.models import ServerTailSisa, sisa_server_spec
-from splitlearning_amd.ops import hip_ops
 
 pytestmark = pytest.mark.gpu
 
@@ -36,64 +35,68 @@ def _full(shards):
     return [(W1, b1), (W2, L[0][1].b), (L[0][2].W, L[0][2].b)]
 
 
-def _gaps(loss, ref, B, steps):
-    return torch.stack([(loss[i * B:(i + 1) * B] - ref[i * B:(i + 1) * B]).abs().max() for i in range(steps)])
+def _sync_shards(ref, rslot, shards, slots):
+    """Every shard := its slice of the TP = 1 reference's weights, biases and optimizer moments."""
+    from splitlearning_amd.engine.tail import _shard_range
+    with torch.no_grad():
+        for sh, sl in zip(shards, slots):
+            for Lr, L in zip(ref.layers, sh.layers):
+                for kind, full, mine in (("weight", Lr.W, L.W), ("bias", Lr.b, L.b)):
+                    name = f"{Lr.spec.name}.{kind}"
+                    pairs = [(full, mine)] + [(rslot.states[name][k], sl.state(name, mine)[k])
+                                              for k in rslot.states[name]]
+                    for src, dst in pairs:
+                        if L.style == "col":
+                            s, e = _shard_range(full.shape[0], sh.tp_rank, sh.tp_size)
+                            src = src[s:e]
+                        elif L.style == "row" and kind == "weight":
+                            s, e = _shard_range(full.shape[1], sh.tp_rank, sh.tp_size)
+                            src = src[:, s:e]
+                        dst.copy_(src)
 
 
 @pytest.mark.parametrize("T", [2, 4, 8])
 @pytest.mark.parametrize("scale", [1.0, 30.0])
 def test_tp_emulated_native_epoch_matches_single_shard(cuda, T, scale):
-    """72 Adam steps.  Training with random labels is chaotic: ANY change of fp32 summation
-    order (e.g. the TP = 1 executor with its other fc2-dgrad form, variant 8 = 2) grows from
-    1e-6 to O(1) loss gaps over tens of steps.  So the TP = T run must (a) agree tightly on
-    the early steps, where a shard-math bug would already show as O(1) gaps, and (b) stay
-    within the rounding-noise envelope of that TP = 1 alternative over the whole run."""
-    B = 16
-    steps = 72
-    n = B * steps
-    acts, labels = _data(cuda, n)
+    """72 Adam steps of the native executor at TP = T (emulated) against TP = 1, as 36 two-step
+    epochs (look-ahead prologue, the wgrad kernel's look-ahead for the second batch, its
+    consumption) each started from the same state: the shards are re-synchronised to the
+    TP = 1 run before every pair.  Free-running fp32 trajectories of this random-label
+    training are chaotic (any summation-order change grows to O(1) loss gaps within tens of
+    steps), so re-synchronisation is what keeps a tight per-step comparison meaningful."""
+    B, pairs, lr = 16, 36, 1e-3
+    acts, labels = _data(cuda, 2 * B * pairs)
     acts = acts * (scale / 30.0)
     torch.manual_seed(0)
     base = ServerTailSisa()
-    lr = 1e-3
-    C = hip_ops.C()
-
-    def tp1(variant, tag):
-        C.set_variant(8, variant)
-        try:
-            t = TailEngine(copy.deepcopy(base), sisa_server_spec(), cuda, seed_base=777, ws_tag=tag)
-            s = OptSlot(adam(lr, 1e-5))
-            t.lookahead_prologue(acts[:B])
-            return t, s, t.run_native_epoch(acts, labels, s, B, True)
-        finally:
-            C.set_variant(8, 0)
-    ref, rslot, loss_ref = tp1(0, "")
-    alt, _, loss_alt = tp1(2, "#alt")
-
+    ref = TailEngine(copy.deepcopy(base), sisa_server_spec(), cuda, seed_base=777)
+    rslot = OptSlot(adam(lr, 1e-5))
+    for L in ref.layers:
+        rslot.state(f"{L.spec.name}.weight", L.W)
+        rslot.state(f"{L.spec.name}.bias", L.b)
     shards = [TailEngine(copy.deepcopy(base), sisa_server_spec(), cuda, tp_rank=r, tp_size=T, allreduce=None,
                          seed_base=777, ws_tag=f"#emu{T}.{r}") for r in range(T)]
     slots = [OptSlot(adam(lr, 1e-5)) for _ in range(T)]
     assert shards[0].layers[0].style == "col" and shards[0].layers[1].style == "row"
-    loss = TailEngine.emulate_tp_epoch(shards, slots, acts, labels, B)
-    torch.cuda.synchronize()
-
-    assert (shards[0].fwd_count, slots[0].t) == (ref.fwd_count, rslot.t) == (steps, steps)
-    # (a) early steps: identical weights at step 1, rounding-level gaps for the next ones
-    torch.testing.assert_close(loss[:B], loss_ref[:B], rtol=1e-5, atol=1e-5)
-    torch.testing.assert_close(loss[:8 * B], loss_ref[:8 * B], rtol=1e-3, atol=1e-3)
-    # (b) the whole run inside the TP = 1 rounding-noise envelope
-    g_tp, g_alt = _gaps(loss, loss_ref, B, steps), _gaps(loss_alt, loss_ref, B, steps)
-    assert g_tp.mean().item() <= 3 * g_alt.mean().item() + 1e-3, (g_tp.mean().item(), g_alt.mean().item())
-    # fc3 is replicated: every shard holds bitwise the same copy (same all-reduced inputs)
-    for sh in shards[1:]:
-        assert torch.equal(sh.layers[2].W, shards[0].layers[2].W)
-    for (Wa, ba), Lr, La in zip(_full(shards), ref.layers, alt.layers):
-        for a, b, c in ((Wa, Lr.W, La.W), (ba, Lr.b, La.b)):
-            assert a.shape == b.shape
-            d, dn = (a - b).abs(), (c - b).abs()
-            assert d.max().item() <= 2 * lr * steps + 1e-6
-            fd, fn = (d > 1e-4).float().mean().item(), (dn > 1e-4).float().mean().item()
-            assert fd <= 3 * fn + 1e-3, (fd, fn)
+    for j in range(pairs):
+        _sync_shards(ref, rslot, shards, slots)
+        a, y = acts[2 * j * B:(2 * j + 2) * B], labels[2 * j * B:(2 * j + 2) * B]
+        ref.lookahead_prologue(a[:B])
+        loss_ref = ref.run_native_epoch(a, y, rslot, B, True)
+        loss = TailEngine.emulate_tp_epoch(shards, slots, a, y, B)
+        torch.cuda.synchronize()
+        assert (shards[0].fwd_count, slots[0].t) == (ref.fwd_count, rslot.t) == (2 * j + 2, 2 * j + 2)
+        torch.testing.assert_close(loss, loss_ref, rtol=1e-4, atol=1e-4)
+        # fc3 is replicated: every shard holds bitwise the same copy (same all-reduced inputs)
+        for sh in shards[1:]:
+            assert torch.equal(sh.layers[2].W, shards[0].layers[2].W)
+        for (Wa, ba), Lr in zip(_full(shards), ref.layers):
+            for a_, b_ in ((Wa, Lr.W), (ba, Lr.b)):
+                d = (a_ - b_).abs()
+                # two Adam steps from one state: rounding level, except elements whose
+                # gradient is ~0 (sign of m / sqrt(v) is rounding noise: <= 2 lr per step)
+                assert d.max().item() <= 4 * lr + 1e-6, (j, d.max().item())
+                assert (d > 1e-6).float().mean().item() < 1e-4, (j, (d > 1e-6).float().mean().item())
 
 
 def test_tp_emulation_shard_equals_tp1_when_T_is_1(cuda):
