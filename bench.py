@@ -140,12 +140,11 @@ def main(argv=None):
         "--world_size", str(ws), "--epochs", str(a.epochs), "--iterations", str(a.iterations),
         "--batch_size", str(a.batch_size), "--partition_alpha", str(a.partition_alpha),
         "--server_epochs", str(a.server_epochs), "--seed", str(a.seed), "--num_samples", str(a.num_samples),
-        "--kernels", a.kernels, "--graphs", a.graphs, "--act_dtype", a.act_dtype, "--no_tqdm",
+        "--kernels", a.kernels, "--graphs", a.graphs, "--act_dtype", a.act_dtype, "--dtype", a.dtype, "--no_tqdm",
         "--log_dir", log_dir, "--watchdog", "off"]
     if a.mode == "concat" and a.concat_unlearn:
         argv_s.append("--concat_unlearn")
     sargs = parse_args(argv_s)
-    sargs.dtype = a.dtype
     pl = Placement.make(ws, N, a.bob_tp if a.bob_tp > 0 else N)
     comm = Comm(rank, N, dev, pl, make_tp_group(pl, "nccl" if use_gpu else "gloo") if N > 1 else None)
     k = ws - 1

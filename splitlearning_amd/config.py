@@ -62,6 +62,11 @@ def build_parser() -> argparse.ArgumentParser:
                    help="wire dtype of every cut-layer activation transfer (per-batch vanilla / U-shape "
                         "messages, eval, SISA's dump and cache); compute stays fp32; bf16 halves the "
                         "traffic, rounding the activations")
+    g.add_argument("--dtype", choices=("fp32", "bf16"), default="fp32",
+                   help="compute dtype of the GEMM-shaped ops (forward, data and weight gradients): "
+                        "fp32 = exact fp32 MFMA (the reference's precision); bf16 = operands rounded to "
+                        "bf16, fp32 accumulation (BASELINE config 2); master weights and optimizer "
+                        "state stay fp32")
     g.add_argument("--kernels", choices=("auto", "hip", "torch"), default="auto",
                    help="compute path: hand-written HIP kernels (GPU) or torch ops")
     g.add_argument("--seed", type=int, default=None, help="seed everything (reference is unseeded)")

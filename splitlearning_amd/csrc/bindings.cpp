@@ -707,5 +707,13 @@ PYBIND11_MODULE(_C, m) {
     sl::g_variant[slot] = (int)v;
   });
   m.def("get_variant", [](int64_t slot) { return (int64_t)sl::g_variant[slot]; });
+  // compute dtype of the GEMM-shaped kernels (forward / data-gradient products): fp32 (exact
+  // v_mfma_f32_*_f32) or bf16 (operands rounded to bf16, bf16 MFMA, fp32 accumulation);
+  // parameters, optimizer state and the fused optimizer update stay fp32 either way
+  m.def("set_compute_dtype", [](const std::string& d) {
+    TORCH_CHECK(d == "fp32" || d == "bf16", "compute dtype fp32 | bf16");
+    sl::g_bf16 = d == "bf16" ? 1 : 0;
+  });
+  m.def("get_compute_dtype", []() { return std::string(sl::g_bf16 ? "bf16" : "fp32"); });
   m.attr("arch") = "gfx950";
 }

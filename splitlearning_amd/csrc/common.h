@@ -25,6 +25,15 @@ __device__ __forceinline__ bool sl_hash_keep(uint32_t seed_lo, uint32_t seed_hi,
   return h >= thresh;
 }
 
+// ------------------------------------------------------------------ bf16 compute
+// `--dtype bf16`: a GEMM operand rounded to bf16 (RNE; v_cvt_pk_bf16_f32) and back.  The
+// product of two such values is exact in fp32, so rounding the operands and accumulating in
+// fp32 has the numerics of a bf16 MFMA with fp32 accumulation (up to summation order); the
+// memory-bound skinny kernels use this form, the compute-bound ones the bf16 MFMA itself.
+__device__ __forceinline__ float bfr(float x) { return (float)(__bf16)x; }
+__device__ __forceinline__ f32x4 bfr4(f32x4 v) { return f32x4{bfr(v[0]), bfr(v[1]), bfr(v[2]), bfr(v[3])}; }
+__device__ __forceinline__ float4 bfr4(float4 v) { return make_float4(bfr(v.x), bfr(v.y), bfr(v.z), bfr(v.w)); }
+
 // ------------------------------------------------------------------ reductions
 __device__ __forceinline__ float sl_wave_sum(float v) {
 #pragma unroll
@@ -151,6 +160,7 @@ __device__ __forceinline__ void sl_opt_update4(const SlOpt& o, f32x4& p, f32x4 g
 // _C.set_variant; 0 = the shipped default everywhere).
 namespace sl {
 extern int g_variant[16];
+extern int g_bf16;      // compute dtype of the GEMM-shaped kernels: 0 = exact fp32, 1 = bf16 operands
 }
 
 #define SL_CHECK_LAUNCH() (hipGetLastError())

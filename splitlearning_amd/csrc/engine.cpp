@@ -104,7 +104,7 @@ class ServerEpoch {
     emulate_ = cfg.contains("emulate_tp") && cfg["emulate_tp"].cast<bool>();
     TORCH_CHECK(!row2_ || comm_ != nullptr || emulate_, "a row-parallel fc2 needs the native communicator");
     B_ = cfg["B"].cast<int>();
-    TORCH_CHECK(B_ >= 1 && B_ <= 16, "batch 1..16 (look-ahead slabs, head kernels)");
+    TORCH_CHECK(B_ >= 1 && B_ <= 64, "batch 1..64 (look-ahead row chunks of the wgrad kernel)");
     pn_ = get(cfg, "pn");
     p2ws_ = get(cfg, "p2ws");
     fwdws_ = get(cfg, "fwdws");

@@ -31,7 +31,7 @@ struct WgGroup {
   // Optional look-ahead forward of layer 0 with its *updated* weights:
   //   pn[kb][m][n] = sum_{k in k-block kb} xn[m, k] * W0_new[n, k]   (kb = 256-column blocks)
   // i.e. the next batch's split-K partial pre-activations, written while W0 is in registers.
-  const float* xn;      // [mn, K0] next batch input (mn <= 16), or nullptr
+  const float* xn;      // [mn, K0] next batch input (mn <= 64), or nullptr
   int ldxn;
   int mn;
   float* pn;            // [ceil(K0/256)][mn][N0]
@@ -40,6 +40,7 @@ struct WgGroup {
   int grid2d;           // 2-D grid (set by wgrad_group: when few of its workgroups are empty)
   int wt;               // write-through (sc1) W/m/v stores (set by wgrad_group)
   int swz;              // look-ahead LDS tile layout: 0 padded, 1 plain, 2 XOR (set by wgrad_group)
+  int bf16;             // bf16 compute: dZ / A / look-ahead operands rounded to bf16 (set by wgrad_group)
 };
 
 int head3_slices(int N2);

@@ -44,7 +44,7 @@ __device__ __forceinline__ void head_slice(int n4, int Q, int q, int& a, int& b)
 // phase): at B = 16 this op is pure latency.
 __global__ void __launch_bounds__(256)
 head_fwd_kernel(const float* __restrict__ P2, int S2, int64_t slab2, Epi e2, const float* __restrict__ W3,
-                int ldw3, float* __restrict__ h2, float* __restrict__ plog, int M, int N2, int C) {
+                int ldw3, float* __restrict__ h2, float* __restrict__ plog, int M, int N2, int C, int bf) {
   __shared__ f32x4 part[8][HS];
   __shared__ f32x4 hs[HS];
   const int m = blockIdx.x, q = blockIdx.y, Q = gridDim.y, tid = threadIdx.x;
@@ -93,13 +93,14 @@ head_fwd_kernel(const float* __restrict__ P2, int S2, int64_t slab2, Epi e2, con
   __syncthreads();
   // 2. partial logits: half-waves (32 lanes = the slice's columns) per output, 8 outputs
   //    per wave instruction group; JU outputs' loads in flight per lane
-  const f32x4 h = hs[c];
+  const f32x4 h = bf ? bfr4(hs[c]) : hs[c];
   for (int j0 = 0; j0 * 8 < C; j0 += JU) {
     if (j0) load_w(j0);
 #pragma unroll
     for (int j = 0; j < JU; ++j) {
       const int o = 8 * (j0 + j) + 2 * wv + half;
-      float d = w[j][0] * h[0] + w[j][1] * h[1] + w[j][2] * h[2] + w[j][3] * h[3];
+      const f32x4 wj = bf ? bfr4(w[j]) : w[j];
+      float d = wj[0] * h[0] + wj[1] * h[1] + wj[2] * h[2] + wj[3] * h[3];
 #pragma unroll
       for (int off = 16; off > 0; off >>= 1) d += __shfl_xor(d, off);
       if (c == 0 && o < C) plog[((int64_t)q * M + m) * C + o] = d;
@@ -113,7 +114,7 @@ __global__ void __launch_bounds__(256)
 head_bwd_kernel(const float* __restrict__ plog, const float* __restrict__ b3, const float* __restrict__ W3,
                 int ldw3, const int64_t* __restrict__ y, int64_t ignore, float scale, float dscale,
                 const float* __restrict__ h2, float* __restrict__ dlog, float* __restrict__ dz2,
-                float* __restrict__ loss_rows, int M, int N2, int C) {
+                float* __restrict__ loss_rows, int M, int N2, int C, int bf) {
   extern __shared__ float lg[];   // C
   __shared__ f32x4 part[8][HS];
   const int m = blockIdx.x, q = blockIdx.y, Q = gridDim.y, tid = threadIdx.x;
@@ -173,7 +174,8 @@ head_bwd_kernel(const float* __restrict__ plog, const float* __restrict__ b3, co
 #pragma unroll
     for (int j = 0; j < JU; ++j) {
       const int o = 8 * (j0 + j) + g;
-      acc += (o < C ? lg[o] : 0.f) * w[j];
+      const float l = o < C ? lg[o] : 0.f;
+      acc += bf ? bfr(l) * bfr4(w[j]) : l * w[j];
     }
   }
   part[g][c] = acc;
@@ -237,9 +239,11 @@ __device__ __forceinline__ void st_wt(float* base, int N, int ld, int boff, f32x
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), rs, boff, 0, 16);
 }
 
-template <bool ADAM, bool FWDN, bool PART>
+template <bool ADAM, int FWDC, bool PART>
 __global__ void __launch_bounds__(1024)
 wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
+  // FWDC: look-ahead row chunks of 16 (0 = no look-ahead; 1: next batch <= 16 rows; 4: <= 64)
+  constexpr bool FWDN = FWDC > 0;
   __shared__ f32x4 sa[16][64];
   __shared__ float sdz[16][16];
   // look-ahead: the updated W tile, rows padded to 65 float4 (variant 1 = 1: plain 64-float4
@@ -273,15 +277,21 @@ wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
   // look-ahead A operand in MFMA layout: lane (li, lq) holds x_next[li][kb + 16*wave + 4*lq .. +3]
   const int li = lane & 15, lq = lane >> 4;
   const int kx = kb + 16 * r + 4 * lq;
-  f32x4 xv = zv;
-  if (FWDN && l0 && li < grp.mn && kx < L.K) xv = *reinterpret_cast<const f32x4*>(grp.xn + (int64_t)li * grp.ldxn + kx);
+  f32x4 xv[FWDC > 0 ? FWDC : 1];
+#pragma unroll
+  for (int c = 0; c < (FWDC > 0 ? FWDC : 1); ++c) {
+    xv[c] = zv;
+    if (FWDN && l0 && 16 * c + li < grp.mn && kx < L.K)
+      xv[c] = *reinterpret_cast<const f32x4*>(grp.xn + (int64_t)(16 * c + li) * grp.ldxn + kx);
+  }
   f32x4 g = zv;
   float gb = 0.f;
   for (int mc = 0; mc < M; mc += 16) {
     if (mc) __syncthreads();
     {
       const int mm = mc + r;
-      sa[r][lane] = (mm < M && k < L.K) ? *reinterpret_cast<const f32x4*>(L.A + (int64_t)mm * L.lda + k) : zv;
+      const f32x4 av = (mm < M && k < L.K) ? *reinterpret_cast<const f32x4*>(L.A + (int64_t)mm * L.lda + k) : zv;
+      sa[r][lane] = grp.bf16 ? bfr4(av) : av;
       if (tid < 256) {
         const int mr = mc + (tid >> 4), nn = n0 + (tid & 15);
         float v = 0.f;
@@ -296,7 +306,7 @@ wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
             v = L.dz[(int64_t)mr * L.ldz + nn];
           }
         }
-        sdz[tid >> 4][tid & 15] = v;
+        sdz[tid >> 4][tid & 15] = grp.bf16 ? bfr(v) : v;
       }
     }
     __syncthreads();
@@ -330,18 +340,26 @@ wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
     const int rs = grp.swz == 0 ? 65 : 64;
     sw[r * rs + wcol] = act ? p : zv;
     __syncthreads();
-    const f32x4 wv4 = sw[li * rs + rcol];
-    f32x4 z = zv;
+    f32x4 wv4 = sw[li * rs + rcol];
+    if (grp.bf16) wv4 = bfr4(wv4);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) z = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[i], wv4[i], z, 0, 0, 0);
-    red[r][lane] = z;                     // z[j] = partial(m = 4*lq + j, n = n0 + li)
-    __syncthreads();
-    if (tid < 256) {
-      const int m = tid >> 4, nn = tid & 15;
-      float v = 0.f;
+    for (int c = 0; c < FWDC; ++c) {
+      if (16 * c >= grp.mn) break;        // uniform
+      f32x4 z = zv;
+      const f32x4 xc = grp.bf16 ? bfr4(xv[c]) : xv[c];
 #pragma unroll
-      for (int w = 0; w < 16; ++w) v += red[w][16 * (m >> 2) + nn][m & 3];
-      if (m < grp.mn && n0 + nn < L.N) grp.pn[((int64_t)bx * grp.mn + m) * L.N + n0 + nn] = v;
+      for (int i = 0; i < 4; ++i) z = __builtin_amdgcn_mfma_f32_16x16x4f32(xc[i], wv4[i], z, 0, 0, 0);
+      if (c) __syncthreads();             // the previous chunk's readers are done with red
+      red[r][lane] = z;                   // z[j] = partial(m = 16c + 4*lq + j, n = n0 + li)
+      __syncthreads();
+      if (tid < 256) {
+        const int m = 16 * c + (tid >> 4), nn = tid & 15;
+        const int mm = tid >> 4;
+        float v = 0.f;
+#pragma unroll
+        for (int w = 0; w < 16; ++w) v += red[w][16 * (mm >> 2) + nn][mm & 3];
+        if (m < grp.mn && n0 + nn < L.N) grp.pn[((int64_t)bx * grp.mn + m) * L.N + n0 + nn] = v;
+      }
     }
   }
   if (L.bias && bx == 0 && lane == 0 && n < L.N) {
@@ -461,9 +479,9 @@ hipError_t server_head3(const float* P2, int S2, int64_t slab2, Epi e2, const fl
   if ((N2 & 3) || (ldw3 & 3)) return hipErrorInvalidValue;
   const int Q = head3_slices(N2);
   if (ws_elems < (int64_t)Q * M * C) return hipErrorInvalidValue;
-  head_fwd_kernel<<<dim3(M, Q), 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C);
+  head_fwd_kernel<<<dim3(M, Q), 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C, g_bf16);
   head_bwd_kernel<<<dim3(M, Q), 256, (size_t)C * sizeof(float), st>>>(ws, b3, W3, ldw3, y, ignore, scale, e2.dscale,
-                                                                      h2, dlog, dz2, loss_rows, M, N2, C);
+                                                                      h2, dlog, dz2, loss_rows, M, N2, C, g_bf16);
   return hipGetLastError();
 }
 
@@ -481,6 +499,7 @@ static void set_traversal(WgGroup& gg) {
   gg.rev0 = v7 == 1 ? 0 : (v7 == 2 ? 1 : (int)(flip++ & 1u));
   gg.wt = g_variant[4] == 1 ? 0 : 1;
   gg.swz = g_variant[1];
+  gg.bf16 = g_bf16;
   for (int i = 0; i < gg.n; ++i)
     if ((int64_t)gg.d[i].N * gg.d[i].ldw * 4 > 2147483647LL) gg.wt = 0;
 }
@@ -500,8 +519,10 @@ hipError_t wgrad_group(const WgGroup& g, int M, SlOpt o, hipStream_t st) {
   gg.nt0 = ((gg.d[0].N + 15) / 16) * ((gg.d[0].K + 255) / 256);
   dim3 grid((kmax + 255) / 256, yb);     // 2-D grid of the all-MFMA variant
   const dim3 grid1(wb);                  // 1-D grid over the real tiles (default kernel)
-  if (gg.xn && (gg.mn <= 0 || gg.mn > 16 || !gg.pn)) return hipErrorInvalidValue;
+  if (gg.xn && (gg.mn <= 0 || gg.mn > 64 || !gg.pn)) return hipErrorInvalidValue;
+  if (gg.xn && gg.mn > 16 && g_variant[3] == 1) return hipErrorInvalidValue;   // MFMA-dW variant: <= 16
   const bool fw = gg.xn != nullptr;
+  const bool fw4 = fw && gg.mn > 16;
   bool part = false;
   for (int i = 0; i < gg.n; ++i) part = part || gg.d[i].dzp != nullptr;
   if (g_variant[3] != 1) {   // default: LDS-staged VALU dW (row-contiguous W streams)
@@ -511,12 +532,13 @@ hipError_t wgrad_group(const WgGroup& g, int M, SlOpt o, hipStream_t st) {
   const int64_t g2 = (int64_t)grid.x * grid.y;
   gg.grid2d = g_variant[2] == 1 ? 1 : (g_variant[2] == 2 ? 0 : ((g2 - wb) * 10 < g2 ? 1 : 0));
 #define SL_WG(A, F, P) wgrad_group_kernel<A, F, P><<<gg.grid2d ? grid : grid1, 1024, 0, st>>>(gg, M, o)
+    const int fc = fw4 ? 4 : (fw ? 1 : 0);
     if (part) {
-      if (o.kind == 2) { if (fw) SL_WG(true, true, true); else SL_WG(true, false, true); }
-      else { if (fw) SL_WG(false, true, true); else SL_WG(false, false, true); }
+      if (o.kind == 2) { if (fc == 4) SL_WG(true, 4, true); else if (fc) SL_WG(true, 1, true); else SL_WG(true, 0, true); }
+      else { if (fc == 4) SL_WG(false, 4, true); else if (fc) SL_WG(false, 1, true); else SL_WG(false, 0, true); }
     } else {
-      if (o.kind == 2) { if (fw) SL_WG(true, true, false); else SL_WG(true, false, false); }
-      else { if (fw) SL_WG(false, true, false); else SL_WG(false, false, false); }
+      if (o.kind == 2) { if (fc == 4) SL_WG(true, 4, false); else if (fc) SL_WG(true, 1, false); else SL_WG(true, 0, false); }
+      else { if (fc == 4) SL_WG(false, 4, false); else if (fc) SL_WG(false, 1, false); else SL_WG(false, 0, false); }
     }
 #undef SL_WG
     return hipGetLastError();

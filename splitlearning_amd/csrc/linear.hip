@@ -25,6 +25,10 @@
 namespace sl {
 
 int g_variant[16] = {0};
+int g_bf16 = 0;
+
+hipError_t gemm_nt(const float* X, int ldx, const float* W, int ldw, float* Y, int ldy, int M, int N, int K, Epi e,
+                   bool bf16, hipStream_t st);
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -117,11 +121,88 @@ skinny_fwd_kernel(const float* __restrict__ X, int ldx, const float* __restrict_
   }
 }
 
+// bf16 compute form of skinny_fwd_kernel (`--dtype bf16`): same grid, split-K and store, but
+// each lane stages 8 consecutive k of its X row and W row (two float4 loads each), rounds
+// them to bf16 and issues one v_mfma_f32_16x16x32_bf16 (lane group q covers k = 8q..8q+7 of
+// a 32-k step); fp32 accumulation.  K slices are 32-aligned.
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ bf16x8_t pack_bf16x8(float4 lo, float4 hi) {
+  bf16x8_t v;
+  v[0] = (__bf16)lo.x; v[1] = (__bf16)lo.y; v[2] = (__bf16)lo.z; v[3] = (__bf16)lo.w;
+  v[4] = (__bf16)hi.x; v[5] = (__bf16)hi.y; v[6] = (__bf16)hi.z; v[7] = (__bf16)hi.w;
+  return v;
+}
+
+template <int NW, int U>
+__global__ void __launch_bounds__(NW * 64)
+skinny_fwd_bf16_kernel(const float* __restrict__ X, int ldx, const float* __restrict__ W, int ldw,
+                       float* __restrict__ Y, int ldy, int M, int N, int K, Epi e,
+                       float* __restrict__ P = nullptr, int64_t slab = 0) {
+  __shared__ f32x4 red[NW][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int n0 = blockIdx.x * 16, m0 = blockIdx.y * 16;
+  const int S = gridDim.z;
+  const int kz = ((K + 32 * S - 1) / (32 * S)) * 32;
+  const int kz0 = min(K, (int)blockIdx.z * kz), kz1 = min(K, kz0 + kz);
+  const int kper = ((kz1 - kz0 + 32 * NW - 1) / (32 * NW)) * 32;
+  const int kb = kz0 + wv * kper;
+  const int ke = min(kz1, kb + kper);
+  const int ra = m0 + (lane & 15), rb = n0 + (lane & 15);
+  const int kq = (lane >> 4) * 8;
+  const bool va = ra < M, vb = rb < N;
+  const float* pa = X + (int64_t)(va ? ra : 0) * ldx;
+  const float* pb = W + (int64_t)(vb ? rb : 0) * ldw;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  int k = kb;
+  for (; k + 32 * U <= ke; k += 32 * U) {
+    float4 a0[U], a1[U], w0[U], w1[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int kk = k + 32 * u + kq;
+      a0[u] = va ? ld4(pa + kk) : z4;
+      a1[u] = va ? ld4(pa + kk + 4) : z4;
+      w0[u] = vb ? ld4(pb + kk) : z4;
+      w1[u] = vb ? ld4(pb + kk + 4) : z4;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pack_bf16x8(a0[u], a1[u]), pack_bf16x8(w0[u], w1[u]), acc, 0, 0, 0);
+  }
+  for (; k < ke; k += 32) {
+    const int kk = k + kq;
+    const bool i0 = kk < ke, i1 = kk + 4 < ke;
+    const float4 a0 = (va && i0) ? ld4(pa + kk) : z4, a1 = (va && i1) ? ld4(pa + kk + 4) : z4;
+    const float4 w0 = (vb && i0) ? ld4(pb + kk) : z4, w1 = (vb && i1) ? ld4(pb + kk + 4) : z4;
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pack_bf16x8(a0, a1), pack_bf16x8(w0, w1), acc, 0, 0, 0);
+  }
+  red[wv][lane] = acc;
+  __syncthreads();
+  if (wv == 0) {
+    f32x4 s = red[0][lane];
+#pragma unroll
+    for (int i = 1; i < NW; ++i) s += red[i][lane];
+    const int n = n0 + (lane & 15);
+    if (n < N) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + (lane >> 4) * 4 + r;
+        if (m >= M) continue;
+        if (S == 1)
+          Y[(int64_t)m * ldy + n] = apply_epi(e, s[r], m, n);
+        else
+          P[(int64_t)blockIdx.z * slab + (int64_t)m * N + n] = s[r];
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------- dgrad
 // dX[M,K] = dZ[M,N] . W[N,K]; grid (ceil(K/64), ceil(M/16), S), block NW*64.
 // S == 1: store with the fused mask (h_prev > 0) * scale.  S > 1: store raw partial
 // sums to P[s][M][K] (reduced by dgrad_reduce_kernel).  Requires K % 4 == 0.
-template <int NW>
+template <int NW, bool BF = false>
 __global__ void __launch_bounds__(NW * 64)
 skinny_dgrad_kernel(const float* __restrict__ dZ, int ldz, const float* __restrict__ W, int ldw,
                     const float* __restrict__ hprev, int ldh, float scale,
@@ -154,6 +235,10 @@ skinny_dgrad_kernel(const float* __restrict__ dZ, int ldz, const float* __restri
       const int nn = n + 4 * u + q;
       a[u] = vm ? za[nn] : 0.f;
       w[u] = vk ? ld4(W + (int64_t)nn * ldw + kcol) : z4;
+      if (BF) {
+        a[u] = bfr(a[u]);
+        w[u] = bfr4(w[u]);
+      }
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -166,8 +251,12 @@ skinny_dgrad_kernel(const float* __restrict__ dZ, int ldz, const float* __restri
   for (; n < ne; n += 4) {
     const int nn = n + q;
     const bool vn = nn < ne;
-    const float a = (vm && vn) ? za[nn] : 0.f;
-    const float4 w = (vk && vn) ? ld4(W + (int64_t)nn * ldw + kcol) : z4;
+    float a = (vm && vn) ? za[nn] : 0.f;
+    float4 w = (vk && vn) ? ld4(W + (int64_t)nn * ldw + kcol) : z4;
+    if (BF) {
+      a = bfr(a);
+      w = bfr4(w);
+    }
     acc[0] = mfma4(a, w.x, acc[0]);
     acc[1] = mfma4(a, w.y, acc[1]);
     acc[2] = mfma4(a, w.z, acc[2]);
@@ -320,7 +409,7 @@ __global__ void __launch_bounds__(1024)
 wgrad_opt_v3_kernel(const float* __restrict__ dZ, int ldz, const float* __restrict__ A, int lda,
                     float* __restrict__ W, int ldw, float* __restrict__ s0, float* __restrict__ s1,
                     float* __restrict__ bias, float* __restrict__ sb0, float* __restrict__ sb1,
-                    int M, int N, int K, SlOpt o) {
+                    int M, int N, int K, SlOpt o, int g_bf) {
   __shared__ f32x4 sa[16][64];
   __shared__ float sdz[16][16];
   const int tid = threadIdx.x;
@@ -342,10 +431,12 @@ wgrad_opt_v3_kernel(const float* __restrict__ dZ, int ldz, const float* __restri
     if (mc) __syncthreads();
     {
       const int m = mc + r, kk = blockIdx.x * 256 + lane * 4;
-      sa[r][lane] = (m < M && kk < K) ? *reinterpret_cast<const f32x4*>(A + (int64_t)m * lda + kk) : zv;
+      const f32x4 av = (m < M && kk < K) ? *reinterpret_cast<const f32x4*>(A + (int64_t)m * lda + kk) : zv;
+      sa[r][lane] = g_bf ? bfr4(av) : av;
       if (tid < 256) {
         const int mm = mc + (tid >> 4), nn = blockIdx.y * 16 + (tid & 15);
-        sdz[tid >> 4][tid & 15] = (mm < M && nn < N) ? dZ[(int64_t)mm * ldz + nn] : 0.f;
+        const float dv = (mm < M && nn < N) ? dZ[(int64_t)mm * ldz + nn] : 0.f;
+        sdz[tid >> 4][tid & 15] = g_bf ? bfr(dv) : dv;
       }
     }
     __syncthreads();
@@ -387,6 +478,8 @@ __global__ void opt_flat_kernel(float* __restrict__ p, const float* __restrict__
 hipError_t linear_fwd(const float* X, int ldx, const float* W, int ldw, float* Y, int ldy, int M, int N,
                       int K, Epi e, float* ws, int64_t ws_elems, hipStream_t st) {
   if (M <= 0 || N <= 0) return hipSuccess;
+  // many rows (evaluation over a whole test set, large batches): the LDS-tiled MFMA GEMM
+  if (M > 128) return gemm_nt(X, ldx, W, ldw, Y, ldy, M, N, K, e, g_bf16 != 0, st);
   dim3 grid((N + 15) / 16, (M + 15) / 16);
   // split K until there are ~8 workgroups per CU, keeping >= 256 k per workgroup: fc1
   // (313 column tiles) runs S = 4 (30.6 us vs 35.2 us at S = 2; profiles/r1_kbench_call17)
@@ -399,7 +492,14 @@ hipError_t linear_fwd(const float* X, int ldx, const float* W, int ldw, float* Y
   const int nw = kz >= 1024 ? 8 : (kz >= 512 ? 4 : 2);
   dim3 g3(grid.x, grid.y, S);
   float* P = S > 1 ? ws : nullptr;
-  if (nw == 8)
+  if (g_bf16) {
+    if (nw == 8)
+      skinny_fwd_bf16_kernel<8, 2><<<g3, 512, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e, P, slab);
+    else if (nw == 4)
+      skinny_fwd_bf16_kernel<4, 2><<<g3, 256, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e, P, slab);
+    else
+      skinny_fwd_bf16_kernel<2, 2><<<g3, 128, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e, P, slab);
+  } else if (nw == 8)
     skinny_fwd_kernel<8, 4, false><<<g3, 512, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e, P, slab);
   else if (nw == 4)
     skinny_fwd_kernel<4, 4, false><<<g3, 256, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e, P, slab);
@@ -423,7 +523,7 @@ hipError_t linear_dgrad(const float* dZ, int ldz, const float* W, int ldw, const
   // 55.6 full-N vs 170.9 / 101.6 / 68.9 / 51.8 split; profiles/r2_dgrad_fulln_ab.txt): with
   // the whole N per workgroup there are only K/32 workgroups (20 at a TP = 8 shard), each a
   // chain of 1000-row strided reads, and the reduce launch is cheaper than that latency.
-  if (g_variant[8] == 2 && M <= 64 && (K & 3) == 0 && (ldw & 1) == 0 && (ldz & 3) == 0) {
+  if (g_variant[8] == 2 && !g_bf16 && M <= 64 && (K & 3) == 0 && (ldw & 1) == 0 && (ldz & 3) == 0) {
     dim3 grid((K + 31) / 32, mt);
     dgrad_fulln_kernel<<<grid, 1024, 0, st>>>(dZ, ldz, W, ldw, hprev, ldh, scale, dX, ldx, M, N, K);
     return hipGetLastError();
@@ -442,9 +542,15 @@ hipError_t linear_dgrad(const float* dZ, int ldz, const float* W, int ldw, const
   while (S > 1 && ws_elems < slab * S) S >>= 1;
   dim3 grid(kt, mt, S);
   if (S == 1) {
-    skinny_dgrad_kernel<8><<<grid, 512, 0, st>>>(dZ, ldz, W, ldw, hprev, ldh, scale, dX, ldx, 0, M, N, K);
+    if (g_bf16)
+      skinny_dgrad_kernel<8, true><<<grid, 512, 0, st>>>(dZ, ldz, W, ldw, hprev, ldh, scale, dX, ldx, 0, M, N, K);
+    else
+      skinny_dgrad_kernel<8><<<grid, 512, 0, st>>>(dZ, ldz, W, ldw, hprev, ldh, scale, dX, ldx, 0, M, N, K);
   } else {
-    skinny_dgrad_kernel<8><<<grid, 512, 0, st>>>(dZ, ldz, W, ldw, nullptr, 0, 1.f, ws, 0, slab, M, N, K);
+    if (g_bf16)
+      skinny_dgrad_kernel<8, true><<<grid, 512, 0, st>>>(dZ, ldz, W, ldw, nullptr, 0, 1.f, ws, 0, slab, M, N, K);
+    else
+      skinny_dgrad_kernel<8><<<grid, 512, 0, st>>>(dZ, ldz, W, ldw, nullptr, 0, 1.f, ws, 0, slab, M, N, K);
     const int64_t tot = (int64_t)M * K;
     dgrad_reduce_kernel<<<(unsigned)((tot + 255) / 256), 256, 0, st>>>(ws, S, slab, hprev, ldh, scale, dX, ldx,
                                                                         M, K);
@@ -471,7 +577,14 @@ hipError_t linear_fwd_partial(const float* X, int ldx, const float* W, int ldw, 
   dim3 g3(grid.x, grid.y, S);
   Epi e{};
   e.dscale = 1.f;
-  if (nw == 8)
+  if (g_bf16) {
+    if (nw == 8)
+      skinny_fwd_bf16_kernel<8, 2><<<g3, 512, 0, st>>>(X, ldx, W, ldw, ws, N, M, N, K, e, ws, slab);
+    else if (nw == 4)
+      skinny_fwd_bf16_kernel<4, 2><<<g3, 256, 0, st>>>(X, ldx, W, ldw, ws, N, M, N, K, e, ws, slab);
+    else
+      skinny_fwd_bf16_kernel<2, 2><<<g3, 128, 0, st>>>(X, ldx, W, ldw, ws, N, M, N, K, e, ws, slab);
+  } else if (nw == 8)
     skinny_fwd_kernel<8, 4, false><<<g3, 512, 0, st>>>(X, ldx, W, ldw, ws, N, M, N, K, e, ws, slab);
   else if (nw == 4)
     skinny_fwd_kernel<4, 4, false><<<g3, 256, 0, st>>>(X, ldx, W, ldw, ws, N, M, N, K, e, ws, slab);
@@ -492,7 +605,10 @@ hipError_t linear_dgrad_partial(const float* dZ, int ldz, const float* W, int ld
   if (ws_elems < slab * S) S = 1;
   if (ws_elems < slab) return hipErrorInvalidValue;
   dim3 grid(kt, mt, S);
-  if (S == 1)
+  if (g_bf16)
+    skinny_dgrad_kernel<8, true><<<grid, 512, 0, st>>>(dZ, ldz, W, ldw, nullptr, 0, 1.f, ws, S == 1 ? K : 0,
+                                                        S == 1 ? 0 : slab, M, N, K);
+  else if (S == 1)
     skinny_dgrad_kernel<8><<<grid, 512, 0, st>>>(dZ, ldz, W, ldw, nullptr, 0, 1.f, ws, K, 0, M, N, K);
   else
     skinny_dgrad_kernel<8><<<grid, 512, 0, st>>>(dZ, ldz, W, ldw, nullptr, 0, 1.f, ws, 0, slab, M, N, K);
@@ -515,9 +631,11 @@ hipError_t linear_wgrad_opt(const float* dZ, int ldz, const float* A, int lda, f
   // v3 layout (5.8 TB/s effective on fc1 at M = 16)
   dim3 g3((K + 255) / 256, (N + 15) / 16);
   if (o.kind == 2)
-    wgrad_opt_v3_kernel<true><<<g3, 1024, 0, st>>>(dZ, ldz, A, lda, W, ldw, s0, s1, bias, sb0, sb1, M, N, K, o);
+    wgrad_opt_v3_kernel<true><<<g3, 1024, 0, st>>>(dZ, ldz, A, lda, W, ldw, s0, s1, bias, sb0, sb1, M, N, K, o,
+                                                    g_bf16);
   else
-    wgrad_opt_v3_kernel<false><<<g3, 1024, 0, st>>>(dZ, ldz, A, lda, W, ldw, s0, s1, bias, sb0, sb1, M, N, K, o);
+    wgrad_opt_v3_kernel<false><<<g3, 1024, 0, st>>>(dZ, ldz, A, lda, W, ldw, s0, s1, bias, sb0, sb1, M, N, K, o,
+                                                     g_bf16);
   return hipGetLastError();
 }
 

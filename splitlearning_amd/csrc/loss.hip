@@ -166,7 +166,10 @@ head_step_kernel(const float* __restrict__ X, const float* __restrict__ W, const
                  const int64_t* __restrict__ y, int64_t ignore, float scale, float* __restrict__ loss_rows,
                  float* __restrict__ dX, float* __restrict__ Wout, float* __restrict__ bout, float* __restrict__ s0w,
                  float* __restrict__ s1w, float* __restrict__ s0b, float* __restrict__ s1b, int M, int K, int C,
-                 SlOpt o, int mask_dx) {
+                 SlOpt o, int mask_dx, int bf) {
+  // bf: bf16 compute (`--dtype bf16`): every product's operands rounded to bf16, fp32 sums;
+  // the master weights the optimizer updates stay fp32
+  auto R = [bf](float v) { return bf ? bfr(v) : v; };
   __shared__ float sx[4096];
   __shared__ float sw[4096];
   __shared__ float sd[1024];     // dlogits [M][C]
@@ -194,7 +197,7 @@ head_step_kernel(const float* __restrict__ X, const float* __restrict__ W, const
   for (int i = tid; i < M * C; i += 256) {
     const int m = i / C, c = i - m * C;
     float v = 0.f;
-    for (int k = 0; k < K; ++k) v = fmaf(sx[m * K + k], sw[c * K + k], v);
+    for (int k = 0; k < K; ++k) v = fmaf(R(sx[m * K + k]), R(sw[c * K + k]), v);
     sd[i] = v + (bias ? bias[c] : 0.f);
   }
   __syncthreads();
@@ -224,14 +227,14 @@ head_step_kernel(const float* __restrict__ X, const float* __restrict__ W, const
   for (int i = tid; i < M * K; i += 256) {
     const int m = i / K, k = i - m * K;
     float v = 0.f;
-    for (int c = 0; c < C; ++c) v = fmaf(sd[m * C + c], sw[c * K + k], v);
+    for (int c = 0; c < C; ++c) v = fmaf(R(sd[m * C + c]), R(sw[c * K + k]), v);
     dX[i] = (mask_dx && !(sx[i] > 0.f)) ? 0.f : v;   // mask_dx: the producer's ReLU backward too
   }
   // weight / bias gradient and the optimizer step
   auto wstep = [&](int i, float a0, float a1) {
     const int c = i / K, k = i - c * K;
     float g = 0.f;
-    for (int m = 0; m < M; ++m) g = fmaf(sd[m * C + c], sx[m * K + k], g);
+    for (int m = 0; m < M; ++m) g = fmaf(R(sd[m * C + c]), R(sx[m * K + k]), g);
     float pp = sw[i];
     sl_opt_update(o, pp, g, a0, a1);
     if (o.kind != 0) Wout[i] = pp;
@@ -259,7 +262,7 @@ hipError_t head_step(const float* X, float* W, float* b, const int64_t* y, int64
   if (M <= 0) return hipSuccess;
   if (M * K > 4096 || C * K > 4096 || M * C > 1024) return hipErrorInvalidValue;
   head_step_kernel<<<1, 256, 0, st>>>(X, W, b, y, ignore, scale, loss_rows, dX, W, b, s0w, s1w, s0b, s1b, M, K, C, o,
-                                      mask_dx ? 1 : 0);
+                                      mask_dx ? 1 : 0, g_bf16);
   return hipGetLastError();
 }
 

@@ -170,7 +170,7 @@ class TailEngine:
         can form the next batch's layer-0 product for m rows (look-ahead)."""
         ok = hasattr(self.ops, "wgrad_group_") and 0 < len(self.layers) <= 3
         if m:
-            ok = ok and hasattr(self.ops, "lookahead_slabs") and 0 < m <= 16
+            ok = ok and hasattr(self.ops, "lookahead_slabs") and 0 < m <= 64
         return ok
 
     def group_step(self, slot: OptSlot, t: int | None = None, prefix: str = "", x_next=None):
@@ -225,7 +225,7 @@ class TailEngine:
 
     def lookahead_ok(self, m: int) -> bool:
         """Whether `fused_step(x_next=...)` can pre-compute the next batch's fc1 product."""
-        return self.fused3_ok() and hasattr(self.ops, "lookahead_slabs") and 0 < m <= 16
+        return self.fused3_ok() and hasattr(self.ops, "lookahead_slabs") and 0 < m <= 64
 
     def lookahead_slabs(self, m: int):
         L1 = self.layers[0]

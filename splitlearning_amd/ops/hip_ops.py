@@ -178,9 +178,15 @@ _TABLE: dict = {}
 
 
 # ---------------------------------------------------------------- linear
-# eval-time inference with many rows goes through hipBLASLt (plain library GEMM)
-# plus the fused epilogue kernel; the skinny kernels cover the training batch sizes.
+# training batches (M <= 128) run the skinny split-K kernels; many rows (evaluation over a
+# test set, large batches) the LDS-tiled MFMA GEMM (csrc/gemm.hip) -- both in-tree HIP.
 LARGE_M = 128
+
+
+def set_compute_dtype(dtype: str):
+    """`--dtype`: GEMM operands in fp32 (exact) or bf16 (fp32 accumulation); master weights
+    and optimizer state stay fp32."""
+    C().set_compute_dtype(dtype)
 
 
 def linear_fwd(x, w, b, relu: bool, drop_p: float, seed: int, col_offset: int = 0, out=None, dseed=None):
@@ -189,12 +195,8 @@ def linear_fwd(x, w, b, relu: bool, drop_p: float, seed: int, col_offset: int = 
         out = torch.empty(M, N, device=x.device, dtype=torch.float32)
     w = w.detach()
     bias = b.detach() if b is not None else None
-    if M > LARGE_M:
-        P = torch.mm(x, w.t())
-        C().linear_epilogue(P, bias, out, relu, float(drop_p), seed & M64, col_offset, _ptr(dseed))
-    else:
-        C().linear_fwd(x, w, bias, out, relu, float(drop_p), seed & M64, col_offset, _ptr(dseed),
-                       _fwd_workspace(x.device, 16 * M * N))
+    ws = _fwd_workspace(x.device, 16 * M * N) if M <= LARGE_M else None
+    C().linear_fwd(x, w, bias, out, relu, float(drop_p), seed & M64, col_offset, _ptr(dseed), ws)
     return out
 
 
@@ -307,7 +309,7 @@ def lookahead_slabs(device, K0: int, mn: int, N0: int, tag: str = ""):
 def wgrad_group_(layers, M: int, cfg, t: int, dyn=None, x_next=None, p_next=None):
     """Fused wgrad+optimizer of up to 3 layers in one launch.  Each layer:
     (dz, dzp, hmask, mscale, A, W, st_w, b, st_b) — exactly one of dz / dzp.
-    With `x_next` (<= 16 rows), also writes layer 0's split-K partial pre-activations of
+    With `x_next` (<= 64 rows), also writes layer 0's split-K partial pre-activations of
     the next batch under the *updated* weights into `p_next` (see lookahead_slabs)."""
     tup = []
     for dz, dzp, hm, ms, A, W, st_w, b, st_b in layers:

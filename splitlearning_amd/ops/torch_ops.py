@@ -54,9 +54,25 @@ def conv_front_bwd(dy, y, am, x_u8, idx, w, b):
 
 
 # ---------------------------------------------------------------- linear
+# `--dtype bf16`: GEMM operands rounded to bf16, fp32 accumulation (the HIP kernels' rule,
+# csrc/common.h bfr); parameters and optimizer state stay fp32
+_BF16 = False
+
+
+def set_compute_dtype(dtype: str):
+    global _BF16
+    if dtype not in ("fp32", "bf16"):
+        raise ValueError(dtype)
+    _BF16 = dtype == "bf16"
+
+
+def _r(t: torch.Tensor) -> torch.Tensor:
+    return t.to(torch.bfloat16).to(t.dtype) if _BF16 else t
+
+
 def linear_fwd(x, w, b, relu: bool, drop_p: float, seed: int, col_offset: int = 0,
                out: torch.Tensor | None = None):
-    y = x @ w.t()
+    y = _r(x) @ _r(w).t()
     if b is not None:
         y = y + b
     if relu:
@@ -84,14 +100,14 @@ def linear_epilogue(P, b, relu: bool, drop_p: float, seed: int, col_offset: int 
 def linear_dgrad(dz, w, h_prev=None, scale: float = 1.0):
     """dx = dz @ w; if h_prev is given, also back-propagate through the previous
     layer's ReLU(+dropout): dx *= scale * [h_prev > 0]."""
-    dx = dz @ w
+    dx = _r(dz) @ _r(w)
     if h_prev is not None:
         dx = dx * (h_prev > 0) * scale
     return dx
 
 
 def linear_wgrad(dz, a):
-    return dz.t() @ a, dz.sum(0)
+    return _r(dz).t() @ _r(a), _r(dz).sum(0)
 
 
 # ---------------------------------------------------------------- optimizers

@@ -62,6 +62,8 @@ class Session:
         self.rank = comm.rank
         self.device = device
         self.ops = ops.impl(device)
+        # compute dtype of the GEMM-shaped kernels (process-wide switch of the op set)
+        self.ops.set_compute_dtype(getattr(args, "dtype", "fp32"))
         self.k = args.client_num_in_total
         self.B = args.batch_size
         self.show = (not args.no_tqdm) and self.rank == 0

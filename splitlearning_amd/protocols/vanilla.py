@@ -118,7 +118,7 @@ class VanillaSession(Session):
             nxt = alice_fwd(spans[i + 1]) if i + 1 < len(spans) else None
             if self.is_bob:
                 if fused:
-                    x_next = nxt[3] if (la and nxt is not None and nxt[3].shape[0] <= 16) else None
+                    x_next = nxt[3] if (la and nxt is not None and nxt[3].shape[0] <= 64) else None
                     self.tail.fused_step(self.bob_slot(cid), x_next=x_next)
                     pre = x_next is not None
                 else:

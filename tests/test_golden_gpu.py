@@ -56,8 +56,8 @@ def _load_adam(ref, opt, te, slot, t):
                             "exp_avg_sq": st["v"].clone()}
 
 
-@pytest.mark.parametrize("scale", [1.0, 30.0])
-def test_sisa_server_epoch_matches_torch_adam_every_step(cuda, scale):
+@pytest.mark.parametrize("scale,B", [(1.0, 16), (30.0, 16), (1.0, 64)])
+def test_sisa_server_epoch_matches_torch_adam_every_step(cuda, scale, B):
     """The production SISA server epoch (fused fwd/dgrad kernels, fc1 look-ahead inside the
     wgrad+Adam kernel), 128 steps, checked against `torch.optim.Adam(lr, weight_decay=1e-5)`
     on `model2_sisa` at EVERY step: before step i torch is given the engine's weights, Adam
@@ -67,7 +67,7 @@ def test_sisa_server_epoch_matches_torch_adam_every_step(cuda, scale):
     gaps within ~30 steps, measured — so per-step re-synchronisation is what makes a tight
     128-step comparison possible.)  The run is also the native executor's: its free-running
     128-step result must be bitwise the per-step Python path's."""
-    B, steps, lr, seed_base = 16, 128, 1e-3, 99
+    steps, lr, seed_base = 128 if B == 16 else 48, 1e-3, 99
     g = torch.Generator().manual_seed(21)
     n = B * steps
     acts = (torch.rand(n, 5408, generator=g) * scale).to(cuda)
@@ -182,3 +182,84 @@ def test_vanilla_split_epoch_matches_composed_torch_sgd(cuda, tmp_path):
             torch.testing.assert_close(e, p.detach(), rtol=1e-4, atol=1e-4, msg=f"batch {i} {name}")
     torch.cuda.synchronize()
     assert bslot.t == -(-n // 16)
+
+
+class _BF16Linear(torch.autograd.Function):
+    """Linear with the `--dtype bf16` rule: every product's operands rounded to bf16 (values
+    only), fp32 accumulation, in forward, data gradient and weight gradient."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        r = lambda t: t.bfloat16().float()  # noqa: E731
+        return r(x) @ r(w).t() + b
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        r = lambda t: t.bfloat16().float()  # noqa: E731
+        return r(dy) @ r(w), r(dy).t() @ r(x), r(dy).sum(0)
+
+
+def _ref_tail_forward_bf16(mod, x, seed_base, step):
+    h = x
+    for i, lin in enumerate(mod.linears()):
+        ls = mod.spec.layers[i]
+        h = _BF16Linear.apply(h, lin.weight, lin.bias)
+        if ls.relu:
+            h = F.relu(h)
+        if ls.dropout:
+            keep = rng.keep_mask(rng.step_seed(seed_base, i, step), h.shape[0], h.shape[1], ls.dropout,
+                                 device=h.device)
+            h = h * keep / (1 - ls.dropout)
+    return h
+
+
+def test_bf16_compute_server_steps_match_torch(cuda):
+    """`--dtype bf16` (BASELINE config 2's precision): the fused SISA server step with bf16
+    operands (bf16 MFMA in the forward, bf16-rounded operands elsewhere, fp32 accumulation,
+    fp32 master weights and Adam state), 32 steps re-synchronised before each, against torch
+    with the same rounding rule (`_BF16Linear`) -- and its losses within bf16 tolerance of
+    the exact-fp32 model's."""
+    from splitlearning_amd.ops import hip_ops
+    B, steps, lr, seed_base = 16, 32, 1e-3, 5
+    g = torch.Generator().manual_seed(2)
+    acts = torch.rand(B * steps, 5408, generator=g).to(cuda)
+    labels = torch.randint(0, 10, (B * steps,), generator=g).to(cuda)
+    torch.manual_seed(6)
+    base = ServerTailSisa()
+    te = TailEngine(copy.deepcopy(base), sisa_server_spec(), cuda, seed_base=seed_base, ws_tag="#bf")
+    slot = OptSlot(adam(lr, 1e-5))
+    for L in te.layers:
+        slot.state(f"{L.spec.name}.weight", L.W)
+        slot.state(f"{L.spec.name}.bias", L.b)
+    ref = copy.deepcopy(base).to(cuda)
+    opt = torch.optim.Adam(ref.parameters(), lr=lr, weight_decay=1e-5)
+    C = hip_ops.C()
+    C.set_compute_dtype("bf16")
+    try:
+        te.lookahead_prologue(acts[:B])
+        pre = True
+        for i in range(steps):
+            x, y = acts[i * B:(i + 1) * B], labels[i * B:(i + 1) * B]
+            _load_adam(ref, opt, te, slot, i)
+            with torch.no_grad():
+                loss32 = F.cross_entropy(_ref_tail_forward(ref, x, seed_base, i + 1), y, reduction="none")
+            opt.zero_grad()
+            loss_r = F.cross_entropy(_ref_tail_forward_bf16(ref, x, seed_base, i + 1), y, reduction="none")
+            loss_r.mean().backward()
+            opt.step()
+            nxt = acts[(i + 1) * B:(i + 2) * B] if i + 1 < steps else None
+            loss_e, _ = te.train_fwd_bwd3(x, y, need_dx=False, pre=pre)
+            te.fused_step(slot, x_next=nxt)
+            pre = nxt is not None
+            torch.testing.assert_close(loss_e, loss_r.detach(), rtol=1e-3, atol=1e-3)
+            torch.testing.assert_close(loss_e, loss32, rtol=3e-2, atol=3e-2)     # bf16 vs exact fp32
+            for name, p in ref.named_parameters():
+                L = te.layers[int(name[2]) - 1]
+                e = L.W if name.endswith("weight") else L.b
+                d = (e - p.detach()).abs()
+                assert d.max().item() <= 2 * lr + 1e-6, (i, name, d.max().item())
+                assert (d > 1e-6).float().mean().item() < 2e-3, (i, name, (d > 1e-6).float().mean().item())
+    finally:
+        C.set_compute_dtype("fp32")

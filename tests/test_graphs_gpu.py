@@ -246,14 +246,14 @@ def test_ushape_pipelined_epoch_matches_per_batch_steps(cuda, tmp_path):
 
 @pytest.mark.parametrize("tp", [1, 8])
 @pytest.mark.parametrize("kind", ["adam", "sgd"])
-def test_native_server_epoch_matches_python(cuda, tp, kind):
+@pytest.mark.parametrize("B", [16, 64])
+def test_native_server_epoch_matches_python(cuda, tp, kind, B):
     """_C.ServerEpoch (csrc/engine.cpp) issues the same launches, seeds and step counts as the
     Python look-ahead loop: bit-identical weights, optimizer state and losses (tp = 8: rank
     0's shard, row-parallel fc2 through the native 1-rank communicator)."""
     from splitlearning_amd.engine import sgd_momentum
     from splitlearning_amd.parallel.rccl import native_allreduce, self_comm
     g = torch.Generator().manual_seed(8)
-    B = 16
     n = B * 9 + 5                                       # full batches + a partial last one
     acts = (torch.rand(n, 5408, generator=g) * 30).to(cuda)
     labels = torch.randint(0, 10, (n,), generator=g).to(cuda)

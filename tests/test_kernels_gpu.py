@@ -74,9 +74,11 @@ def test_conv_bwd(cuda, kind):
 
 
 @pytest.mark.parametrize("M,N,K", [(16, 5000, 5408), (16, 1000, 5000), (16, 100, 1000), (5, 10, 100),
-                                    (16, 37, 52), (200, 100, 1000)])
+                                    (16, 37, 52), (200, 100, 1000), (1000, 5000, 5408), (8000, 1000, 5000),
+                                    (129, 130, 36), (300, 10, 100)])
 @pytest.mark.parametrize("relu,drop", [(False, 0.0), (True, 0.0), (True, 0.5)])
 def test_linear_fwd(cuda, M, N, K, relu, drop):
+    """M <= 128: the skinny split-K kernels; M > 128: the LDS-tiled MFMA GEMM (gemm.hip)."""
     x = torch.randn(M, K, device=cuda)
     w = torch.randn(N, K, device=cuda) / K ** 0.5
     b = torch.randn(N, device=cuda)
@@ -197,9 +199,12 @@ def test_conv_local_step(cuda, kind, B):
 @pytest.mark.parametrize("variant", [0, 1])          # 0 = LDS-staged (default), 1 = all-MFMA
 @pytest.mark.parametrize("kind", ["sgd", "adam"])
 @pytest.mark.parametrize("M,shapes,mn", [(16, [(5000, 5408), (1000, 5000)], 16), (20, [(100, 1000), (33, 20)], 5),
-                                         (7, [(10, 100)], 0)])
+                                         (7, [(10, 100)], 0), (64, [(1000, 5408), (100, 1000)], 64),
+                                         (48, [(300, 1000)], 37)])
 def test_wgrad_group(cuda, variant, kind, M, shapes, mn):
-    """Grouped wgrad+optimizer (+ layer-0 look-ahead forward) == per-layer fp32 reference."""
+    """Grouped wgrad+optimizer (+ layer-0 look-ahead forward, up to 64 rows) == per-layer fp32 reference."""
+    if variant == 1 and mn > 16:
+        pytest.skip("the all-MFMA dW variant's look-ahead covers <= 16 rows")
     C = hip_ops.C()
     cfg = OptimCfg("adam", 1e-3, weight_decay=1e-5) if kind == "adam" else OptimCfg("sgd", 1e-2, momentum=0.9)
 
@@ -450,3 +455,22 @@ def test_multi_alice_local_epoch_is_bitwise_per_alice(cuda, kind):
         for name, st in p1.states.items():
             for k, v in st.items():
                 assert torch.equal(v, p2.states[name][k]), (name, k)
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 5000, 5408), (300, 130, 1000), (16, 1000, 5000)])
+def test_linear_fwd_bf16_compute(cuda, M, N, K):
+    """--dtype bf16: operands rounded to bf16 (RNE), fp32 accumulation: equals the fp32 product
+    of the bf16-rounded operands up to summation order."""
+    C = hip_ops.C()
+    x = torch.randn(M, K, device=cuda)
+    w = torch.randn(N, K, device=cuda) / K ** 0.5
+    b = torch.randn(N, device=cuda)
+    C.set_compute_dtype("bf16")
+    try:
+        y = hip_ops.linear_fwd(x, w, b, True, 0.0, 0)
+    finally:
+        C.set_compute_dtype("fp32")
+    yr = torch.relu(x.bfloat16().float() @ w.bfloat16().float().t() + b)
+    _close(y, yr, rtol=1e-4, atol=2e-4)
+    # and it is NOT the exact-fp32 product (the mode is really on)
+    assert (y - torch.relu(x @ w.t() + b)).abs().max().item() > 1e-3

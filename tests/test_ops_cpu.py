@@ -106,3 +106,24 @@ def test_eval_counters():
     c = torch_ops.eval_counters(logits, labels, omit_label=1).tolist()
     assert c == [2, 3, 2, 3, 0, 0]
     _ = np  # keep numpy import (shared fixtures elsewhere)
+
+
+def test_bf16_compute_rule_torch_ops():
+    """--dtype bf16 on the torch path: operands rounded to bf16, fp32 accumulation."""
+    from splitlearning_amd.ops import torch_ops as K
+    g = torch.Generator().manual_seed(0)
+    x, w, b = torch.randn(8, 40, generator=g), torch.randn(12, 40, generator=g), torch.randn(12, generator=g)
+    dz = torch.randn(8, 12, generator=g)
+    r = lambda t: t.bfloat16().float()  # noqa: E731
+    K.set_compute_dtype("bf16")
+    try:
+        y = K.linear_fwd(x, w, b, False, 0.0, 0)
+        dx = K.linear_dgrad(dz, w)
+        dw, db = K.linear_wgrad(dz, x)
+    finally:
+        K.set_compute_dtype("fp32")
+    torch.testing.assert_close(y, r(x) @ r(w).t() + b)
+    torch.testing.assert_close(dx, r(dz) @ r(w))
+    torch.testing.assert_close(dw, r(dz).t() @ r(x))
+    torch.testing.assert_close(db, r(dz).sum(0))
+    assert not torch.allclose(y, x @ w.t() + b, rtol=1e-5, atol=1e-5)
