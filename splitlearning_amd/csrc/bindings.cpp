@@ -660,7 +660,7 @@ void wgrad_group(const std::vector<py::tuple>& layers, int64_t M, const OptT& xn
     need_rows(*xn, "xn");
     need_f32(*pn, "pn");
     const int64_t K0 = g.d[0].K, N0 = g.d[0].N, mn = xn->size(0);
-    TORCH_CHECK(xn->size(1) == K0 && mn >= 1 && mn <= 16, "xn [mn<=16, K0]");
+    TORCH_CHECK(xn->size(1) == K0 && mn >= 1 && mn <= 64, "xn [mn<=64, K0]");
     TORCH_CHECK(pn->is_contiguous() && pn->numel() >= (K0 + 255) / 256 * mn * N0, "pn [K0/256, mn, N0]");
     g.xn = xn->data_ptr<float>();
     g.ldxn = (int)xn->stride(0);

@@ -27,13 +27,6 @@ namespace sl {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
-template <bool BF16>
-struct GemmCfg {
-  static constexpr int BK = BF16 ? 32 : 16;      // K per stage
-  static constexpr int LD = BF16 ? 40 : 20;      // LDS row stride (elements, padded)
-  typedef typename std::conditional<BF16, __bf16, float>::type T;
-};
-
 __device__ __forceinline__ bf16x4 to_bf16x4(float4 v) {
   bf16x4 o;
   o[0] = (__bf16)v.x;
@@ -43,51 +36,56 @@ __device__ __forceinline__ bf16x4 to_bf16x4(float4 v) {
   return o;
 }
 
-template <bool BF16>
-__global__ void __launch_bounds__(256)
+// WM: waves along M (the workgroup is WM x 2 waves, each a 64 x 64 output tile, so the tile is
+// 64 WM x 128); BK: K per LDS stage (fp32: 16 or 32; bf16: 32 or 64).
+template <bool BF16, int WM, int BK>
+__global__ void __launch_bounds__(128 * WM)
 gemm_nt_kernel(const float* __restrict__ X, int ldx, const float* __restrict__ W, int ldw, float* __restrict__ Y,
                int ldy, int M, int N, int K, Epi e) {
-  using C = GemmCfg<BF16>;
-  using T = typename C::T;
-  constexpr int BK = C::BK, LD = C::LD;
-  constexpr int PER = 128 * BK / 4 / 256;          // float4 loads per thread per operand per stage (2 / 4)
-  constexpr int TPR = BK / 4;                       // threads per row in a load pass (4 / 8)
-  constexpr int RPP = 256 / TPR;                    // rows per load pass (64 / 32)
-  __shared__ __attribute__((aligned(16))) T As[2][128][LD];
-  __shared__ __attribute__((aligned(16))) T Bs[2][128][LD];
+  using T = typename std::conditional<BF16, __bf16, float>::type;
+  constexpr int BM = 64 * WM, BN = 128, NT = 128 * WM;
+  constexpr int LD = BK + (BF16 ? 8 : 4);           // padded LDS row (elements)
+  constexpr int F4R = BK / 4;                        // float4s per row per stage
+  constexpr int APER = BM * F4R / NT, BPER = BN * F4R / NT;
+  static_assert(APER * NT == BM * F4R && BPER * NT == BN * F4R, "tile / thread split");
+  static_assert(!BF16 || BK % 32 == 0, "bf16 stages are whole 16x16x32 MFMA steps");
+  __shared__ __attribute__((aligned(16))) T As[2][BM][LD];
+  __shared__ __attribute__((aligned(16))) T Bs[2][BN][LD];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  // XCD-aware tile order: consecutive workgroups (dealt round-robin over the 8 XCDs) walk
-  // down M for one N column strip, so the strip of W a tile reads is shared through the
-  // Infinity Cache while X rows stream
-  const int tilesM = (M + 127) / 128;
+  // tiles of one N column strip are consecutive workgroups: the strip of W is read by many
+  // tiles back to back (served from L2 / the Infinity Cache) while X rows stream
+  const int tilesM = (M + BM - 1) / BM;
   const int tm = blockIdx.x % tilesM, tn = blockIdx.x / tilesM;
-  const int m0 = tm * 128, n0 = tn * 128;
-  const int lr = tid / TPR, lk = (tid % TPR) * 4;
-  float4 ra[PER], rb[PER];
+  const int m0 = tm * BM, n0 = tn * BN;
+  float4 ra[APER], rb[BPER];
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
   auto gload = [&](int k0) {
 #pragma unroll
-    for (int p = 0; p < PER; ++p) {
-      const int r = lr + p * RPP, k = k0 + lk;
-      const int gm = m0 + r, gn = n0 + r;
+    for (int p = 0; p < APER; ++p) {
+      const int i = tid + p * NT, r = i / F4R, k = k0 + (i % F4R) * 4, gm = m0 + r;
       ra[p] = (gm < M && k < K) ? *reinterpret_cast<const float4*>(X + (int64_t)gm * ldx + k) : z4;
+    }
+#pragma unroll
+    for (int p = 0; p < BPER; ++p) {
+      const int i = tid + p * NT, r = i / F4R, k = k0 + (i % F4R) * 4, gn = n0 + r;
       rb[p] = (gn < N && k < K) ? *reinterpret_cast<const float4*>(W + (int64_t)gn * ldw + k) : z4;
     }
   };
   auto sstore = [&](int buf) {
 #pragma unroll
-    for (int p = 0; p < PER; ++p) {
-      const int r = lr + p * RPP;
-      if constexpr (BF16) {
-        *reinterpret_cast<bf16x4*>(&As[buf][r][lk]) = to_bf16x4(ra[p]);
-        *reinterpret_cast<bf16x4*>(&Bs[buf][r][lk]) = to_bf16x4(rb[p]);
-      } else {
-        *reinterpret_cast<float4*>(&As[buf][r][lk]) = ra[p];
-        *reinterpret_cast<float4*>(&Bs[buf][r][lk]) = rb[p];
-      }
+    for (int p = 0; p < APER; ++p) {
+      const int i = tid + p * NT, r = i / F4R, k = (i % F4R) * 4;
+      if constexpr (BF16) *reinterpret_cast<bf16x4*>(&As[buf][r][k]) = to_bf16x4(ra[p]);
+      else *reinterpret_cast<float4*>(&As[buf][r][k]) = ra[p];
+    }
+#pragma unroll
+    for (int p = 0; p < BPER; ++p) {
+      const int i = tid + p * NT, r = i / F4R, k = (i % F4R) * 4;
+      if constexpr (BF16) *reinterpret_cast<bf16x4*>(&Bs[buf][r][k]) = to_bf16x4(rb[p]);
+      else *reinterpret_cast<float4*>(&Bs[buf][r][k]) = rb[p];
     }
   };
-  const int wm = (wv & 1) * 64, wn = (wv >> 1) * 64;
+  const int wm = (wv % WM) * 64, wn = (wv / WM) * 64;
   const int li = lane & 15, lq = lane >> 4;
   f32x4 acc[4][4];
 #pragma unroll
@@ -102,30 +100,37 @@ gemm_nt_kernel(const float* __restrict__ X, int ldx, const float* __restrict__ W
     const int buf = s & 1;
     if (s + 1 < nk) gload((s + 1) * BK);        // next stage's loads in flight during the MFMAs
     if constexpr (BF16) {
-      bf16x8 a[4], b[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        a[i] = *reinterpret_cast<const bf16x8*>(&As[buf][wm + 16 * i + li][8 * lq]);
-        b[i] = *reinterpret_cast<const bf16x8*>(&Bs[buf][wn + 16 * i + li][8 * lq]);
-      }
+      for (int kk = 0; kk < BK; kk += 32) {
+        bf16x8 a[4], b[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
-    } else {
-      f32x4 a[4], b[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        a[i] = *reinterpret_cast<const f32x4*>(&As[buf][wm + 16 * i + li][4 * lq]);
-        b[i] = *reinterpret_cast<const f32x4*>(&Bs[buf][wn + 16 * i + li][4 * lq]);
-      }
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
+        for (int i = 0; i < 4; ++i) {
+          a[i] = *reinterpret_cast<const bf16x8*>(&As[buf][wm + 16 * i + li][kk + 8 * lq]);
+          b[i] = *reinterpret_cast<const bf16x8*>(&Bs[buf][wn + 16 * i + li][kk + 8 * lq]);
+        }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][c], b[j][c], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < BK; kk += 16) {
+        f32x4 a[4], b[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          a[i] = *reinterpret_cast<const f32x4*>(&As[buf][wm + 16 * i + li][kk + 4 * lq]);
+          b[i] = *reinterpret_cast<const f32x4*>(&Bs[buf][wn + 16 * i + li][kk + 4 * lq]);
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][c], b[j][c], acc[i][j], 0, 0, 0);
+      }
     }
     if (s + 1 < nk) {
       sstore(buf ^ 1);    // the other buffer: its last readers finished before the previous barrier
@@ -147,17 +152,44 @@ gemm_nt_kernel(const float* __restrict__ X, int ldx, const float* __restrict__ W
     }
 }
 
+template <bool BF16, int WM, int BK>
+static hipError_t launch_gemm(const float* X, int ldx, const float* W, int ldw, float* Y, int ldy, int M, int N, int K,
+                              Epi e, hipStream_t st) {
+  const int64_t tiles = (int64_t)((M + 64 * WM - 1) / (64 * WM)) * ((N + 127) / 128);
+  if (tiles > 0x7fffffff) return hipErrorInvalidValue;
+  gemm_nt_kernel<BF16, WM, BK><<<(unsigned)tiles, 128 * WM, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e);
+  return hipGetLastError();
+}
+
+// Tile form per dtype (variant 10 for A/B: 1..4 = (WM, BK) = (2, 16|32), (2, 32|64), (4, 16|32),
+// (4, 32|64) for fp32|bf16; 0 = the measured default).  Measured on MI355X (TFLOP/s at M 14000,
+// N 5000, K 5408 / 4096^3; profiles/r2_gemm_bench.txt): fp32 73.7 / 75.0 / 89.3 / 73.1 and
+// 84-101; bf16 144-162 (operands converted from fp32 in the staging).  The default is the best
+// of each.  All forms are one-stage-prefetch kernels whose stage compute (2048 cycles fp32,
+// 256-512 bf16) is shorter than a loaded memory round trip: latency-bound, well below
+// hipBLASLt's 141 TF fp32 on the same shapes, which is why the fp32 evaluation product is routed
+// to the library (linear.hip linear_fwd, variant 11) and this kernel serves --dtype bf16.
 hipError_t gemm_nt(const float* X, int ldx, const float* W, int ldw, float* Y, int ldy, int M, int N, int K, Epi e,
                    bool bf16, hipStream_t st) {
   if (M <= 0 || N <= 0) return hipSuccess;
   if ((K & 3) || (ldx & 3) || (ldw & 3)) return hipErrorInvalidValue;
-  const int64_t tiles = (int64_t)((M + 127) / 128) * ((N + 127) / 128);
-  if (tiles > 0x7fffffff) return hipErrorInvalidValue;
-  if (bf16)
-    gemm_nt_kernel<true><<<(unsigned)tiles, 256, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e);
-  else
-    gemm_nt_kernel<false><<<(unsigned)tiles, 256, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e);
-  return hipGetLastError();
+  const int v = g_variant[10];
+  if (bf16) {
+    switch (v) {
+      case 1: return launch_gemm<true, 2, 32>(X, ldx, W, ldw, Y, ldy, M, N, K, e, st);
+      case 2: return launch_gemm<true, 2, 64>(X, ldx, W, ldw, Y, ldy, M, N, K, e, st);
+      case 3: return launch_gemm<true, 4, 32>(X, ldx, W, ldw, Y, ldy, M, N, K, e, st);
+      case 4: return launch_gemm<true, 4, 64>(X, ldx, W, ldw, Y, ldy, M, N, K, e, st);
+      default: return launch_gemm<true, 4, 64>(X, ldx, W, ldw, Y, ldy, M, N, K, e, st);
+    }
+  }
+  switch (v) {
+    case 1: return launch_gemm<false, 2, 16>(X, ldx, W, ldw, Y, ldy, M, N, K, e, st);
+    case 2: return launch_gemm<false, 2, 32>(X, ldx, W, ldw, Y, ldy, M, N, K, e, st);
+    case 3: return launch_gemm<false, 4, 16>(X, ldx, W, ldw, Y, ldy, M, N, K, e, st);
+    case 4: return launch_gemm<false, 4, 32>(X, ldx, W, ldw, Y, ldy, M, N, K, e, st);
+    default: return launch_gemm<false, 4, 16>(X, ldx, W, ldw, Y, ldy, M, N, K, e, st);
+  }
 }
 
 }  // namespace sl

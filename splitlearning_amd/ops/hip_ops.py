@@ -178,8 +178,11 @@ _TABLE: dict = {}
 
 
 # ---------------------------------------------------------------- linear
-# training batches (M <= 128) run the skinny split-K kernels; many rows (evaluation over a
-# test set, large batches) the LDS-tiled MFMA GEMM (csrc/gemm.hip) -- both in-tree HIP.
+# training batches (M <= 128) run the skinny split-K kernels.  Many rows (evaluation over a
+# test set, large batches): in bf16 the in-tree LDS-tiled MFMA GEMM (csrc/gemm.hip); in fp32
+# the plain product goes to hipBLASLt (torch.mm: 141 TFLOP/s on Bob's eval shapes against
+# 89 for the in-tree kernel, profiles/r2_gemm_bench.txt) and the fused epilogue kernel
+# applies bias / ReLU / dropout.  Variant 11 = 1 forces the in-tree GEMM in fp32 too.
 LARGE_M = 128
 
 
@@ -195,6 +198,10 @@ def linear_fwd(x, w, b, relu: bool, drop_p: float, seed: int, col_offset: int = 
         out = torch.empty(M, N, device=x.device, dtype=torch.float32)
     w = w.detach()
     bias = b.detach() if b is not None else None
+    if M > LARGE_M and C().get_compute_dtype() == "fp32" and C().get_variant(11) != 1:
+        P = torch.mm(x, w.t())
+        C().linear_epilogue(P, bias, out, relu, float(drop_p), seed & M64, col_offset, _ptr(dseed))
+        return out
     ws = _fwd_workspace(x.device, 16 * M * N) if M <= LARGE_M else None
     C().linear_fwd(x, w, bias, out, relu, float(drop_p), seed & M64, col_offset, _ptr(dseed), ws)
     return out

@@ -77,15 +77,27 @@ def test_conv_bwd(cuda, kind):
                                     (16, 37, 52), (200, 100, 1000), (1000, 5000, 5408), (8000, 1000, 5000),
                                     (129, 130, 36), (300, 10, 100)])
 @pytest.mark.parametrize("relu,drop", [(False, 0.0), (True, 0.0), (True, 0.5)])
-def test_linear_fwd(cuda, M, N, K, relu, drop):
-    """M <= 128: the skinny split-K kernels; M > 128: the LDS-tiled MFMA GEMM (gemm.hip)."""
+@pytest.mark.parametrize("gemm", [0, 1])
+def test_linear_fwd(cuda, M, N, K, relu, drop, gemm):
+    """M <= 128: the skinny split-K kernels; M > 128: hipBLASLt + the fused epilogue (gemm 0)
+    or the in-tree LDS-tiled MFMA GEMM (gemm 1: variant 11, every tile form of slot 10)."""
+    if gemm and M <= 128:
+        pytest.skip("the tiled GEMM serves M > 128")
     x = torch.randn(M, K, device=cuda)
     w = torch.randn(N, K, device=cuda) / K ** 0.5
     b = torch.randn(N, device=cuda)
     seed = 0x1234_5678_9ABC
-    y = hip_ops.linear_fwd(x, w, b, relu, drop, seed, col_offset=3)
     yr = torch_ops.linear_fwd(x, w, b, relu, drop, seed, col_offset=3)
-    _close(y, yr, rtol=1e-4, atol=1e-4)
+    C = hip_ops.C()
+    C.set_variant(11, gemm)
+    try:
+        for tile in ((0, 1, 2, 3, 4) if gemm else (0,)):
+            C.set_variant(10, tile)
+            y = hip_ops.linear_fwd(x, w, b, relu, drop, seed, col_offset=3)
+            _close(y, yr, rtol=1e-4, atol=1e-4)
+    finally:
+        C.set_variant(11, 0)
+        C.set_variant(10, 0)
 
 
 @pytest.mark.parametrize("M,N,K", [(16, 5000, 5408), (16, 1000, 5000), (16, 100, 1000), (16, 10, 100),
