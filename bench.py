@@ -95,7 +95,8 @@ def main(argv=None):
     ap.add_argument("--partition_alpha", type=float, default=0.5)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--kernels", choices=("auto", "hip", "torch"), default="auto")
-    ap.add_argument("--bob_tp", type=int, default=0, help="0 = all ranks")
+    ap.add_argument("--bob_tp", type=int, default=0,
+                    help="0 = the policy (parallel/dist.py choose_bob_tp: all GPUs for the SISA modes)")
     ap.add_argument("--graphs", choices=("auto", "on", "off"), default="auto")
     ap.add_argument("--act_dtype", choices=("fp32", "bf16"), default="fp32")
     ap.add_argument("--dtype", choices=("fp32", "bf16"), default="fp32", help="compute dtype")
@@ -109,7 +110,7 @@ def main(argv=None):
     from splitlearning_amd import ops
     from splitlearning_amd.config import parse_args
     from splitlearning_amd.data.mnist import make_client_shards, synthetic_mnist
-    from splitlearning_amd.parallel.dist import Comm, Placement, make_tp_group
+    from splitlearning_amd.parallel.dist import Comm, Placement, choose_bob_tp, make_tp_group
     from splitlearning_amd.protocols import SESSIONS
     from splitlearning_amd.protocols.schedule import build_steps
 
@@ -145,7 +146,7 @@ def main(argv=None):
     if a.mode == "concat" and a.concat_unlearn:
         argv_s.append("--concat_unlearn")
     sargs = parse_args(argv_s)
-    pl = Placement.make(ws, N, a.bob_tp if a.bob_tp > 0 else N)
+    pl = Placement.make(ws, N, a.bob_tp if a.bob_tp > 0 else (choose_bob_tp(sargs.mode, N) if use_gpu else N))
     comm = Comm(rank, N, dev, pl, make_tp_group(pl, "nccl" if use_gpu else "gloo") if N > 1 else None)
     k = ws - 1
 

@@ -118,6 +118,13 @@ def build_parser() -> argparse.ArgumentParser:
     g.add_argument("--python_epoch", dest="native_epoch", action="store_false",
                    help="issue Bob's eager server steps from Python instead of the native "
                         "executor (_C.ServerEpoch); numerics are identical")
+    g.add_argument("--torch_p2p", dest="native_comm", action="store_false",
+                   help="GPU: move data-plane messages with torch.distributed isend/irecv instead of "
+                        "the native RCCL communicators (per-batch p2p on the compute stream, TP "
+                        "all-reduce inside the server step)")
+    g.add_argument("--msg_log", action="store_true",
+                   help="record every data-plane message (op, src, dst, bytes) of this rank in "
+                        "<log_dir>/messages_rank<r>.json (tests pin the per-batch message sequence)")
     g.add_argument("--serial_alices", dest="multi_alice", action="store_false",
                    help="step co-located Alices' SISA local epochs one after another instead of "
                         "together (one launch per step for all of them); numerics are identical")

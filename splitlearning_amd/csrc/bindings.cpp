@@ -599,6 +599,41 @@ void server_head3(const at::Tensor& P2, const OptT& b2, bool relu2, double drop2
         "server_head3");
 }
 
+// Single-shard server head from fc1's output: fc2 forward (full K per workgroup) + fc2
+// epilogue + partial fc3 logits in one launch, then the softmax-CE / fc3-dgrad kernel
+// (fused.hip server_fc2_head).  Returns nothing; writes h2, dlog, dz2, loss_rows.
+void server_fc2_head(const at::Tensor& h1, const at::Tensor& W2, const OptT& b2, bool relu2, double drop2,
+                     uint64_t seed2, int64_t dseed2, const at::Tensor& W3, const OptT& b3, const at::Tensor& y,
+                     int64_t ignore, double scale, at::Tensor& h2, at::Tensor& dlog, at::Tensor& dz2,
+                     at::Tensor& loss_rows, at::Tensor& ws) {
+  need_rows(h1, "h1");
+  need_rows(W2, "W2");
+  const int64_t M = h1.size(0), K = h1.size(1), N2 = W2.size(0);
+  TORCH_CHECK(W2.size(1) == K && K % 4 == 0, "W2 [N2, K]");
+  need_rows(W3, "W3");
+  const int64_t C = W3.size(0);
+  TORCH_CHECK(W3.size(1) == N2 && N2 % 4 == 0 && C <= 4096, "W3 [C, N2], N2 % 4 == 0");
+  need_f32(ws, "ws");
+  TORCH_CHECK(ws.is_contiguous() && ws.numel() >= (int64_t)sl::fc2_head_tiles((int)N2) * M * C, "head workspace");
+  need_cuda(y, "labels");
+  TORCH_CHECK(y.scalar_type() == at::kLong && y.numel() == M && y.is_contiguous(), "labels int64 [M]");
+  for (auto* t : {&h2, &dz2}) {
+    need_f32(*t, "h2/dz2");
+    TORCH_CHECK(t->is_contiguous() && t->size(0) == M && t->size(1) == N2, "h2/dz2 [M,N2]");
+  }
+  need_f32(dlog, "dlog");
+  TORCH_CHECK(dlog.is_contiguous() && dlog.size(0) == M && dlog.size(1) == C, "dlog [M,C]");
+  need_f32(loss_rows, "loss_rows");
+  TORCH_CHECK(loss_rows.numel() >= M, "loss_rows");
+  if (b2.has_value() && b2->defined()) TORCH_CHECK(b2->numel() == N2, "b2 [N2]");
+  check(sl::server_fc2_head(h1.data_ptr<float>(), (int)h1.stride(0), W2.data_ptr<float>(), (int)W2.stride(0),
+                            make_epi(b2, relu2, drop2, seed2, 0, dseed2), W3.data_ptr<float>(), (int)W3.stride(0),
+                            fptr(b3), y.data_ptr<int64_t>(), ignore, (float)scale, h2.data_ptr<float>(),
+                            dlog.data_ptr<float>(), dz2.data_ptr<float>(), loss_rows.data_ptr<float>(),
+                            ws.data_ptr<float>(), ws.numel(), (int)M, (int)K, (int)N2, (int)C, cur_stream()),
+        "server_fc2_head");
+}
+
 // layers: up to 3 tuples (dz, dzp, hmask, mscale, A, W, s0, s1, bias, sb0, sb1); exactly one of dz / dzp
 // (dzp = [S, M, N] split-N partial slabs of the layer's output gradient, masked by hmask > 0).
 // xn / pn (optional): next batch [mn, K0] -> its split-K partial pre-activations of layer 0
@@ -699,6 +734,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("relu_mask", &relu_mask);
   m.def("server_head3", &server_head3);
   m.def("head3_slices", [](int64_t n2) { return (int64_t)sl::head3_slices((int)n2); });
+  m.def("server_fc2_head", &server_fc2_head);
+  m.def("fc2_head_tiles", [](int64_t n2) { return (int64_t)sl::fc2_head_tiles((int)n2); });
   m.def("linear_fwd_partial", &linear_fwd_partial);
   m.def("linear_dgrad_partial", &linear_dgrad_partial);
   m.def("wgrad_group", &wgrad_group);

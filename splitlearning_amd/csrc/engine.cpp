@@ -121,7 +121,9 @@ class ServerEpoch {
     TORCH_CHECK(h2_.numel() >= (int64_t)B_ * L_[1].N && dz2_.numel() >= (int64_t)B_ * L_[1].N, "h2 / dz2");
     TORCH_CHECK(dlog_.numel() >= (int64_t)B_ * L_[2].N, "dlog");
     TORCH_CHECK(p2ws_.numel() >= 16LL * B_ * L_[1].N, "fc2 slab workspace");
-    TORCH_CHECK(headws_.numel() >= (int64_t)sl::head3_slices(L_[1].N) * B_ * L_[2].N, "head workspace");
+    TORCH_CHECK(headws_.numel() >= (int64_t)std::max(sl::head3_slices(L_[1].N), sl::fc2_head_tiles(L_[1].N)) * B_ *
+                                        L_[2].N,
+                "head workspace");
   }
 
   // One epoch over acts [n, K1] / labels [n] in batches of B.  `pre`: fc1's product for the
@@ -201,6 +203,7 @@ class ServerEpoch {
                         fwdws_.numel(), sm),
          "fc1 forward");
     S2_ = 1;
+    if (fuse_head()) return;              // fc2's product is formed by the fused head (finish)
     if (row2_) {
       if (N1 <= 1280) {
         ck(sl::linear_fwd_partial(h1, N1, L_[1].W.data_ptr<float>(), N1, M, N2, N1, P2, p2ws_.numel(), 1, &S2_, sm),
@@ -235,11 +238,18 @@ class ServerEpoch {
     float* dlog = dlog_.data_ptr<float>();
     const double s1 = p1_ > 0 ? 1.0 / (1.0 - p1_) : 1.0;
     const Epi e2 = sl::make_epi_raw(L_[1].b.data_ptr<float>(), true, p2_, st.sd1, 0, nullptr);
-    ck(sl::server_head3(p2ws_.data_ptr<float>(), S2_, (int64_t)M * N2, e2, L_[2].W.data_ptr<float>(), N2,
-                        L_[2].b.data_ptr<float>(), st.labels->data_ptr<int64_t>() + st.s, -100, (float)(1.0 / M), h2,
-                        dlog, dz2, loss_rows.data_ptr<float>() + st.s, headws_.data_ptr<float>(), headws_.numel(), M,
-                        N2, C, sm),
-       "server head");
+    if (fuse_head())
+      ck(sl::server_fc2_head(h1, N1, L_[1].W.data_ptr<float>(), N1, e2, L_[2].W.data_ptr<float>(), N2,
+                             L_[2].b.data_ptr<float>(), st.labels->data_ptr<int64_t>() + st.s, -100, (float)(1.0 / M),
+                             h2, dlog, dz2, loss_rows.data_ptr<float>() + st.s, headws_.data_ptr<float>(),
+                             headws_.numel(), M, N1, N2, C, sm),
+         "server fc2 + head");
+    else
+      ck(sl::server_head3(p2ws_.data_ptr<float>(), S2_, (int64_t)M * N2, e2, L_[2].W.data_ptr<float>(), N2,
+                          L_[2].b.data_ptr<float>(), st.labels->data_ptr<int64_t>() + st.s, -100, (float)(1.0 / M),
+                          h2, dlog, dz2, loss_rows.data_ptr<float>() + st.s, headws_.data_ptr<float>(),
+                          headws_.numel(), M, N2, C, sm),
+         "server head");
     ck(sl::linear_dgrad(dz2, N2, L_[1].W.data_ptr<float>(), N1, h1, N1, (float)s1, dz1, N1, dgws_.data_ptr<float>(),
                         dgws_.numel(), M, N2, N1, sm),
        "fc2 dgrad");
@@ -279,6 +289,9 @@ class ServerEpoch {
   }
 
   at::Tensor product_view(int M) const { return p2ws_.narrow(0, 0, (int64_t)M * L_[1].N); }
+  // single-shard tail: fc2's forward fused into the head (fused.hip fc2_head_fwd_kernel);
+  // variant 12 = 1 keeps the split-K fc2 forward + head_fwd pair (A/B)
+  bool fuse_head() const { return !row2_ && sl::g_variant[12] != 1; }
   bool row_parallel() const { return row2_; }
   int batch() const { return B_; }
 

@@ -48,5 +48,10 @@ hipError_t server_head3(const float* P2, int S2, int64_t slab2, Epi e2, const fl
                         const int64_t* y, int64_t ignore, float scale, float* h2, float* dlog, float* dz2,
                         float* loss_rows, float* ws, int64_t ws_elems, int M, int N2, int C, hipStream_t st);
 hipError_t wgrad_group(const WgGroup& g, int M, SlOpt o, hipStream_t st);
+int fc2_head_tiles(int N2);
+hipError_t server_fc2_head(const float* X, int ldx, const float* W2, int ldw2, Epi e2, const float* W3, int ldw3,
+                           const float* b3, const int64_t* y, int64_t ignore, float scale, float* h2, float* dlog,
+                           float* dz2, float* loss_rows, float* ws, int64_t ws_elems, int M, int K, int N2, int C,
+                           hipStream_t st);
 
 }  // namespace sl

@@ -108,13 +108,114 @@ head_fwd_kernel(const float* __restrict__ P2, int S2, int64_t slab2, Epi e2, con
   }
 }
 
+// fc2_head_fwd_kernel (single-shard tail, fc2 not row-parallel): fc2's forward WITHOUT
+// split-K — a workgroup owns NT = 8 output columns and reduces the whole K inside itself (16
+// waves x 1/16 of K, exact-fp32 MFMA, LDS sum) — so it can apply fc2's bias / ReLU /
+// dropout (-> h2) and form its columns' share of the fc3 logits (plog[tile][m][c]) itself.
+// Replaces the split-K fc2 forward + head_fwd pair (two launches and a slab round trip).
+// grid (ceil(N/8), ceil(M/16)), 1024 threads.  bf: bf16 compute (operands rounded).
+template <int NT>
+__global__ void __launch_bounds__(1024)
+fc2_head_fwd_kernel(const float* __restrict__ X, int ldx, const float* __restrict__ W, int ldw, Epi e,
+                    const float* __restrict__ W3, int ldw3, float* __restrict__ h2, float* __restrict__ plog, int M,
+                    int N, int K, int C, int bf) {
+  __shared__ f32x4 red[16][64];
+  __shared__ float sh[16][NT];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, tid = threadIdx.x;
+  const int n0 = blockIdx.x * NT, m0 = blockIdx.y * 16, tile = blockIdx.x;
+  const int li = lane & 15, q = lane >> 4;
+  const bool va = m0 + li < M, vb = li < NT && n0 + li < N;
+  const float* pa = X + (int64_t)(va ? m0 + li : 0) * ldx;
+  const float* pb = W + (int64_t)(vb ? n0 + li : 0) * ldw;
+  const int kper = ((K + 16 * 16 - 1) / (16 * 16)) * 16;
+  const int kb = wv * kper, ke = min(K, kb + kper);
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  constexpr int U = 8;
+  int k = kb;
+  for (; k + 16 * U <= ke; k += 16 * U) {
+    float4 a[U], w[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int kk = k + 16 * u + 4 * q;
+      a[u] = va ? *reinterpret_cast<const float4*>(pa + kk) : z4;
+      w[u] = vb ? *reinterpret_cast<const float4*>(pb + kk) : z4;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (bf) {
+        a[u] = bfr4(a[u]);
+        w[u] = bfr4(w[u]);
+      }
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u].x, w[u].x, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u].y, w[u].y, acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u].z, w[u].z, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u].w, w[u].w, acc1, 0, 0, 0);
+    }
+  }
+  for (; k < ke; k += 16) {
+    const int kk = k + 4 * q;
+    const bool in = kk < ke;
+    float4 a = (va && in) ? *reinterpret_cast<const float4*>(pa + kk) : z4;
+    float4 w = (vb && in) ? *reinterpret_cast<const float4*>(pb + kk) : z4;
+    if (bf) {
+      a = bfr4(a);
+      w = bfr4(w);
+    }
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, w.x, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, w.y, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, w.z, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, w.w, acc1, 0, 0, 0);
+  }
+  red[wv][lane] = acc0 + acc1;
+  __syncthreads();
+  // lane (li = column, q): rows 4q + r.  Waves are summed in order 0..15 (deterministic).
+  if (wv == 0) {
+    f32x4 sum = red[0][lane];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) sum += red[i][lane];
+    if (li < NT) {
+      const int n = n0 + li;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + 4 * q + r;
+        float v = 0.f;
+        if (n < N && m < M) {
+          v = apply_epi(e, sum[r], m, n);
+          h2[(int64_t)m * N + n] = v;
+        }
+        sh[4 * q + r][li] = v;
+      }
+    }
+  }
+  __syncthreads();
+  // this tile's share of the fc3 logits: plog[tile][m][c] = sum_j h2[m][n0 + j] * W3[c][n0 + j]
+  for (int i = tid; i < 16 * C; i += 1024) {
+    const int mm = i / C, c = i - mm * C;
+    const int m = m0 + mm;
+    if (m >= M) continue;
+    float d = 0.f;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int n = n0 + j;
+      if (n < N) {
+        const float w3 = W3[(int64_t)c * ldw3 + n];
+        d = fmaf(bf ? bfr(sh[mm][j]) : sh[mm][j], bf ? bfr(w3) : w3, d);
+      }
+    }
+    plog[((int64_t)tile * M + m) * C + c] = d;
+  }
+}
+
 // head_bwd_kernel: workgroup (m, q) sums row m's partial logits (+ b3), softmax-CE (loss and
 // dlogits written by q == 0), then dz2 = (dlogits . W3) * dscale * [h2 > 0] for its slice.
 __global__ void __launch_bounds__(256)
 head_bwd_kernel(const float* __restrict__ plog, const float* __restrict__ b3, const float* __restrict__ W3,
                 int ldw3, const int64_t* __restrict__ y, int64_t ignore, float scale, float dscale,
                 const float* __restrict__ h2, float* __restrict__ dlog, float* __restrict__ dz2,
-                float* __restrict__ loss_rows, int M, int N2, int C, int bf) {
+                float* __restrict__ loss_rows, int M, int N2, int C, int bf, int Qp) {
+  // Qp: number of partial-logit slabs in plog (head_fwd: one per column slice = gridDim.y;
+  // fc2_head_fwd: one per 8-column tile)
   extern __shared__ float lg[];   // C
   __shared__ f32x4 part[8][HS];
   const int m = blockIdx.x, q = blockIdx.y, Q = gridDim.y, tid = threadIdx.x;
@@ -140,7 +241,7 @@ head_bwd_kernel(const float* __restrict__ plog, const float* __restrict__ b3, co
   for (int o = tid; o < C; o += 256) {
     float v = b3 ? b3[o] : 0.f;
 #pragma unroll 8
-    for (int s = 0; s < Q; ++s) v += plog[((int64_t)s * M + m) * C + o];
+    for (int s = 0; s < Qp; ++s) v += plog[((int64_t)s * M + m) * C + o];
     lg[o] = v;
   }
   __syncthreads();
@@ -481,7 +582,26 @@ hipError_t server_head3(const float* P2, int S2, int64_t slab2, Epi e2, const fl
   if (ws_elems < (int64_t)Q * M * C) return hipErrorInvalidValue;
   head_fwd_kernel<<<dim3(M, Q), 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C, g_bf16);
   head_bwd_kernel<<<dim3(M, Q), 256, (size_t)C * sizeof(float), st>>>(ws, b3, W3, ldw3, y, ignore, scale, e2.dscale,
-                                                                      h2, dlog, dz2, loss_rows, M, N2, C, g_bf16);
+                                                                      h2, dlog, dz2, loss_rows, M, N2, C, g_bf16, Q);
+  return hipGetLastError();
+}
+
+int fc2_head_tiles(int N2) { return (N2 + 7) / 8; }
+
+// fc2 forward (full K per workgroup) + fc2 epilogue + partial fc3 logits in one launch, then
+// head_bwd: the single-shard server head in 2 launches instead of fc2 forward + 2.
+hipError_t server_fc2_head(const float* X, int ldx, const float* W2, int ldw2, Epi e2, const float* W3, int ldw3,
+                           const float* b3, const int64_t* y, int64_t ignore, float scale, float* h2, float* dlog,
+                           float* dz2, float* loss_rows, float* ws, int64_t ws_elems, int M, int K, int N2, int C,
+                           hipStream_t st) {
+  if (M <= 0) return hipSuccess;
+  if ((N2 & 3) || (ldw3 & 3) || (K & 3) || (ldx & 3) || (ldw2 & 3)) return hipErrorInvalidValue;
+  const int T = fc2_head_tiles(N2), Q = head3_slices(N2);
+  if (ws_elems < (int64_t)T * M * C) return hipErrorInvalidValue;
+  fc2_head_fwd_kernel<8><<<dim3(T, (M + 15) / 16), 1024, 0, st>>>(X, ldx, W2, ldw2, e2, W3, ldw3, h2, ws, M, N2, K, C,
+                                                                  g_bf16);
+  head_bwd_kernel<<<dim3(M, Q), 256, (size_t)C * sizeof(float), st>>>(ws, b3, W3, ldw3, y, ignore, scale, e2.dscale,
+                                                                      h2, dlog, dz2, loss_rows, M, N2, C, g_bf16, T);
   return hipGetLastError();
 }
 

@@ -264,7 +264,11 @@ class TailEngine:
         else:
             self._pre = None
             h1 = ops.linear_fwd(x, L1.W, L1.b, True, p1, seeds[0], L1.col_off, **ds(0))
-        if L2.style == "row":
+        if L2.style != "row" and hasattr(ops, "server_fc2_head") and ops.C().get_variant(12) != 1:
+            # single shard: fc2's forward is fused into the head (one launch less, no slabs)
+            h2, dlog, dz2, loss = ops.server_fc2_head(h1, L2.W, L2.b, True, p2, seeds[1], L3.W, L3.b, labels,
+                                                      1.0 / M, **ds(1))
+        elif L2.style == "row":
             if L2.W.shape[1] <= 1280:
                 # small K shard (TP >= 4): one unsplit product, all-reduced as is — no
                 # split-K reduce launch before the collective
@@ -274,7 +278,9 @@ class TailEngine:
             self.allreduce(P2)
         else:
             P2 = ops.linear_fwd_partial(h1, L2.W)
-        h2, dlog, dz2, loss = ops.server_head3(P2, L2.b, True, p2, seeds[1], L3.W, L3.b, labels, 1.0 / M, **ds(1))
+        if L2.style == "row" or not hasattr(ops, "server_fc2_head") or ops.C().get_variant(12) == 1:
+            h2, dlog, dz2, loss = ops.server_head3(P2, L2.b, True, p2, seeds[1], L3.W, L3.b, labels, 1.0 / M,
+                                                   **ds(1))
         s1 = 1.0 / (1.0 - p1) if p1 else 1.0
         dx = None
         # dz1 is materialised (split-N dgrad + reduce/mask kernel): reducing the split-N
@@ -365,7 +371,8 @@ class TailEngine:
              "pn": self.lookahead_slabs(B), "p2ws": ops._workspace(dev, 16 * B * N2, "fc2p" + tg),
              "fwdws": ops._workspace(dev, 16 * B * nmax, "fwd" + tg),
              "dgws": ops._workspace(dev, 16 * B * kmax, "dgrad" + tg),
-             "headws": ops._workspace(dev, ops.C().head3_slices(N2) * B * C, "head" + tg),
+             "headws": ops._workspace(dev, max(ops.C().head3_slices(N2), ops.C().fc2_head_tiles(N2)) * B * C,
+                                      "head" + tg),
              "h1": torch.empty(B, N1, device=dev), "h2": torch.empty(B, N2, device=dev),
              "dz1": torch.empty(B, N1, device=dev), "dz2": torch.empty(B, N2, device=dev),
              "dlog": torch.empty(B, C, device=dev)}

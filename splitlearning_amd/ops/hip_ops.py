@@ -307,6 +307,23 @@ def server_head3(P2, b2, relu2: bool, drop2: float, seed2: int, W3, b3, labels, 
     return h2, dlog, dz2, loss
 
 
+def server_fc2_head(h1, W2, b2, relu2: bool, drop2: float, seed2: int, W3, b3, labels, scale: float,
+                    ignore_index: int = -100, dseed=None):
+    """Single-shard server head from fc1's output: fc2 forward + epilogue + fc3 + softmax-CE +
+    fc3 dgrad + fc2 ReLU/dropout backward in two launches.  Returns (h2, dlogits, dz2, loss_rows)."""
+    M, N2 = h1.shape[0], W2.shape[0]
+    dev = h1.device
+    h2 = torch.empty(M, N2, device=dev)
+    dz2 = torch.empty(M, N2, device=dev)
+    dlog = torch.empty(M, W3.shape[0], device=dev)
+    loss = torch.empty(M, device=dev)
+    ws = _workspace(dev, max(C().head3_slices(N2), C().fc2_head_tiles(N2)) * M * W3.shape[0], "head")
+    C().server_fc2_head(h1, W2.detach(), b2.detach() if b2 is not None else None, relu2, float(drop2), seed2 & M64,
+                        _ptr(dseed), W3.detach(), b3.detach() if b3 is not None else None, labels, int(ignore_index),
+                        float(scale), h2, dlog, dz2, loss, ws)
+    return h2, dlog, dz2, loss
+
+
 def lookahead_slabs(device, K0: int, mn: int, N0: int, tag: str = ""):
     """Workspace for wgrad_group_'s look-ahead forward: [ceil(K0/256), mn, N0]."""
     S = (K0 + 255) // 256

@@ -106,6 +106,20 @@ class Comm:
         self.msgs_sent = 0
         self.progress = _noop        # watchdog tick (runtime/watchdog.py), called per data-plane op
         self.tracer = NULL_TRACER    # utils/trace.py: one "comm" span per data-plane op
+        # GPU data plane: a native RCCL communicator over ALL ranks (`_C.TpComm`, set by the
+        # session).  Every p2p op below is then issued from C++ on the current HIP stream,
+        # grouped, without a host-side wait (torch.distributed isend/irecv + req.wait() from
+        # Python otherwise).  None on CPU (gloo).
+        self.native = None
+        self.msg_log = None          # list of (op, src, dst, nbytes) when a test enables it
+
+    def _count(self, t: torch.Tensor, n: int, op: str, dst=None):
+        nb = t.numel() * t.element_size()
+        self.bytes_sent += nb * n
+        self.msgs_sent += n
+        if self.msg_log is not None:
+            for d in (dst if isinstance(dst, (list, tuple)) else [dst]):
+                self.msg_log.append((op, self.rank, d, nb))
 
     @property
     def distributed(self) -> bool:
@@ -117,18 +131,27 @@ class Comm:
         """`src` sends `t` to every rank in `dsts` (concurrent p2p).  Returns the tensor on
         src and on each dst (freshly received), None elsewhere."""
         dsts = [d for d in dict.fromkeys(dsts) if d != src]
+        nat = self.native
         if self.rank == src:
             if dsts:
                 t = t.contiguous()
-                reqs = [dist.isend(t, d) for d in dsts]
-                for r in reqs:
-                    r.wait()
-                self.bytes_sent += t.numel() * t.element_size() * len(dsts)
-                self.msgs_sent += len(dsts)
+                if nat is not None:
+                    nat.group_start()
+                    for d in dsts:
+                        nat.send(t, d)
+                    nat.group_end()
+                else:
+                    reqs = [dist.isend(t, d) for d in dsts]
+                    for r in reqs:
+                        r.wait()
+                self._count(t, len(dsts), "multicast", dsts)
             return t
         if self.rank in dsts:
             buf = torch.empty(shape, dtype=dtype, device=self.device)
-            dist.recv(buf, src)
+            if nat is not None:
+                nat.recv(buf, src)
+            else:
+                dist.recv(buf, src)
             return buf
         return None
 
@@ -138,16 +161,25 @@ class Comm:
         `recvs` = [(buffer, src)] (this rank's side of every pair).  All transfers are
         posted together (RCCL groups them), so distinct peers' xGMI links run
         concurrently instead of one message after another."""
-        ops = [dist.P2POp(dist.isend, t.contiguous(), d) for t, d in sends if d != self.rank]
-        ops += [dist.P2POp(dist.irecv, b, s) for b, s in recvs if s != self.rank]
-        if not ops:
+        sends = [(t.contiguous(), d) for t, d in sends if d != self.rank]
+        recvs = [(b, s) for b, s in recvs if s != self.rank]
+        if not sends and not recvs:
             return
-        for r in dist.batch_isend_irecv(ops):
-            r.wait()
+        if self.native is not None:
+            nat = self.native
+            nat.group_start()
+            for t, d in sends:
+                nat.send(t, d)
+            for b, s in recvs:
+                nat.recv(b, s)
+            nat.group_end()
+        else:
+            ops = [dist.P2POp(dist.isend, t, d) for t, d in sends]
+            ops += [dist.P2POp(dist.irecv, b, s) for b, s in recvs]
+            for r in dist.batch_isend_irecv(ops):
+                r.wait()
         for t, d in sends:
-            if d != self.rank:
-                self.bytes_sent += t.numel() * t.element_size()
-                self.msgs_sent += 1
+            self._count(t, 1, "exchange", d)
 
     @_dataplane
     def reduce_to_async(self, t: torch.Tensor | None, dst: int, srcs, shape=None, dtype=None):
@@ -157,12 +189,21 @@ class Comm:
         transfer of the cut-layer gradient."""
         srcs = list(dict.fromkeys(srcs))
         others = [s for s in srcs if s != dst]
+        nat = self.native
         if self.rank == dst:
             mine = t if self.rank in srcs else None
             if not others:
                 return lambda: mine
             bufs = [torch.empty(shape, dtype=dtype, device=self.device) for _ in others]
-            reqs = [dist.irecv(b, s) for b, s in zip(bufs, others)]
+            if nat is not None:
+                # every partial arrives on the compute stream; the sum is stream-ordered after it
+                nat.group_start()
+                for b, s in zip(bufs, others):
+                    nat.recv(b, s)
+                nat.group_end()
+                reqs = []
+            else:
+                reqs = [dist.irecv(b, s) for b, s in zip(bufs, others)]
 
             def finish():
                 for r in reqs:
@@ -174,9 +215,11 @@ class Comm:
             return finish
         if self.rank in others:
             t = t.contiguous()
+            self._count(t, 1, "reduce_to", dst)
+            if nat is not None:
+                nat.send(t, dst)
+                return lambda: None
             req = dist.isend(t, dst)
-            self.bytes_sent += t.numel() * t.element_size()
-            self.msgs_sent += 1
 
             def finish_send():
                 req.wait()
@@ -192,13 +235,19 @@ class Comm:
         if src == dst:
             return t
         if self.rank == src:
-            dist.send(t.contiguous(), dst)
-            self.bytes_sent += t.numel() * t.element_size()
-            self.msgs_sent += 1
+            t = t.contiguous()
+            if self.native is not None:
+                self.native.send(t, dst)
+            else:
+                dist.send(t, dst)
+            self._count(t, 1, "send_recv", dst)
             return t
         if self.rank == dst:
             buf = torch.empty(shape, dtype=dtype, device=self.device)
-            dist.recv(buf, src)
+            if self.native is not None:
+                self.native.recv(buf, src)
+            else:
+                dist.recv(buf, src)
             return buf
         return None
 
@@ -251,6 +300,39 @@ class Comm:
                 dist.barrier(device_ids=[self.device.index])
             else:
                 dist.barrier()
+
+
+# Bob's TP degree policy (`--bob_tp 0`).  SISA / concat / control: all GPUs — the server phase
+# is Bob-local (no per-batch messages), so a shard's share of the optimizer stream is pure
+# gain and the only added cost is one fc2 all-reduce per step.  The serial split modes move
+# messages every batch, and each extra TP rank adds message rounds on the critical path:
+# the fc2 all-reduce, the activation multicast to the shards and the reduction of their
+# partial cut gradients (U-shape also multicasts the head's gradient and returns the
+# middle's output).  Cost model per batch, us:
+#     t(T) = STREAM_B * params / T / HBM  +  rounds(T) * MSG_US
+# STREAM_B = bytes per parameter per step (SGD-m 16 + the fc1 forward read 4 without the
+# look-ahead, Adam 24 + 4); HBM = 5.5 TB/s (the fused wgrad stream, docs/PERF.md);
+# MSG_US = 20 us per p2p / small-collective round on xGMI (RCCL launch + latency, assumed:
+# no multi-GPU box was available to measure it).  T = 1 keeps the Alice <-> Bob pair's own
+# rounds (2 vanilla, 4 U-shape) for a remote Alice and none for the co-located one.
+MSG_US = 20.0
+HBM_BPS = 5.5e12
+_SERIAL = {"vanilla": (32.146e6, 20, 2, 3), "ushape": (5.509e6, 28, 4, 5)}   # params, B/param, rounds T=1, T>1
+
+
+def choose_bob_tp(mode: str, nprocs: int) -> int:
+    """Bob's tensor-parallel degree for `mode` on `nprocs` GPUs (see the cost model above)."""
+    if nprocs <= 1:
+        return 1
+    if mode not in _SERIAL:
+        return nprocs
+    params, bpp, r1, rt = _SERIAL[mode]
+    remote = (nprocs - 1) / nprocs                 # Alices round-robin over the GPUs; Bob on rank 0
+
+    def cost(T):
+        return bpp * params / T / HBM_BPS * 1e6 + (rt if T > 1 else r1 * remote) * MSG_US
+    cands = [T for T in (1, 2, 4, 8, 16) if T <= nprocs and nprocs % T == 0] or [1]
+    return min(cands, key=lambda T: (cost(T), T))
 
 
 def init_process(rank: int, world: int, backend: str, addr: str, port: int, timeout_s: float,

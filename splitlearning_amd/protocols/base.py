@@ -78,6 +78,7 @@ class Session:
         self._build_alices()
         self._exchange_meta()
         self.is_bob = self.pl.is_bob(self.rank)
+        self._native_data_plane()                          # collective over all ranks
         self.tp_allreduce = self._tp_allreduce()          # collective over all ranks
         self.tail: TailEngine | None = None
         self.bob_slots: dict = {}
@@ -148,6 +149,15 @@ class Session:
         dist.all_gather_object(out, obj)
         return out
 
+    def _native_data_plane(self):
+        """GPU, several processes: every p2p transfer (per-batch activation + labels, cut
+        gradients, weight relay, SISA dump, eval traffic) through a native RCCL communicator
+        over all ranks, issued on the compute stream (parallel/dist.py Comm.native)."""
+        if (self.device.type == "cuda" and self.comm.distributed and self.comm.native is None
+                and getattr(self.args, "native_comm", True)):
+            from ..parallel.rccl import make_native_comm
+            self.comm.native = make_native_comm(list(range(self.comm.world)), self.rank)
+
     def _tp_allreduce(self):
         """Bob's TP all-reduce: a native RCCL communicator on GPUs (capturable in the
         server-step graph), the torch.distributed group otherwise (gloo on CPU)."""
@@ -194,6 +204,16 @@ class Session:
         if self.hosts(cid) and self.rank == self.pl.bob_root:
             return t
         return out
+
+    def split_lookahead(self, cid: int) -> bool:
+        """Whether a split-mode epoch of Alice_cid may use Bob's fc1 look-ahead (Bob's update of
+        batch i waits for Alice's forward of batch i+1 so its kernel can pre-form that batch's
+        fc1 product).  Only when Bob is entirely on Alice_cid's own GPU: there the launches are
+        serial anyway and the look-ahead just removes fc1's forward read.  With Bob (or a TP
+        shard) on another GPU it would put the whole cut-gradient round trip (reduce to Alice,
+        her backward and next forward, the activation multicast) in front of Bob's wgrad;
+        without it Bob's wgrad + optimizer overlaps exactly that round trip."""
+        return set(self.bob_ranks) == {self.host(cid)}
 
     @property
     def act_dtype(self):

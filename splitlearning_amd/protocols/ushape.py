@@ -138,6 +138,7 @@ class UShapeSession(Session):
         if not spans:
             return
         grouped = self.is_bob and self.tail.grouped_ok()
+        la = self.split_lookahead(cid)
 
         def alice_fwd(span):
             s, e = span
@@ -168,7 +169,7 @@ class UShapeSession(Session):
             pre = False
             if self.is_bob:
                 if grouped:
-                    x_next = nxt[4] if (nxt is not None and self.tail.grouped_ok(nxt[4].shape[0])) else None
+                    x_next = nxt[4] if (la and nxt is not None and self.tail.grouped_ok(nxt[4].shape[0])) else None
                     self.tail.group_step(self.bob_slot(cid), x_next=x_next)
                     pre = x_next is not None
                 else:

@@ -87,7 +87,7 @@ class VanillaSession(Session):
         spans = [(s, min(s + B, n)) for s in range(0, n, B)]
         if not spans:
             return
-        la = self.is_bob and self.tail.fused3_ok() and self.tail.lookahead_ok(B)
+        la = self.is_bob and self.tail.fused3_ok() and self.tail.lookahead_ok(B) and self.split_lookahead(cid)
 
         def alice_fwd(span):
             s, e = span

@@ -46,7 +46,8 @@ def resolve(args):
     if args.backend == "auto":
         args.backend = "nccl" if use_gpu else "gloo"
     if args.bob_tp <= 0:
-        args.bob_tp = args.nprocs if use_gpu else 1
+        from ..parallel.dist import choose_bob_tp
+        args.bob_tp = choose_bob_tp(args.mode, args.nprocs) if use_gpu else 1
     if args.kernels == "torch":
         from .. import ops
         ops.set_backend("torch")
@@ -101,6 +102,8 @@ def worker(rank: int, nprocs: int, args, result_q=None):
         init_process(rank, nprocs, args.backend, args.master_addr, args.master_port, args.timeout_s, dev)
         tp_group = make_tp_group(pl, args.backend)
     comm = Comm(rank, nprocs, dev, pl, tp_group)
+    if getattr(args, "msg_log", False):
+        comm.msg_log = []
     if getattr(args, "prep_in_worker", False) and getattr(args, "ckpt_dir", ""):
         # torchrun: every rank ran main(); rank 0's view of job.json is the agreed seed
         if rank == 0:
@@ -132,6 +135,9 @@ def worker(rank: int, nprocs: int, args, result_q=None):
         if result_q is not None:
             result_q.put({"phases": out["phases"], **extra})
     sess.tracer.dump()
+    if comm.msg_log is not None:
+        with open(os.path.join(args.log_dir, f"messages_rank{rank}.json"), "w") as f:
+            json.dump(comm.msg_log, f)
     sess.close()
     if wd is not None:
         wd.stop()

@@ -231,3 +231,48 @@ def test_resume_without_seed_flag(tmp_path):
         b = torch.load(run / "out" / f, weights_only=True)
         for k in a:
             assert torch.equal(a[k], b[k]), (f, k)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("tp", [1, 2])
+def test_vanilla_per_batch_message_sequence(tmp_path, tp):
+    """The split-learning data plane, pinned: one packed [activation | labels] message per
+    batch from the training Alice's host to every Bob rank that is not on it, and one cut-
+    gradient message per batch back from each such Bob rank (the reference needs ~4 RPC round
+    trips per batch); one weight-relay message per hand-off.  Reference topology
+    (one process per role, Bob on rank 0) with a TP = 1 Bob, and Bob tensor-parallel over
+    ranks 0-1 (TP = 2)."""
+    B = 16
+    m, bob, logs = _run(tmp_path, ["--vanilla"], 3, 3, tp, extra=["--msg_log"])
+    msgs = []
+    for r in range(3):
+        msgs += [tuple(x) for x in json.loads((logs / f"messages_rank{r}.json").read_text())]
+    import math
+    from splitlearning_amd.data.mnist import load_shard
+    data = tmp_path / "data"
+    n_tr = {c: int(load_shard(str(data), c)[0]["y"].numel()) for c in (1, 2)}
+    y1 = load_shard(str(data), 1)[0]["y"]
+    n_unl = int((y1 != 9).sum())
+    bob_ranks = list(range(tp))
+
+    def packs(src, dst):
+        return [x for x in msgs if x[0] == "multicast" and x[1] == src and x[2] == dst
+                and x[3] % (4 * (5408 + 1)) == 0 and x[3] <= 4 * B * (5408 + 1)]
+
+    def grads(src, dst):
+        return [x for x in msgs if x[0] == "reduce_to" and x[1] == src and x[2] == dst]
+    # Alice_c lives on rank c; batches of train_request(c), plus Alice_1's unlearn epoch
+    for c in (1, 2):
+        nb = math.ceil(n_tr[c] / B) + (math.ceil(n_unl / B) if c == 1 else 0)
+        for b in bob_ranks:
+            if b == c:
+                continue
+            assert len(packs(c, b)) == nb, (c, b, len(packs(c, b)), nb)
+            assert len(grads(b, c)) == nb, (c, b, len(grads(b, c)), nb)
+            assert all(x[3] <= 4 * B * 5408 for x in grads(b, c))
+    # the round-robin hand-off Alice_1 -> Alice_2: one flat 320-float buffer
+    relay = [x for x in msgs if x[0] == "send_recv" and x[1] == 1 and x[2] == 2 and x[3] == 4 * 320]
+    assert len(relay) == 1
+    # nothing else goes Bob -> Alice per batch
+    assert not [x for x in msgs if x[0] == "multicast" and x[1] in bob_ranks and x[2] in (1, 2)
+                and x[3] >= 4 * B * 5408 and x[1] != x[2] and x[1] not in (1, 2)]

@@ -344,6 +344,31 @@ def test_server_head3(cuda, M, S2, N2, C):
     _close(dz2, dz2r, rtol=1e-4, atol=1e-6)
 
 
+@pytest.mark.parametrize("M,K,N2,C", [(16, 5000, 1000, 100), (7, 628, 1000, 100), (64, 5000, 1000, 100),
+                                       (20, 132, 36, 7)])
+def test_server_fc2_head(cuda, M, K, N2, C):
+    """fc2 forward (whole K per workgroup) + epilogue + partial fc3 logits, then softmax-CE,
+    fc3 dgrad and fc2 ReLU/dropout backward, against the eager composition."""
+    g = torch.Generator().manual_seed(9)
+    h1 = torch.relu(torch.randn(M, K, generator=g)).to(cuda)
+    W2 = (torch.randn(N2, K, generator=g) / K ** 0.5).to(cuda)
+    b2 = (torch.randn(N2, generator=g) * 0.1).to(cuda)
+    W3 = (torch.randn(C, N2, generator=g) * 0.05).to(cuda)
+    b3 = (torch.randn(C, generator=g) * 0.1).to(cuda)
+    y = torch.randint(0, min(C, 10), (M,), generator=g).to(cuda)
+    y[0] = -100                                        # ignored row
+    seed = 7654321
+    h2, dlog, dz2, loss = hip_ops.server_fc2_head(h1, W2, b2, True, 0.5, seed, W3, b3, y, 1.0 / M)
+    h2r = torch_ops.linear_fwd(h1.cpu(), W2.cpu(), b2.cpu(), True, 0.5, seed)
+    logits = h2r @ W3.cpu().t() + b3.cpu()
+    lossr, dlogr = torch_ops.softmax_ce(logits, y.cpu(), 1.0 / M)
+    dz2r = (dlogr @ W3.cpu()) * (h2r > 0) * 2.0
+    _close(h2, h2r, rtol=1e-4, atol=1e-4)
+    _close(loss, lossr, rtol=1e-4, atol=1e-4)
+    _close(dlog, dlogr, rtol=1e-4, atol=1e-6)
+    _close(dz2, dz2r, rtol=1e-4, atol=1e-6)
+
+
 def test_relu_mask(cuda):
     g = torch.Generator().manual_seed(11)
     d, h = torch.randn(16, 100, generator=g).to(cuda), torch.randn(16, 100, generator=g).to(cuda)
