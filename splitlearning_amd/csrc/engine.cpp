@@ -289,9 +289,12 @@ class ServerEpoch {
   }
 
   at::Tensor product_view(int M) const { return p2ws_.narrow(0, 0, (int64_t)M * L_[1].N); }
-  // single-shard tail: fc2's forward fused into the head (fused.hip fc2_head_fwd_kernel);
-  // variant 12 = 1 keeps the split-K fc2 forward + head_fwd pair (A/B)
-  bool fuse_head() const { return !row2_ && sl::g_variant[12] != 1; }
+  // single-shard tail, variant 12 = 2: fc2's forward fused into the head (fused.hip
+  // fc2_head_fwd_kernel).  Measured slower (native executor, TP = 1: 250.9 vs 178.4 us per
+  // step; profiles/r2_fused_head_ab.txt): 125 workgroups that each reduce the whole K = 5000
+  // re-read all of h1 (320 KB) per 8 output columns and run 6 dependent load rounds per wave;
+  // the 1008-workgroup split-K forward + head_fwd pair stays the default.
+  bool fuse_head() const { return !row2_ && sl::g_variant[12] == 2; }
   bool row_parallel() const { return row2_; }
   int batch() const { return B_; }
 

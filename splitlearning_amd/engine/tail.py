@@ -264,8 +264,8 @@ class TailEngine:
         else:
             self._pre = None
             h1 = ops.linear_fwd(x, L1.W, L1.b, True, p1, seeds[0], L1.col_off, **ds(0))
-        if L2.style != "row" and hasattr(ops, "server_fc2_head") and ops.C().get_variant(12) != 1:
-            # single shard: fc2's forward is fused into the head (one launch less, no slabs)
+        if L2.style != "row" and hasattr(ops, "server_fc2_head") and ops.C().get_variant(12) == 2:
+            # variant 12 = 2: fc2's forward fused into the head (measured slower: csrc/engine.cpp)
             h2, dlog, dz2, loss = ops.server_fc2_head(h1, L2.W, L2.b, True, p2, seeds[1], L3.W, L3.b, labels,
                                                       1.0 / M, **ds(1))
         elif L2.style == "row":
@@ -278,7 +278,7 @@ class TailEngine:
             self.allreduce(P2)
         else:
             P2 = ops.linear_fwd_partial(h1, L2.W)
-        if L2.style == "row" or not hasattr(ops, "server_fc2_head") or ops.C().get_variant(12) == 1:
+        if L2.style == "row" or not hasattr(ops, "server_fc2_head") or ops.C().get_variant(12) != 2:
             h2, dlog, dz2, loss = ops.server_head3(P2, L2.b, True, p2, seeds[1], L3.W, L3.b, labels, 1.0 / M,
                                                    **ds(1))
         s1 = 1.0 / (1.0 - p1) if p1 else 1.0
