@@ -122,6 +122,9 @@ def build_parser() -> argparse.ArgumentParser:
                    help="GPU: move data-plane messages with torch.distributed isend/irecv instead of "
                         "the native RCCL communicators (per-batch p2p on the compute stream, TP "
                         "all-reduce inside the server step)")
+    g.add_argument("--native_p2p_shim", action="store_true",
+                   help="CPU tests: run the GPU data-plane code path (grouped p2p with RCCL ordering "
+                        "semantics) over gloo (parallel/dist.py GlooP2PShim)")
     g.add_argument("--msg_log", action="store_true",
                    help="record every data-plane message (op, src, dst, bytes) of this rank in "
                         "<log_dir>/messages_rank<r>.json (tests pin the per-batch message sequence)")

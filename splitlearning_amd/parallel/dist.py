@@ -335,6 +335,40 @@ def choose_bob_tp(mode: str, nprocs: int) -> int:
     return min(cands, key=lambda T: (cost(T), T))
 
 
+class GlooP2PShim:
+    """The native RCCL communicator's p2p interface (`_C.TpComm`: send / recv / group_start /
+    group_end, ranks = world ranks) over torch.distributed, for CPU tests of the GPU data-plane
+    code path in `Comm` (`--native_p2p_shim`).  It keeps RCCL's ordering semantics: an
+    un-grouped send or recv blocks until its peer's matching op (on the GPU that blocks the
+    stream: a protocol that would deadlock there deadlocks here), and the ops between
+    group_start and group_end are posted together and complete together."""
+
+    def __init__(self):
+        self._group = None
+
+    def group_start(self):
+        assert self._group is None, "nested RCCL group"
+        self._group = []
+
+    def group_end(self):
+        ops, self._group = self._group, None
+        if ops:
+            for r in dist.batch_isend_irecv(ops):
+                r.wait()
+
+    def send(self, t: torch.Tensor, peer: int):
+        if self._group is not None:
+            self._group.append(dist.P2POp(dist.isend, t, peer))
+        else:
+            dist.send(t, peer)
+
+    def recv(self, t: torch.Tensor, peer: int):
+        if self._group is not None:
+            self._group.append(dist.P2POp(dist.irecv, t, peer))
+        else:
+            dist.recv(t, peer)
+
+
 def init_process(rank: int, world: int, backend: str, addr: str, port: int, timeout_s: float,
                  device: torch.device):
     os.environ.setdefault("MASTER_ADDR", addr)

@@ -206,14 +206,16 @@ class Session:
         return out
 
     def split_lookahead(self, cid: int) -> bool:
-        """Whether a split-mode epoch of Alice_cid may use Bob's fc1 look-ahead (Bob's update of
-        batch i waits for Alice's forward of batch i+1 so its kernel can pre-form that batch's
-        fc1 product).  Only when Bob is entirely on Alice_cid's own GPU: there the launches are
-        serial anyway and the look-ahead just removes fc1's forward read.  With Bob (or a TP
-        shard) on another GPU it would put the whole cut-gradient round trip (reduce to Alice,
-        her backward and next forward, the activation multicast) in front of Bob's wgrad;
-        without it Bob's wgrad + optimizer overlaps exactly that round trip."""
-        return set(self.bob_ranks) == {self.host(cid)}
+        """Whether a split-mode epoch of Alice_cid uses Bob's fc1 look-ahead (Bob's update of
+        batch i is issued after Alice's forward of batch i+1, so its kernel also forms that
+        batch's fc1 product and Bob never re-reads fc1 for a forward).  Always, by measurement
+        and by the critical path: on one GPU the launches are serial anyway, and with Bob
+        tensor-parallel over all GPUs the Alice's GPU also runs a Bob shard on the same stream,
+        so ordering that shard's update before her backward / forward (the textbook §3.2
+        overlap) moves no work off the critical path — it only adds fc1's forward read back.
+        Overlapping the update with the cut-gradient round trip needs the Alice's work on a
+        second stream of her GPU (docs/ARCHITECTURE.md, data plane)."""
+        return True
 
     @property
     def act_dtype(self):

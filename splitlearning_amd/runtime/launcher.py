@@ -104,6 +104,9 @@ def worker(rank: int, nprocs: int, args, result_q=None):
     comm = Comm(rank, nprocs, dev, pl, tp_group)
     if getattr(args, "msg_log", False):
         comm.msg_log = []
+    if getattr(args, "native_p2p_shim", False) and nprocs > 1:
+        from ..parallel.dist import GlooP2PShim
+        comm.native = GlooP2PShim()
     if getattr(args, "prep_in_worker", False) and getattr(args, "ckpt_dir", ""):
         # torchrun: every rank ran main(); rank 0's view of job.json is the agreed seed
         if rank == 0:

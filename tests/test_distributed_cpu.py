@@ -276,3 +276,29 @@ def test_vanilla_per_batch_message_sequence(tmp_path, tp):
     # nothing else goes Bob -> Alice per batch
     assert not [x for x in msgs if x[0] == "multicast" and x[1] in bob_ranks and x[2] in (1, 2)
                 and x[3] >= 4 * B * 5408 and x[1] != x[2] and x[1] not in (1, 2)]
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("flags,ws,np_,tp", [
+    (["--vanilla"], 3, 3, 2),                 # per-batch multicast + cut-gradient reduce + relay
+    (["--sisa"], 3, 2, 2),                    # the batched dump exchange, eval traffic
+    ([], 3, 3, 1),                            # U-shape: four messages per batch
+    (["--sisa", "--concat", "--concat_unlearn"], 3, 3, 2),
+])
+def test_native_data_plane_protocol_matches_torch_p2p(tmp_path, flags, ws, np_, tp):
+    """The GPU data plane (Comm.native: grouped RCCL p2p on the compute stream) with RCCL's
+    ordering semantics, run over gloo (GlooP2PShim): the protocol completes (no stream-order
+    deadlock) and the job is bitwise the torch.distributed p2p run."""
+    a, b = tmp_path / "a", tmp_path / "b"
+    a.mkdir()
+    b.mkdir()
+    m_ref, _, _ = _run(a, flags, ws, np_, tp, extra=["--save_dir", str(a / "out")])
+    m_nat, _, _ = _run(b, flags, ws, np_, tp, extra=["--native_p2p_shim", "--save_dir", str(b / "out")])
+    assert m_nat["last_eval"] == m_ref["last_eval"]
+    for f in sorted(p.name for p in (a / "out").iterdir()):
+        x = torch.load(a / "out" / f, weights_only=True)
+        y = torch.load(b / "out" / f, weights_only=True)
+        fx = x if "model1" not in x else {**x["model1"], **x["model3"]}
+        fy = y if "model1" not in y else {**y["model1"], **y["model3"]}
+        for k in fx:
+            assert torch.equal(fx[k], fy[k]), (f, k)
