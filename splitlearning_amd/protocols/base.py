@@ -208,14 +208,17 @@ class Session:
     def split_lookahead(self, cid: int) -> bool:
         """Whether a split-mode epoch of Alice_cid uses Bob's fc1 look-ahead (Bob's update of
         batch i is issued after Alice's forward of batch i+1, so its kernel also forms that
-        batch's fc1 product and Bob never re-reads fc1 for a forward).  Always, by measurement
-        and by the critical path: on one GPU the launches are serial anyway, and with Bob
-        tensor-parallel over all GPUs the Alice's GPU also runs a Bob shard on the same stream,
-        so ordering that shard's update before her backward / forward (the textbook §3.2
-        overlap) moves no work off the critical path — it only adds fc1's forward read back.
-        Overlapping the update with the cut-gradient round trip needs the Alice's work on a
-        second stream of her GPU (docs/ARCHITECTURE.md, data plane)."""
-        return True
+        batch's fc1 product and Bob never re-reads fc1 for a forward) — or the §3.2 overlap
+        order (Bob's update issued right after the cut gradient leaves, so it runs while the
+        Alice does her backward and next forward; Bob then re-reads fc1 for that forward).
+
+        Placement decides (docs/ARCHITECTURE.md, "Split-mode schedule"): when the Alice's GPU
+        runs a Bob shard (one GPU; Bob tensor-parallel over every GPU, the vanilla default)
+        her work and that shard's update share one stream, so the overlap order moves nothing
+        off the critical path and only adds fc1's forward read back: look-ahead.  When no Bob
+        shard lives on her GPU (U-shape's TP = 1 policy on several GPUs, or `--bob_tp` < N)
+        the update of batch i can hide behind her step: overlap order."""
+        return self.host(cid) in self.bob_ranks
 
     @property
     def act_dtype(self):

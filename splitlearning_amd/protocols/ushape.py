@@ -130,7 +130,9 @@ class UShapeSession(Session):
         Alice, Bob's data gradients, Alice's conv backward + step and her forward of batch
         i+1 (sent to Bob) — and only then Bob's wgrad + Adam of both layers in one launch,
         which also forms batch i+1's fc1 product with the updated weights (no separate fc1
-        forward read).  Same per-batch math and update order as `split_step`."""
+        forward read).  Same per-batch math and update order as `split_step`.  When no Bob
+        shard shares the Alice's GPU (`split_lookahead`), Bob's update is issued right after
+        the cut gradient leaves instead, so it runs during her backward and next forward."""
         B = self.B
         a = self.alices.get(cid)
         host = self.host(cid)
@@ -163,11 +165,16 @@ class UShapeSession(Session):
             dxp = (self.tail.backward_dgrad(dmid_b, need_dx=True, premasked=self.head_fused(M))
                    if self.is_bob else None)
             dx = self.comm.reduce_to(dxp, host, self.bob_ranks, (M, CUT_FEATURES), torch.float32)
+            pre = False
+            if self.is_bob and not la:           # Alice remote from every Bob shard: the
+                if grouped:                      # update overlaps her backward + next forward
+                    self.tail.group_step(self.bob_slot(cid), x_next=None)
+                else:
+                    self.tail.backward_step(self.bob_slot(cid))
             if a is not None:
                 a.front.backward_step(dx, act, am, a.train, idx, a.slot, t=t, prefix="front.", defer=True)
             nxt = alice_fwd(spans[i + 1]) if i + 1 < len(spans) else None
-            pre = False
-            if self.is_bob:
+            if self.is_bob and la:
                 if grouped:
                     x_next = nxt[4] if (la and nxt is not None and self.tail.grouped_ok(nxt[4].shape[0])) else None
                     self.tail.group_step(self.bob_slot(cid), x_next=x_next)

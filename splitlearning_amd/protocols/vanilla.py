@@ -80,14 +80,24 @@ class VanillaSession(Session):
         fc1 product with the freshly updated weights (look-ahead, TailEngine.fused_step).
         Same math and update order as `split_step` per batch (both sides step on batch i
         before either runs batch i+1); on one GPU the reordering is free because the
-        launches were serial anyway."""
+        launches were serial anyway.  When no Bob shard shares the Alice's GPU
+        (`split_lookahead`), Bob's update is issued right after the cut gradient leaves
+        instead, so it runs during her backward and next forward (§3.2 overlap)."""
         B = self.B
         a = self.alices.get(cid)
         host = self.host(cid)
         spans = [(s, min(s + B, n)) for s in range(0, n, B)]
         if not spans:
             return
-        la = self.is_bob and self.tail.fused3_ok() and self.tail.lookahead_ok(B) and self.split_lookahead(cid)
+        ahead = self.split_lookahead(cid)        # False: Alice remote from every Bob shard
+        la = self.is_bob and self.tail.fused3_ok() and self.tail.lookahead_ok(B) and ahead
+
+        def bob_update(x_next):
+            if self.tail.fused3_ok():
+                self.tail.fused_step(self.bob_slot(cid), x_next=x_next)
+                return x_next is not None
+            self.tail.backward_step(self.bob_slot(cid))
+            return False
 
         def alice_fwd(span):
             s, e = span
@@ -113,16 +123,14 @@ class VanillaSession(Session):
                     _, dout = self.ops.softmax_ce(out, lab_b, 1.0 / M)
                     dxp = self.tail.backward_dgrad(dout, need_dx=True)
             dx = self.comm.reduce_to(dxp, host, self.bob_ranks, (M, CUT_FEATURES), torch.float32)
+            pre = False
+            if self.is_bob and not ahead:
+                bob_update(None)                  # overlaps the Alice's backward + next forward
             if a is not None:
                 a.front.backward_step(dx, act, am, a.train, idx, a.slot, defer=True)
             nxt = alice_fwd(spans[i + 1]) if i + 1 < len(spans) else None
-            if self.is_bob:
-                if fused:
-                    x_next = nxt[3] if (la and nxt is not None and nxt[3].shape[0] <= 64) else None
-                    self.tail.fused_step(self.bob_slot(cid), x_next=x_next)
-                    pre = x_next is not None
-                else:
-                    self.tail.backward_step(self.bob_slot(cid))
+            if self.is_bob and ahead:
+                pre = bob_update(nxt[3] if (la and nxt is not None and nxt[3].shape[0] <= 64) else None)
             cur = nxt
         if a is not None:
             a.front.flush()          # the last step's deferred client update

@@ -195,11 +195,14 @@ def _vanilla_session(cuda, tmp_path):
     return VanillaSession(args, comm, cuda)
 
 
-def test_vanilla_pipelined_epoch_matches_per_batch_steps(cuda, tmp_path):
+@pytest.mark.parametrize("ahead", [True, False])
+def test_vanilla_pipelined_epoch_matches_per_batch_steps(cuda, tmp_path, ahead):
     """split_epoch (Alice's next forward before Bob's update, fc1 look-ahead in Bob's
-    wgrad kernel) follows the same trajectory as one split_step per batch."""
+    wgrad kernel; or, ahead=False, the overlap order used when no Bob shard shares the
+    Alice's GPU) follows the same trajectory as one split_step per batch."""
     sa = _vanilla_session(cuda, tmp_path)
     sb = _vanilla_session(cuda, tmp_path)
+    sb.split_lookahead = lambda cid: ahead
     assert sb.tail.lookahead_ok(16)
     a = sa.alices[1]
     order = a.train.shuffled_order(torch.Generator().manual_seed(9))[:16 * 6 + 5]   # a partial last batch
@@ -217,8 +220,10 @@ def test_vanilla_pipelined_epoch_matches_per_batch_steps(cuda, tmp_path):
         torch.testing.assert_close(wa[k], wb[k], rtol=1e-3, atol=1e-4)
 
 
-def test_ushape_pipelined_epoch_matches_per_batch_steps(cuda, tmp_path):
-    """U-shape split_epoch (grouped Bob step with the fc1 look-ahead) == per-batch split_step."""
+@pytest.mark.parametrize("ahead", [True, False])
+def test_ushape_pipelined_epoch_matches_per_batch_steps(cuda, tmp_path, ahead):
+    """U-shape split_epoch (grouped Bob step with the fc1 look-ahead, or the overlap order)
+    == per-batch split_step."""
     from splitlearning_amd.config import parse_args
     from splitlearning_amd.data.mnist import write_shards
     from splitlearning_amd.parallel.dist import Comm, Placement
@@ -228,6 +233,7 @@ def test_ushape_pipelined_epoch_matches_per_batch_steps(cuda, tmp_path):
     write_shards(args, verbose=False)
     mk = lambda: UShapeSession(args, Comm(0, 1, cuda, Placement.make(2, 1, 1)), cuda)  # noqa: E731
     sa, sb = mk(), mk()
+    sb.split_lookahead = lambda cid: ahead
     assert sb.tail.grouped_ok(16)
     order = sa.alices[1].train.shuffled_order(torch.Generator().manual_seed(3))[:16 * 6 + 7]
     n = order.numel()
