@@ -22,6 +22,8 @@
 //   row-blocked and loads-first wgrad) were removed after measurement (docs/PERF.md).
 #include "common.h"
 
+#include <algorithm>
+
 namespace sl {
 
 int g_variant[16] = {0};
@@ -119,6 +121,84 @@ skinny_fwd_kernel(const float* __restrict__ X, int ldx, const float* __restrict_
       }
     }
   }
+}
+
+// One-round-trip form (the default; variant 14 = 2 selects skinny_fwd_kernel): every wave
+// owns exactly 16 U consecutive k of its 16-column tile and issues ALL its loads (U float4 of
+// X and of W per lane) before the first MFMA, so a wave costs one memory round trip; the
+// workgroup is NW = blockDim / 64 waves (NW 16 U k per split-K slice), summed through LDS in
+// wave order.  skinny_fwd_kernel walks its k range in dependent U-batches (at fc2's shape, K =
+// 5000 in 16 slices of 320 k over 2 waves, 4 round trips per wave).  Native executor, us per
+// server step (profiles/r2_chain_probe.txt): TP = 1 177.8 vs 178.1 and 174.9 vs 175.3, TP = 8
+// 52.3 vs 53.0 and 53.2 vs 53.9 — small, but the same sign in both interleaved runs.
+template <int U>
+__global__ void __launch_bounds__(1024)
+skinny_fwd_once_kernel(const float* __restrict__ X, int ldx, const float* __restrict__ W, int ldw,
+                       float* __restrict__ Y, int ldy, int M, int N, int K, Epi e, float* __restrict__ P,
+                       int64_t slab) {
+  __shared__ f32x4 red[16][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, NW = blockDim.x >> 6;
+  const int n0 = blockIdx.x * 16, m0 = blockIdx.y * 16;
+  const int S = gridDim.z;
+  const int kb = ((int)blockIdx.z * NW + wv) * 16 * U;
+  const int ra = m0 + (lane & 15), rb = n0 + (lane & 15);
+  const int kq = (lane >> 4) * 4;
+  const bool va = ra < M, vb = rb < N;
+  const float* pa = X + (int64_t)(va ? ra : 0) * ldx;
+  const float* pb = W + (int64_t)(vb ? rb : 0) * ldw;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 a[U], w[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int kk = kb + 16 * u + kq;
+    const bool in = kk < K;                      // K % 4 == 0: a float4 never straddles K
+    a[u] = (va && in) ? ld4(pa + kk) : z4;
+    w[u] = (vb && in) ? ld4(pb + kk) : z4;
+  }
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    acc0 = mfma4(a[u].x, w[u].x, acc0);
+    acc1 = mfma4(a[u].y, w[u].y, acc1);
+    acc0 = mfma4(a[u].z, w[u].z, acc0);
+    acc1 = mfma4(a[u].w, w[u].w, acc1);
+  }
+  red[wv][lane] = acc0 + acc1;
+  __syncthreads();
+  if (wv == 0) {
+    f32x4 s = red[0][lane];
+    for (int i = 1; i < NW; ++i) s += red[i][lane];
+    const int n = n0 + (lane & 15);
+    if (n < N) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + (lane >> 4) * 4 + r;
+        if (m >= M) continue;
+        if (S == 1)
+          Y[(int64_t)m * ldy + n] = apply_epi(e, s[r], m, n);
+        else
+          P[(int64_t)blockIdx.z * slab + (int64_t)m * N + n] = s[r];
+      }
+    }
+  }
+}
+
+// Launch plan of skinny_fwd_once_kernel (U = 4: 64 k per wave): NW waves per workgroup and S
+// split-K slices with S <= max_split and S M N <= ws_elems (S == 1 needs no workspace).
+// Returns false when K does not fit (the caller keeps skinny_fwd_kernel).
+static bool fwd_once_plan(int M, int N, int K, int max_split, int64_t ws_elems, int& NW, int& S) {
+  constexpr int KW = 64;
+  const int waves = (K + KW - 1) / KW;            // waves per 16 x 16 output tile
+  const int64_t slab = (int64_t)M * N;
+  const int64_t fit = ws_elems / (slab > 0 ? slab : 1);
+  const int smax = (int)std::max<int64_t>(1, std::min<int64_t>(max_split, fit));
+  NW = std::min(waves, 8);
+  S = (waves + NW - 1) / NW;
+  if (S > smax) {
+    S = smax;
+    NW = (waves + S - 1) / S;
+  }
+  return NW <= 16;
 }
 
 // bf16 compute form of skinny_fwd_kernel (`--dtype bf16`): same grid, split-K and store, but
@@ -483,6 +563,16 @@ hipError_t linear_fwd(const float* X, int ldx, const float* W, int ldw, float* Y
   // the epilogue runs here, unless variant 11 = 1 forces this kernel (gemm.hip measurements).
   if (M > 128 && (g_bf16 || g_variant[11] == 1)) return gemm_nt(X, ldx, W, ldw, Y, ldy, M, N, K, e, g_bf16 != 0, st);
   dim3 grid((N + 15) / 16, (M + 15) / 16);
+  int NW1, S1;
+  if (!g_bf16 && g_variant[14] != 2 && fwd_once_plan(M, N, K, 16, ws ? ws_elems : 0, NW1, S1)) {
+    skinny_fwd_once_kernel<4><<<dim3(grid.x, grid.y, S1), NW1 * 64, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e, ws,
+                                                                          (int64_t)M * N);
+    if (S1 > 1) {
+      const int64_t tot = (int64_t)M * N;
+      epilogue_kernel<<<(unsigned)((tot + 255) / 256), 256, 0, st>>>(ws, N, Y, ldy, M, N, e, S1, (int64_t)M * N);
+    }
+    return hipGetLastError();
+  }
   // split K until there are ~8 workgroups per CU, keeping >= 256 k per workgroup: fc1
   // (313 column tiles) runs S = 4 (30.6 us vs 35.2 us at S = 2; profiles/r1_kbench_call17)
   const int tiles = grid.x * grid.y;
@@ -574,6 +664,15 @@ hipError_t linear_fwd_partial(const float* X, int ldx, const float* W, int ldw, 
   const int64_t slab = (int64_t)M * N;
   if (ws_elems < slab * S) S = 1;
   if (ws_elems < slab) return hipErrorInvalidValue;
+  int NW1, S1;
+  if (!g_bf16 && g_variant[14] != 2 && fwd_once_plan(M, N, K, max_split, ws_elems, NW1, S1)) {
+    Epi e1{};
+    e1.dscale = 1.f;
+    skinny_fwd_once_kernel<4><<<dim3(grid.x, grid.y, S1), NW1 * 64, 0, st>>>(X, ldx, W, ldw, ws, N, M, N, K, e1, ws,
+                                                                          slab);
+    *S_out = S1;
+    return hipGetLastError();
+  }
   const int kz = (K + S - 1) / S;
   const int nw = kz >= 1024 ? 8 : (kz >= 512 ? 4 : 2);
   dim3 g3(grid.x, grid.y, S);

@@ -93,11 +93,34 @@ def test_linear_fwd(cuda, M, N, K, relu, drop, gemm):
     try:
         for tile in ((0, 1, 2, 3, 4) if gemm else (0,)):
             C.set_variant(10, tile)
-            y = hip_ops.linear_fwd(x, w, b, relu, drop, seed, col_offset=3)
-            _close(y, yr, rtol=1e-4, atol=1e-4)
+            for once in ((0,) if gemm else (0, 2)):      # variant 14: 2 = the k-loop skinny form
+                C.set_variant(14, once)
+                y = hip_ops.linear_fwd(x, w, b, relu, drop, seed, col_offset=3)
+                _close(y, yr, rtol=1e-4, atol=1e-4)
     finally:
         C.set_variant(11, 0)
         C.set_variant(10, 0)
+        C.set_variant(14, 0)
+
+
+@pytest.mark.parametrize("M,N,K,max_split", [(16, 1000, 5000, 16), (16, 1000, 628, 1), (16, 1000, 1000, 1),
+                                              (64, 1000, 5000, 16), (16, 100, 1000, 16), (5, 37, 52, 16),
+                                              (16, 1000, 1252, 2)])
+@pytest.mark.parametrize("once", [0, 2])
+def test_linear_fwd_partial(cuda, M, N, K, max_split, once):
+    """Un-reduced split-K slabs of x @ w.T (fc2 forward of the server step; max_split 1 = the
+    row-parallel TP shard's plain partial product) in both skinny forms (variant 14 = 2: the
+    k-loop form)."""
+    C = hip_ops.C()
+    C.set_variant(14, once)
+    try:
+        x = torch.randn(M, K, device=cuda)
+        w = torch.randn(N, K, device=cuda) / K ** 0.5
+        P = hip_ops.linear_fwd_partial(x, w, max_split=max_split, key=f"t{once}")
+        assert 1 <= P.shape[0] <= max_split
+        _close(P.sum(0), x @ w.t(), rtol=1e-4, atol=1e-4)
+    finally:
+        C.set_variant(14, 0)
 
 
 @pytest.mark.parametrize("M,N,K", [(16, 5000, 5408), (16, 1000, 5000), (16, 100, 1000), (16, 10, 100),
@@ -320,7 +343,7 @@ def test_conv_local_epoch_matches_steps(cuda, kind, variant):
         assert torch.equal(s[0][k], s[2][k]) and torch.equal(s[1][k], s[3][k])
 
 
-@pytest.mark.parametrize("M,S2,N2,C", [(16, 4, 1000, 100), (7, 1, 1000, 100), (16, 8, 1000, 10),
+@pytest.mark.parametrize("M,S2,N2,C", [(16, 4, 1000, 100), (7, 1, 1000, 100), (16, 8, 1000, 10), (16, 16, 1000, 100), (16, 20, 1000, 100),
                                        (3, 2, 512, 97), (16, 1, 1000, 300)])
 def test_server_head3(cuda, M, S2, N2, C):
     """fc2 slab reduce + epilogue, fc3, softmax-CE, fc3 dgrad, fc2 ReLU/dropout backward
