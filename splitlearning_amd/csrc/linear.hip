@@ -477,6 +477,23 @@ __global__ void epilogue_kernel(const float* __restrict__ P, int ldp, float* __r
   Y[(int64_t)m * ldy + n] = apply_epi(e, v, m, n);
 }
 
+// The slab reductions stay scalar (one column per thread): float4 forms (4 columns per
+// thread, 256- or 64-thread workgroups) won a graph-replay probe with the slabs L2-hot
+// (scripts/probe/dgrad_probe.hip: 2.0 vs 2.7 us) but lost 0.3-1.5 us per server step in the
+// native executor at every TP degree (profiles/r2_chain_probe.txt): with the slabs cold, a
+// quarter of the threads is a quarter of the loads in flight.
+static void launch_epilogue(const float* P, int ldp, float* Y, int ldy, int M, int N, Epi e, int S, int64_t slab,
+                            hipStream_t st) {
+  const int64_t tot = (int64_t)M * N;
+  epilogue_kernel<<<(unsigned)((tot + 255) / 256), 256, 0, st>>>(P, ldp, Y, ldy, M, N, e, S, slab);
+}
+
+static void launch_dgrad_reduce(const float* P, int S, int64_t slab, const float* hprev, int ldh, float scale,
+                                float* out, int ldo, int M, int K, hipStream_t st) {
+  const int64_t tot = (int64_t)M * K;
+  dgrad_reduce_kernel<<<(unsigned)((tot + 255) / 256), 256, 0, st>>>(P, S, slab, hprev, ldh, scale, out, ldo, M, K);
+}
+
 // ---------------------------------------------------------------------------- wgrad + optimizer
 // v3: memory-level parallelism first.  A 1024-thread workgroup owns a 16-row x 256-column
 // tile; every wave covers one row's 256 contiguous weights (1 KB per instruction), so each
@@ -568,8 +585,7 @@ hipError_t linear_fwd(const float* X, int ldx, const float* W, int ldw, float* Y
     skinny_fwd_once_kernel<4><<<dim3(grid.x, grid.y, S1), NW1 * 64, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e, ws,
                                                                           (int64_t)M * N);
     if (S1 > 1) {
-      const int64_t tot = (int64_t)M * N;
-      epilogue_kernel<<<(unsigned)((tot + 255) / 256), 256, 0, st>>>(ws, N, Y, ldy, M, N, e, S1, (int64_t)M * N);
+      launch_epilogue(ws, N, Y, ldy, M, N, e, S1, (int64_t)M * N, st);
     }
     return hipGetLastError();
   }
@@ -598,8 +614,7 @@ hipError_t linear_fwd(const float* X, int ldx, const float* W, int ldw, float* Y
   else
     skinny_fwd_kernel<2, 4, false><<<g3, 128, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e, P, slab);
   if (S > 1) {
-    const int64_t tot = (int64_t)M * N;
-    epilogue_kernel<<<(unsigned)((tot + 255) / 256), 256, 0, st>>>(ws, N, Y, ldy, M, N, e, S, slab);
+    launch_epilogue(ws, N, Y, ldy, M, N, e, S, slab, st);
   }
   return hipGetLastError();
 }
@@ -627,7 +642,9 @@ hipError_t linear_dgrad(const float* dZ, int ldz, const float* W, int ldw, const
   // server step unsplit vs 51.8 us split; profiles/r1_dgrad_split_ab.txt).
   const int v5 = g_variant[5];
   const int smax = v5 > 0 ? v5 : 16;
-  const int rmin = v5 > 1 ? 16 : 64;
+  // few K tiles (a TP shard's fc2, K = 628 at TP = 8): N slices down to 32 rows (S = 16):
+  // 3.1 vs 3.7 us per launch in the graph-replay probe (scripts/probe/dgrad_probe.hip)
+  const int rmin = v5 > 1 ? 16 : (kt * mt <= 64 ? 32 : 64);
   while (S < smax && kt * mt * S < 768 && N / (S * 2) >= rmin) S *= 2;
   const int64_t slab = (int64_t)M * K;
   if (ws == nullptr) S = 1;
@@ -643,9 +660,7 @@ hipError_t linear_dgrad(const float* dZ, int ldz, const float* W, int ldw, const
       skinny_dgrad_kernel<8, true><<<grid, 512, 0, st>>>(dZ, ldz, W, ldw, nullptr, 0, 1.f, ws, 0, slab, M, N, K);
     else
       skinny_dgrad_kernel<8><<<grid, 512, 0, st>>>(dZ, ldz, W, ldw, nullptr, 0, 1.f, ws, 0, slab, M, N, K);
-    const int64_t tot = (int64_t)M * K;
-    dgrad_reduce_kernel<<<(unsigned)((tot + 255) / 256), 256, 0, st>>>(ws, S, slab, hprev, ldh, scale, dX, ldx,
-                                                                        M, K);
+    launch_dgrad_reduce(ws, S, slab, hprev, ldh, scale, dX, ldx, M, K, st);
   }
   return hipGetLastError();
 }
@@ -719,9 +734,8 @@ hipError_t linear_dgrad_partial(const float* dZ, int ldz, const float* W, int ld
 
 hipError_t linear_epilogue(const float* P, int ldp, float* Y, int ldy, int M, int N, Epi e, int S, int64_t slab,
                            hipStream_t st) {
-  const int64_t tot = (int64_t)M * N;
-  if (tot <= 0) return hipSuccess;
-  epilogue_kernel<<<(unsigned)((tot + 255) / 256), 256, 0, st>>>(P, ldp, Y, ldy, M, N, e, S, slab);
+  if ((int64_t)M * N <= 0) return hipSuccess;
+  launch_epilogue(P, ldp, Y, ldy, M, N, e, S, slab, st);
   return hipGetLastError();
 }
 

@@ -33,8 +33,15 @@ class DeviceShard:
         return dict(Counter(ys.tolist()))
 
     def shuffled_order(self, gen: torch.Generator) -> torch.Tensor:
-        """One epoch's sample order (DataLoader(shuffle=True) semantics)."""
-        return torch.randperm(self.n, generator=gen).to(self.device)
+        """One epoch's sample order (DataLoader(shuffle=True) semantics).  Drawn from the
+        Alice's host generator, so a seeded run gives the same orders on every backend and
+        the order is part of the generator state a snapshot saves; on a GPU it is copied from
+        pinned memory without blocking the host (a pageable copy would wait for the stream
+        to drain before the epoch's launches could be queued)."""
+        perm = torch.randperm(self.n, generator=gen)
+        if self.device.type != "cuda":
+            return perm
+        return perm.pin_memory().to(self.device, non_blocking=True)
 
     def sequential_order(self) -> torch.Tensor:
         return torch.arange(self.n, device=self.device)
