@@ -14,6 +14,162 @@ using namespace sl;
 
 static hipStream_t g_probe_stream = 0;
 
+// head_fwd_v0_kernel (the round-1 form, kept here for the A/B): workgroup (m, q) reduces fc2's split-K slabs for its column slice of row
+// m, applies fc2's epilogue (-> h2) and writes the slice's partial fc3 logits plog[q][m][:].
+// Every load of a phase is issued before the first is consumed (one memory round trip per
+// phase): at B = 16 this op is pure latency.
+__global__ void __launch_bounds__(256)
+head_fwd_v0_kernel(const float* __restrict__ P2, int S2, int64_t slab2, Epi e2, const float* __restrict__ W3,
+                int ldw3, float* __restrict__ h2, float* __restrict__ plog, int M, int N2, int C, int bf) {
+  __shared__ f32x4 part[8][HS];
+  __shared__ f32x4 hs[HS];
+  const int m = blockIdx.x, q = blockIdx.y, Q = gridDim.y, tid = threadIdx.x;
+  int qa, qb;
+  head_slice(N2 >> 2, Q, q, qa, qb);
+  const int ncol = qb - qa;
+  const int lane = tid & 63, wv = tid >> 6, half = lane >> 5, c = lane & 31;
+  constexpr int JU = 13;
+  // W3 loads of the first output group do not depend on anything: issue them first so
+  // they overlap the slab reduction (one memory round trip for the whole kernel at C <= 104)
+  f32x4 w[JU];
+  auto load_w = [&](int j0) {
+#pragma unroll
+    for (int j = 0; j < JU; ++j) {
+      const int o = 8 * (j0 + j) + 2 * wv + half;
+      w[j] = (o < C && c < ncol) ? *reinterpret_cast<const f32x4*>(W3 + (int64_t)o * ldw3 + 4 * (qa + c))
+                                 : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  load_w(0);
+  // 1. slab reduction: 32 columns x 8 slab groups
+  {
+    const int c = tid & (HS - 1), sg = tid >> 5;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (c < ncol) {
+      const f32x4* src = reinterpret_cast<const f32x4*>(P2 + (int64_t)m * N2) + qa + c;
+#pragma unroll 4
+      for (int s = sg; s < S2; s += 8) v += src[s * (slab2 >> 2)];
+    }
+    part[sg][c] = v;
+  }
+  __syncthreads();
+  if (tid < HS) {
+    f32x4 v = part[0][tid];
+#pragma unroll
+    for (int g = 1; g < 8; ++g) v += part[g][tid];
+    f32x4 o = {0.f, 0.f, 0.f, 0.f};
+    if (tid < ncol) {
+      const int col = 4 * (qa + tid);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[i] = apply_epi(e2, v[i], m, col + i);
+      reinterpret_cast<f32x4*>(h2 + (int64_t)m * N2)[qa + tid] = o;
+    }
+    hs[tid] = o;
+  }
+  __syncthreads();
+  // 2. partial logits: half-waves (32 lanes = the slice's columns) per output, 8 outputs
+  //    per wave instruction group; JU outputs' loads in flight per lane
+  const f32x4 h = bf ? bfr4(hs[c]) : hs[c];
+  for (int j0 = 0; j0 * 8 < C; j0 += JU) {
+    if (j0) load_w(j0);
+#pragma unroll
+    for (int j = 0; j < JU; ++j) {
+      const int o = 8 * (j0 + j) + 2 * wv + half;
+      const f32x4 wj = bf ? bfr4(w[j]) : w[j];
+      float d = wj[0] * h[0] + wj[1] * h[1] + wj[2] * h[2] + wj[3] * h[3];
+#pragma unroll
+      for (int off = 16; off > 0; off >>= 1) d += __shfl_xor(d, off);
+      if (c == 0 && o < C) plog[((int64_t)q * M + m) * C + o] = d;
+    }
+  }
+}
+
+// head_bwd_v0_kernel (the round-1 form, kept here for the A/B): workgroup (m, q) sums row m's partial logits (+ b3), softmax-CE (loss and
+// dlogits written by q == 0), then dz2 = (dlogits . W3) * dscale * [h2 > 0] for its slice.
+__global__ void __launch_bounds__(256)
+head_bwd_v0_kernel(const float* __restrict__ plog, const float* __restrict__ b3, const float* __restrict__ W3,
+                int ldw3, const int64_t* __restrict__ y, int64_t ignore, float scale, float dscale,
+                const float* __restrict__ h2, float* __restrict__ dlog, float* __restrict__ dz2,
+                float* __restrict__ loss_rows, int M, int N2, int C, int bf, int Qp) {
+  // Qp: number of partial-logit slabs in plog (head_fwd: one per column slice = gridDim.y;
+  // fc2_head_fwd: one per 8-column tile)
+  extern __shared__ float lg[];   // C
+  __shared__ f32x4 part[8][HS];
+  const int m = blockIdx.x, q = blockIdx.y, Q = gridDim.y, tid = threadIdx.x;
+  const int lane = tid & 63, wv = tid >> 6;
+  int qa, qb;
+  head_slice(N2 >> 2, Q, q, qa, qb);
+  const int ncol = qb - qa;
+  const int c = tid & (HS - 1), g = tid >> 5;
+  constexpr int JU = 13;
+  // independent loads first: this slice's W3 columns (first output group) and h2 mask
+  f32x4 w[JU];
+  auto load_w = [&](int j0) {
+#pragma unroll
+    for (int j = 0; j < JU; ++j) {
+      const int o = 8 * (j0 + j) + g;
+      w[j] = (o < C && c < ncol) ? *reinterpret_cast<const f32x4*>(W3 + (int64_t)o * ldw3 + 4 * (qa + c))
+                                 : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  load_w(0);
+  f32x4 hh = {0.f, 0.f, 0.f, 0.f};
+  if (tid < ncol) hh = reinterpret_cast<const f32x4*>(h2 + (int64_t)m * N2)[qa + tid];
+  for (int o = tid; o < C; o += 256) {
+    float v = b3 ? b3[o] : 0.f;
+#pragma unroll 8
+    for (int s = 0; s < Qp; ++s) v += plog[((int64_t)s * M + m) * C + o];
+    lg[o] = v;
+  }
+  __syncthreads();
+  const int64_t lab = y[m];
+  if (wv == 0) {
+    if (lab == ignore) {
+      for (int c = lane; c < C; c += 64) lg[c] = 0.f;
+      if (lane == 0 && q == 0) loss_rows[m] = 0.f;
+    } else {
+      float mx = -INFINITY;
+      for (int c = lane; c < C; c += 64) mx = fmaxf(mx, lg[c]);
+      for (int o_ = 32; o_ > 0; o_ >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o_, 64));
+      float se = 0.f;
+      for (int c = lane; c < C; c += 64) se += expf(lg[c] - mx);
+      for (int o_ = 32; o_ > 0; o_ >>= 1) se += __shfl_xor(se, o_, 64);
+      if (lane == 0 && q == 0) loss_rows[m] = mx + logf(se) - lg[lab];
+      const float inv = 1.f / se;
+      for (int c = lane; c < C; c += 64) {
+        float p = expf(lg[c] - mx) * inv;
+        if (c == lab) p -= 1.f;
+        lg[c] = p * scale;
+      }
+    }
+  }
+  __syncthreads();
+  if (q == 0)
+    for (int cc = tid; cc < C; cc += 256) dlog[(int64_t)m * C + cc] = lg[cc];
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int j0 = 0; j0 * 8 < C; j0 += JU) {
+    if (j0) load_w(j0);
+#pragma unroll
+    for (int j = 0; j < JU; ++j) {
+      const int o = 8 * (j0 + j) + g;
+      const float l = o < C ? lg[o] : 0.f;
+      acc += bf ? bfr(l) * bfr4(w[j]) : l * w[j];
+    }
+  }
+  part[g][c] = acc;
+  __syncthreads();
+  if (tid < ncol) {
+    f32x4 v = part[0][tid];
+#pragma unroll
+    for (int gg = 1; gg < 8; ++gg) v += part[gg][tid];
+    f32x4 out;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[i] = hh[i] > 0.f ? v[i] * dscale : 0.f;
+    reinterpret_cast<f32x4*>(dz2 + (int64_t)m * N2)[qa + tid] = out;
+  }
+}
+
+
 static int head3m_slices(int N2) { return max(1, (N2 / 4 + 15) / 16); }
 
 // head_fwd_mfma_kernel (measured here; not in the package): workgroup q owns a slice of <= 64 fc2 columns
@@ -262,6 +418,85 @@ head_fwd_part(const float* __restrict__ P2, int S2, int64_t slab2, Epi e2, const
   }
 }
 
+
+// head_bwd dissected: SKIP bit 1 = no plog reduction (logits = b3), 2 = no softmax (dlogits =
+// logits), 4 = no dz2 phase (W3 loads and FMAs dropped, zeros stored)
+template <int SKIP>
+__global__ void __launch_bounds__(256)
+head_bwd_part(const float* __restrict__ plog, const float* __restrict__ b3, const float* __restrict__ W3, int ldw3,
+              const int64_t* __restrict__ y, int64_t ignore, float scale, float dscale, const float* __restrict__ h2,
+              float* __restrict__ dlog, float* __restrict__ dz2, float* __restrict__ loss_rows, int M, int N2, int C,
+              int Qp) {
+  extern __shared__ float lg[];
+  __shared__ f32x4 part[8][HS];
+  const int m = blockIdx.x, q = blockIdx.y, Q = gridDim.y, tid = threadIdx.x;
+  const int lane = tid & 63, wv = tid >> 6;
+  int qa, qb;
+  head_slice(N2 >> 2, Q, q, qa, qb);
+  const int ncol = qb - qa;
+  const int c = tid & (HS - 1), g = tid >> 5;
+  constexpr int JU = 13;
+  f32x4 w[JU];
+  if (!(SKIP & 4)) {
+#pragma unroll
+    for (int j = 0; j < JU; ++j) {
+      const int o = 8 * j + g;
+      w[j] = (o < C && c < ncol) ? *reinterpret_cast<const f32x4*>(W3 + (int64_t)o * ldw3 + 4 * (qa + c))
+                                 : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  f32x4 hh = {0.f, 0.f, 0.f, 0.f};
+  if (tid < ncol) hh = reinterpret_cast<const f32x4*>(h2 + (int64_t)m * N2)[qa + tid];
+  for (int o = tid; o < C; o += 256) {
+    float v = b3 ? b3[o] : 0.f;
+    if (!(SKIP & 1)) {
+#pragma unroll 8
+      for (int s = 0; s < Qp; ++s) v += plog[((int64_t)s * M + m) * C + o];
+    }
+    lg[o] = v;
+  }
+  __syncthreads();
+  const int64_t lab = y[m];
+  if (!(SKIP & 2) && wv == 0) {
+    float mx = -INFINITY;
+    for (int cc = lane; cc < C; cc += 64) mx = fmaxf(mx, lg[cc]);
+    mx = sl_wave_max(mx);
+    float se = 0.f;
+    for (int cc = lane; cc < C; cc += 64) se += expf(lg[cc] - mx);
+    se = sl_wave_sum(se);
+    if (lane == 0 && q == 0) loss_rows[m] = mx + logf(se) - lg[lab];
+    const float inv = 1.f / se;
+    for (int cc = lane; cc < C; cc += 64) {
+      float p = expf(lg[cc] - mx) * inv;
+      if (cc == lab) p -= 1.f;
+      lg[cc] = p * scale;
+    }
+  }
+  __syncthreads();
+  if (q == 0)
+    for (int cc = tid; cc < C; cc += 256) dlog[(int64_t)m * C + cc] = lg[cc];
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (!(SKIP & 4)) {
+#pragma unroll
+    for (int j = 0; j < JU; ++j) {
+      const int o = 8 * j + g;
+      const float l = o < C ? lg[o] : 0.f;
+      acc += l * w[j];
+    }
+  }
+  part[g][c] = acc;
+  __syncthreads();
+  if (tid < ncol) {
+    f32x4 v = part[0][tid];
+#pragma unroll
+    for (int gg = 1; gg < 8; ++gg) v += part[gg][tid];
+    f32x4 out;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[i] = hh[i] > 0.f ? v[i] * dscale : 0.f;
+    reinterpret_cast<f32x4*>(dz2 + (int64_t)m * N2)[qa + tid] = out;
+  }
+}
+
 #define CK(x)                                                                  \
   do {                                                                         \
     hipError_t e_ = (x);                                                       \
@@ -359,11 +594,22 @@ int main() {
   auto k_empty = [&] { empty_kernel<<<1, 64, 0, g_probe_stream>>>(scratch); };
   auto k_empty256 = [&] { empty_kernel<<<256, 256, 0, g_probe_stream>>>(scratch); };
   auto k_fwd = [&] {
-    head_fwd_kernel<<<dim3(M, Q), 256, 0, g_probe_stream>>>(P2, S2, slab2, e2, W3, N2, h2, ws, M, N2, C, 0);
+    head_fwd_kernel<false><<<dim3(M, Q), 256, 0, g_probe_stream>>>(P2, S2, slab2, e2, W3, N2, h2, ws, M, N2, C);
   };
   auto k_bwd = [&] {
-    head_bwd_kernel<<<dim3(M, Q), 256, (size_t)C * sizeof(float), g_probe_stream>>>(ws, b3, W3, N2, y, -100, 1.f / M, 2.f, h2, dlog,
-                                                                        dz2, loss, M, N2, C, 0, Q);
+    head_bwd_kernel<false><<<dim3(M, Q), 256, (size_t)C * sizeof(float), g_probe_stream>>>(ws, b3, W3, N2, y, -100, 1.f / M,
+                                                                               2.f, h2, dlog, dz2, loss, M, N2, C, Q);
+  };
+  auto k_fwd0 = [&] {
+    head_fwd_v0_kernel<<<dim3(M, Q), 256, 0, g_probe_stream>>>(P2, S2, slab2, e2, W3, N2, h2, ws, M, N2, C, 0);
+  };
+  auto k_bwd0 = [&] {
+    head_bwd_v0_kernel<<<dim3(M, Q), 256, (size_t)C * sizeof(float), g_probe_stream>>>(ws, b3, W3, N2, y, -100, 1.f / M,
+                                                                           2.f, h2, dlog, dz2, loss, M, N2, C, 0, Q);
+  };
+  auto k_pair0 = [&] {
+    k_fwd0();
+    k_bwd0();
   };
   auto k_pair = [&] {
     k_fwd();
@@ -375,9 +621,9 @@ int main() {
   };
   auto k_pair_m = [&] {
     k_fwd_m();
-    head_bwd_kernel<<<dim3(M, 8), 256, (size_t)C * sizeof(float), g_probe_stream>>>(ws, b3, W3, N2, y, -100, 1.f / M,
-                                                                                   2.f, h2, dlog, dz2, loss, M, N2, C,
-                                                                                   0, Qm);
+    head_bwd_kernel<false><<<dim3(M, 8), 256, (size_t)C * sizeof(float), g_probe_stream>>>(ws, b3, W3, N2, y, -100,
+                                                                                          1.f / M, 2.f, h2, dlog, dz2,
+                                                                                          loss, M, N2, C, Qm);
   };
   auto k_pair_mm = [&] {
     k_fwd_m();
@@ -408,6 +654,18 @@ int main() {
     k_fwd2();
     k_dgrad_pair();
   };
+  auto bwdp = [&](int skip) {
+    return [&, skip] {
+      const size_t sh = (size_t)C * sizeof(float);
+      switch (skip) {
+        case 1: head_bwd_part<1><<<dim3(M, Q), 256, sh, g_probe_stream>>>(ws, b3, W3, N2, y, -100, 1.f / M, 2.f, h2, dlog, dz2, loss, M, N2, C, Q); break;
+        case 2: head_bwd_part<2><<<dim3(M, Q), 256, sh, g_probe_stream>>>(ws, b3, W3, N2, y, -100, 1.f / M, 2.f, h2, dlog, dz2, loss, M, N2, C, Q); break;
+        case 4: head_bwd_part<4><<<dim3(M, Q), 256, sh, g_probe_stream>>>(ws, b3, W3, N2, y, -100, 1.f / M, 2.f, h2, dlog, dz2, loss, M, N2, C, Q); break;
+        case 7: head_bwd_part<7><<<dim3(M, Q), 256, sh, g_probe_stream>>>(ws, b3, W3, N2, y, -100, 1.f / M, 2.f, h2, dlog, dz2, loss, M, N2, C, Q); break;
+        default: head_bwd_part<0><<<dim3(M, Q), 256, sh, g_probe_stream>>>(ws, b3, W3, N2, y, -100, 1.f / M, 2.f, h2, dlog, dz2, loss, M, N2, C, Q); break;
+      }
+    };
+  };
   auto k_p1 = [&] { head_fwd_part<1><<<dim3(M, Q), 256, 0, g_probe_stream>>>(P2, S2, slab2, e2, W3, N2, h2, ws, M, N2, C); };
   auto k_p2 = [&] { head_fwd_part<2><<<dim3(M, Q), 256, 0, g_probe_stream>>>(P2, S2, slab2, e2, W3, N2, h2, ws, M, N2, C); };
   struct Row {
@@ -415,13 +673,16 @@ int main() {
     std::function<void()> f;
   };
   std::vector<Row> rows = {{"empty 1 WG", k_empty},      {"empty 256 WG", k_empty256}, {"head_fwd", k_fwd},
-                           {"head_bwd", k_bwd},          {"head pair", k_pair},        {"head_fwd slab phase", k_p1},
+                           {"head_bwd", k_bwd},          {"head pair", k_pair}, {"head_fwd v0", k_fwd0}, {"head_bwd v0", k_bwd0}, {"head pair v0", k_pair0},        {"head_fwd slab phase", k_p1},
                            {"head_fwd logits phase", k_p2}, {"head_fwd_mfma", k_fwd_m},
                            {"head pair (fwd_mfma)", k_pair_m},
                            {"head_bwd_mfma", k_bwd_mm}, {"head pair (both mfma)", k_pair_mm},
                            {"fc2 dgrad (split-N 8)", k_dgrad}, {"fc2 dgrad reduce", k_dred},
                            {"fc2 dgrad + reduce", k_dgrad_pair}, {"fc2 fwd (once, S 10)", k_fwd2},
-                           {"fc2 fwd + dgrad + reduce", k_fwd_dgrad}};
+                           {"fc2 fwd + dgrad + reduce", k_fwd_dgrad},
+                           {"head_bwd copy", bwdp(0)}, {"head_bwd no plog reduce", bwdp(1)},
+                           {"head_bwd no softmax", bwdp(2)}, {"head_bwd no dz2 phase", bwdp(4)},
+                           {"head_bwd skeleton", bwdp(7)}};
   for (int qv : {8}) {
     Q = qv;
     printf("Q = %d column slices\n", Q);

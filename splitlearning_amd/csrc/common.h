@@ -35,14 +35,53 @@ __device__ __forceinline__ f32x4 bfr4(f32x4 v) { return f32x4{bfr(v[0]), bfr(v[1
 __device__ __forceinline__ float4 bfr4(float4 v) { return make_float4(bfr(v.x), bfr(v.y), bfr(v.z), bfr(v.w)); }
 
 // ------------------------------------------------------------------ reductions
-__device__ __forceinline__ float sl_wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+
+// Row (16-lane) reductions on DPP lane moves instead of LDS-routed ds_bpermute shuffles:
+// xor 1 and xor 2 (quad_perm), then row_half_mirror (lane i <-> 7 - i) and row_mirror (lane
+// i <-> 15 - i).  Every lane of a row ends with the same, bitwise identical total.  A wave
+// total is the four row totals read with v_readlane (sl_wave_sum_dpp / sl_wave_max_dpp).
+template <int CTRL>
+__device__ __forceinline__ float sl_dpp(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float sl_row16_sum(float v) {
+  v += sl_dpp<0xB1>(v);
+  v += sl_dpp<0x4E>(v);
+  v += sl_dpp<0x141>(v);
+  v += sl_dpp<0x140>(v);
   return v;
 }
-__device__ __forceinline__ float sl_wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+__device__ __forceinline__ float sl_row16_max(float v) {
+  v = fmaxf(v, sl_dpp<0xB1>(v));
+  v = fmaxf(v, sl_dpp<0x4E>(v));
+  v = fmaxf(v, sl_dpp<0x141>(v));
+  v = fmaxf(v, sl_dpp<0x140>(v));
+  return v;
+}
+__device__ __forceinline__ float sl_lane(float v, int l) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+__device__ __forceinline__ float sl_wave_sum_dpp(float v) {
+  v = sl_row16_sum(v);
+  return (sl_lane(v, 0) + sl_lane(v, 16)) + (sl_lane(v, 32) + sl_lane(v, 48));
+}
+__device__ __forceinline__ float sl_wave_max_dpp(float v) {
+  v = sl_row16_max(v);
+  return fmaxf(fmaxf(sl_lane(v, 0), sl_lane(v, 16)), fmaxf(sl_lane(v, 32), sl_lane(v, 48)));
+}
+// Whole-wave sum / max, returned to every lane.  Call with all 64 lanes active.
+__device__ __forceinline__ float sl_wave_sum(float v) { return sl_wave_sum_dpp(v); }
+__device__ __forceinline__ float sl_wave_max(float v) { return sl_wave_max_dpp(v); }
+// Sum over aligned groups of SUB consecutive lanes (SUB a power of two <= 64), returned to
+// every lane of the group: DPP moves inside a 16-lane row, ds_bpermute across rows.
+template <int SUB>
+__device__ __forceinline__ float sl_group_sum(float v) {
+  if (SUB >= 2) v += sl_dpp<0xB1>(v);
+  if (SUB >= 4) v += sl_dpp<0x4E>(v);
+  if (SUB >= 8) v += sl_dpp<0x141>(v);
+  if (SUB >= 16) v += sl_dpp<0x140>(v);
+  if (SUB >= 32) v += __shfl_xor(v, 16, 64);
+  if (SUB >= 64) v += __shfl_xor(v, 32, 64);
   return v;
 }
 

@@ -151,10 +151,7 @@ template <int SUB>
 __device__ __forceinline__ void slab_write(float* acc, float* dst, int sub) {
 #pragma unroll
   for (int j = 0; j < 10; ++j) {
-    float v = acc[j];
-#pragma unroll
-    for (int off = 1; off < SUB; off <<= 1) v += __shfl_xor(v, off, 64);
-    acc[j] = v;
+    acc[j] = sl_group_sum<SUB>(acc[j]);
   }
   if (sub == 0) {
 #pragma unroll

@@ -41,10 +41,14 @@ __device__ __forceinline__ void head_slice(int n4, int Q, int q, int& a, int& b)
 // head_fwd_kernel: workgroup (m, q) reduces fc2's split-K slabs for its column slice of row
 // m, applies fc2's epilogue (-> h2) and writes the slice's partial fc3 logits plog[q][m][:].
 // Every load of a phase is issued before the first is consumed (one memory round trip per
-// phase): at B = 16 this op is pure latency.
+// phase): at B = 16 this op is pure latency.  The per-output dot products over the slice's
+// 32 float4 columns are reduced on DPP lane moves within each 16-lane row plus two
+// v_readlane pairs (a 5-step ds_bpermute shuffle per output cost 2.6 us of the kernel in the
+// graph-replay probe, scripts/probe/head_probe.hip).  BF: bf16 compute (operands rounded).
+template <bool BF>
 __global__ void __launch_bounds__(256)
 head_fwd_kernel(const float* __restrict__ P2, int S2, int64_t slab2, Epi e2, const float* __restrict__ W3,
-                int ldw3, float* __restrict__ h2, float* __restrict__ plog, int M, int N2, int C, int bf) {
+                int ldw3, float* __restrict__ h2, float* __restrict__ plog, int M, int N2, int C) {
   __shared__ f32x4 part[8][HS];
   __shared__ f32x4 hs[HS];
   const int m = blockIdx.x, q = blockIdx.y, Q = gridDim.y, tid = threadIdx.x;
@@ -67,14 +71,14 @@ head_fwd_kernel(const float* __restrict__ P2, int S2, int64_t slab2, Epi e2, con
   load_w(0);
   // 1. slab reduction: 32 columns x 8 slab groups
   {
-    const int c = tid & (HS - 1), sg = tid >> 5;
+    const int cc = tid & (HS - 1), sg = tid >> 5;
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if (c < ncol) {
-      const f32x4* src = reinterpret_cast<const f32x4*>(P2 + (int64_t)m * N2) + qa + c;
+    if (cc < ncol) {
+      const f32x4* src = reinterpret_cast<const f32x4*>(P2 + (int64_t)m * N2) + qa + cc;
 #pragma unroll 4
       for (int s = sg; s < S2; s += 8) v += src[s * (slab2 >> 2)];
     }
-    part[sg][c] = v;
+    part[sg][cc] = v;
   }
   __syncthreads();
   if (tid < HS) {
@@ -91,19 +95,21 @@ head_fwd_kernel(const float* __restrict__ P2, int S2, int64_t slab2, Epi e2, con
     hs[tid] = o;
   }
   __syncthreads();
-  // 2. partial logits: half-waves (32 lanes = the slice's columns) per output, 8 outputs
-  //    per wave instruction group; JU outputs' loads in flight per lane
-  const f32x4 h = bf ? bfr4(hs[c]) : hs[c];
+  // 2. partial logits: half-wave h (32 lanes = the slice's columns) owns output 8 j + 2 wv + h
+  const f32x4 h = BF ? bfr4(hs[c]) : hs[c];
+  float* dst = plog + ((int64_t)q * M + m) * C;
   for (int j0 = 0; j0 * 8 < C; j0 += JU) {
     if (j0) load_w(j0);
 #pragma unroll
     for (int j = 0; j < JU; ++j) {
-      const int o = 8 * (j0 + j) + 2 * wv + half;
-      const f32x4 wj = bf ? bfr4(w[j]) : w[j];
-      float d = wj[0] * h[0] + wj[1] * h[1] + wj[2] * h[2] + wj[3] * h[3];
-#pragma unroll
-      for (int off = 16; off > 0; off >>= 1) d += __shfl_xor(d, off);
-      if (c == 0 && o < C) plog[((int64_t)q * M + m) * C + o] = d;
+      const f32x4 wj = BF ? bfr4(w[j]) : w[j];
+      const float d = sl_row16_sum(wj[0] * h[0] + wj[1] * h[1] + wj[2] * h[2] + wj[3] * h[3]);
+      const float s0 = sl_lane(d, 0) + sl_lane(d, 16), s1 = sl_lane(d, 32) + sl_lane(d, 48);
+      const int o = 8 * (j0 + j) + 2 * wv;
+      if (lane == 0) {
+        if (o < C) dst[o] = s0;
+        if (o + 1 < C) dst[o + 1] = s1;
+      }
     }
   }
 }
@@ -209,11 +215,14 @@ fc2_head_fwd_kernel(const float* __restrict__ X, int ldx, const float* __restric
 
 // head_bwd_kernel: workgroup (m, q) sums row m's partial logits (+ b3), softmax-CE (loss and
 // dlogits written by q == 0), then dz2 = (dlogits . W3) * dscale * [h2 > 0] for its slice.
+// The softmax's two wave reductions run on DPP row moves + v_readlane, and each exponential
+// is computed once (kept in LDS for the normalisation).  BF: bf16 compute.
+template <bool BF>
 __global__ void __launch_bounds__(256)
 head_bwd_kernel(const float* __restrict__ plog, const float* __restrict__ b3, const float* __restrict__ W3,
                 int ldw3, const int64_t* __restrict__ y, int64_t ignore, float scale, float dscale,
                 const float* __restrict__ h2, float* __restrict__ dlog, float* __restrict__ dz2,
-                float* __restrict__ loss_rows, int M, int N2, int C, int bf, int Qp) {
+                float* __restrict__ loss_rows, int M, int N2, int C, int Qp) {
   // Qp: number of partial-logit slabs in plog (head_fwd: one per column slice = gridDim.y;
   // fc2_head_fwd: one per 8-column tile)
   extern __shared__ float lg[];   // C
@@ -248,21 +257,26 @@ head_bwd_kernel(const float* __restrict__ plog, const float* __restrict__ b3, co
   const int64_t lab = y[m];
   if (wv == 0) {
     if (lab == ignore) {
-      for (int c = lane; c < C; c += 64) lg[c] = 0.f;
+      for (int cc = lane; cc < C; cc += 64) lg[cc] = 0.f;
       if (lane == 0 && q == 0) loss_rows[m] = 0.f;
     } else {
+      const float zl = lg[lab];
       float mx = -INFINITY;
-      for (int c = lane; c < C; c += 64) mx = fmaxf(mx, lg[c]);
-      mx = sl_wave_max(mx);
+      for (int cc = lane; cc < C; cc += 64) mx = fmaxf(mx, lg[cc]);
+      mx = sl_wave_max_dpp(mx);
       float se = 0.f;
-      for (int c = lane; c < C; c += 64) se += expf(lg[c] - mx);
-      se = sl_wave_sum(se);
-      if (lane == 0 && q == 0) loss_rows[m] = mx + logf(se) - lg[lab];
+      for (int cc = lane; cc < C; cc += 64) {
+        const float e = expf(lg[cc] - mx);
+        lg[cc] = e;
+        se += e;
+      }
+      se = sl_wave_sum_dpp(se);
+      if (lane == 0 && q == 0) loss_rows[m] = mx + logf(se) - zl;
       const float inv = 1.f / se;
-      for (int c = lane; c < C; c += 64) {
-        float p = expf(lg[c] - mx) * inv;
-        if (c == lab) p -= 1.f;
-        lg[c] = p * scale;
+      for (int cc = lane; cc < C; cc += 64) {
+        float p = lg[cc] * inv;
+        if (cc == lab) p -= 1.f;
+        lg[cc] = p * scale;
       }
     }
   }
@@ -276,7 +290,7 @@ head_bwd_kernel(const float* __restrict__ plog, const float* __restrict__ b3, co
     for (int j = 0; j < JU; ++j) {
       const int o = 8 * (j0 + j) + g;
       const float l = o < C ? lg[o] : 0.f;
-      acc += bf ? bfr(l) * bfr4(w[j]) : l * w[j];
+      acc += BF ? bfr(l) * bfr4(w[j]) : l * w[j];
     }
   }
   part[g][c] = acc;
@@ -573,6 +587,18 @@ wgrad_group_mfma_kernel(WgGroup grp, int M, SlOpt o) {
 
 int head3_slices(int N2) { return max(1, (N2 / 4 + HS - 1) / HS); }
 
+static void launch_head_bwd(const float* plog, const float* b3, const float* W3, int ldw3, const int64_t* y,
+                            int64_t ignore, float scale, float dscale, const float* h2, float* dlog, float* dz2,
+                            float* loss_rows, int M, int N2, int C, int Q, int Qp, hipStream_t st) {
+  const size_t sh = (size_t)C * sizeof(float);
+  if (g_bf16)
+    head_bwd_kernel<true><<<dim3(M, Q), 256, sh, st>>>(plog, b3, W3, ldw3, y, ignore, scale, dscale, h2, dlog, dz2,
+                                                        loss_rows, M, N2, C, Qp);
+  else
+    head_bwd_kernel<false><<<dim3(M, Q), 256, sh, st>>>(plog, b3, W3, ldw3, y, ignore, scale, dscale, h2, dlog, dz2,
+                                                         loss_rows, M, N2, C, Qp);
+}
+
 hipError_t server_head3(const float* P2, int S2, int64_t slab2, Epi e2, const float* W3, int ldw3, const float* b3,
                         const int64_t* y, int64_t ignore, float scale, float* h2, float* dlog, float* dz2,
                         float* loss_rows, float* ws, int64_t ws_elems, int M, int N2, int C, hipStream_t st) {
@@ -580,9 +606,11 @@ hipError_t server_head3(const float* P2, int S2, int64_t slab2, Epi e2, const fl
   if ((N2 & 3) || (ldw3 & 3)) return hipErrorInvalidValue;
   const int Q = head3_slices(N2);
   if (ws_elems < (int64_t)Q * M * C) return hipErrorInvalidValue;
-  head_fwd_kernel<<<dim3(M, Q), 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C, g_bf16);
-  head_bwd_kernel<<<dim3(M, Q), 256, (size_t)C * sizeof(float), st>>>(ws, b3, W3, ldw3, y, ignore, scale, e2.dscale,
-                                                                      h2, dlog, dz2, loss_rows, M, N2, C, g_bf16, Q);
+  if (g_bf16)
+    head_fwd_kernel<true><<<dim3(M, Q), 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C);
+  else
+    head_fwd_kernel<false><<<dim3(M, Q), 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C);
+  launch_head_bwd(ws, b3, W3, ldw3, y, ignore, scale, e2.dscale, h2, dlog, dz2, loss_rows, M, N2, C, Q, Q, st);
   return hipGetLastError();
 }
 
@@ -600,8 +628,7 @@ hipError_t server_fc2_head(const float* X, int ldx, const float* W2, int ldw2, E
   if (ws_elems < (int64_t)T * M * C) return hipErrorInvalidValue;
   fc2_head_fwd_kernel<8><<<dim3(T, (M + 15) / 16), 1024, 0, st>>>(X, ldx, W2, ldw2, e2, W3, ldw3, h2, ws, M, N2, K, C,
                                                                   g_bf16);
-  head_bwd_kernel<<<dim3(M, Q), 256, (size_t)C * sizeof(float), st>>>(ws, b3, W3, ldw3, y, ignore, scale, e2.dscale,
-                                                                      h2, dlog, dz2, loss_rows, M, N2, C, g_bf16, T);
+  launch_head_bwd(ws, b3, W3, ldw3, y, ignore, scale, e2.dscale, h2, dlog, dz2, loss_rows, M, N2, C, Q, T, st);
   return hipGetLastError();
 }
 

@@ -131,14 +131,26 @@ def test_fused_server_step_matches_generic(cuda, need_dx, kind, tp):
         torch.testing.assert_close(loss_b, loss_a, rtol=1e-4, atol=1e-5)
         if need_dx:
             torch.testing.assert_close(dxb, dxa, rtol=1e-3, atol=2e-4)
-    torch.cuda.synchronize()
-    for L1, L2 in zip(ta.layers, tb.layers):
-        # Summation-order rounding differs between the two kernel paths. Adam turns noise on
-        # ~zero gradients into moves of up to lr; with SGD-momentum a hidden unit sitting on
-        # the ReLU boundary can flip in one path and not the other, moving a handful of
-        # weights by lr * grad. Both are rare: bound the fraction of affected weights.
-        d = (L1.W - L2.W).abs()
-        assert d.max().item() < 0.1 and (d > 1e-4).float().mean().item() < 1e-4
+        torch.cuda.synchronize()
+        for L1, L2 in zip(ta.layers, tb.layers):
+            # one step from the same state: summation-order rounding only, except rare
+            # elements (Adam: a ~zero gradient's sign is noise, a move of up to lr; SGD-m: a
+            # hidden unit on the ReLU boundary flips in one path)
+            dw = (L1.W - L2.W).abs()
+            assert dw.max().item() < 2e-2 and (dw > 1e-5).float().mean().item() < 1e-4
+        _resync(ta, sa, tb, sb)      # free-running fp32 trajectories of this training are chaotic
+
+
+def _resync(src, src_slot, dst, dst_slot):
+    """dst := src (weights, biases, optimizer moments, step count)."""
+    with torch.no_grad():
+        for La, Lb in zip(src.layers, dst.layers):
+            Lb.W.copy_(La.W)
+            Lb.b.copy_(La.b)
+        for name, st in src_slot.states.items():
+            for k, v in st.items():
+                dst_slot.states[name][k].copy_(v)
+    dst_slot.t = src_slot.t
 
 
 def test_lookahead_matches_plain_fused(cuda):
