@@ -19,14 +19,23 @@ namespace sl {
 
 // One pooled output: 4x4 input patch -> 2x2 conv outputs -> bias, max (first max, torch
 // order), ReLU; `arg` is the 2-bit position of the max for the backward.
+// The 28 x 28 image in LDS, split by column parity: column c of row r sits at
+// (c & 1) * IMG_PLANE + r * IMG_RS + (c >> 1).  Lanes own consecutive pooled columns pw, so
+// a plain row-major image has them read columns 2 pw + j (stride 2: 2-way bank conflicts,
+// 34-45 % of the conv kernels' LDS cycles in an SQ counter pass, profiles/r1_pmc_bench_lds.txt);
+// here each read is consecutive words within a plane, and the 39-word row stride (78 = 14
+// mod 64 banks per pooled row) keeps the ~5 pooled rows of a wave on distinct banks.
+constexpr int IMG_RS = 39, IMG_PLANE = 28 * IMG_RS, IMG_LDS = 2 * IMG_PLANE;
+__device__ __forceinline__ int img_idx(int r, int c) { return (c & 1) * IMG_PLANE + r * IMG_RS + (c >> 1); }
+
 __device__ __forceinline__ void conv_pool_at(const float* img, const float* wk, float bias, int ph, int pw,
                                              float& y, int& arg) {
-  const float* base = img + (2 * ph) * 28 + 2 * pw;
+  const float* base = img + (2 * ph) * IMG_RS + pw;
   float patch[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) patch[i][j] = base[i * 28 + j];
+    for (int j = 0; j < 4; ++j) patch[i][j] = base[(j & 1) * IMG_PLANE + i * IMG_RS + (j >> 1)];
   float best = 0.f;
   arg = 0;
 #pragma unroll
@@ -77,7 +86,7 @@ conv_relu_pool_fwd_kernel(const XT* __restrict__ x, const int64_t* __restrict__ 
                           const float* __restrict__ s1w = nullptr, const float* __restrict__ s0b = nullptr,
                           const float* __restrict__ s1b = nullptr, SlOpt o = SlOpt{}) {
   constexpr int CH = 8, NO = CH * 169, PER = (NO + 255) / 256;
-  __shared__ float img[28 * 28];
+  __shared__ float img[IMG_LDS];
   __shared__ float sw[CH * 9];
   __shared__ float sb[CH];
   const int s = blockIdx.x, q = blockIdx.y;
@@ -103,10 +112,10 @@ conv_relu_pool_fwd_kernel(const XT* __restrict__ x, const int64_t* __restrict__ 
     if (tid < CH * 9) sw[tid] = wv;
     if (tid < CH) sb[tid] = bv;
   }
-  img[tid] = p0;
-  img[256 + tid] = p1;
-  img[512 + tid] = p2;
-  if (tid < 784 - 768) img[768 + tid] = p3;
+  img[img_idx(tid / 28, tid % 28)] = p0;
+  img[img_idx((256 + tid) / 28, (256 + tid) % 28)] = p1;
+  img[img_idx((512 + tid) / 28, (512 + tid) % 28)] = p2;
+  if (tid < 784 - 768) img[img_idx((768 + tid) / 28, (768 + tid) % 28)] = p3;
   __syncthreads();
   float* yo = y + (int64_t)s * 5408 + q * NO;
   uint8_t* ao = am + (int64_t)s * 5408 + q * NO;
@@ -138,11 +147,11 @@ conv_relu_pool_fwd_kernel(const XT* __restrict__ x, const int64_t* __restrict__ 
 // activation (Q5): the activation never leaves registers.
 
 __device__ __forceinline__ void conv_acc_grad(const float* img, int ph, int pw, int a, float g, float* acc) {
-  const float* xr = img + (2 * ph + (a >> 1)) * 28 + 2 * pw + (a & 1);
+  const int r0 = 2 * ph + (a >> 1), c0 = 2 * pw + (a & 1);
 #pragma unroll
   for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
-    for (int kw = 0; kw < 3; ++kw) acc[kh * 3 + kw] = fmaf(g, xr[kh * 28 + kw], acc[kh * 3 + kw]);
+    for (int kw = 0; kw < 3; ++kw) acc[kh * 3 + kw] = fmaf(g, img[img_idx(r0 + kh, c0 + kw)], acc[kh * 3 + kw]);
   acc[9] += g;
 }
 
@@ -165,7 +174,7 @@ __device__ __forceinline__ void stage_sample(const XT* x, int64_t src, const flo
                                              float* sw, float* sb) {
   const int tid = threadIdx.x, nt = blockDim.x;
   const XT* xr = x + src * 784;
-  for (int i = tid; i < 784; i += nt) img[i] = (float)xr[i];
+  for (int i = tid; i < 784; i += nt) img[img_idx(i / 28, i % 28)] = (float)xr[i];
   for (int i = tid; i < 288; i += nt) sw[i] = w[i];
   if (tid < 32) sb[tid] = b[tid];
   __syncthreads();
@@ -191,7 +200,7 @@ conv_step_body(const XT* __restrict__ x, const int64_t* __restrict__ idx, const 
                float* __restrict__ pout, SlOpt o, const int s) {
   constexpr int NJ = (169 + SUB - 1) / SUB;
   constexpr int NW = 32 * SUB / 64;
-  __shared__ float img[28 * 28];
+  __shared__ float img[IMG_LDS];
   __shared__ float sw[32 * 9];
   __shared__ float sb[32];
   __shared__ float red[2 * NW];
@@ -220,7 +229,7 @@ conv_step_body(const XT* __restrict__ x, const int64_t* __restrict__ idx, const 
       }
       if (k < 288) sw[k] = pp; else sb[k - 288] = pp;
     }
-    if (tid < 784) img[tid] = px;
+    if (tid < 784) img[img_idx(tid / 28, tid % 28)] = px;
     __syncthreads();
   } else if (FUSE) {
     const float* pin = w;
@@ -240,7 +249,7 @@ conv_step_body(const XT* __restrict__ x, const int64_t* __restrict__ idx, const 
       if (k < 288) sw[k] = pp; else sb[k - 288] = pp;
     }
     const XT* xr = x + src * 784;
-    for (int i = tid; i < 784; i += 32 * SUB) img[i] = (float)xr[i];
+    for (int i = tid; i < 784; i += 32 * SUB) img[img_idx(i / 28, i % 28)] = (float)xr[i];
     __syncthreads();
   } else {
     stage_sample(x, src, w, b, img, sw, sb);
@@ -355,7 +364,7 @@ conv_wgrad_partial_kernel(const float* __restrict__ dy, const float* __restrict_
                           float* __restrict__ b = nullptr, float* __restrict__ s0w = nullptr,
                           float* __restrict__ s1w = nullptr, float* __restrict__ s0b = nullptr,
                           float* __restrict__ s1b = nullptr, SlOpt o = SlOpt{}) {
-  __shared__ float img[28 * 28];
+  __shared__ float img[IMG_LDS];
   constexpr int SUB = 32, P = (169 + SUB - 1) / SUB;
   const int s = blockIdx.x, tid = threadIdx.x;
   if (pslab && s == 0 && tid < 320) {
@@ -388,7 +397,7 @@ conv_wgrad_partial_kernel(const float* __restrict__ dy, const float* __restrict_
     av[j] = in ? am[row + r] : 0;
   }
   const XT* xr = x + idx[s] * 784;
-  for (int i = tid; i < 784; i += 1024) img[i] = (float)xr[i];
+  for (int i = tid; i < 784; i += 1024) img[img_idx(i / 28, i % 28)] = (float)xr[i];
   __syncthreads();
   float acc[10];
 #pragma unroll
