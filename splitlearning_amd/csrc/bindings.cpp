@@ -739,6 +739,15 @@ PYBIND11_MODULE(_C, m) {
   m.def("linear_fwd_partial", &linear_fwd_partial);
   m.def("linear_dgrad_partial", &linear_dgrad_partial);
   m.def("wgrad_group", &wgrad_group);
+  // Kernel-variant slots (0 = the measured default everywhere), for A/B scripts and tests:
+  //   1 look-ahead LDS layout (1 plain, 2 XOR)     2 wgrad grid (1 2-D, 2 1-D)
+  //   3 wgrad dW form (1 all-MFMA)                 4 wgrad stores (1 plain, not write-through)
+  //   5 dgrad split cap                            6 client local step (1 8-lane per-step launches)
+  //   7 wgrad tile walk (1 forward, 2 reversed)    8 dgrad form (2 full-N)
+  //   10 tiled GEMM tile form                      11 fp32 M > 128 product (1 in-tree GEMM)
+  //   12 single-shard fc2 + head (2 fused)         13 executor launch-skip probe (timing only)
+  //   14 skinny forward (2 k-loop form)
+  // The measurements behind each default are in the comment at the slot's use and docs/PERF.md.
   m.def("set_variant", [](int64_t slot, int64_t v) {
     TORCH_CHECK(slot >= 0 && slot < 16, "variant slot");
     sl::g_variant[slot] = (int)v;
