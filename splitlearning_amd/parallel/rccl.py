@@ -13,14 +13,39 @@ import torch.distributed as dist
 
 def make_native_comm(ranks: list[int], my_rank: int, group=None):
     """Collective over every process: returns a `_C.TpComm` on members of `ranks`,
-    None elsewhere.  `group` is the torch.distributed group containing `ranks`."""
+    None elsewhere — and None everywhere when any member could not create it (the
+    callers then keep the torch.distributed path).  `group` is the torch.distributed group
+    containing `ranks`."""
     from .. import _native
     C = _native.load()
-    box = [C.nccl_unique_id() if my_rank == ranks[0] else None]
+    err = None
+    uid = None
+    if my_rank == ranks[0]:
+        try:
+            uid = C.nccl_unique_id()
+        except RuntimeError as e:
+            err = e
+    box = [uid]
     dist.broadcast_object_list(box, src=ranks[0], group=group)
-    if my_rank not in ranks:
+    comm = None
+    if box[0] is None and err is None:
+        err = "no RCCL unique id from rank %d" % ranks[0]
+    if my_rank in ranks and box[0] is not None:
+        try:
+            comm = C.TpComm(box[0], len(ranks), ranks.index(my_rank))
+        except RuntimeError as e:           # e.g. an RCCL the process cannot initialise
+            err = e
+    # every rank agrees: if any member failed, nobody uses a native communicator and the
+    # caller keeps the torch.distributed path (same protocol, Python-issued)
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
+    ok = torch.tensor([0 if err is not None else 1], dtype=torch.int32, device=dev)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+    if int(ok.item()) == 0:
+        import warnings
+        warnings.warn(f"native RCCL communicator unavailable ({err or 'failed on another rank'}); "
+                      "using torch.distributed p2p / collectives")
         return None
-    return C.TpComm(box[0], len(ranks), ranks.index(my_rank))
+    return comm
 
 
 def self_comm():
