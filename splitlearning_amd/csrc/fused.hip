@@ -354,18 +354,11 @@ __device__ __forceinline__ void st_wt(float* base, int N, int ld, int boff, f32x
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), rs, boff, 0, 16);
 }
 
-// RT: weight rows per workgroup (one wave per row, 64 lanes x float4 = 256 columns).  RT = 16
-// is the default; RT = 8 (variant 9 = 1, A/B) halves the workgroup so four fit a CU instead of
-// two, letting one workgroup's look-ahead tail overlap three others' streams, at the price of
-// staging each 16 x 256 A tile twice as often (each wave then owns two 16-column k-groups of
-// the look-ahead; rows RT..15 of the staged W tile are zero).
-template <bool ADAM, int FWDC, bool PART, int RT = 16>
-__global__ void __launch_bounds__(64 * RT)
+template <bool ADAM, int FWDC, bool PART>
+__global__ void __launch_bounds__(1024)
 wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
   // FWDC: look-ahead row chunks of 16 (0 = no look-ahead; 1: next batch <= 16 rows; 4: <= 64)
   constexpr bool FWDN = FWDC > 0;
-  constexpr int KG = 16 / RT;              // look-ahead k-groups (16 columns each) per wave
-  static_assert(RT == 16 || RT == 8, "rows per workgroup");
   __shared__ f32x4 sa[16][64];
   __shared__ float sdz[16][16];
   // look-ahead: the updated W tile, rows padded to 65 float4 (variant 1 = 1: plain 64-float4
@@ -374,7 +367,7 @@ wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
   // 16 hit the same LDS banks (rocprofv3 SQ_LDS_BANK_CONFLICT 3.96 M cycles per TP = 1
   // step, 0 without the look-ahead); one float4 of padding spreads them over all banks.
   __shared__ f32x4 sw[FWDN ? 16 * 65 : 1];
-  __shared__ f32x4 red[FWDN ? RT : 1][64];   // look-ahead: per-wave 16x16 partials
+  __shared__ f32x4 red[FWDN ? 16 : 1][64];   // look-ahead: per-wave 16x16 partials
   // pick the layer with selects (no runtime-indexed access to the by-value argument)
   int bx, by;
   const int layer = wg_tile(grp, bx, by);
@@ -384,7 +377,7 @@ wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
   if (kb >= L.K) return;                 // 2-D grid only; uniform per workgroup
   const int tid = threadIdx.x;
   const int r = tid >> 6, lane = tid & 63;
-  const int n0 = by * RT;
+  const int n0 = by * 16;
   const int n = n0 + r;
   const int k = kb + lane * 4;
   const bool act = (n < L.N) && (k < L.K);
@@ -396,34 +389,28 @@ wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
     q0 = *reinterpret_cast<const f32x4*>(L.s0 + off);
     if (ADAM) q1 = *reinterpret_cast<const f32x4*>(L.s1 + off);
   }
-  // look-ahead A operand in MFMA layout: lane (li, lq) holds x_next[li][kb + 16*g + 4*lq .. +3]
-  // for the wave's k-groups g = r + RT * i
+  // look-ahead A operand in MFMA layout: lane (li, lq) holds x_next[li][kb + 16*wave + 4*lq .. +3]
   const int li = lane & 15, lq = lane >> 4;
-  f32x4 xv[FWDC > 0 ? FWDC : 1][KG];
+  const int kx = kb + 16 * r + 4 * lq;
+  f32x4 xv[FWDC > 0 ? FWDC : 1];
 #pragma unroll
-  for (int c = 0; c < (FWDC > 0 ? FWDC : 1); ++c)
-#pragma unroll
-    for (int i = 0; i < KG; ++i) {
-      const int kx = kb + 16 * (r + RT * i) + 4 * lq;
-      xv[c][i] = zv;
-      if (FWDN && l0 && 16 * c + li < grp.mn && kx < L.K)
-        xv[c][i] = *reinterpret_cast<const f32x4*>(grp.xn + (int64_t)(16 * c + li) * grp.ldxn + kx);
-    }
+  for (int c = 0; c < (FWDC > 0 ? FWDC : 1); ++c) {
+    xv[c] = zv;
+    if (FWDN && l0 && 16 * c + li < grp.mn && kx < L.K)
+      xv[c] = *reinterpret_cast<const f32x4*>(grp.xn + (int64_t)(16 * c + li) * grp.ldxn + kx);
+  }
   f32x4 g = zv;
   float gb = 0.f;
   for (int mc = 0; mc < M; mc += 16) {
     if (mc) __syncthreads();
     {
-#pragma unroll
-      for (int rr = r; rr < 16; rr += RT) {
-        const int mm = mc + rr;
-        const f32x4 av = (mm < M && k < L.K) ? *reinterpret_cast<const f32x4*>(L.A + (int64_t)mm * L.lda + k) : zv;
-        sa[rr][lane] = grp.bf16 ? bfr4(av) : av;
-      }
+      const int mm = mc + r;
+      const f32x4 av = (mm < M && k < L.K) ? *reinterpret_cast<const f32x4*>(L.A + (int64_t)mm * L.lda + k) : zv;
+      sa[r][lane] = grp.bf16 ? bfr4(av) : av;
       if (tid < 256) {
         const int mr = mc + (tid >> 4), nn = n0 + (tid & 15);
         float v = 0.f;
-        if (mr < M && nn < L.N && (tid & 15) < RT) {
+        if (mr < M && nn < L.N) {
           if (PART && L.dzp) {
             // every slab load (and the mask load) in flight at once: bit-identical to
             // dgrad_reduce_kernel's sum, one round trip instead of S dependent ones
@@ -460,34 +447,23 @@ wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
   }
   if (FWDN && l0) {
     // next batch's partial pre-activations with the updated tile: stage W_new through LDS
-    // into MFMA B layout; wave w covers columns [16g, 16g+16) of its k-groups g with 4 exact-fp32
-    // MFMAs each (B[k][n] = W_new[n][k]: lane (n = li, k-group lq) reads one float4 of the tile)
+    // into MFMA B layout; wave w covers columns [16w, 16w+16) with 4 exact-fp32 MFMAs
+    // (B[k][n] = W_new[n][k]: lane (n = li, k-group lq) reads one float4 of the tile)
     // layout: grp.swz 0 = rows padded to 65 float4, 1 = plain 64, 2 = column XOR (row & 15)
+    const int wcol = grp.swz == 2 ? (lane ^ r) : lane;
+    const int rcol = grp.swz == 2 ? ((4 * r + lq) ^ li) : 4 * r + lq;
     const int rs = grp.swz == 0 ? 65 : 64;
-#pragma unroll
-    for (int rr = r; rr < 16; rr += RT) {
-      const int wcol = grp.swz == 2 ? (lane ^ rr) : lane;
-      sw[rr * rs + wcol] = (rr == r && act) ? p : zv;
-    }
+    sw[r * rs + wcol] = act ? p : zv;
     __syncthreads();
-    f32x4 wv4[KG];
-#pragma unroll
-    for (int i = 0; i < KG; ++i) {
-      const int kgc = 4 * (r + RT * i) + lq;
-      const int rcol = grp.swz == 2 ? (kgc ^ li) : kgc;
-      wv4[i] = sw[li * rs + rcol];
-      if (grp.bf16) wv4[i] = bfr4(wv4[i]);
-    }
+    f32x4 wv4 = sw[li * rs + rcol];
+    if (grp.bf16) wv4 = bfr4(wv4);
 #pragma unroll
     for (int c = 0; c < FWDC; ++c) {
       if (16 * c >= grp.mn) break;        // uniform
       f32x4 z = zv;
+      const f32x4 xc = grp.bf16 ? bfr4(xv[c]) : xv[c];
 #pragma unroll
-      for (int i = 0; i < KG; ++i) {
-        const f32x4 xc = grp.bf16 ? bfr4(xv[c][i]) : xv[c][i];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) z = __builtin_amdgcn_mfma_f32_16x16x4f32(xc[j], wv4[i][j], z, 0, 0, 0);
-      }
+      for (int i = 0; i < 4; ++i) z = __builtin_amdgcn_mfma_f32_16x16x4f32(xc[i], wv4[i], z, 0, 0, 0);
       if (c) __syncthreads();             // the previous chunk's readers are done with red
       red[r][lane] = z;                   // z[j] = partial(m = 16c + 4*lq + j, n = n0 + li)
       __syncthreads();
@@ -496,8 +472,8 @@ wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
         const int mm = tid >> 4;
         float v = 0.f;
 #pragma unroll
-        for (int w = 0; w < RT; ++w) v += red[w][16 * (mm >> 2) + nn][mm & 3];
-        if (m < grp.mn && nn < RT && n0 + nn < L.N) grp.pn[((int64_t)bx * grp.mn + m) * L.N + n0 + nn] = v;
+        for (int w = 0; w < 16; ++w) v += red[w][16 * (mm >> 2) + nn][mm & 3];
+        if (m < grp.mn && n0 + nn < L.N) grp.pn[((int64_t)bx * grp.mn + m) * L.N + n0 + nn] = v;
       }
     }
   }
@@ -679,25 +655,23 @@ hipError_t wgrad_group(const WgGroup& g, int M, SlOpt o, hipStream_t st) {
   int kmax = 0, yb = 0, wb = 0;
   WgGroup gg = g;
   set_traversal(gg);
-  bool part = false;
-  for (int i = 0; i < gg.n; ++i) part = part || gg.d[i].dzp != nullptr;
-  // rows per workgroup: 16, or 8 (variant 9 = 1; the LDS-staged kernel without partial dZ)
-  const int RT = (g_variant[9] == 1 && g_variant[3] != 1 && !part) ? 8 : 16;
   for (int i = 0; i < gg.n; ++i) {
     gg.d[i].yb0 = yb;
     gg.d[i].wb0 = wb;
-    yb += (gg.d[i].N + RT - 1) / RT;
-    wb += ((gg.d[i].N + RT - 1) / RT) * ((gg.d[i].K + 255) / 256);
+    yb += (gg.d[i].N + 15) / 16;
+    wb += ((gg.d[i].N + 15) / 16) * ((gg.d[i].K + 255) / 256);
     kmax = max(kmax, gg.d[i].K);
   }
   if (yb == 0 || kmax == 0) return hipSuccess;
-  gg.nt0 = ((gg.d[0].N + RT - 1) / RT) * ((gg.d[0].K + 255) / 256);
+  gg.nt0 = ((gg.d[0].N + 15) / 16) * ((gg.d[0].K + 255) / 256);
   dim3 grid((kmax + 255) / 256, yb);     // 2-D grid of the all-MFMA variant
   const dim3 grid1(wb);                  // 1-D grid over the real tiles (default kernel)
   if (gg.xn && (gg.mn <= 0 || gg.mn > 64 || !gg.pn)) return hipErrorInvalidValue;
   if (gg.xn && gg.mn > 16 && g_variant[3] == 1) return hipErrorInvalidValue;   // MFMA-dW variant: <= 16
   const bool fw = gg.xn != nullptr;
   const bool fw4 = fw && gg.mn > 16;
+  bool part = false;
+  for (int i = 0; i < gg.n; ++i) part = part || gg.d[i].dzp != nullptr;
   if (g_variant[3] != 1) {   // default: LDS-staged VALU dW (row-contiguous W streams)
   // 2-D grid when it wastes < 10 % of its workgroups (TP = 1: 3 %, measured 1.4 us per step
   // faster there), else the 1-D grid (TP = 2 / 4 / 8: 18-55 % empty, 0.3-1.2 us faster);
@@ -705,12 +679,8 @@ hipError_t wgrad_group(const WgGroup& g, int M, SlOpt o, hipStream_t st) {
   const int64_t g2 = (int64_t)grid.x * grid.y;
   gg.grid2d = g_variant[2] == 1 ? 1 : (g_variant[2] == 2 ? 0 : ((g2 - wb) * 10 < g2 ? 1 : 0));
 #define SL_WG(A, F, P) wgrad_group_kernel<A, F, P><<<gg.grid2d ? grid : grid1, 1024, 0, st>>>(gg, M, o)
-#define SL_WG8(A, F) wgrad_group_kernel<A, F, false, 8><<<gg.grid2d ? grid : grid1, 512, 0, st>>>(gg, M, o)
     const int fc = fw4 ? 4 : (fw ? 1 : 0);
-    if (RT == 8) {
-      if (o.kind == 2) { if (fc == 4) SL_WG8(true, 4); else if (fc) SL_WG8(true, 1); else SL_WG8(true, 0); }
-      else { if (fc == 4) SL_WG8(false, 4); else if (fc) SL_WG8(false, 1); else SL_WG8(false, 0); }
-    } else if (part) {
+    if (part) {
       if (o.kind == 2) { if (fc == 4) SL_WG(true, 4, true); else if (fc) SL_WG(true, 1, true); else SL_WG(true, 0, true); }
       else { if (fc == 4) SL_WG(false, 4, true); else if (fc) SL_WG(false, 1, true); else SL_WG(false, 0, true); }
     } else {
@@ -718,7 +688,6 @@ hipError_t wgrad_group(const WgGroup& g, int M, SlOpt o, hipStream_t st) {
       else { if (fc == 4) SL_WG(false, 4, false); else if (fc) SL_WG(false, 1, false); else SL_WG(false, 0, false); }
     }
 #undef SL_WG
-#undef SL_WG8
     return hipGetLastError();
   }
   // variant 1: all-MFMA form (64-byte row segments per wave: measured slower, see above)

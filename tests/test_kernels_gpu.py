@@ -231,7 +231,7 @@ def test_conv_local_step(cuda, kind, B):
     _close(b1, b2, rtol=1e-3, atol=3e-4 if kind == "adam" else 1e-6)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2])       # 0 = LDS-staged (default), 1 = all-MFMA, 2 = 8-row tiles
+@pytest.mark.parametrize("variant", [0, 1])          # 0 = LDS-staged (default), 1 = all-MFMA
 @pytest.mark.parametrize("kind", ["sgd", "adam"])
 @pytest.mark.parametrize("M,shapes,mn", [(16, [(5000, 5408), (1000, 5000)], 16), (20, [(100, 1000), (33, 20)], 5),
                                          (7, [(10, 100)], 0), (64, [(1000, 5408), (100, 1000)], 64),
@@ -259,12 +259,10 @@ def test_wgrad_group(cuda, variant, kind, M, shapes, mn):
         xn = torch.randn(mn, shapes[0][1], device=cuda)
         kw = {"x_next": xn, "p_next": hip_ops.lookahead_slabs(cuda, shapes[0][1], mn, shapes[0][0])}
     try:
-        C.set_variant(3, 1 if variant == 1 else 0)
-        C.set_variant(9, 1 if variant == 2 else 0)
+        C.set_variant(3, variant)
         hip_ops.wgrad_group_(layers, M, cfg, 4, **kw)
     finally:
         C.set_variant(3, 0)
-        C.set_variant(9, 0)
     for (dz, a, w2, b2, sw2, sb2), L in zip(refs, layers):
         torch_ops.linear_wgrad_step_(dz, a, w2, b2, cfg, sw2, sb2, 4)
         _close(L[5], w2, rtol=1e-4, atol=1e-5)
