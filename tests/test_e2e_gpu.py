@@ -32,6 +32,22 @@ def test_sisa_unlearning_on_gpu(cuda, tmp_path):
     assert cu / tu < 0.5 * (cr / tr)
 
 
+@pytest.mark.parametrize("ws", [5, 9])
+def test_sisa_colocated_alices_on_gpu(cuda, tmp_path, ws):
+    """ws - 1 Alices on one GPU, stepped together (conv_local_epoch_multi): every Alice
+    trains and is evaluated, and the concat variant runs with k = ws - 1 heads.  (The other
+    Alices keep label 9, so the all-client breakdown is not an unlearning check here.)"""
+    m, bob = _run(tmp_path, ["--sisa"], ws=ws)
+    assert m["world_size"] == ws and m["nprocs"] == 1
+    corr, tot, cu, tu, cr, tr = m["last_eval"]
+    assert tot > 0 and corr / tot > 0.3          # learnable synthetic data: well above chance
+    for c in range(1, ws):
+        log = (tmp_path / "logs" / f"alice{c}.log").read_text()
+        assert f"Alice-{c} Evaluating Data" in log
+    mc, _ = _run(tmp_path / "concat", ["--sisa", "--concat"], ws=ws)
+    assert mc["world_size"] == ws
+
+
 @pytest.mark.parametrize("flags", [["--vanilla"], [], ["--control"], ["--sisa", "--concat", "--concat_unlearn"]])
 def test_modes_on_gpu(cuda, tmp_path, flags):
     m, bob = _run(tmp_path, flags)
