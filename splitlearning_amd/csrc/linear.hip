@@ -575,10 +575,10 @@ __global__ void opt_flat_kernel(float* __restrict__ p, const float* __restrict__
 hipError_t linear_fwd(const float* X, int ldx, const float* W, int ldw, float* Y, int ldy, int M, int N,
                       int K, Epi e, float* ws, int64_t ws_elems, hipStream_t st) {
   if (M <= 0 || N <= 0) return hipSuccess;
-  // many rows (evaluation over a whole test set, large batches) in bf16: the LDS-tiled MFMA
-  // GEMM.  In fp32 the caller (hip_ops.linear_fwd) hands plain products to hipBLASLt and only
-  // the epilogue runs here, unless variant 11 = 1 forces this kernel (gemm.hip measurements).
-  if (M > 128 && (g_bf16 || g_variant[11] == 1)) return gemm_nt(X, ldx, W, ldw, Y, ldy, M, N, K, e, g_bf16 != 0, st);
+  // many rows (evaluation over a whole test set, large batches): the LDS-tiled MFMA GEMM.
+  // In fp32 the caller (hip_ops.linear_fwd) hands plain products to hipBLASLt and only the
+  // epilogue runs here, except inside a HIP graph capture or under variant 11 = 1.
+  if (M > 128) return gemm_nt(X, ldx, W, ldw, Y, ldy, M, N, K, e, g_bf16 != 0, st);
   dim3 grid((N + 15) / 16, (M + 15) / 16);
   int NW1, S1;
   if (!g_bf16 && g_variant[14] != 2 && fwd_once_plan(M, N, K, 16, ws ? ws_elems : 0, NW1, S1)) {

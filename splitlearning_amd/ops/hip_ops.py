@@ -192,13 +192,21 @@ def set_compute_dtype(dtype: str):
     C().set_compute_dtype(dtype)
 
 
+def _library_gemm(M: int) -> bool:
+    """fp32 products of many rows go to hipBLASLt (measured faster than the in-tree tiled
+    GEMM, csrc/gemm.hip) — except inside a HIP graph capture, where the library may not
+    allocate or initialise, and under variant 11 = 1 (the in-tree kernels, A/B and tests)."""
+    return (M > LARGE_M and C().get_compute_dtype() == "fp32" and C().get_variant(11) != 1
+            and not torch.cuda.is_current_stream_capturing())
+
+
 def linear_fwd(x, w, b, relu: bool, drop_p: float, seed: int, col_offset: int = 0, out=None, dseed=None):
     M, N = x.shape[0], w.shape[0]
     if out is None:
         out = torch.empty(M, N, device=x.device, dtype=torch.float32)
     w = w.detach()
     bias = b.detach() if b is not None else None
-    if M > LARGE_M and C().get_compute_dtype() == "fp32" and C().get_variant(11) != 1:
+    if _library_gemm(M):
         P = torch.mm(x, w.t())
         C().linear_epilogue(P, bias, out, relu, float(drop_p), seed & M64, col_offset, _ptr(dseed))
         return out
@@ -247,6 +255,16 @@ def linear_dgrad(dz, w, h_prev=None, scale: float = 1.0, out=None, ws=None):
     M, K = dz.shape[0], w.shape[1]
     if out is None:
         out = torch.empty(M, K, device=dz.device, dtype=torch.float32)
+    if _library_gemm(M):
+        # many rows (large --batch_size): the skinny kernel would re-read W once per 16 rows;
+        # the product goes to hipBLASLt (as the forward does) and the previous layer's
+        # ReLU/dropout mask + scale is one in-tree elementwise launch
+        P = torch.mm(dz, w.detach())
+        if h_prev is not None:                   # scale belongs to the mask (dropout 1/(1-p))
+            C().relu_mask(P, h_prev.contiguous(), float(scale), out)
+        else:
+            out.copy_(P)
+        return out
     if ws is None:
         ws = _workspace(dz.device, 16 * M * K)
     C().linear_dgrad(dz, w.detach(), h_prev, float(scale), out, ws)

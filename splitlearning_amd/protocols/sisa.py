@@ -244,6 +244,11 @@ class SisaSession(Session):
             # per step, and skips the graph's per-chunk staging copies (187.9 vs 190.0 us per
             # step at TP = 1, 54.4 vs 56.1 at TP = 8)
             return False
+        if mode == "auto" and self.B > 128:
+            # batches past the skinny kernels' range: eagerly the fp32 products go to
+            # hipBLASLt, which cannot be captured (a graph would fall back to the in-tree
+            # kernels: 299.7 k vs 386.6 k samples/s at batch 256 vs 128 captured)
+            return False
         if self.tail.tp_size != 1:
             # A TP shard step is GPU-bound even eagerly (measured 58 us eager vs 59 us
             # replayed at TP=8, docs/PERF.md), so "auto" keeps the collective out of the

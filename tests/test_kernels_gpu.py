@@ -125,7 +125,7 @@ def test_linear_fwd_partial(cuda, M, N, K, max_split, once):
 
 @pytest.mark.parametrize("M,N,K", [(16, 5000, 5408), (16, 1000, 5000), (16, 100, 1000), (16, 10, 100),
                                     (3, 37, 52), (16, 1000, 628), (64, 1000, 5000), (40, 1000, 604),
-                                    (16, 12, 8)])
+                                    (16, 12, 8), (200, 1000, 5000), (1000, 100, 1000)])
 @pytest.mark.parametrize("masked", [False, True])
 @pytest.mark.parametrize("variant", [0, 2])
 def test_linear_dgrad(cuda, M, N, K, masked, variant):
