@@ -48,6 +48,16 @@ def test_sisa_colocated_alices_on_gpu(cuda, tmp_path, ws):
     assert mc["world_size"] == ws
 
 
+@pytest.mark.parametrize("flags", [["--vanilla"], [], ["--sisa"], ["--sisa", "--concat"]])
+def test_modes_at_large_batch_on_gpu(cuda, tmp_path, flags):
+    """--batch_size 256: past the fused executor (<= 64 rows) and the skinny kernels (<= 128):
+    library products eagerly, the in-tree tiled GEMM under graph capture."""
+    m, bob = _run(tmp_path, flags, extra=["--batch_size", "256"])
+    assert "Accuracy over all data" in bob
+    corr, tot = m["last_eval"][0], m["last_eval"][1]
+    assert tot > 0 and corr / tot > 0.15          # above chance after ~19 batches of 256
+
+
 @pytest.mark.parametrize("flags", [["--vanilla"], [], ["--control"], ["--sisa", "--concat", "--concat_unlearn"]])
 def test_modes_on_gpu(cuda, tmp_path, flags):
     m, bob = _run(tmp_path, flags)
