@@ -192,7 +192,9 @@ static bool fwd_once_plan(int M, int N, int K, int max_split, int64_t ws_elems, 
   const int64_t slab = (int64_t)M * N;
   const int64_t fit = ws_elems / (slab > 0 ? slab : 1);
   const int smax = (int)std::max<int64_t>(1, std::min<int64_t>(max_split, fit));
-  NW = std::min(waves, 8);
+  // waves per workgroup (variant 14: 3 -> 4, 4 -> 16, for A/B; default 8)
+  const int nwt = g_variant[14] == 3 ? 4 : (g_variant[14] == 4 ? 16 : 8);
+  NW = std::min(waves, nwt);
   S = (waves + NW - 1) / NW;
   if (S > smax) {
     S = smax;
