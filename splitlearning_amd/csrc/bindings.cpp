@@ -747,6 +747,7 @@ PYBIND11_MODULE(_C, m) {
   //   10 tiled GEMM tile form                      11 fp32 M > 128 product (1 in-tree GEMM)
   //   12 single-shard fc2 + head (2 fused)         13 executor launch-skip probe (timing only)
   //   14 skinny forward (2 k-loop form; 3 / 4: 4 / 16 waves per workgroup)
+  //   15 U-shape head step (1 per-thread FMA form)
   // The measurements behind each default are in the comment at the slot's use and docs/PERF.md.
   m.def("set_variant", [](int64_t slot, int64_t v) {
     TORCH_CHECK(slot >= 0 && slot < 16, "variant slot");

@@ -58,6 +58,12 @@ __device__ __forceinline__ float sl_row16_max(float v) {
   v = fmaxf(v, sl_dpp<0x140>(v));
   return v;
 }
+// value of lane (row base + j) of this lane's 16-lane row (j uniform within the row or not:
+// ds_bpermute-free via a DPP-built row, here simply a bpermute inside the row)
+__device__ __forceinline__ float sl_dpp_pick(float v, int j) {
+  const int src = ((int)(__lane_id()) & ~15) + (j & 15);
+  return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src << 2, __builtin_bit_cast(int, v)));
+}
 __device__ __forceinline__ float sl_lane(float v, int l) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
 }

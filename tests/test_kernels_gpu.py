@@ -399,10 +399,20 @@ def test_relu_mask(cuda):
 
 
 @pytest.mark.parametrize("kind", ["sgd", "adam"])
-@pytest.mark.parametrize("M", [16, 7])
-def test_head_step_matches_torch(cuda, kind, M):
+@pytest.mark.parametrize("M", [16, 7, 32])
+@pytest.mark.parametrize("form", [0, 1])
+def test_head_step_matches_torch(cuda, kind, M, form):
     """_C.head_step (the U-shape head's forward + CE + dgrad + optimizer in one launch) ==
-    the fp32 torch reference of the same step."""
+    the fp32 torch reference of the same step.  form 0: the MFMA kernel (<= 16 rows; more
+    rows take the FMA kernel), 1: the FMA kernel (variant 15 = 1)."""
+    hip_ops.C().set_variant(15, form)
+    try:
+        _head_step_check(cuda, kind, M)
+    finally:
+        hip_ops.C().set_variant(15, 0)
+
+
+def _head_step_check(cuda, kind, M):
     cfg = OptimCfg("adam", 1e-3) if kind == "adam" else OptimCfg("sgd", 1e-2, momentum=0.9)
     g = torch.Generator().manual_seed(2)
     x = torch.rand(M, 100, generator=g)
