@@ -644,9 +644,11 @@ hipError_t linear_dgrad(const float* dZ, int ldz, const float* W, int ldw, const
   // server step unsplit vs 51.8 us split; profiles/r1_dgrad_split_ab.txt).
   const int v5 = g_variant[5];
   const int smax = v5 > 0 ? v5 : 16;
-  // few K tiles (a TP shard's fc2, K = 628 at TP = 8): N slices down to 32 rows (S = 16):
-  // 3.1 vs 3.7 us per launch in the graph-replay probe (scripts/probe/dgrad_probe.hip)
-  const int rmin = v5 > 1 ? 16 : (kt * mt <= 64 ? 32 : 64);
+  // few K tiles over a long N (a TP shard's fc2: K = 628, N = 1000 at TP = 8): N slices down
+  // to 32 rows (S = 16): 3.1 vs 3.7 us per launch in the graph-replay probe
+  // (scripts/probe/dgrad_probe.hip).  Short N (the U-shape fc2, N = 100) stays unsplit: one
+  // launch with the mask fused beats a split plus a reduce launch.
+  const int rmin = v5 > 1 ? 16 : ((kt * mt <= 64 && N >= 512) ? 32 : 64);
   while (S < smax && kt * mt * S < 768 && N / (S * 2) >= rmin) S *= 2;
   const int64_t slab = (int64_t)M * K;
   if (ws == nullptr) S = 1;
