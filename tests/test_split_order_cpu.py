@@ -59,3 +59,17 @@ def test_split_epoch_order_matches_per_batch_steps(kind, ahead, tmp_path):
     for ma, mb in mods:
         for (k, va), vb in zip(ma.state_dict().items(), mb.state_dict().values()):
             torch.testing.assert_close(va, vb, rtol=1e-5, atol=1e-6, msg=k)
+
+
+def test_bob_tp_policy():
+    """--bob_tp 0 (parallel/dist.py::choose_bob_tp): the server-phase modes use every GPU;
+    the serial split modes weigh the optimizer stream a shard saves against the message
+    rounds it adds — vanilla's 32 M-parameter Bob shards across every GPU, the U-shape
+    middle (5.5 M) stays on one."""
+    from splitlearning_amd.parallel.dist import choose_bob_tp
+    for n in (1, 2, 4, 8):
+        for mode in ("sisa", "concat", "control"):
+            assert choose_bob_tp(mode, n) == n
+        assert choose_bob_tp("vanilla", n) == n
+        assert choose_bob_tp("ushape", n) == 1
+    assert choose_bob_tp("vanilla", 6) in (1, 2, 6) and 6 % choose_bob_tp("vanilla", 6) == 0
