@@ -192,6 +192,13 @@ static bool fwd_once_plan(int M, int N, int K, int max_split, int64_t ws_elems, 
   const int64_t slab = (int64_t)M * N;
   const int64_t fit = ws_elems / (slab > 0 ? slab : 1);
   const int smax = (int)std::max<int64_t>(1, std::min<int64_t>(max_split, fit));
+  // a product that one 16-wave workgroup per tile covers (K <= 1024: the U-shape fc2, a TP
+  // shard's fc2) runs unsplit, so the epilogue is fused and no slab-reduce launch follows
+  if (waves <= 16) {
+    NW = waves;
+    S = 1;
+    return true;
+  }
   // waves per workgroup (variant 14: 3 -> 4, 4 -> 16, for A/B; default 8)
   const int nwt = g_variant[14] == 3 ? 4 : (g_variant[14] == 4 ? 16 : 8);
   NW = std::min(waves, nwt);
