@@ -98,6 +98,8 @@ def main(argv=None):
     ap.add_argument("--bob_tp", type=int, default=0,
                     help="0 = the policy (parallel/dist.py choose_bob_tp: all GPUs for the SISA modes)")
     ap.add_argument("--graphs", choices=("auto", "on", "off"), default="auto")
+    ap.add_argument("--tp_allreduce", choices=("auto", "rccl"), default="auto",
+                    help="Bob's TP all-reduce: peer-mapped one-kernel path when it passes set-up (auto) or RCCL")
     ap.add_argument("--act_dtype", choices=("fp32", "bf16"), default="fp32")
     ap.add_argument("--dtype", choices=("fp32", "bf16"), default="fp32", help="compute dtype")
     ap.add_argument("--concat_unlearn", action="store_true", default=True,
@@ -142,6 +144,7 @@ def main(argv=None):
         "--batch_size", str(a.batch_size), "--partition_alpha", str(a.partition_alpha),
         "--server_epochs", str(a.server_epochs), "--seed", str(a.seed), "--num_samples", str(a.num_samples),
         "--kernels", a.kernels, "--graphs", a.graphs, "--act_dtype", a.act_dtype, "--dtype", a.dtype, "--no_tqdm",
+        "--tp_allreduce", a.tp_allreduce,
         "--log_dir", log_dir, "--watchdog", "off"]
     if a.mode == "concat" and a.concat_unlearn:
         argv_s.append("--concat_unlearn")
@@ -239,6 +242,8 @@ def main(argv=None):
                 "baseline_basis": ("reference CPU phase rates from BASELINE.md composed over this schedule's "
                                    "sample counts" if base else None),
                 "dist_world": N, "rccl_nranks": int(tpc.size) if tpc is not None else (1 if use_gpu else 0),
+                "tp_allreduce": ("ipc" if getattr(sess, "tp_ipc", None) is not None else
+                                 "rccl" if tpc is not None else "torch.distributed" if N > 1 else "none"),
                 "bytes_sent_per_rank_per_step": sent,
             },
         }

@@ -122,6 +122,10 @@ def build_parser() -> argparse.ArgumentParser:
                    help="GPU: move data-plane messages with torch.distributed isend/irecv instead of "
                         "the native RCCL communicators (per-batch p2p on the compute stream, TP "
                         "all-reduce inside the server step)")
+    g.add_argument("--tp_allreduce", choices=("auto", "rccl"), default="auto",
+                   help="Bob's per-step TP all-reduce: 'auto' = one kernel over peer-mapped HBM "
+                        "(csrc/ipc_ar.h) when every Bob rank sets it up and passes its self-test, "
+                        "RCCL otherwise; 'rccl' = always RCCL")
     g.add_argument("--native_p2p_shim", action="store_true",
                    help="CPU tests: run the GPU data-plane code path (grouped p2p with RCCL ordering "
                         "semantics) over gloo (parallel/dist.py GlooP2PShim)")

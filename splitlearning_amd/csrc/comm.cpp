@@ -38,6 +38,14 @@ TpComm::~TpComm() {
 }
 
 void TpComm::allreduce_sum_f32(float* p, size_t n, hipStream_t st) {
+  if (ipc_ != nullptr && (int64_t)n <= ipc_->cap()) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    // a captured launch would freeze the flag generation into the graph: RCCL there
+    if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
+      ipc_->allreduce_sum_f32(p, n, st);
+      return;
+    }
+  }
   SL_NCCL(ncclAllReduce(p, p, n, ncclFloat32, ncclSum, comm_, st));
 }
 
@@ -66,6 +74,10 @@ void need(const at::Tensor& t) {
 // Python-facing methods on tensors (the class itself is sl::TpComm, comm.h)
 void allreduce_sum(sl::TpComm& c, at::Tensor& t) {
   need(t);
+  if (t.scalar_type() == at::kFloat) {
+    c.allreduce_sum_f32(t.data_ptr<float>(), (size_t)t.numel(), stream());
+    return;
+  }
   SL_NCCL(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), dtype_of(t), ncclSum, c.get(), stream()));
 }
 void broadcast(sl::TpComm& c, at::Tensor& t, int root) {
@@ -107,8 +119,29 @@ void sl_register_comm(py::module& m) {
       .def("recv", &recv)
       .def("group_start", [](sl::TpComm&) { SL_NCCL(ncclGroupStart()); })
       .def("group_end", [](sl::TpComm&) { SL_NCCL(ncclGroupEnd()); })
+      .def("attach_ipc", [](sl::TpComm& c, sl::IpcAllReduce* a) { c.attach_ipc(a); }, py::keep_alive<1, 2>(),
+           py::arg("ipc").none(true))
+      .def_property_readonly("ipc_attached", [](const sl::TpComm& c) { return c.ipc() != nullptr; })
       .def_property_readonly("rank", &sl::TpComm::rank)
       .def_property_readonly("size", &sl::TpComm::size);
+  py::class_<sl::IpcAllReduce>(m, "IpcAllReduce")
+      .def(py::init<int, int, int64_t>(), py::arg("nranks"), py::arg("rank"), py::arg("cap"))
+      .def("handle", [](const sl::IpcAllReduce& a) { return py::bytes(a.handle()); })
+      .def("open", [](sl::IpcAllReduce& a, const std::vector<py::bytes>& hs) {
+        std::vector<std::string> v;
+        for (const auto& h : hs) v.emplace_back(std::string(h));
+        a.open(v);
+      })
+      .def("allreduce_sum", [](sl::IpcAllReduce& a, at::Tensor& t) {
+        need(t);
+        TORCH_CHECK(t.scalar_type() == at::kFloat, "IpcAllReduce: f32");
+        a.allreduce_sum_f32(t.data_ptr<float>(), (size_t)t.numel(), stream());
+      })
+      .def("error", &sl::IpcAllReduce::error)
+      .def("set_timeout_s", &sl::IpcAllReduce::set_timeout_s)
+      .def_property_readonly("cap", &sl::IpcAllReduce::cap)
+      .def_property_readonly("rank", &sl::IpcAllReduce::rank)
+      .def_property_readonly("size", &sl::IpcAllReduce::size);
   m.def("nccl_unique_id", &unique_id);
   int v = 0;
   ncclGetVersion(&v);

@@ -7,6 +7,8 @@
 #include <cstddef>
 #include <string>
 
+#include "ipc_ar.h"
+
 namespace sl {
 
 class TpComm {
@@ -15,8 +17,12 @@ class TpComm {
   ~TpComm();
   TpComm(const TpComm&) = delete;
   TpComm& operator=(const TpComm&) = delete;
-  // in-place sum of n floats on stream st (capturable; the data plane of Bob's TP step)
+  // in-place sum of n floats on stream st (the data plane of Bob's TP step): the attached
+  // peer-mapped all-reduce (ipc_ar.h) when one is attached, n fits and the stream is not
+  // being captured; ncclAllReduce otherwise (capturable)
   void allreduce_sum_f32(float* p, size_t n, hipStream_t st);
+  void attach_ipc(IpcAllReduce* a) { ipc_ = a; }
+  IpcAllReduce* ipc() const { return ipc_; }
   ncclComm_t get() const { return comm_; }
   int rank() const { return rank_; }
   int size() const { return nranks_; }
@@ -24,6 +30,7 @@ class TpComm {
  private:
   ncclComm_t comm_ = nullptr;
   int nranks_, rank_;
+  IpcAllReduce* ipc_ = nullptr;
 };
 
 }  // namespace sl

@@ -1,0 +1,74 @@
+// Bob's tensor-parallel all-reduce over peer-mapped HBM (`_C.IpcAllReduce`).
+//
+// The row-parallel fc2 of Bob's TP step needs one in-place sum of a 16 x 1000 fp32 partial
+// (64 KB) per optimizer step, a latency-bound message: RCCL's ring / tree all-reduce costs
+// several dependent link hops per call.  Here every rank exports a small receive region
+// (hipIpcGetMemHandle over uncached device memory) and maps every peer's region once;
+// the all-reduce is then ONE kernel per step: each workgroup pushes its chunk of the
+// partial into slot [me] of every rank's region over the xGMI links (all peers at once,
+// one hop), raises a per-chunk flag on every rank, waits for the T flags of its chunk and
+// sums the T slots in rank order 0..T-1 — so every rank computes bitwise the same sum, which
+// keeps the replicated fc3 and the fc2 epilogue identical across ranks.  Regions are
+// double-buffered by step parity and flags carry a monotonic generation, so no reset or
+// closing barrier is needed.  Waits are bounded (a timeout raises the error word).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace sl {
+
+constexpr int kIpcMaxRanks = 8;
+constexpr int kIpcThreads = 256;
+constexpr int kIpcChunk = kIpcThreads * 4;   // floats per workgroup (one float4 per thread)
+
+struct IpcPeers {
+  float* data[kIpcMaxRanks];       // rank r's receive region [2][T][cap] floats
+  uint32_t* flags[kIpcMaxRanks];   // rank r's flags [2][T][max_chunks]
+};
+
+hipError_t ipc_allreduce_launch(const IpcPeers& P, float* x, int64_t n, int T, int me, uint32_t gen, int64_t cap,
+                                int max_chunks, int* err, int64_t timeout_ticks, hipStream_t st);
+
+class IpcAllReduce {
+ public:
+  // cap: the largest all-reduce (floats) this object serves
+  IpcAllReduce(int nranks, int rank, int64_t cap);
+  ~IpcAllReduce();
+  IpcAllReduce(const IpcAllReduce&) = delete;
+  IpcAllReduce& operator=(const IpcAllReduce&) = delete;
+  // this rank's two IPC handles (data region, flag region), concatenated
+  std::string handle() const;
+  // every rank's handle() in rank order; maps the peers' regions
+  void open(const std::vector<std::string>& handles);
+  // in-place sum of n <= cap floats over the ranks, on stream st (stream-ordered; NOT
+  // capturable: the flag generation is a launch argument, TpComm uses RCCL under capture)
+  void allreduce_sum_f32(float* p, size_t n, hipStream_t st);
+  int64_t cap() const { return cap_; }
+  int rank() const { return rank_; }
+  int size() const { return nranks_; }
+  bool opened() const { return opened_; }
+  // device error word: nonzero after a wait timed out (synchronising read)
+  int error() const;
+  // bound on every flag wait (default 30 s: far above any host skew between ranks)
+  void set_timeout_s(double s) { timeout_ = (int64_t)(s * 1000.0 * clock_khz_); }
+
+ private:
+  int nranks_, rank_;
+  int64_t cap_;
+  int max_chunks_;
+  float* data_ = nullptr;
+  uint32_t* flags_ = nullptr;
+  int* err_ = nullptr;
+  IpcPeers peers_{};
+  std::vector<void*> mapped_;
+  uint32_t gen_ = 0;
+  bool opened_ = false;
+  int64_t timeout_ = 0;
+  int clock_khz_ = 100000;
+};
+
+}  // namespace sl

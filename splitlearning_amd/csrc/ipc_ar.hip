@@ -1,0 +1,175 @@
+// One-kernel all-reduce over peer-mapped HBM for Bob's tensor-parallel step (see ipc_ar.h).
+//
+// Memory protocol (CDNA4, xGMI peers): the receive regions and flags are allocated
+// uncached, so a peer's stores land in this GPU's HBM and no L2 line can go stale between
+// parity reuses.  A workgroup's payload stores are drained (`s_waitcnt vmcnt(0)` in every
+// wave) before the workgroup barrier, and only then does one lane per destination raise
+// that destination's flag; the reader polls its own flag words with system-scope loads,
+// then reads the slots after a workgroup barrier.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+#include "ipc_ar.h"
+
+namespace sl {
+namespace {
+
+#define SL_HIP_THROW(cmd)                                                                    \
+  do {                                                                                       \
+    hipError_t e_ = (cmd);                                                                   \
+    if (e_ != hipSuccess) throw std::runtime_error(std::string(#cmd ": ") + hipGetErrorString(e_)); \
+  } while (0)
+
+__device__ __forceinline__ uint32_t poll_flag(const uint32_t* f) {
+  return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ void raise_flag(uint32_t* f, uint32_t v) {
+  __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(kIpcThreads) void ipc_allreduce_kernel(IpcPeers P, float* __restrict__ x, int64_t n,
+                                                                    int T, int me, int par, uint32_t gen,
+                                                                    int64_t cap, int max_chunks, int* err,
+                                                                    int64_t timeout) {
+  const int c = blockIdx.x;
+  const int64_t off = (int64_t)c * kIpcChunk + threadIdx.x * 4;
+  const bool live = off < n;   // n % 4 == 0 (checked by the launcher)
+  float4 v = {0.f, 0.f, 0.f, 0.f};
+  if (live) v = *reinterpret_cast<const float4*>(x + off);
+  // push: this chunk into slot [par][me] of every rank's region (this rank's own included)
+  const int64_t slot = ((int64_t)par * T + me) * cap + off;
+  if (live)
+    for (int r = 0; r < T; ++r) *reinterpret_cast<float4*>(P.data[r] + slot) = v;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int64_t fme = ((int64_t)par * T + me) * max_chunks + c;
+  if (threadIdx.x < T) raise_flag(P.flags[threadIdx.x] + fme, gen);
+  // wait for every rank's chunk c of this generation (lane r polls source r)
+  if (threadIdx.x < T) {
+    const uint32_t* f = P.flags[me] + ((int64_t)par * T + threadIdx.x) * max_chunks + c;
+    const uint64_t t0 = wall_clock64();
+    while ((int32_t)(poll_flag(f) - gen) < 0) {
+      __builtin_amdgcn_s_sleep(1);
+      if ((int64_t)(wall_clock64() - t0) > timeout) {
+        atomicOr(err, 1);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  if (!live) return;
+  // every slot's load in flight at once, then the fixed-order sum over ranks 0..T-1
+  // (bitwise identical on every rank)
+  const float* base = P.data[me] + (int64_t)par * T * cap + off;
+  float4 u[kIpcMaxRanks];
+#pragma unroll
+  for (int r = 0; r < kIpcMaxRanks; ++r)
+    if (r < T) u[r] = *reinterpret_cast<const float4*>(base + (int64_t)r * cap);
+  float4 acc = u[0];
+#pragma unroll
+  for (int r = 1; r < kIpcMaxRanks; ++r) {
+    if (r < T) {
+      acc.x += u[r].x;
+      acc.y += u[r].y;
+      acc.z += u[r].z;
+      acc.w += u[r].w;
+    }
+  }
+  *reinterpret_cast<float4*>(x + off) = acc;
+}
+
+}  // namespace
+
+hipError_t ipc_allreduce_launch(const IpcPeers& P, float* x, int64_t n, int T, int me, uint32_t gen, int64_t cap,
+                                int max_chunks, int* err, int64_t timeout_ticks, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  if (n > cap || n % 4 != 0 || T < 1 || T > kIpcMaxRanks || me < 0 || me >= T) return hipErrorInvalidValue;
+  const int chunks = (int)((n + kIpcChunk - 1) / kIpcChunk);
+  if (chunks > max_chunks) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(ipc_allreduce_kernel, dim3(chunks), dim3(kIpcThreads), 0, st, P, x, n, T, me,
+                     (int)(gen & 1u), gen, cap, max_chunks, err, timeout_ticks);
+  return hipGetLastError();
+}
+
+IpcAllReduce::IpcAllReduce(int nranks, int rank, int64_t cap) : nranks_(nranks), rank_(rank) {
+  if (nranks < 1 || nranks > kIpcMaxRanks || rank < 0 || rank >= nranks)
+    throw std::runtime_error("IpcAllReduce: 1..8 ranks");
+  if (cap < 1) throw std::runtime_error("IpcAllReduce: capacity");
+  cap_ = (cap + kIpcChunk - 1) / kIpcChunk * kIpcChunk;
+  max_chunks_ = (int)(cap_ / kIpcChunk);
+  const size_t dbytes = sizeof(float) * 2 * (size_t)nranks * (size_t)cap_;
+  const size_t fbytes = sizeof(uint32_t) * 2 * (size_t)nranks * (size_t)max_chunks_;
+  SL_HIP_THROW(hipExtMallocWithFlags(reinterpret_cast<void**>(&data_), dbytes, hipDeviceMallocUncached));
+  SL_HIP_THROW(hipExtMallocWithFlags(reinterpret_cast<void**>(&flags_), fbytes, hipDeviceMallocUncached));
+  SL_HIP_THROW(hipMemset(flags_, 0, fbytes));
+  SL_HIP_THROW(hipMalloc(reinterpret_cast<void**>(&err_), sizeof(int)));
+  SL_HIP_THROW(hipMemset(err_, 0, sizeof(int)));
+  SL_HIP_THROW(hipDeviceSynchronize());
+  int dev = 0, khz = 0;
+  SL_HIP_THROW(hipGetDevice(&dev));
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) khz = 100000;
+  clock_khz_ = khz;
+  set_timeout_s(30.0);
+}
+
+IpcAllReduce::~IpcAllReduce() {
+  for (void* p : mapped_) hipIpcCloseMemHandle(p);
+  if (data_) hipFree(data_);
+  if (flags_) hipFree(flags_);
+  if (err_) hipFree(err_);
+}
+
+std::string IpcAllReduce::handle() const {
+  hipIpcMemHandle_t hd, hf;
+  SL_HIP_THROW(hipIpcGetMemHandle(&hd, data_));
+  SL_HIP_THROW(hipIpcGetMemHandle(&hf, flags_));
+  std::string s(2 * sizeof(hipIpcMemHandle_t), '\0');
+  std::memcpy(&s[0], &hd, sizeof(hd));
+  std::memcpy(&s[sizeof(hd)], &hf, sizeof(hf));
+  return s;
+}
+
+void IpcAllReduce::open(const std::vector<std::string>& handles) {
+  if ((int)handles.size() != nranks_) throw std::runtime_error("IpcAllReduce.open: one handle per rank");
+  if (opened_) throw std::runtime_error("IpcAllReduce.open: already open");
+  for (int r = 0; r < nranks_; ++r) {
+    if (r == rank_) {
+      peers_.data[r] = data_;
+      peers_.flags[r] = flags_;
+      continue;
+    }
+    if (handles[r].size() != 2 * sizeof(hipIpcMemHandle_t)) throw std::runtime_error("IpcAllReduce.open: bad handle");
+    hipIpcMemHandle_t hd, hf;
+    std::memcpy(&hd, handles[r].data(), sizeof(hd));
+    std::memcpy(&hf, handles[r].data() + sizeof(hd), sizeof(hf));
+    void* pd = nullptr;
+    void* pf = nullptr;
+    SL_HIP_THROW(hipIpcOpenMemHandle(&pd, hd, hipIpcMemLazyEnablePeerAccess));
+    mapped_.push_back(pd);
+    SL_HIP_THROW(hipIpcOpenMemHandle(&pf, hf, hipIpcMemLazyEnablePeerAccess));
+    mapped_.push_back(pf);
+    peers_.data[r] = static_cast<float*>(pd);
+    peers_.flags[r] = static_cast<uint32_t*>(pf);
+  }
+  opened_ = true;
+}
+
+void IpcAllReduce::allreduce_sum_f32(float* p, size_t n, hipStream_t st) {
+  if (!opened_) throw std::runtime_error("IpcAllReduce: open() first");
+  if ((int64_t)n > cap_) throw std::runtime_error("IpcAllReduce: message above capacity");
+  ++gen_;
+  SL_HIP_THROW(ipc_allreduce_launch(peers_, p, (int64_t)n, nranks_, rank_, gen_, cap_, max_chunks_, err_, timeout_,
+                                    st));
+}
+
+int IpcAllReduce::error() const {
+  int e = 0;
+  SL_HIP_THROW(hipMemcpy(&e, err_, sizeof(int), hipMemcpyDeviceToHost));
+  return e;
+}
+
+}  // namespace sl

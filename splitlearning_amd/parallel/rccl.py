@@ -62,3 +62,86 @@ def native_allreduce(tpc):
     _ar.capturable = True
     _ar.comm = tpc            # the native executor (engine.ServerEpoch) issues it from C++
     return _ar
+
+
+# Largest all-reduce the peer-mapped path serves (floats): Bob's row-parallel fc2 partial is
+# B x 1000 (64 x 1000 at the largest fused batch); anything larger goes to RCCL.
+IPC_AR_CAP = 64 * 1024
+
+
+def _agree(flag: bool, group=None) -> bool:
+    """Every process learns whether `flag` holds on all of them (MIN all-reduce)."""
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(int(t.item()))
+
+
+def ipc_self_test(ipc, iters: int = 24) -> bool:
+    """Run the peer-mapped all-reduce on known data (every size class it serves, both parity
+    buffers many times over) and check every element against the fixed-order sum.  The
+    values are small multiples of 1/2, so the fp32 sums are exact."""
+    T, me = ipc.size, ipc.rank
+    dev = torch.device("cuda", torch.cuda.current_device())
+    old = 30.0
+    ipc.set_timeout_s(5.0)                 # a broken mapping fails the test, not the job
+    try:
+        for it in range(iters):
+            n = (16 * 1000, 4, 1028, ipc.cap)[it % 4]
+            base = (torch.arange(n, dtype=torch.float32) % 97) * 0.5 + it
+            x = (base + (me + 1)).to(dev)
+            ipc.allreduce_sum(x)
+            want = base * T + T * (T + 1) / 2
+            torch.cuda.synchronize(dev)
+            if ipc.error() != 0 or not torch.equal(x.cpu(), want):
+                return False
+        return True
+    finally:
+        ipc.set_timeout_s(old)
+
+
+def make_ipc_allreduce(ranks: list[int], my_rank: int, cap: int = IPC_AR_CAP, group=None):
+    """Collective over every process: a peer-mapped all-reduce (`_C.IpcAllReduce`, csrc/ipc_ar.h)
+    among `ranks`, returned on members after set-up (IPC handle exchange, peer mapping) AND a
+    self-test passed on every member; None everywhere otherwise (the caller keeps RCCL).
+    `group` is the torch.distributed group containing `ranks` (default: the world)."""
+    from .. import _native
+    C = _native.load()
+    member = my_rank in ranks and len(ranks) > 1
+    ipc, h, err = None, None, None
+    if member:
+        try:
+            ipc = C.IpcAllReduce(len(ranks), ranks.index(my_rank), cap)
+            h = ipc.handle()
+        except RuntimeError as e:
+            ipc, err = None, e
+    world = dist.get_world_size(group)
+    hs = [None] * world
+    dist.all_gather_object(hs, h, group=group)
+    if member and ipc is not None:
+        mine = [hs[r] for r in ranks] if group is None else None
+        if group is not None:
+            gr = dist.get_process_group_ranks(group)
+            mine = [hs[gr.index(r)] for r in ranks]
+        if any(x is None for x in mine):
+            err = "a peer could not export its region"
+        else:
+            try:
+                ipc.open(mine)
+            except RuntimeError as e:
+                err = e
+    if not _agree(err is None, group):
+        import warnings
+        warnings.warn(f"peer-mapped all-reduce unavailable ({err or 'failed on another rank'}); using RCCL")
+        return None
+    ok = True
+    if member:
+        try:
+            ok = ipc_self_test(ipc)
+        except RuntimeError:
+            ok = False
+    if not _agree(ok, group):
+        import warnings
+        warnings.warn("peer-mapped all-reduce failed its self-test on some rank; using RCCL")
+        return None
+    return ipc if member else None

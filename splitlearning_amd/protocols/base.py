@@ -167,6 +167,15 @@ class Session:
             from ..parallel.rccl import make_native_comm, native_allreduce
             tpc = make_native_comm(self.pl.bob_ranks, self.rank)
             self.tp_native_comm = tpc
+            self.tp_ipc = None
+            if tpc is not None and getattr(self.args, "tp_allreduce", "auto") == "auto":
+                # one-kernel all-reduce over peer-mapped HBM for the per-step fc2 partial;
+                # RCCL keeps every larger message and any rank set where set-up or the
+                # self-test fails (decided together)
+                from ..parallel.rccl import make_ipc_allreduce
+                self.tp_ipc = make_ipc_allreduce(self.pl.bob_ranks, self.rank)
+                if self.tp_ipc is not None:
+                    tpc.attach_ipc(self.tp_ipc)
             return native_allreduce(tpc) if tpc is not None else self.comm.tp_allreduce
         return self.comm.tp_allreduce
 

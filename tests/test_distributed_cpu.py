@@ -302,3 +302,24 @@ def test_native_data_plane_protocol_matches_torch_p2p(tmp_path, flags, ws, np_, 
         fy = y if "model1" not in y else {**y["model1"], **y["model3"]}
         for k in fx:
             assert torch.equal(fx[k], fy[k]), (f, k)
+
+
+def _ipc_fallback_worker(rank, world, port, out_dir):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from splitlearning_amd.parallel.rccl import make_ipc_allreduce
+    # no GPU here: the region allocation fails on every member, so all ranks (members or
+    # not) must come back with None together rather than hang in the handle exchange
+    got = make_ipc_allreduce([0, 1], rank)
+    with open(os.path.join(out_dir, f"ipc{rank}.txt"), "w") as f:
+        f.write("none" if got is None else "up")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_ipc_allreduce_setup_falls_back_together(tmp_path):
+    import torch.multiprocessing as mp
+    mp.spawn(_ipc_fallback_worker, args=(3, _free_port(), str(tmp_path)), nprocs=3, join=True)
+    assert [open(tmp_path / f"ipc{r}.txt").read() for r in range(3)] == ["none"] * 3

@@ -1,0 +1,37 @@
+"""Peer-mapped all-reduce (csrc/ipc_ar.h, parallel/rccl.make_ipc_allreduce) across real
+processes on the box's one GPU: set-up + self-test agree on every rank, and random fp32
+messages come back bitwise equal to the rank-ordered sum (scripts/ipc_allreduce_one_gpu.py).
+"""
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("T", [2, 4])
+def test_ipc_allreduce_across_processes(T):
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "ipc_allreduce_one_gpu.py"), str(T)],
+                         capture_output=True, text=True, timeout=110, cwd=ROOT)
+    text = out.stdout + out.stderr
+    assert out.returncode == 0, text[-3000:]
+    assert out.stdout.count("ipc allreduce up") == T, text[-3000:]
+    assert out.stdout.count("PASS") == T, text[-3000:]
+
+
+def test_ipc_allreduce_single_rank_identity(cuda):
+    import torch
+    from splitlearning_amd import _native
+    C = _native.load()
+    ipc = C.IpcAllReduce(1, 0, 4096)
+    ipc.open([ipc.handle()])
+    x = torch.randn(4000, device=cuda)
+    y = x.clone()
+    for _ in range(3):
+        ipc.allreduce_sum(y)
+    torch.cuda.synchronize()
+    assert torch.equal(x, y) and ipc.error() == 0
