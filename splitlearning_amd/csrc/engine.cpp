@@ -99,10 +99,14 @@ class ServerEpoch {
     col_off1_ = cfg["col_off1"].cast<int>();
     row2_ = cfg["row2"].cast<bool>();
     if (!cfg["comm"].is_none()) comm_ = cfg["comm"].cast<sl::TpComm*>();
+    // a peer-mapped all-reduce without an RCCL communicator (ranks that share a GPU, where
+    // RCCL refuses the pair: tests/test_tp_processes_gpu.py)
+    if (comm_ == nullptr && cfg.contains("ipc") && !cfg["ipc"].is_none()) ipc_ = cfg["ipc"].cast<sl::IpcAllReduce*>();
     // emulate_tp: a shard executor of a single-process tensor-parallel emulation
     // (tp_emulate_epoch does the all-reduce); otherwise a row-parallel fc2 needs RCCL
     emulate_ = cfg.contains("emulate_tp") && cfg["emulate_tp"].cast<bool>();
-    TORCH_CHECK(!row2_ || comm_ != nullptr || emulate_, "a row-parallel fc2 needs the native communicator");
+    TORCH_CHECK(!row2_ || comm_ != nullptr || ipc_ != nullptr || emulate_,
+                "a row-parallel fc2 needs the native communicator");
     B_ = cfg["B"].cast<int>();
     TORCH_CHECK(B_ >= 1 && B_ <= 64, "batch 1..64 (look-ahead row chunks of the wgrad kernel)");
     pn_ = get(cfg, "pn");
@@ -136,7 +140,7 @@ class ServerEpoch {
     for (int64_t s = 0; s < n; s += B_) {
       Step st = begin(acts, labels, s, seed_base, fwd_count, t, pre, lookahead);
       forward_product(st);
-      if (row2_) comm_->allreduce_sum_f32(p2ws_.data_ptr<float>(), (size_t)st.M * L_[1].N, stream());
+      if (row2_) allreduce(p2ws_.data_ptr<float>(), (size_t)st.M * L_[1].N);
       finish(st, loss_rows);
       fwd_count = st.fwd_count;
       t = st.t;
@@ -294,6 +298,13 @@ class ServerEpoch {
     st.next_pre = next_full;
   }
 
+  void allreduce(float* p, size_t n) {
+    if (comm_ != nullptr)
+      comm_->allreduce_sum_f32(p, n, stream());   // the attached peer-mapped path or RCCL
+    else
+      ipc_->allreduce_sum_f32(p, n, stream());
+  }
+
   at::Tensor product_view(int M) const { return p2ws_.narrow(0, 0, (int64_t)M * L_[1].N); }
   // single-shard tail, variant 12 = 2: fc2's forward fused into the head (fused.hip
   // fc2_head_fwd_kernel).  Measured slower (native executor, TP = 1: 250.9 vs 178.4 us per
@@ -316,6 +327,7 @@ class ServerEpoch {
   int col_off1_ = 0;
   bool row2_ = false;
   sl::TpComm* comm_ = nullptr;
+  sl::IpcAllReduce* ipc_ = nullptr;
   int B_ = 16;
   bool emulate_ = false;
   int S2_ = 1, S2_probe_ = 1;

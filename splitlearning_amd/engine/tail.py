@@ -322,7 +322,8 @@ class TailEngine:
         if self.device.type != "cuda" or not self.lookahead_ok(B) or not hasattr(self.ops, "C"):
             return False
         if self.layers[1].style == "row":
-            return getattr(self.allreduce, "comm", None) is not None
+            return (getattr(self.allreduce, "comm", None) is not None
+                    or getattr(self.allreduce, "ipc", None) is not None)
         return self.tp_size == 1
 
     def run_native_epoch(self, acts: torch.Tensor, labels: torch.Tensor, slot: OptSlot, B: int, pre: bool,
@@ -366,7 +367,8 @@ class TailEngine:
         d = {"layers": layers, "kind": {"sgd": 1, "adam": 2}[cfg.kind], "lr": cfg.lr, "beta1": cfg.beta1,
              "beta2": cfg.beta2, "eps": cfg.eps, "wd": cfg.weight_decay, "momentum": cfg.momentum,
              "p1": L1.spec.dropout, "p2": L2.spec.dropout, "col_off1": L1.col_off, "row2": L2.style == "row",
-             "comm": getattr(self.allreduce, "comm", None) if L2.style == "row" else None, "B": B,
+             "comm": getattr(self.allreduce, "comm", None) if L2.style == "row" else None,
+             "ipc": getattr(self.allreduce, "ipc", None) if L2.style == "row" else None, "B": B,
              "emulate_tp": L2.style == "row" and self.allreduce is None,
              "pn": self.lookahead_slabs(B), "p2ws": ops._workspace(dev, 16 * B * N2, "fc2p" + tg),
              "fwdws": ops._workspace(dev, 16 * B * nmax, "fwd" + tg),

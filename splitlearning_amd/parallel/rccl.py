@@ -55,6 +55,17 @@ def self_comm():
     return C.TpComm(C.nccl_unique_id(), 1, 0)
 
 
+def ipc_allreduce(ipc):
+    """The TailEngine all-reduce hook over a bare `_C.IpcAllReduce` (no RCCL communicator:
+    ranks that share one GPU).  Not capturable (the flag generation is a launch argument)."""
+    def _ar(t: torch.Tensor):
+        ipc.allreduce_sum(t)
+        return t
+    _ar.capturable = False
+    _ar.ipc = ipc             # the native executor (engine.ServerEpoch) issues it from C++
+    return _ar
+
+
 def native_allreduce(tpc):
     def _ar(t: torch.Tensor):
         tpc.allreduce_sum(t)
