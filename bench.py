@@ -105,6 +105,10 @@ def main(argv=None):
     ap.add_argument("--concat_unlearn", action="store_true", default=True,
                     help="concat: add the unlearning retrain (BASELINE config 5)")
     ap.add_argument("--json_out", type=str, default="")
+    ap.add_argument("--ranks_share_gpu", action="store_true",
+                    help="rehearsal of the N > 1 path on a one-GPU box: every rank on cuda:0, gloo "
+                         "control + host-staged data plane, Bob's TP all-reduce peer-mapped (RCCL "
+                         "refuses two ranks on one device).  Not a scaling measurement.")
     ap.add_argument("--kernel_variant", action="append", default=[], metavar="SLOT=VALUE",
                     help="A/B hook: select a measured-alternative kernel form (_C.set_variant)")
     a = ap.parse_args(argv)
@@ -128,13 +132,15 @@ def main(argv=None):
     if world > 1 and world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
     use_gpu = torch.cuda.device_count() > 0
-    dev = torch.device("cuda", local) if use_gpu else torch.device("cpu")
+    share = a.ranks_share_gpu and use_gpu and world > 1
+    dev = torch.device("cuda", 0 if share else local) if use_gpu else torch.device("cpu")
     if use_gpu:
         torch.cuda.set_device(dev)
+    backend = "nccl" if use_gpu and not share else "gloo"
     if world > 1:
         import datetime
-        kw = {"device_id": dev} if use_gpu else {}
-        dist.init_process_group("nccl" if use_gpu else "gloo", rank=rank, world_size=world,
+        kw = {"device_id": dev} if backend == "nccl" else {}
+        dist.init_process_group(backend, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=900), **kw)
     N = world
     ws = a.world_size if a.world_size > 0 else N + 1
@@ -150,7 +156,8 @@ def main(argv=None):
         argv_s.append("--concat_unlearn")
     sargs = parse_args(argv_s)
     pl = Placement.make(ws, N, a.bob_tp if a.bob_tp > 0 else (choose_bob_tp(sargs.mode, N) if use_gpu else N))
-    comm = Comm(rank, N, dev, pl, make_tp_group(pl, "nccl" if use_gpu else "gloo") if N > 1 else None)
+    comm = Comm(rank, N, dev, pl, make_tp_group(pl, backend) if N > 1 else None)
+    comm.host_staging = share
     k = ws - 1
 
     # the reference's data volume and data path: one MNIST-sized set, Dirichlet-partitioned
@@ -196,7 +203,7 @@ def main(argv=None):
         step()
     sync()
     dt = time.perf_counter() - t0
-    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    t = torch.tensor([dt], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
@@ -234,14 +241,15 @@ def main(argv=None):
                 "num_samples": a.num_samples, "partition": f"dirichlet(alpha={a.partition_alpha}) + 80/20 split",
                 "train_samples_per_client": {c: int(len(shards[c][1])) for c in all_alices},
                 "parallelism": f"alices{k}_on_{N}gpus+bob_tp{pl.bob_tp}",
-                "device": "MI355X" if use_gpu else "cpu", "kernels": kern, "act_cache_dtype": a.act_dtype,
+                "device": "MI355X" if use_gpu else "cpu", "ranks_share_gpu": share,
+                "kernels": kern, "act_cache_dtype": a.act_dtype,
                 "train_samples_per_step": samples // a.steps,
                 "phase_seconds": {p: round(v, 4) for p, v in phase_s.items()},
                 "phase_train_samples": phase_n,
                 "baseline_samples_per_s": round(base, 2) if base else None,
                 "baseline_basis": ("reference CPU phase rates from BASELINE.md composed over this schedule's "
                                    "sample counts" if base else None),
-                "dist_world": N, "rccl_nranks": int(tpc.size) if tpc is not None else (1 if use_gpu else 0),
+                "dist_world": N, "rccl_nranks": int(tpc.size) if tpc is not None else (1 if use_gpu and N == 1 else 0),
                 "tp_allreduce": ("ipc" if getattr(sess, "tp_ipc", None) is not None else
                                  "rccl" if tpc is not None else "torch.distributed" if N > 1 else "none"),
                 "bytes_sent_per_rank_per_step": sent,

@@ -29,7 +29,7 @@ def worker(rank, world, port):
     print(f"rank {rank}: ipc allreduce {'up' if ipc is not None else 'unavailable'}", flush=True)
     ok = ipc is not None
     if ok:
-        for it, n in enumerate((16000, 16000, 64000, 100, 16000, 5000, 16000, 16000)):
+        for it, n in enumerate((16000, 16000, 64000, 100, 16000, 5000, 200000, 16000)):
             xs = [torch.randn(n, generator=torch.Generator().manual_seed(1000 * it + r)) for r in range(world)]
             want = xs[0].clone()
             for r in range(1, world):

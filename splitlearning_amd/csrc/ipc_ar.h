@@ -44,7 +44,7 @@ class IpcAllReduce {
   std::string handle() const;
   // every rank's handle() in rank order; maps the peers' regions
   void open(const std::vector<std::string>& handles);
-  // in-place sum of n <= cap floats over the ranks, on stream st (stream-ordered; NOT
+  // in-place sum of n floats (n % 4 == 0; above cap: cap-sized pieces) over the ranks, on stream st (stream-ordered; NOT
   // capturable: the flag generation is a launch argument, TpComm uses RCCL under capture)
   void allreduce_sum_f32(float* p, size_t n, hipStream_t st);
   int64_t cap() const { return cap_; }

@@ -8,6 +8,7 @@
 // then reads the slots after a workgroup barrier.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -160,10 +161,14 @@ void IpcAllReduce::open(const std::vector<std::string>& handles) {
 
 void IpcAllReduce::allreduce_sum_f32(float* p, size_t n, hipStream_t st) {
   if (!opened_) throw std::runtime_error("IpcAllReduce: open() first");
-  if ((int64_t)n > cap_) throw std::runtime_error("IpcAllReduce: message above capacity");
-  ++gen_;
-  SL_HIP_THROW(ipc_allreduce_launch(peers_, p, (int64_t)n, nranks_, rank_, gen_, cap_, max_chunks_, err_, timeout_,
-                                    st));
+  if (n % 4 != 0) throw std::runtime_error("IpcAllReduce: n % 4 != 0");
+  // a message above the capacity goes as consecutive cap-sized pieces (every rank issues
+  // the same sequence, so the generations stay in step)
+  for (size_t o = 0; o < n; o += (size_t)cap_) {
+    const int64_t m = std::min<int64_t>(cap_, (int64_t)(n - o));
+    ++gen_;
+    SL_HIP_THROW(ipc_allreduce_launch(peers_, p + o, m, nranks_, rank_, gen_, cap_, max_chunks_, err_, timeout_, st));
+  }
 }
 
 int IpcAllReduce::error() const {

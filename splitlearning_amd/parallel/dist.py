@@ -112,6 +112,19 @@ class Comm:
         # Python otherwise).  None on CPU (gloo).
         self.native = None
         self.msg_log = None          # list of (op, src, dst, nbytes) when a test enables it
+        # GPU tensors over a gloo group (several ranks sharing ONE GPU, where RCCL refuses the
+        # pair: the N > 1 rehearsal of bench.py --ranks_share_gpu): p2p and collectives are
+        # staged through host memory.  Never set on a real multi-GPU run.
+        self.host_staging = False
+
+    def _wire(self, t: torch.Tensor) -> torch.Tensor:
+        return t.cpu() if self.host_staging else t
+
+    def _buf(self, shape, dtype) -> torch.Tensor:
+        return torch.empty(shape, dtype=dtype, device="cpu" if self.host_staging else self.device)
+
+    def _land(self, b: torch.Tensor) -> torch.Tensor:
+        return b.to(self.device) if self.host_staging else b
 
     def _count(self, t: torch.Tensor, n: int, op: str, dst=None):
         nb = t.numel() * t.element_size()
@@ -141,18 +154,20 @@ class Comm:
                         nat.send(t, d)
                     nat.group_end()
                 else:
-                    reqs = [dist.isend(t, d) for d in dsts]
+                    w = self._wire(t)
+                    reqs = [dist.isend(w, d) for d in dsts]
                     for r in reqs:
                         r.wait()
                 self._count(t, len(dsts), "multicast", dsts)
             return t
         if self.rank in dsts:
-            buf = torch.empty(shape, dtype=dtype, device=self.device)
             if nat is not None:
+                buf = torch.empty(shape, dtype=dtype, device=self.device)
                 nat.recv(buf, src)
-            else:
-                dist.recv(buf, src)
-            return buf
+                return buf
+            buf = self._buf(shape, dtype)
+            dist.recv(buf, src)
+            return self._land(buf)
         return None
 
     @_dataplane
@@ -174,10 +189,14 @@ class Comm:
                 nat.recv(b, s)
             nat.group_end()
         else:
-            ops = [dist.P2POp(dist.isend, t, d) for t, d in sends]
-            ops += [dist.P2POp(dist.irecv, b, s) for b, s in recvs]
+            stage = [self._buf(b.shape, b.dtype) if self.host_staging else b for b, _ in recvs]
+            ops = [dist.P2POp(dist.isend, self._wire(t), d) for t, d in sends]
+            ops += [dist.P2POp(dist.irecv, h, s) for h, (_, s) in zip(stage, recvs)]
             for r in dist.batch_isend_irecv(ops):
                 r.wait()
+            if self.host_staging:
+                for h, (b, _) in zip(stage, recvs):
+                    b.copy_(h)
         for t, d in sends:
             self._count(t, 1, "exchange", d)
 
@@ -194,7 +213,8 @@ class Comm:
             mine = t if self.rank in srcs else None
             if not others:
                 return lambda: mine
-            bufs = [torch.empty(shape, dtype=dtype, device=self.device) for _ in others]
+            bufs = [(torch.empty(shape, dtype=dtype, device=self.device) if nat is not None
+                     else self._buf(shape, dtype)) for _ in others]
             if nat is not None:
                 # every partial arrives on the compute stream; the sum is stream-ordered after it
                 nat.group_start()
@@ -208,6 +228,8 @@ class Comm:
             def finish():
                 for r in reqs:
                     r.wait()
+                if nat is None and self.host_staging:
+                    bufs[:] = [self._land(b) for b in bufs]
                 acc = mine
                 for b in bufs:
                     acc = b if acc is None else acc.add_(b) if acc is not mine else acc + b
@@ -219,7 +241,7 @@ class Comm:
             if nat is not None:
                 nat.send(t, dst)
                 return lambda: None
-            req = dist.isend(t, dst)
+            req = dist.isend(self._wire(t), dst)
 
             def finish_send():
                 req.wait()
@@ -239,22 +261,26 @@ class Comm:
             if self.native is not None:
                 self.native.send(t, dst)
             else:
-                dist.send(t, dst)
+                dist.send(self._wire(t), dst)
             self._count(t, 1, "send_recv", dst)
             return t
         if self.rank == dst:
-            buf = torch.empty(shape, dtype=dtype, device=self.device)
             if self.native is not None:
+                buf = torch.empty(shape, dtype=dtype, device=self.device)
                 self.native.recv(buf, src)
-            else:
-                dist.recv(buf, src)
-            return buf
+                return buf
+            buf = self._buf(shape, dtype)
+            dist.recv(buf, src)
+            return self._land(buf)
         return None
 
     # ---------------------------------------------------------------- collectives
     def tp_allreduce(self, t: torch.Tensor):
         if self.tp_group is not None:
-            dist.all_reduce(t, group=self.tp_group)
+            w = self._wire(t)
+            dist.all_reduce(w, group=self.tp_group)
+            if w is not t:
+                t.copy_(w)
         return t
 
     @_dataplane
@@ -262,21 +288,26 @@ class Comm:
         if self.tp_group is None:
             return [t]
         n = dist.get_world_size(self.tp_group)
+        dev = t.device
+        t = self._wire(t)
         # shards may differ in size by a few rows: gather padded
-        size = torch.tensor([t.shape[0] if t.dim() else 1], device=self.device)
+        size = torch.tensor([t.shape[0] if t.dim() else 1], device=t.device)
         sizes = [torch.zeros_like(size) for _ in range(n)]
         dist.all_gather(sizes, size, group=self.tp_group)
         mx = int(max(s.item() for s in sizes))
-        pad = torch.zeros((mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=self.device)
+        pad = torch.zeros((mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         pad[:t.shape[0]] = t
         outs = [torch.empty_like(pad) for _ in range(n)]
         dist.all_gather(outs, pad, group=self.tp_group)
-        return [o[:int(s.item())] for o, s in zip(outs, sizes)]
+        return [o[:int(s.item())].to(dev) for o, s in zip(outs, sizes)]
 
     @_dataplane
     def allreduce_sum_(self, t: torch.Tensor):
         if self.distributed:
-            dist.all_reduce(t)
+            w = self._wire(t)
+            dist.all_reduce(w)
+            if w is not t:
+                t.copy_(w)
         return t
 
     def broadcast_obj(self, obj, src: int = 0):
@@ -296,7 +327,7 @@ class Comm:
     @_dataplane
     def barrier(self):
         if self.distributed:
-            if self.device.type == "cuda":
+            if self.device.type == "cuda" and not self.host_staging:
                 dist.barrier(device_ids=[self.device.index])
             else:
                 dist.barrier()

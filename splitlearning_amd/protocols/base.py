@@ -176,6 +176,12 @@ class Session:
                 self.tp_ipc = make_ipc_allreduce(self.pl.bob_ranks, self.rank)
                 if self.tp_ipc is not None:
                     tpc.attach_ipc(self.tp_ipc)
+            if tpc is None and getattr(self.args, "tp_allreduce", "auto") == "auto":
+                # no RCCL communicator (ranks sharing one GPU): the peer-mapped all-reduce alone
+                from ..parallel.rccl import ipc_allreduce, make_ipc_allreduce
+                self.tp_ipc = make_ipc_allreduce(self.pl.bob_ranks, self.rank)
+                if self.tp_ipc is not None:
+                    return ipc_allreduce(self.tp_ipc)
             return native_allreduce(tpc) if tpc is not None else self.comm.tp_allreduce
         return self.comm.tp_allreduce
 
