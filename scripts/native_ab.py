@@ -37,6 +37,9 @@ def main():
     ap.add_argument("--variants", nargs="+", default=["5=0", "5=99"])
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--epochs", type=int, default=4, help="timed epochs (64 steps each) per variant per round")
+    ap.add_argument("--allreduce", choices=("rccl", "ipc"), default="rccl",
+                    help="TP > 1 stand-in all-reduce: a 1-rank RCCL communicator or a 1-rank peer-mapped "
+                         "all-reduce (csrc/ipc_ar.h: its kernel runs, with no peer to wait for)")
     a = ap.parse_args()
     C = H.C()
     dev = torch.device("cuda", 0)
@@ -49,8 +52,13 @@ def main():
         labels = torch.randint(0, 10, (B * nb,), device=dev)
         ar = None
         if tp > 1:
-            from splitlearning_amd.parallel.rccl import native_allreduce, self_comm
-            ar = native_allreduce(self_comm())
+            from splitlearning_amd.parallel.rccl import ipc_allreduce, native_allreduce, self_comm
+            if a.allreduce == "ipc":
+                ipc = C.IpcAllReduce(1, 0, 64 * 1024)
+                ipc.open([ipc.handle()])
+                ar = ipc_allreduce(ipc)
+            else:
+                ar = native_allreduce(self_comm())
         tail = TailEngine(ServerTailSisa(), sisa_server_spec(), dev, tp_rank=0, tp_size=tp, allreduce=ar)
         slot = OptSlot(adam(1e-3, 1e-5))
         assert tail.native_epoch_ok(B)

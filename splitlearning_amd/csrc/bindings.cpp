@@ -748,12 +748,17 @@ PYBIND11_MODULE(_C, m) {
   //   12 single-shard fc2 + head (2 fused)         13 executor launch-skip probe (timing only)
   //   14 skinny forward (2 k-loop form; 3 / 4: 4 / 16 waves per workgroup)
   //   15 U-shape head step (1 per-thread FMA form)
+  //   16 TP server step: 1 = separate peer-mapped all-reduce launch instead of the one fused
+  //      into head_fwd
   // The measurements behind each default are in the comment at the slot's use and docs/PERF.md.
   m.def("set_variant", [](int64_t slot, int64_t v) {
-    TORCH_CHECK(slot >= 0 && slot < 16, "variant slot");
+    TORCH_CHECK(slot >= 0 && slot < 24, "variant slot");
     sl::g_variant[slot] = (int)v;
   });
-  m.def("get_variant", [](int64_t slot) { return (int64_t)sl::g_variant[slot]; });
+  m.def("get_variant", [](int64_t slot) {
+    TORCH_CHECK(slot >= 0 && slot < 24, "variant slot");
+    return (int64_t)sl::g_variant[slot];
+  });
   // compute dtype of the GEMM-shaped kernels (forward / data-gradient products): fp32 (exact
   // v_mfma_f32_*_f32) or bf16 (operands rounded to bf16, bf16 MFMA, fp32 accumulation);
   // parameters, optimizer state and the fused optimizer update stay fp32 either way

@@ -140,7 +140,7 @@ class ServerEpoch {
     for (int64_t s = 0; s < n; s += B_) {
       Step st = begin(acts, labels, s, seed_base, fwd_count, t, pre, lookahead);
       forward_product(st);
-      if (row2_) allreduce(p2ws_.data_ptr<float>(), (size_t)st.M * L_[1].N);
+      if (row2_ && !ipc_head(st.M)) allreduce(p2ws_.data_ptr<float>(), (size_t)st.M * L_[1].N);
       finish(st, loss_rows);
       fwd_count = st.fwd_count;
       t = st.t;
@@ -253,12 +253,21 @@ class ServerEpoch {
                              h2, dlog, dz2, loss_rows.data_ptr<float>() + st.s, headws_.data_ptr<float>(),
                              headws_.numel(), M, N1, N2, C, sm),
          "server fc2 + head");
-    else
+    else {
+      // tensor-parallel fc2 with a peer-mapped all-reduce: head_fwd performs it (run() issued
+      // no separate all-reduce for this step)
+      sl::IpcStep step;
+      const sl::IpcStep* ip = nullptr;
+      if (row2_ && ipc_head(M)) {
+        step = ipc_obj()->begin_step();
+        ip = &step;
+      }
       ck(sl::server_head3(p2ws_.data_ptr<float>(), S2_, (int64_t)M * N2, e2, L_[2].W.data_ptr<float>(), N2,
                           L_[2].b.data_ptr<float>(), st.labels->data_ptr<int64_t>() + st.s, -100, (float)(1.0 / M),
                           h2, dlog, dz2, loss_rows.data_ptr<float>() + st.s, headws_.data_ptr<float>(),
-                          headws_.numel(), M, N2, C, sm),
+                          headws_.numel(), M, N2, C, sm, ip),
          "server head");
+    }
     if (!skip(8))
       ck(sl::linear_dgrad(dz2, N2, L_[1].W.data_ptr<float>(), N1, h1, N1, (float)s1, dz1, N1, dgws_.data_ptr<float>(),
                           dgws_.numel(), M, N2, N1, sm),
@@ -296,6 +305,19 @@ class ServerEpoch {
     const SlOpt o = sl::make_opt_raw(kind_, lr_, beta1_, beta2_, eps_, wd_, mom_, st.t, nullptr);
     if (!skip(16)) ck(sl::wgrad_group(g, M, o, sm), "wgrad_group");
     st.next_pre = next_full;
+  }
+
+  // the peer-mapped all-reduce in use for this executor (attached to the RCCL communicator
+  // or given bare), or null
+  sl::IpcAllReduce* ipc_obj() const { return comm_ != nullptr ? comm_->ipc() : ipc_; }
+  // whether step rows M run the all-reduce inside head_fwd (variant 16 = 1: the separate
+  // all-reduce kernel; a stream being captured: RCCL, see TpComm::allreduce_sum_f32)
+  bool ipc_head(int M) const {
+    const sl::IpcAllReduce* a = ipc_obj();
+    if (a == nullptr || sl::g_variant[16] == 1 || skip(2) || skip(4)) return false;
+    if ((int64_t)M * L_[1].N > a->cap() || (int64_t)M * sl::head3_slices(L_[1].N) > sl::kIpcFlags) return false;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(stream(), &cs) == hipSuccess && cs == hipStreamCaptureStatusNone;
   }
 
   void allreduce(float* p, size_t n) {

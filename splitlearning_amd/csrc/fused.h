@@ -1,6 +1,7 @@
 // Descriptors shared by the fused server-step kernels (fused.hip) and the bindings.
 #pragma once
 #include "common.h"
+#include "ipc_ar.h"
 
 namespace sl {
 
@@ -44,9 +45,13 @@ struct WgGroup {
 };
 
 int head3_slices(int N2);
+// ipc (tensor-parallel fc2): P2 is this rank's unreduced [M, N2] partial; head_fwd pushes its
+// slice to every rank, waits for the T slices and sums them in rank order (the fc2 all-reduce
+// fused into the slab reduction: ipc_ar.h)
 hipError_t server_head3(const float* P2, int S2, int64_t slab2, Epi e2, const float* W3, int ldw3, const float* b3,
                         const int64_t* y, int64_t ignore, float scale, float* h2, float* dlog, float* dz2,
-                        float* loss_rows, float* ws, int64_t ws_elems, int M, int N2, int C, hipStream_t st);
+                        float* loss_rows, float* ws, int64_t ws_elems, int M, int N2, int C, hipStream_t st,
+                        const IpcStep* ipc = nullptr);
 hipError_t wgrad_group(const WgGroup& g, int M, SlOpt o, hipStream_t st);
 int fc2_head_tiles(int N2);
 hipError_t server_fc2_head(const float* X, int ldx, const float* W2, int ldw2, Epi e2, const float* W3, int ldw3,

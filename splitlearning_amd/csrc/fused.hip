@@ -45,10 +45,17 @@ __device__ __forceinline__ void head_slice(int n4, int Q, int q, int& a, int& b)
 // 32 float4 columns are reduced on DPP lane moves within each 16-lane row plus two
 // v_readlane pairs (a 5-step ds_bpermute shuffle per output cost 2.6 us of the kernel in the
 // graph-replay probe, scripts/probe/head_probe.hip).  BF: bf16 compute (operands rounded).
-template <bool BF>
+//
+// IPC (tensor-parallel fc2, peer-mapped all-reduce fused in; ipc_ar.h): P2 is this rank's
+// unreduced partial.  Wave 0 pushes the workgroup's slice of row m into slot [me] of every
+// rank's region, drains its stores, raises flag (m, q) on every rank and waits for the T
+// flags (m, q) of this generation; the slab reduction then reads the T slots (S2 = T, in rank
+// order: bitwise the same sum on every rank).  One launch per step less than a separate
+// all-reduce kernel, and the wait overlaps the W3 loads already in flight.
+template <bool BF, bool IPC>
 __global__ void __launch_bounds__(256)
 head_fwd_kernel(const float* __restrict__ P2, int S2, int64_t slab2, Epi e2, const float* __restrict__ W3,
-                int ldw3, float* __restrict__ h2, float* __restrict__ plog, int M, int N2, int C) {
+                int ldw3, float* __restrict__ h2, float* __restrict__ plog, int M, int N2, int C, IpcStep ip) {
   __shared__ f32x4 part[8][HS];
   __shared__ f32x4 hs[HS];
   const int m = blockIdx.x, q = blockIdx.y, Q = gridDim.y, tid = threadIdx.x;
@@ -69,6 +76,23 @@ head_fwd_kernel(const float* __restrict__ P2, int S2, int64_t slab2, Epi e2, con
     }
   };
   load_w(0);
+  if constexpr (IPC) {
+    if (wv == 0) {
+      if (lane < ncol) {
+        const f32x4 v = reinterpret_cast<const f32x4*>(P2 + (int64_t)m * N2)[qa + lane];
+        const int64_t slot = ((int64_t)ip.par * ip.T + ip.me) * ip.cap + (int64_t)m * N2;
+        for (int r = 0; r < ip.T; ++r) reinterpret_cast<f32x4*>(ip.P.data[r] + slot)[qa + lane] = v;
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int fi = m * Q + q;
+      if (lane < ip.T) ipc_raise_flag(ip.P.flags[lane] + ((int64_t)ip.par * ip.T + ip.me) * ip.nflags + fi, ip.gen);
+      ipc_wait_flags(ip, lane, fi);
+    }
+    __syncthreads();
+    P2 = ip.P.data[ip.me] + (int64_t)ip.par * ip.T * ip.cap;
+    S2 = ip.T;
+    slab2 = ip.cap;
+  }
   // 1. slab reduction: 32 columns x 8 slab groups
   {
     const int cc = tid & (HS - 1), sg = tid >> 5;
@@ -601,15 +625,30 @@ static void launch_head_bwd(const float* plog, const float* b3, const float* W3,
 
 hipError_t server_head3(const float* P2, int S2, int64_t slab2, Epi e2, const float* W3, int ldw3, const float* b3,
                         const int64_t* y, int64_t ignore, float scale, float* h2, float* dlog, float* dz2,
-                        float* loss_rows, float* ws, int64_t ws_elems, int M, int N2, int C, hipStream_t st) {
+                        float* loss_rows, float* ws, int64_t ws_elems, int M, int N2, int C, hipStream_t st,
+                        const IpcStep* ipc) {
   if (M <= 0) return hipSuccess;
   if ((N2 & 3) || (ldw3 & 3)) return hipErrorInvalidValue;
   const int Q = head3_slices(N2);
   if (ws_elems < (int64_t)Q * M * C) return hipErrorInvalidValue;
-  if (g_bf16)
-    head_fwd_kernel<true><<<dim3(M, Q), 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C);
-  else
-    head_fwd_kernel<false><<<dim3(M, Q), 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C);
+  const dim3 g(M, Q);
+  if (ipc != nullptr) {
+    // the fused all-reduce: one flag word per workgroup, one [M, N2] partial per slot; the
+    // local partial is unsplit (S2 = 1)
+    if (S2 != 1 || (int64_t)M * Q > ipc->nflags || (int64_t)M * N2 > ipc->cap || ipc->T < 1 ||
+        ipc->T > kIpcMaxRanks)
+      return hipErrorInvalidValue;
+    if (g_bf16)
+      head_fwd_kernel<true, true><<<g, 256, 0, st>>>(P2, 1, slab2, e2, W3, ldw3, h2, ws, M, N2, C, *ipc);
+    else
+      head_fwd_kernel<false, true><<<g, 256, 0, st>>>(P2, 1, slab2, e2, W3, ldw3, h2, ws, M, N2, C, *ipc);
+  } else {
+    const IpcStep none{};
+    if (g_bf16)
+      head_fwd_kernel<true, false><<<g, 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C, none);
+    else
+      head_fwd_kernel<false, false><<<g, 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C, none);
+  }
   launch_head_bwd(ws, b3, W3, ldw3, y, ignore, scale, e2.dscale, h2, dlog, dz2, loss_rows, M, N2, C, Q, Q, st);
   return hipGetLastError();
 }

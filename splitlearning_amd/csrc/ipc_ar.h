@@ -30,6 +30,46 @@ struct IpcPeers {
   uint32_t* flags[kIpcMaxRanks];   // rank r's flags [2][T][max_chunks]
 };
 
+// Flag words per (parity, source) beyond the all-reduce's chunks: the fused server head
+// (fused.hip head_fwd_kernel<.., true>) raises one per (row, column slice) workgroup.
+constexpr int kIpcFlags = 1024;
+
+// One generation of the protocol handed to a kernel that does the push / wait itself (the
+// server head fuses the fc2 all-reduce into its slab reduction, csrc/fused.hip).
+struct IpcStep {
+  IpcPeers P;
+  int T, me, par;
+  uint32_t gen;
+  int64_t cap;        // floats per slot
+  int nflags;         // flag words per (parity, source)
+  int* err;
+  int64_t timeout;    // wall-clock ticks
+};
+
+__device__ __forceinline__ uint32_t ipc_poll_flag(const uint32_t* f) {
+  return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ void ipc_raise_flag(uint32_t* f, uint32_t v) {
+  __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Lanes 0..T-1 of the calling wave each wait for source rank `lane`'s flag word `idx` of this
+// generation (bounded: a timeout raises *err and gives up).
+__device__ __forceinline__ void ipc_wait_flags(const IpcStep& s, int lane, int idx) {
+  if (lane < s.T) {
+    const uint32_t* f = s.P.flags[s.me] + ((int64_t)s.par * s.T + lane) * s.nflags + idx;
+    const uint64_t t0 = wall_clock64();
+    while ((int32_t)(ipc_poll_flag(f) - s.gen) < 0) {
+      __builtin_amdgcn_s_sleep(1);
+      if ((int64_t)(wall_clock64() - t0) > s.timeout) {
+        atomicOr(s.err, 1);
+        break;
+      }
+    }
+  }
+}
+
 hipError_t ipc_allreduce_launch(const IpcPeers& P, float* x, int64_t n, int T, int me, uint32_t gen, int64_t cap,
                                 int max_chunks, int* err, int64_t timeout_ticks, hipStream_t st);
 
@@ -47,6 +87,8 @@ class IpcAllReduce {
   // in-place sum of n floats (n % 4 == 0; above cap: cap-sized pieces) over the ranks, on stream st (stream-ordered; NOT
   // capturable: the flag generation is a launch argument, TpComm uses RCCL under capture)
   void allreduce_sum_f32(float* p, size_t n, hipStream_t st);
+  // the next generation for a fused consumer (same sequence as allreduce_sum_f32's calls)
+  IpcStep begin_step();
   int64_t cap() const { return cap_; }
   int rank() const { return rank_; }
   int size() const { return nranks_; }

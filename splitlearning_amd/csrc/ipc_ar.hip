@@ -24,14 +24,6 @@ namespace {
     if (e_ != hipSuccess) throw std::runtime_error(std::string(#cmd ": ") + hipGetErrorString(e_)); \
   } while (0)
 
-__device__ __forceinline__ uint32_t poll_flag(const uint32_t* f) {
-  return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-__device__ __forceinline__ void raise_flag(uint32_t* f, uint32_t v) {
-  __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 __global__ __launch_bounds__(kIpcThreads) void ipc_allreduce_kernel(IpcPeers P, float* __restrict__ x, int64_t n,
                                                                     int T, int me, int par, uint32_t gen,
                                                                     int64_t cap, int max_chunks, int* err,
@@ -48,12 +40,12 @@ __global__ __launch_bounds__(kIpcThreads) void ipc_allreduce_kernel(IpcPeers P, 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   const int64_t fme = ((int64_t)par * T + me) * max_chunks + c;
-  if (threadIdx.x < T) raise_flag(P.flags[threadIdx.x] + fme, gen);
+  if (threadIdx.x < T) ipc_raise_flag(P.flags[threadIdx.x] + fme, gen);
   // wait for every rank's chunk c of this generation (lane r polls source r)
   if (threadIdx.x < T) {
     const uint32_t* f = P.flags[me] + ((int64_t)par * T + threadIdx.x) * max_chunks + c;
     const uint64_t t0 = wall_clock64();
-    while ((int32_t)(poll_flag(f) - gen) < 0) {
+    while ((int32_t)(ipc_poll_flag(f) - gen) < 0) {
       __builtin_amdgcn_s_sleep(1);
       if ((int64_t)(wall_clock64() - t0) > timeout) {
         atomicOr(err, 1);
@@ -101,7 +93,7 @@ IpcAllReduce::IpcAllReduce(int nranks, int rank, int64_t cap) : nranks_(nranks),
     throw std::runtime_error("IpcAllReduce: 1..8 ranks");
   if (cap < 1) throw std::runtime_error("IpcAllReduce: capacity");
   cap_ = (cap + kIpcChunk - 1) / kIpcChunk * kIpcChunk;
-  max_chunks_ = (int)(cap_ / kIpcChunk);
+  max_chunks_ = std::max((int)(cap_ / kIpcChunk), kIpcFlags);
   const size_t dbytes = sizeof(float) * 2 * (size_t)nranks * (size_t)cap_;
   const size_t fbytes = sizeof(uint32_t) * 2 * (size_t)nranks * (size_t)max_chunks_;
   SL_HIP_THROW(hipExtMallocWithFlags(reinterpret_cast<void**>(&data_), dbytes, hipDeviceMallocUncached));
@@ -169,6 +161,22 @@ void IpcAllReduce::allreduce_sum_f32(float* p, size_t n, hipStream_t st) {
     ++gen_;
     SL_HIP_THROW(ipc_allreduce_launch(peers_, p + o, m, nranks_, rank_, gen_, cap_, max_chunks_, err_, timeout_, st));
   }
+}
+
+IpcStep IpcAllReduce::begin_step() {
+  if (!opened_) throw std::runtime_error("IpcAllReduce: open() first");
+  ++gen_;
+  IpcStep s;
+  s.P = peers_;
+  s.T = nranks_;
+  s.me = rank_;
+  s.par = (int)(gen_ & 1u);
+  s.gen = gen_;
+  s.cap = cap_;
+  s.nflags = max_chunks_;
+  s.err = err_;
+  s.timeout = timeout_;
+  return s;
 }
 
 int IpcAllReduce::error() const {

@@ -26,7 +26,7 @@
 
 namespace sl {
 
-int g_variant[16] = {0};
+int g_variant[24] = {0};
 int g_bf16 = 0;
 
 hipError_t gemm_nt(const float* X, int ldx, const float* W, int ldw, float* Y, int ldy, int M, int N, int K, Epi e,
