@@ -212,7 +212,12 @@ class ServerEpoch {
     if (skip(2)) {
       S2_ = row2_ ? 1 : S2_probe_;
     } else if (row2_) {
-      if (N1 <= 1280) {
+      if (N1 > 1280 && ipc_head(M)) {
+        // the fused head sums the local split-K slabs before its push: no epilogue launch
+        // (same plan as linear_fwd's split-K, so the same slabs the epilogue would sum)
+        ck(sl::linear_fwd_partial(h1, N1, L_[1].W.data_ptr<float>(), N1, M, N2, N1, P2, p2ws_.numel(), 16, &S2_, sm),
+           "fc2 forward");
+      } else if (N1 <= 1280) {
         ck(sl::linear_fwd_partial(h1, N1, L_[1].W.data_ptr<float>(), N1, M, N2, N1, P2, p2ws_.numel(), 1, &S2_, sm),
            "fc2 forward");
       } else {

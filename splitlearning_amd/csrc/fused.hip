@@ -47,7 +47,7 @@ __device__ __forceinline__ void head_slice(int n4, int Q, int q, int& a, int& b)
 // graph-replay probe, scripts/probe/head_probe.hip).  BF: bf16 compute (operands rounded).
 //
 // IPC (tensor-parallel fc2, peer-mapped all-reduce fused in; ipc_ar.h): P2 is this rank's
-// unreduced partial.  Wave 0 pushes the workgroup's slice of row m into slot [me] of every
+// unreduced partial (S2 split-K slabs, summed first).  Wave 0 pushes the workgroup's slice of row m into slot [me] of every
 // rank's region, drains its stores, raises flag (m, q) on every rank and waits for the T
 // flags (m, q) of this generation; the slab reduction then reads the T slots (S2 = T, in rank
 // order: bitwise the same sum on every rank).  One launch per step less than a separate
@@ -79,7 +79,11 @@ head_fwd_kernel(const float* __restrict__ P2, int S2, int64_t slab2, Epi e2, con
   if constexpr (IPC) {
     if (wv == 0) {
       if (lane < ncol) {
-        const f32x4 v = reinterpret_cast<const f32x4*>(P2 + (int64_t)m * N2)[qa + lane];
+        // this rank's split-K slabs (S2 >= 1) summed in slab order: the plain product the
+        // separate-launch path would all-reduce
+        const f32x4* src = reinterpret_cast<const f32x4*>(P2 + (int64_t)m * N2) + qa + lane;
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        for (int s = 0; s < S2; ++s) v += src[s * (slab2 >> 2)];
         const int64_t slot = ((int64_t)ip.par * ip.T + ip.me) * ip.cap + (int64_t)m * N2;
         for (int r = 0; r < ip.T; ++r) reinterpret_cast<f32x4*>(ip.P.data[r] + slot)[qa + lane] = v;
       }
@@ -634,14 +638,14 @@ hipError_t server_head3(const float* P2, int S2, int64_t slab2, Epi e2, const fl
   const dim3 g(M, Q);
   if (ipc != nullptr) {
     // the fused all-reduce: one flag word per workgroup, one [M, N2] partial per slot; the
-    // local partial is unsplit (S2 = 1)
-    if (S2 != 1 || (int64_t)M * Q > ipc->nflags || (int64_t)M * N2 > ipc->cap || ipc->T < 1 ||
+    // local partial may be S2 split-K slabs (summed before the push)
+    if (S2 < 1 || (slab2 & 3) || (int64_t)M * Q > ipc->nflags || (int64_t)M * N2 > ipc->cap || ipc->T < 1 ||
         ipc->T > kIpcMaxRanks)
       return hipErrorInvalidValue;
     if (g_bf16)
-      head_fwd_kernel<true, true><<<g, 256, 0, st>>>(P2, 1, slab2, e2, W3, ldw3, h2, ws, M, N2, C, *ipc);
+      head_fwd_kernel<true, true><<<g, 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C, *ipc);
     else
-      head_fwd_kernel<false, true><<<g, 256, 0, st>>>(P2, 1, slab2, e2, W3, ldw3, h2, ws, M, N2, C, *ipc);
+      head_fwd_kernel<false, true><<<g, 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C, *ipc);
   } else {
     const IpcStep none{};
     if (g_bf16)
