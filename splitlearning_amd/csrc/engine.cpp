@@ -212,9 +212,10 @@ class ServerEpoch {
     if (skip(2)) {
       S2_ = row2_ ? 1 : S2_probe_;
     } else if (row2_) {
-      if (N1 > 1280 && ipc_head(M)) {
-        // the fused head sums the local split-K slabs before its push: no epilogue launch
-        // (same plan as linear_fwd's split-K, so the same slabs the epilogue would sum)
+      if (ipc_head(M) || emulate_) {
+        // the fused head sums this rank's split-K slabs before its push (no epilogue launch,
+        // and a split product at every shard width); the single-process emulation follows
+        // the same decomposition (tp_emulate_epoch sums each shard's slabs, then the shards)
         ck(sl::linear_fwd_partial(h1, N1, L_[1].W.data_ptr<float>(), N1, M, N2, N1, P2, p2ws_.numel(), 16, &S2_, sm),
            "fc2 forward");
       } else if (N1 <= 1280) {
@@ -333,6 +334,18 @@ class ServerEpoch {
   }
 
   at::Tensor product_view(int M) const { return p2ws_.narrow(0, 0, (int64_t)M * L_[1].N); }
+  // this shard's fc2 product: its split-K slabs summed in slab order (as the fused head does)
+  at::Tensor local_product(int M) const {
+    const int64_t sl = (int64_t)M * L_[1].N;
+    at::Tensor acc = p2ws_.narrow(0, 0, sl).clone();
+    for (int s = 1; s < S2_; ++s) acc.add_(p2ws_.narrow(0, (int64_t)s * sl, sl));
+    return acc;
+  }
+  // after the emulated all-reduce: the product is one reduced slab
+  void set_reduced(const at::Tensor& sum, int M) {
+    product_view(M).copy_(sum);
+    S2_ = 1;
+  }
   // single-shard tail, variant 12 = 2: fc2's forward fused into the head (fused.hip
   // fc2_head_fwd_kernel).  Measured slower (native executor, TP = 1: 250.9 vs 178.4 us per
   // step; profiles/r2_fused_head_ab.txt): 125 workgroups that each reduce the whole K = 5000
@@ -388,9 +401,9 @@ py::tuple tp_emulate_epoch(py::list exs, const at::Tensor& acts, const at::Tenso
     for (size_t i = 0; i < E.size(); ++i) E[i]->forward_product(st[i]);
     if (row && E.size() > 1) {
       const int M = st[0].M;
-      at::Tensor sum = E[0]->product_view(M).clone();
-      for (size_t i = 1; i < E.size(); ++i) sum.add_(E[i]->product_view(M));
-      for (auto* e : E) e->product_view(M).copy_(sum);
+      at::Tensor sum = E[0]->local_product(M);
+      for (size_t i = 1; i < E.size(); ++i) sum.add_(E[i]->local_product(M));
+      for (auto* e : E) e->set_reduced(sum, M);
     }
     for (size_t i = 0; i < E.size(); ++i) E[i]->finish(st[i], losses[i]);
     fwd_count = st[0].fwd_count;
