@@ -55,6 +55,20 @@ def worker(rank, world, port):
         us = (time.perf_counter() - t0) / iters * 1e6
         ok = ok and ipc.error() == 0
         print(f"rank {rank}: {iters} x 64 KB all-reduce {us:.1f} us/call", flush=True)
+    if ok and os.environ.get("SL_IPC_TIMEOUT_CHECK") == "1":
+        # a peer that never arrives: rank 0's waits must give up (bounded) and raise the
+        # error word instead of hanging the GPU; the other ranks issue nothing
+        dist.barrier()
+        if rank == 0:
+            ipc.set_timeout_s(0.5)
+            y = torch.ones(16000, device=dev)
+            t0 = time.perf_counter()
+            ipc.allreduce_sum(y)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            print(f"rank 0: lone all-reduce returned after {dt:.2f} s, error word {ipc.error()}", flush=True)
+            ok = ipc.error() == 1 and dt < 10.0
+        dist.barrier()
     print(f"rank {rank}: {'PASS' if ok else 'FAIL'}", flush=True)
     dist.barrier()
     dist.destroy_process_group()

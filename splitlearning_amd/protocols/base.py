@@ -80,6 +80,7 @@ class Session:
         self.is_bob = self.pl.is_bob(self.rank)
         self._native_data_plane()                          # collective over all ranks
         self.tp_allreduce = self._tp_allreduce()          # collective over all ranks
+        self.timer.check = self._check_transport
         self.tail: TailEngine | None = None
         self.bob_slots: dict = {}
         self.last_alice_id = None
@@ -184,6 +185,14 @@ class Session:
                     return ipc_allreduce(self.tp_ipc)
             return native_allreduce(tpc) if tpc is not None else self.comm.tp_allreduce
         return self.comm.tp_allreduce
+
+    def _check_transport(self):
+        """Phase-end check (after the device sync): the peer-mapped all-reduce's bounded waits
+        raise an error word instead of hanging; a phase that hit one fails loudly here."""
+        ipc = getattr(self, "tp_ipc", None)
+        if ipc is not None and ipc.error() != 0:
+            raise RuntimeError("peer-mapped TP all-reduce: a flag wait timed out on this rank (a peer "
+                               "stalled or the mapping is broken); rerun with --tp_allreduce rccl")
 
     def _build_bob(self):
         module, spec = self.bob_module_and_spec()

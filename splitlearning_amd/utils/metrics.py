@@ -29,6 +29,7 @@ class PhaseTimer:
         self.barrier = barrier
         self.beacon = beacon          # progress callback (runtime/watchdog.py): beacon(tag)
         self.tracer = NULL_TRACER     # utils/trace.py: one "phase" span per phase
+        self.check = None             # phase-end health check after the sync (raises on failure)
         self.records: list[dict] = []
 
     @contextmanager
@@ -46,6 +47,8 @@ class PhaseTimer:
             info["samples"] = box["samples"]
             span.__exit__(None, None, None)
             sync(self.device)
+            if self.check is not None:
+                self.check()
             if self.barrier is not None:
                 self.barrier()
             dt = time.perf_counter() - t0

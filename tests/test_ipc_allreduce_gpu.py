@@ -35,3 +35,15 @@ def test_ipc_allreduce_single_rank_identity(cuda):
         ipc.allreduce_sum(y)
     torch.cuda.synchronize()
     assert torch.equal(x, y) and ipc.error() == 0
+
+
+def test_ipc_allreduce_wait_is_bounded():
+    """A rank whose peer never issues the matching all-reduce gives up after its timeout and
+    raises the error word (checked at every phase end: protocols/base.py _check_transport)
+    instead of spinning forever."""
+    env = dict(os.environ, SL_IPC_TIMEOUT_CHECK="1")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "ipc_allreduce_one_gpu.py"), "2"],
+                         capture_output=True, text=True, timeout=110, cwd=ROOT, env=env)
+    text = out.stdout + out.stderr
+    assert out.returncode == 0, text[-3000:]
+    assert "error word 1" in out.stdout and out.stdout.count("PASS") == 2, text[-3000:]
