@@ -130,10 +130,9 @@ def make_ipc_allreduce(ranks: list[int], my_rank: int, cap: int = IPC_AR_CAP, gr
     hs = [None] * world
     dist.all_gather_object(hs, h, group=group)
     if member and ipc is not None:
-        mine = [hs[r] for r in ranks] if group is None else None
-        if group is not None:
-            gr = dist.get_process_group_ranks(group)
-            mine = [hs[gr.index(r)] for r in ranks]
+        # hs is indexed by group rank; `ranks` are global ranks
+        order = dist.get_process_group_ranks(group) if group is not None else list(range(world))
+        mine = [hs[order.index(r)] for r in ranks]
         if any(x is None for x in mine):
             err = "a peer could not export its region"
         else:
