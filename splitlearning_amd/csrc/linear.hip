@@ -389,22 +389,33 @@ skinny_dgrad_kernel(const float* __restrict__ dZ, int ldz, const float* __restri
 // The 16 waves' partial tiles are summed through LDS in a fixed order (deterministic).
 // At B = 16 this reads W once (fc2: 20 MB) from 157 workgroups; the split-N form it replaces
 // needed ~630 workgroups plus a reduce launch over the slabs.
+template <int NC>   // columns per lane: 2 (32-column tiles, float2 loads) or 1 (16-column tiles)
 __global__ void __launch_bounds__(1024)
 dgrad_fulln_kernel(const float* __restrict__ dZ, int ldz, const float* __restrict__ W, int ldw,
                    const float* __restrict__ hprev, int ldh, float scale, float* __restrict__ out, int ldo,
                    int M, int N, int K) {
-  __shared__ f32x4 red[16][2][64];
+  __shared__ f32x4 red[16][NC][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int k0 = blockIdx.x * 32, m0 = blockIdx.y * 16;
+  const int k0 = blockIdx.x * 16 * NC, m0 = blockIdx.y * 16;
   const int j = lane & 15, q = lane >> 4;
-  const int kc = k0 + 2 * j;                       // this lane's two columns kc, kc + 1
-  const bool vk = kc + 1 < K;                      // K % 4 == 0 (host check): pairs never straddle K
+  const int kc = k0 + NC * j;                      // this lane's NC columns kc ..
+  const bool vk = kc + NC - 1 < K;                 // K % 4 == 0 (host check): never straddles K
   const bool vm = (m0 + j) < M;
   // N slice of this wave: multiples of 16
   const int nper = ((N + 16 * 16 - 1) / (16 * 16)) * 16;
   const int nb = wv * nper, ne = min(N, nb + nper);
   const float* za = dZ + (int64_t)(vm ? m0 + j : 0) * ldz;
-  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  f32x4 acc[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto ldw_ = [&](int nn) {
+    float2 r = make_float2(0.f, 0.f);
+    if (NC == 2)
+      r = *reinterpret_cast<const float2*>(W + (int64_t)nn * ldw + kc);
+    else
+      r.x = W[(int64_t)nn * ldw + kc];
+    return r;
+  };
   constexpr int U = 4;                             // 16-n groups in flight per lane
   int n = nb;
   for (; n + 16 * U <= ne; n += 16 * U) {
@@ -415,16 +426,15 @@ dgrad_fulln_kernel(const float* __restrict__ dZ, int ldz, const float* __restric
       const int nq = n + 16 * u + 4 * q;
       a[u] = vm ? *reinterpret_cast<const float4*>(za + nq) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
-        w[u][s] = vk ? *reinterpret_cast<const float2*>(W + (int64_t)(nq + s) * ldw + kc) : make_float2(0.f, 0.f);
+      for (int s = 0; s < 4; ++s) w[u][s] = vk ? ldw_(nq + s) : make_float2(0.f, 0.f);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const float av[4] = {a[u].x, a[u].y, a[u].z, a[u].w};
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        acc0 = mfma4(av[s], w[u][s].x, acc0);
-        acc1 = mfma4(av[s], w[u][s].y, acc1);
+        acc[0] = mfma4(av[s], w[u][s].x, acc[0]);
+        if (NC == 2) acc[NC - 1] = mfma4(av[s], w[u][s].y, acc[NC - 1]);
       }
     }
   }
@@ -435,29 +445,28 @@ dgrad_fulln_kernel(const float* __restrict__ dZ, int ldz, const float* __restric
       const int nn = nq + s;
       const bool in = nn < ne;
       const float av = (vm && in) ? za[nn] : 0.f;
-      const float2 wv2 = (vk && in) ? *reinterpret_cast<const float2*>(W + (int64_t)nn * ldw + kc)
-                                     : make_float2(0.f, 0.f);
-      acc0 = mfma4(av, wv2.x, acc0);
-      acc1 = mfma4(av, wv2.y, acc1);
+      const float2 wv2 = (vk && in) ? ldw_(nn) : make_float2(0.f, 0.f);
+      acc[0] = mfma4(av, wv2.x, acc[0]);
+      if (NC == 2) acc[NC - 1] = mfma4(av, wv2.y, acc[NC - 1]);
     }
   }
-  red[wv][0][lane] = acc0;
-  red[wv][1][lane] = acc1;
-  __syncthreads();
-  // 512 outputs: thread t -> (half h, lane l); D_h[row][col]: row = 4*(l>>4) + r, col j = l & 15
-  const int t = threadIdx.x;
-  if (t < 128) {
-    const int h = t >> 6, l = t & 63;
-    f32x4 s = red[0][h][l];
 #pragma unroll
-    for (int v = 1; v < 16; ++v) s += red[v][h][l];
-    const int kk = k0 + 2 * (l & 15) + h;
+  for (int c = 0; c < NC; ++c) red[wv][c][lane] = acc[c];
+  __syncthreads();
+  // 256 NC outputs: thread t -> (column half h, lane l); D_h[row][col]: row = 4*(l>>4) + r, col j = l & 15
+  const int t = threadIdx.x;
+  if (t < 64 * NC) {
+    const int h = t >> 6, l = t & 63;
+    f32x4 sm = red[0][h][l];
+#pragma unroll
+    for (int v = 1; v < 16; ++v) sm += red[v][h][l];
+    const int kk = k0 + NC * (l & 15) + h;
     if (kk < K) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = m0 + 4 * (l >> 4) + r;
         if (m >= M) continue;
-        float v = s[r];
+        float v = sm[r];
         if (hprev) v = (hprev[(int64_t)m * ldh + kk] > 0.f) ? v * scale : 0.f;
         out[(int64_t)m * ldo + kk] = v;
       }
@@ -639,9 +648,18 @@ hipError_t linear_dgrad(const float* dZ, int ldz, const float* W, int ldw, const
   // 55.6 full-N vs 170.9 / 101.6 / 68.9 / 51.8 split; profiles/r2_dgrad_fulln_ab.txt): with
   // the whole N per workgroup there are only K/32 workgroups (20 at a TP = 8 shard), each a
   // chain of 1000-row strided reads, and the reduce launch is cheaper than that latency.
-  if (g_variant[8] == 2 && !g_bf16 && M <= 64 && (K & 3) == 0 && (ldw & 1) == 0 && (ldz & 3) == 0) {
-    dim3 grid((K + 31) / 32, mt);
-    dgrad_fulln_kernel<<<grid, 1024, 0, st>>>(dZ, ldz, W, ldw, hprev, ldh, scale, dX, ldx, M, N, K);
+  // variant 8 = 3: the same with 16-column tiles (twice the workgroups, one float per lane):
+  // also slower than the split pair, us per step at TP = 1 / 2 / 4 / 8: 179.2 / 103.2 / 70.8 /
+  // 54.6 vs 176.8 / 101.0 / 68.5 / 51.8 (profiles/r2_dgrad_fulln16_ab.txt).
+  if ((g_variant[8] == 2 || g_variant[8] == 3) && !g_bf16 && M <= 64 && (K & 3) == 0 && (ldw & 1) == 0 &&
+      (ldz & 3) == 0) {
+    if (g_variant[8] == 3) {
+      dgrad_fulln_kernel<1><<<dim3((K + 15) / 16, mt), 1024, 0, st>>>(dZ, ldz, W, ldw, hprev, ldh, scale, dX, ldx, M,
+                                                                       N, K);
+    } else {
+      dgrad_fulln_kernel<2><<<dim3((K + 31) / 32, mt), 1024, 0, st>>>(dZ, ldz, W, ldw, hprev, ldh, scale, dX, ldx, M,
+                                                                       N, K);
+    }
     return hipGetLastError();
   }
   int S = 1;

@@ -127,10 +127,11 @@ def test_linear_fwd_partial(cuda, M, N, K, max_split, once):
                                     (3, 37, 52), (16, 1000, 628), (64, 1000, 5000), (40, 1000, 604),
                                     (16, 12, 8), (200, 1000, 5000), (1000, 100, 1000)])
 @pytest.mark.parametrize("masked", [False, True])
-@pytest.mark.parametrize("variant", [0, 2])
+@pytest.mark.parametrize("variant", [0, 2, 3])
 def test_linear_dgrad(cuda, M, N, K, masked, variant):
-    """variant 0: the split-N + reduce pair (default); 2: the full-N kernel (whole reduction
-    in one workgroup, masked store) where it applies (N % 4 == 0, M <= 64)."""
+    """variant 0: the split-N + reduce pair (default); 2 / 3: the full-N kernel (whole
+    reduction in one workgroup, masked store; 32- / 16-column tiles) where it applies
+    (N % 4 == 0, M <= 64)."""
     C = hip_ops.C()
     old = C.get_variant(8)
     C.set_variant(8, variant)
