@@ -85,7 +85,7 @@ head_fwd_kernel(const float* __restrict__ P2, int S2, int64_t slab2, Epi e2, con
         f32x4 v = {0.f, 0.f, 0.f, 0.f};
         for (int s = 0; s < S2; ++s) v += src[s * (slab2 >> 2)];
         const int64_t slot = ((int64_t)ip.par * ip.T + ip.me) * ip.cap + (int64_t)m * N2;
-        for (int r = 0; r < ip.T; ++r) reinterpret_cast<f32x4*>(ip.P.data[r] + slot)[qa + lane] = v;
+        for (int r = 0; r < ip.T; ++r) ipc_st4(ip.P.data[r] + slot + 4 * (qa + lane), make_float4(v[0], v[1], v[2], v[3]));
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const int fi = m * Q + q;
@@ -103,8 +103,16 @@ head_fwd_kernel(const float* __restrict__ P2, int S2, int64_t slab2, Epi e2, con
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
     if (cc < ncol) {
       const f32x4* src = reinterpret_cast<const f32x4*>(P2 + (int64_t)m * N2) + qa + cc;
+      if constexpr (IPC) {
+        // the T slots of the peer-mapped region (S2 = T <= 8: one per slab group)
+        for (int s = sg; s < S2; s += 8) {
+          const float4 u = ipc_ld4(reinterpret_cast<const float*>(src + s * (slab2 >> 2)));
+          v += f32x4{u.x, u.y, u.z, u.w};
+        }
+      } else {
 #pragma unroll 4
-      for (int s = sg; s < S2; s += 8) v += src[s * (slab2 >> 2)];
+        for (int s = sg; s < S2; s += 8) v += src[s * (slab2 >> 2)];
+      }
     }
     part[sg][cc] = v;
   }

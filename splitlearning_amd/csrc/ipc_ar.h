@@ -54,6 +54,28 @@ __device__ __forceinline__ void ipc_raise_flag(uint32_t* f, uint32_t v) {
   __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Payload moves at system scope (each dword a relaxed system-scope atomic: global_store /
+// global_load with sc0 sc1), so the protocol follows the memory model whatever cache type
+// the driver gives a peer's mapping: a store leaves no dirty line in this GPU's L2 and is
+// complete at `s_waitcnt vmcnt(0)`; a load never hits a stale line of an earlier generation.
+__device__ __forceinline__ void ipc_st4(float* p, float4 v) {
+  uint32_t* q = reinterpret_cast<uint32_t*>(p);
+  __hip_atomic_store(q + 0, __float_as_uint(v.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(q + 1, __float_as_uint(v.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(q + 2, __float_as_uint(v.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(q + 3, __float_as_uint(v.w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ float4 ipc_ld4(const float* p) {
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(p);
+  float4 v;
+  v.x = __uint_as_float(__hip_atomic_load(q + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+  v.y = __uint_as_float(__hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+  v.z = __uint_as_float(__hip_atomic_load(q + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+  v.w = __uint_as_float(__hip_atomic_load(q + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+  return v;
+}
+
 // Lanes 0..T-1 of the calling wave each wait for source rank `lane`'s flag word `idx` of this
 // generation (bounded: a timeout raises *err and gives up).
 __device__ __forceinline__ void ipc_wait_flags(const IpcStep& s, int lane, int idx) {

@@ -1,11 +1,12 @@
 // One-kernel all-reduce over peer-mapped HBM for Bob's tensor-parallel step (see ipc_ar.h).
 //
 // Memory protocol (CDNA4, xGMI peers): the receive regions and flags are allocated
-// uncached, so a peer's stores land in this GPU's HBM and no L2 line can go stale between
-// parity reuses.  A workgroup's payload stores are drained (`s_waitcnt vmcnt(0)` in every
-// wave) before the workgroup barrier, and only then does one lane per destination raise
-// that destination's flag; the reader polls its own flag words with system-scope loads,
-// then reads the slots after a workgroup barrier.
+// uncached, and every payload / flag access is a system-scope one (sc0 sc1: ipc_ar.h
+// ipc_st4 / ipc_ld4), so a peer's stores land in this GPU's HBM and no L2 line can go stale
+// between parity reuses whatever cache type a mapping gets.  A workgroup's payload stores
+// are drained (`s_waitcnt vmcnt(0)` in every wave) before the workgroup barrier, and only
+// then does one lane per destination raise that destination's flag; the reader polls its
+// own flag words with system-scope loads, then reads the slots after a workgroup barrier.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -36,7 +37,7 @@ __global__ __launch_bounds__(kIpcThreads) void ipc_allreduce_kernel(IpcPeers P, 
   // push: this chunk into slot [par][me] of every rank's region (this rank's own included)
   const int64_t slot = ((int64_t)par * T + me) * cap + off;
   if (live)
-    for (int r = 0; r < T; ++r) *reinterpret_cast<float4*>(P.data[r] + slot) = v;
+    for (int r = 0; r < T; ++r) ipc_st4(P.data[r] + slot, v);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   const int64_t fme = ((int64_t)par * T + me) * max_chunks + c;
@@ -61,7 +62,7 @@ __global__ __launch_bounds__(kIpcThreads) void ipc_allreduce_kernel(IpcPeers P, 
   float4 u[kIpcMaxRanks];
 #pragma unroll
   for (int r = 0; r < kIpcMaxRanks; ++r)
-    if (r < T) u[r] = *reinterpret_cast<const float4*>(base + (int64_t)r * cap);
+    if (r < T) u[r] = ipc_ld4(base + (int64_t)r * cap);
   float4 acc = u[0];
 #pragma unroll
   for (int r = 1; r < kIpcMaxRanks; ++r) {
