@@ -38,7 +38,7 @@ TpComm::~TpComm() {
 }
 
 void TpComm::allreduce_sum_f32(float* p, size_t n, hipStream_t st) {
-  if (ipc_ != nullptr && (int64_t)n <= ipc_->cap()) {
+  if (ipc_ != nullptr && (int64_t)n <= ipc_->cap() && n % 4 == 0) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     // a captured launch would freeze the flag generation into the graph: RCCL there
     if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {

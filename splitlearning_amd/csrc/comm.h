@@ -18,8 +18,8 @@ class TpComm {
   TpComm(const TpComm&) = delete;
   TpComm& operator=(const TpComm&) = delete;
   // in-place sum of n floats on stream st (the data plane of Bob's TP step): the attached
-  // peer-mapped all-reduce (ipc_ar.h) when one is attached, n fits and the stream is not
-  // being captured; ncclAllReduce otherwise (capturable)
+  // peer-mapped all-reduce (ipc_ar.h) when one is attached, n fits (n <= cap, n % 4 == 0)
+  // and the stream is not being captured; ncclAllReduce otherwise (capturable)
   void allreduce_sum_f32(float* p, size_t n, hipStream_t st);
   void attach_ipc(IpcAllReduce* a) { ipc_ = a; }
   IpcAllReduce* ipc() const { return ipc_; }
