@@ -46,6 +46,9 @@ hipError_t linear_dgrad(const float* dZ, int ldz, const float* W, int ldw, const
                         hipStream_t st);
 hipError_t linear_epilogue(const float* P, int ldp, float* Y, int ldy, int M, int N, Epi e, int S, int64_t slab,
                            hipStream_t st);
+int lookahead_fc2_slices(int N1);
+hipError_t lookahead_fc2_fwd(const float* pn, int S1, int64_t slab1, Epi e1, float* h1, const float* W2, float* P2,
+                             int64_t p2_elems, int M, int N1, int N2, int* S2_out, hipStream_t st);
 hipError_t linear_fwd_partial(const float* X, int ldx, const float* W, int ldw, int M, int N, int K, float* ws,
                               int64_t ws_elems, int max_split, int* S_out, hipStream_t st);
 hipError_t linear_dgrad_partial(const float* dZ, int ldz, const float* W, int ldw, int M, int N, int K, float* ws,
@@ -553,6 +556,28 @@ int64_t linear_fwd_partial(const at::Tensor& X, const at::Tensor& W, at::Tensor&
   return S;
 }
 
+// fc1 look-ahead slabs P1 [S1, M, N1] -> h1 (fc1 epilogue) and fc2's split-K product slabs in
+// ws ([S2, M, N2], one per 64-wide k-slice of h1); returns S2
+int64_t lookahead_fc2_fwd(const at::Tensor& P1, const OptT& b1, double drop1, uint64_t seed1, int64_t col_off,
+                          int64_t dseed1, at::Tensor& h1, const at::Tensor& W2, at::Tensor& ws) {
+  need_f32(P1, "P1");
+  TORCH_CHECK(P1.dim() == 3 && P1.is_contiguous(), "P1 [S, M, N1] contiguous");
+  need_2d(h1, "h1");
+  need_rows(W2, "W2");
+  need_f32(ws, "ws");
+  const int64_t S1 = P1.size(0), M = P1.size(1), N1 = P1.size(2), N2 = W2.size(0);
+  TORCH_CHECK(h1.size(0) == M && h1.size(1) == N1 && h1.stride(0) == N1, "h1 [M, N1] dense");
+  TORCH_CHECK(W2.size(1) == N1 && W2.stride(0) == N1 && N1 % 4 == 0, "W2 [N2, N1] dense, N1 % 4 == 0");
+  TORCH_CHECK(ws.is_contiguous(), "ws contiguous");
+  if (b1.has_value() && b1->defined()) TORCH_CHECK(b1->numel() == N1, "b1 [N1]");
+  int S2 = 0;
+  check(sl::lookahead_fc2_fwd(P1.data_ptr<float>(), (int)S1, M * N1, make_epi(b1, true, drop1, seed1, col_off, dseed1),
+                              h1.data_ptr<float>(), W2.data_ptr<float>(), ws.data_ptr<float>(), ws.numel(), (int)M,
+                              (int)N1, (int)N2, &S2, cur_stream()),
+        "lookahead_fc2_fwd");
+  return S2;
+}
+
 int64_t linear_dgrad_partial(const at::Tensor& dZ, const at::Tensor& W, at::Tensor& ws) {
   need_2d(dZ, "dZ");
   need_rows(W, "W");
@@ -737,6 +762,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("server_fc2_head", &server_fc2_head);
   m.def("fc2_head_tiles", [](int64_t n2) { return (int64_t)sl::fc2_head_tiles((int)n2); });
   m.def("linear_fwd_partial", &linear_fwd_partial);
+  m.def("lookahead_fc2_fwd", &lookahead_fc2_fwd);
+  m.def("lookahead_fc2_slices", [](int64_t N1) { return (int64_t)sl::lookahead_fc2_slices((int)N1); });
   m.def("linear_dgrad_partial", &linear_dgrad_partial);
   m.def("wgrad_group", &wgrad_group);
   // Kernel-variant slots (0 = the measured default everywhere), for A/B scripts and tests:
@@ -750,6 +777,7 @@ PYBIND11_MODULE(_C, m) {
   //   15 U-shape head step (1 per-thread FMA form)
   //   16 TP server step: 1 = separate peer-mapped all-reduce launch instead of the one fused
   //      into head_fwd
+  //   18 single-shard look-ahead step: 1 = fc1's epilogue inside fc2's split-K forward
   // The measurements behind each default are in the comment at the slot's use and docs/PERF.md.
   m.def("set_variant", [](int64_t slot, int64_t v) {
     TORCH_CHECK(slot >= 0 && slot < 24, "variant slot");

@@ -39,6 +39,9 @@ hipError_t linear_epilogue(const float* P, int ldp, float* Y, int ldy, int M, in
                            hipStream_t st);
 hipError_t linear_fwd_partial(const float* X, int ldx, const float* W, int ldw, int M, int N, int K, float* ws,
                               int64_t ws_elems, int max_split, int* S_out, hipStream_t st);
+int lookahead_fc2_slices(int N1);
+hipError_t lookahead_fc2_fwd(const float* pn, int S1, int64_t slab1, Epi e1, float* h1, const float* W2, float* P2,
+                             int64_t p2_elems, int M, int N1, int N2, int* S2_out, hipStream_t st);
 }  // namespace sl
 
 namespace py = pybind11;
@@ -124,7 +127,8 @@ class ServerEpoch {
     TORCH_CHECK(h1_.numel() >= (int64_t)B_ * L_[0].N && dz1_.numel() >= (int64_t)B_ * L_[0].N, "h1 / dz1");
     TORCH_CHECK(h2_.numel() >= (int64_t)B_ * L_[1].N && dz2_.numel() >= (int64_t)B_ * L_[1].N, "h2 / dz2");
     TORCH_CHECK(dlog_.numel() >= (int64_t)B_ * L_[2].N, "dlog");
-    TORCH_CHECK(p2ws_.numel() >= 16LL * B_ * L_[1].N, "fc2 slab workspace");
+    TORCH_CHECK(p2ws_.numel() >= (int64_t)std::max(16, sl::lookahead_fc2_slices(L_[0].N)) * B_ * L_[1].N,
+                "fc2 slab workspace");
     TORCH_CHECK(headws_.numel() >= (int64_t)std::max(sl::head3_slices(L_[1].N), sl::fc2_head_tiles(L_[1].N)) * B_ *
                                         L_[2].N,
                 "head workspace");
@@ -199,6 +203,13 @@ class ServerEpoch {
     float* h1 = h1_.data_ptr<float>();
     float* P2 = p2ws_.data_ptr<float>();
     const Epi e1 = sl::make_epi_raw(L_[0].b.data_ptr<float>(), true, p1_, st.sd0, col_off1_, nullptr);
+    if (lookahead_fc2(st)) {
+      // variant 18 = 1: the look-ahead epilogue inside fc2's split-K forward (one launch)
+      ck(sl::lookahead_fc2_fwd(pn_.data_ptr<float>(), (int)S1, (int64_t)M * N1, e1, h1, L_[1].W.data_ptr<float>(),
+                               P2, p2ws_.numel(), M, N1, N2, &S2_, sm),
+         "fc1 epilogue + fc2 forward");
+      return;
+    }
     if (skip(1)) {
     } else if (st.pre)
       ck(sl::linear_epilogue(pn_.data_ptr<float>(), N1, h1, N1, M, N1, e1, (int)S1, (int64_t)M * N1, sm),
@@ -352,6 +363,9 @@ class ServerEpoch {
   // re-read all of h1 (320 KB) per 8 output columns and run 6 dependent load rounds per wave;
   // the 1008-workgroup split-K forward + head_fwd pair stays the default.
   bool fuse_head() const { return !row2_ && sl::g_variant[12] == 2; }
+  bool lookahead_fc2(const Step& st) const {
+    return st.pre && !row2_ && !fuse_head() && sl::g_variant[18] >= 1 && !skip(1) && !skip(2);
+  }
   bool row_parallel() const { return row2_; }
   // Timing probe (variant 13, a bit mask; never set outside scripts/native_ab.py): skip
   // launches to price each one in the real stream and cache state — 1 fc1 epilogue, 2 fc2

@@ -694,6 +694,113 @@ hipError_t linear_dgrad(const float* dZ, int ldz, const float* W, int ldw, const
   return hipGetLastError();
 }
 
+// fc1's look-ahead epilogue fused into fc2's split-K forward (single-shard tail, variant 18
+// = 1).  Workgroup (ks, nr, mt) owns the 64-wide k-slice ks of h1 for 16 rows: it reduces
+// the S1 look-ahead slabs of that slice in slab order (bitwise the epilogue kernel's sum),
+// applies fc1's bias / ReLU / dropout (writing h1 when nr == 0), stages the tile in LDS and
+// forms the slice's partial product with fc2's 128 output columns nr on exact-fp32 MFMA;
+// P2 gets one slab per k-slice for the head to reduce.  The W2 loads are issued first, so
+// they overlap the slab reduction.  The k-slice runs fastest in the grid, padded to a
+// multiple of 8, so the 8 column ranges of one slice share an XCD (and its L2 copy of the
+// slabs).  Removes the epilogue launch — and measured slower through the native executor
+// (us per TP = 1 step, profiles/r2_lookahead_fc2_fused_ab.txt): 173.0 (64-wide slices) and
+// 176.5 (128-wide) vs 170.8 for the epilogue + split-K forward pair.  The slab round trip now
+// sits in front of every workgroup's MFMAs, and the head reduces 79 / 40 product slabs
+// instead of the forward's 16: more latency than the launch boundary it saves.  Opt-in.
+template <int LKS>
+__global__ void __launch_bounds__(256)
+lookahead_fc2_fwd_kernel(const float* __restrict__ pn, int S1, int64_t slab1, Epi e1, float* __restrict__ h1,
+                         const float* __restrict__ W2, float* __restrict__ P2, int64_t slab2, int M, int N1, int N2,
+                         int nks) {
+  __shared__ float At[16][LKS + 4];
+  const int ks = blockIdx.x;
+  if (ks >= nks) return;                                 // grid padding (XCD grouping)
+  const int nr = blockIdx.y, m0 = blockIdx.z * 16, k0 = ks * LKS;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int q4 = (lane >> 4) * 4, j = lane & 15;
+  constexpr int U = LKS / 16;
+  // W2 rows of this wave's two 16-column tiles: every load before anything else
+  float4 w[2][U];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int n = (nr * 8 + 2 * wv + t) * 16 + j;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int kk = k0 + 16 * u + q4;
+      w[t][u] = (n < N2 && kk < N1) ? ld4(W2 + (int64_t)n * N1 + kk) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  // h1 tile: thread -> (row r, float4 columns c4, c4 + 16, ...); the slabs summed in order
+  // from 0
+  const int r = tid >> 4;
+#pragma unroll
+  for (int c4 = tid & 15; c4 < LKS / 4; c4 += 16) {
+    const int m = m0 + r, k = k0 + 4 * c4;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (m < M && k < N1) {
+      const float* p = pn + (int64_t)m * N1 + k;
+      constexpr int SU = 32;
+      for (int s0 = 0; s0 < S1; s0 += SU) {
+        float4 rr[SU];
+#pragma unroll
+        for (int i = 0; i < SU; ++i)
+          rr[i] = (s0 + i < S1) ? ld4(p + (int64_t)(s0 + i) * slab1) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int i = 0; i < SU; ++i) v += f32x4{rr[i].x, rr[i].y, rr[i].z, rr[i].w};
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = apply_epi(e1, v[i], m, k + i);
+      if (nr == 0) *reinterpret_cast<f32x4*>(h1 + (int64_t)m * N1 + k) = v;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) At[r][4 * c4 + i] = v[i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int n0 = (nr * 8 + 2 * wv + t) * 16;
+    if (n0 >= N2) break;
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float* ar = &At[j][16 * u + q4];
+      acc0 = mfma4(ar[0], w[t][u].x, acc0);
+      acc1 = mfma4(ar[1], w[t][u].y, acc1);
+      acc0 = mfma4(ar[2], w[t][u].z, acc0);
+      acc1 = mfma4(ar[3], w[t][u].w, acc1);
+    }
+    const f32x4 sm = acc0 + acc1;
+    const int n = n0 + j;
+    if (n < N2) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + q4 + r;
+        if (m < M) P2[(int64_t)ks * slab2 + (int64_t)m * N2 + n] = sm[r];
+      }
+    }
+  }
+}
+
+// k-slice width: variant 18 = 1 -> 64, = 2 -> 128
+static int lookahead_ks() { return g_variant[18] == 2 ? 128 : 64; }
+int lookahead_fc2_slices(int N1) { return (N1 + 63) / 64; }   // capacity bound (the narrower slice)
+
+hipError_t lookahead_fc2_fwd(const float* pn, int S1, int64_t slab1, Epi e1, float* h1, const float* W2, float* P2,
+                             int64_t p2_elems, int M, int N1, int N2, int* S2_out, hipStream_t st) {
+  *S2_out = 0;
+  if (M <= 0) return hipSuccess;
+  const int ks = lookahead_ks();
+  const int nks = (N1 + ks - 1) / ks;
+  if ((N1 & 3) || S1 < 1 || (int64_t)nks * M * N2 > p2_elems) return hipErrorInvalidValue;
+  const dim3 g((nks + 7) / 8 * 8, (N2 + 127) / 128, (M + 15) / 16);
+  if (ks == 128)
+    lookahead_fc2_fwd_kernel<128><<<g, 256, 0, st>>>(pn, S1, slab1, e1, h1, W2, P2, (int64_t)M * N2, M, N1, N2, nks);
+  else
+    lookahead_fc2_fwd_kernel<64><<<g, 256, 0, st>>>(pn, S1, slab1, e1, h1, W2, P2, (int64_t)M * N2, M, N1, N2, nks);
+  *S2_out = nks;
+  return hipGetLastError();
+}
+
 // Partial-output variants for fused consumers (server_head3 / wgrad_group reduce the slabs
 // themselves): the split-K (fwd) or split-N (dgrad) slabs, or the plain product when no
 // split is chosen, land in ws as [S][M][cols]; *S_out receives S.

@@ -256,11 +256,17 @@ class TailEngine:
         def ds(i):
             return {} if dseeds is None else {"dseed": dseeds[i]}
         p1, p2 = L1.spec.dropout, L2.spec.dropout
+        P2 = None
         if pre:
             P1 = self._pre
             assert P1 is not None and P1.shape[1] == M, "no pending look-ahead for this batch"
             self._pre = None
-            h1 = ops.linear_epilogue(P1, L1.b, True, p1, seeds[0], L1.col_off, **ds(0))
+            if self._lookahead_fc2():
+                # variant 18 = 1: the epilogue inside fc2's split-K forward (as the native
+                # executor does: csrc/engine.cpp lookahead_fc2)
+                h1, P2 = ops.lookahead_fc2_fwd(P1, L1.b, p1, seeds[0], L1.col_off, L2.W, **ds(0))
+            else:
+                h1 = ops.linear_epilogue(P1, L1.b, True, p1, seeds[0], L1.col_off, **ds(0))
         else:
             self._pre = None
             h1 = ops.linear_fwd(x, L1.W, L1.b, True, p1, seeds[0], L1.col_off, **ds(0))
@@ -276,7 +282,7 @@ class TailEngine:
             else:
                 P2 = ops.linear_fwd(h1, L2.W, None, False, 0.0, 0, 0)
             self.allreduce(P2)
-        else:
+        elif P2 is None:
             P2 = ops.linear_fwd_partial(h1, L2.W)
         if L2.style == "row" or not hasattr(ops, "server_fc2_head") or ops.C().get_variant(12) != 2:
             h2, dlog, dz2, loss = ops.server_head3(P2, L2.b, True, p2, seeds[1], L3.W, L3.b, labels, 1.0 / M,
@@ -296,6 +302,13 @@ class TailEngine:
         self._wg = [src1 + (x,), (dz2, None, None, 1.0, h1), (dlog, None, None, 1.0, h2)]
         self._train_fwd = True
         return loss, dx
+
+    def _lookahead_fc2(self) -> bool:
+        """Single-shard tail with the fused look-ahead epilogue + fc2 forward (variant 18 = 1)."""
+        ops = self.ops
+        L2 = self.layers[1]
+        return (L2.style != "row" and hasattr(ops, "lookahead_fc2_fwd") and ops.C().get_variant(18) >= 1
+                and ops.C().get_variant(12) != 2)
 
     def fused_step(self, slot: OptSlot, t: int | None = None, dyn=None, prefix: str = "", x_next=None):
         """Optimizer step of all three layers in one launch.  `x_next`: the next batch's
@@ -370,7 +383,8 @@ class TailEngine:
              "comm": getattr(self.allreduce, "comm", None) if L2.style == "row" else None,
              "ipc": getattr(self.allreduce, "ipc", None) if L2.style == "row" else None, "B": B,
              "emulate_tp": L2.style == "row" and self.allreduce is None,
-             "pn": self.lookahead_slabs(B), "p2ws": ops._workspace(dev, 16 * B * N2, "fc2p" + tg),
+             "pn": self.lookahead_slabs(B),
+             "p2ws": ops._workspace(dev, max(16, ops.C().lookahead_fc2_slices(N1)) * B * N2, "fc2p" + tg),
              "fwdws": ops._workspace(dev, 16 * B * nmax, "fwd" + tg),
              "dgws": ops._workspace(dev, 16 * B * kmax, "dgrad" + tg),
              "headws": ops._workspace(dev, max(ops.C().head3_slices(N2), ops.C().fc2_head_tiles(N2)) * B * C,

@@ -300,6 +300,19 @@ def linear_fwd_partial(x, w, max_split: int = 16, key: str = "fc2p"):
     return ws[:S * M * N].view(S, M, N)
 
 
+def lookahead_fc2_fwd(P1, b1, drop_p: float, seed: int, col_offset: int, w2, dseed=None, key: str = "fc2p"):
+    """fc1's look-ahead slabs P1 [S1, M, N1] -> (h1 [M, N1], fc2's split-K product slabs
+    [S2, M, N2]) in one launch (csrc/linear.hip lookahead_fc2_fwd_kernel, variant 18 = 1)."""
+    S1, M, N1 = P1.shape
+    N2 = w2.shape[0]
+    c = C()
+    ws = _workspace(P1.device, max(16, c.lookahead_fc2_slices(N1)) * M * N2, key)
+    h1 = torch.empty(M, N1, device=P1.device, dtype=torch.float32)
+    S2 = c.lookahead_fc2_fwd(P1, b1.detach() if b1 is not None else None, float(drop_p), seed & M64, col_offset,
+                             _ptr(dseed), h1, w2.detach(), ws)
+    return h1, ws[:S2 * M * N2].view(S2, M, N2)   # S2 = ceil(N1 / k-slice width)
+
+
 def linear_dgrad_partial(dz, w, key: str = "dz1p"):
     """dz @ w as un-reduced split-N slabs [S, M, K] (no mask)."""
     M, K = dz.shape[0], w.shape[1]

@@ -262,10 +262,21 @@ def test_ushape_pipelined_epoch_matches_per_batch_steps(cuda, tmp_path, ahead):
             torch.testing.assert_close(va, vb, rtol=1e-3, atol=1e-4, msg=k)
 
 
+@pytest.fixture(params=[0, 1, 2], ids=["v18=0", "v18=1", "v18=2"])
+def lookahead_fc2_variant(request):
+    """Variant 18: the single-shard look-ahead epilogue inside fc2's forward (1) or separate (0)."""
+    from splitlearning_amd.ops import hip_ops
+    C = hip_ops.C()
+    old = C.get_variant(18)
+    C.set_variant(18, request.param)
+    yield request.param
+    C.set_variant(18, old)
+
+
 @pytest.mark.parametrize("tp", [1, 8])
 @pytest.mark.parametrize("kind", ["adam", "sgd"])
 @pytest.mark.parametrize("B", [16, 64])
-def test_native_server_epoch_matches_python(cuda, tp, kind, B):
+def test_native_server_epoch_matches_python(cuda, tp, kind, B, lookahead_fc2_variant):
     """_C.ServerEpoch (csrc/engine.cpp) issues the same launches, seeds and step counts as the
     Python look-ahead loop: bit-identical weights, optimizer state and losses (tp = 8: rank
     0's shard, row-parallel fc2 through the native 1-rank communicator)."""

@@ -545,3 +545,25 @@ def test_linear_fwd_bf16_compute(cuda, M, N, K):
     _close(y, yr, rtol=1e-4, atol=2e-4)
     # and it is NOT the exact-fp32 product (the mode is really on)
     assert (y - torch.relu(x @ w.t() + b)).abs().max().item() > 1e-3
+
+
+@pytest.mark.parametrize("M,N1,N2,S1", [(16, 5000, 1000, 22), (64, 5000, 1000, 22), (16, 628, 1000, 22),
+                                        (5, 100, 37, 3), (16, 1000, 100, 7)])
+@pytest.mark.parametrize("ks", [1, 2])
+def test_lookahead_fc2_fwd(cuda, M, N1, N2, S1, ks):
+    """fc1's look-ahead epilogue inside fc2's split-K forward: h1 bitwise the epilogue kernel
+    (same slab order, same bias / ReLU / dropout), the product slabs sum to h1 @ W2^T."""
+    C = hip_ops.C()
+    old = C.get_variant(18)
+    C.set_variant(18, ks)                 # k-slice width 64 / 128
+    P1 = torch.randn(S1, M, N1, device=cuda)
+    b1 = torch.randn(N1, device=cuda)
+    W2 = torch.randn(N2, N1, device=cuda) / N1 ** 0.5
+    try:
+        h1, P2 = hip_ops.lookahead_fc2_fwd(P1, b1, 0.5, 77, 8, W2)
+    finally:
+        C.set_variant(18, old)
+    ref = hip_ops.linear_epilogue(P1, b1, True, 0.5, 77, 8)
+    assert torch.equal(h1, ref)
+    assert P2.shape[1:] == (M, N2) and P2.shape[0] <= hip_ops.C().lookahead_fc2_slices(N1)
+    _close(P2.sum(0), h1 @ W2.t(), rtol=1e-4, atol=1e-4)
