@@ -778,6 +778,8 @@ PYBIND11_MODULE(_C, m) {
   //   16 TP server step: 1 = separate peer-mapped all-reduce launch instead of the one fused
   //      into head_fwd
   //   18 single-shard look-ahead step: 1 = fc1's epilogue inside fc2's split-K forward
+  //   19 fc2 forward / dgrad: 2 = plain tile order (default: XCD-grouped, W2 rows stay in one
+  //      XCD's L2 from the forward to the dgrad)
   // The measurements behind each default are in the comment at the slot's use and docs/PERF.md.
   m.def("set_variant", [](int64_t slot, int64_t v) {
     TORCH_CHECK(slot >= 0 && slot < 24, "variant slot");

@@ -135,12 +135,25 @@ template <int U>
 __global__ void __launch_bounds__(1024)
 skinny_fwd_once_kernel(const float* __restrict__ X, int ldx, const float* __restrict__ W, int ldw,
                        float* __restrict__ Y, int ldy, int M, int N, int K, Epi e, float* __restrict__ P,
-                       int64_t slab) {
+                       int64_t slab, int nt_real = 0) {
   __shared__ f32x4 red[16][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, NW = blockDim.x >> 6;
-  const int n0 = blockIdx.x * 16, m0 = blockIdx.y * 16;
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (nt_real > 0) {
+    // XCD-grouped order (default; variant 19 = 2 off; grid x padded to 64 column tiles): dispatch slot L
+    // goes to XCD L % 8 (round robin), and every slot of XCD g takes a column tile of the
+    // 128 W rows [128 g, 128 g + 128), so one XCD's L2 holds those rows for the fc2 dgrad
+    // that follows (skinny_dgrad_kernel, same grouping).  Tile math and sums unchanged.
+    const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const int j = L >> 3;
+    bx = 8 * (L & 7) + (j & 7);
+    by = (j >> 3) % gridDim.y;
+    bz = (j >> 3) / gridDim.y;
+    if (bx >= nt_real) return;
+  }
+  const int n0 = bx * 16, m0 = by * 16;
   const int S = gridDim.z;
-  const int kb = ((int)blockIdx.z * NW + wv) * 16 * U;
+  const int kb = (bz * NW + wv) * 16 * U;
   const int ra = m0 + (lane & 15), rb = n0 + (lane & 15);
   const int kq = (lane >> 4) * 4;
   const bool va = ra < M, vb = rb < N;
@@ -177,7 +190,7 @@ skinny_fwd_once_kernel(const float* __restrict__ X, int ldx, const float* __rest
         if (S == 1)
           Y[(int64_t)m * ldy + n] = apply_epi(e, s[r], m, n);
         else
-          P[(int64_t)blockIdx.z * slab + (int64_t)m * N + n] = s[r];
+          P[(int64_t)bz * slab + (int64_t)m * N + n] = s[r];
       }
     }
   }
@@ -295,11 +308,21 @@ template <int NW, bool BF = false>
 __global__ void __launch_bounds__(NW * 64)
 skinny_dgrad_kernel(const float* __restrict__ dZ, int ldz, const float* __restrict__ W, int ldw,
                     const float* __restrict__ hprev, int ldh, float scale,
-                    float* __restrict__ out, int ldo, int64_t slab, int M, int N, int K) {
+                    float* __restrict__ out, int ldo, int64_t slab, int M, int N, int K, int xcd8 = 0) {
   __shared__ f32x4 red[NW][4][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int k0 = blockIdx.x * 64, m0 = blockIdx.y * 16;
-  const int S = gridDim.z, sidx = blockIdx.z;
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (xcd8) {
+    // XCD-grouped order (default; S = 8 slices of 128 rows): dispatch slot L goes to
+    // XCD L % 8 and takes N slice L % 8, i.e. the W rows the forward's XCD-grouped order
+    // left in that XCD's L2 (skinny_fwd_once_kernel).  Tile math and sums unchanged.
+    const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    bz = L & 7;
+    bx = (L >> 3) % gridDim.x;
+    by = (L >> 3) / gridDim.x;
+  }
+  const int k0 = bx * 64, m0 = by * 16;
+  const int S = gridDim.z, sidx = bz;
   // N range for this workgroup, then for this wave (multiples of 4)
   const int nblk = ((N + 4 * S - 1) / (4 * S)) * 4;
   const int nb0 = sidx * nblk, ne0 = min(N, nb0 + nblk);
@@ -685,10 +708,13 @@ hipError_t linear_dgrad(const float* dZ, int ldz, const float* W, int ldw, const
     else
       skinny_dgrad_kernel<8><<<grid, 512, 0, st>>>(dZ, ldz, W, ldw, hprev, ldh, scale, dX, ldx, 0, M, N, K);
   } else {
+    // XCD-grouped order when the 8 N slices are 128 rows (the forward's groups; variant 19 = 2:
+    // plain order)
+    const int xg = (g_variant[19] != 2 && S == 8 && ((N + 4 * S - 1) / (4 * S)) * 4 == 128) ? 1 : 0;
     if (g_bf16)
-      skinny_dgrad_kernel<8, true><<<grid, 512, 0, st>>>(dZ, ldz, W, ldw, nullptr, 0, 1.f, ws, 0, slab, M, N, K);
+      skinny_dgrad_kernel<8, true><<<grid, 512, 0, st>>>(dZ, ldz, W, ldw, nullptr, 0, 1.f, ws, 0, slab, M, N, K, xg);
     else
-      skinny_dgrad_kernel<8><<<grid, 512, 0, st>>>(dZ, ldz, W, ldw, nullptr, 0, 1.f, ws, 0, slab, M, N, K);
+      skinny_dgrad_kernel<8><<<grid, 512, 0, st>>>(dZ, ldz, W, ldw, nullptr, 0, 1.f, ws, 0, slab, M, N, K, xg);
     launch_dgrad_reduce(ws, S, slab, hprev, ldh, scale, dX, ldx, M, K, st);
   }
   return hipGetLastError();
@@ -819,8 +845,12 @@ hipError_t linear_fwd_partial(const float* X, int ldx, const float* W, int ldw, 
   if (!g_bf16 && g_variant[14] != 2 && fwd_once_plan(M, N, K, max_split, ws_elems, NW1, S1)) {
     Epi e1{};
     e1.dscale = 1.f;
-    skinny_fwd_once_kernel<4><<<dim3(grid.x, grid.y, S1), NW1 * 64, 0, st>>>(X, ldx, W, ldw, ws, N, M, N, K, e1, ws,
-                                                                          slab);
+    // XCD-grouped tile order (at most 64 column tiles: grid padded to 64); variant 19 = 2:
+    // plain order.  Native executor, us per TP = 1 step: 174.4 vs 175.5 and 176.9 vs 178.1 in
+    // two interleaved runs (profiles/r2_xcd_grouped_fc2_ab.txt); bitwise the same products.
+    const bool xg = g_variant[19] != 2 && grid.x <= 64;
+    skinny_fwd_once_kernel<4><<<dim3(xg ? 64 : grid.x, grid.y, S1), NW1 * 64, 0, st>>>(
+        X, ldx, W, ldw, ws, N, M, N, K, e1, ws, slab, xg ? (int)grid.x : 0);
     *S_out = S1;
     return hipGetLastError();
   }

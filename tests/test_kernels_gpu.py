@@ -567,3 +567,26 @@ def test_lookahead_fc2_fwd(cuda, M, N1, N2, S1, ks):
     assert torch.equal(h1, ref)
     assert P2.shape[1:] == (M, N2) and P2.shape[0] <= hip_ops.C().lookahead_fc2_slices(N1)
     _close(P2.sum(0), h1 @ W2.t(), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("M", [16, 64])
+def test_xcd_grouped_order_is_bitwise_identical(cuda, M):
+    """The XCD-grouped workgroup order of the fc2 forward / dgrad (default; variant 19 = 2 is
+    the plain order) only permutes which dispatch slot runs which tile: bitwise the same."""
+    C = hip_ops.C()
+    x = torch.randn(M, 5000, device=cuda)
+    w = torch.randn(1000, 5000, device=cuda) / 70.0
+    dz = torch.randn(M, 1000, device=cuda)
+    h = torch.relu(torch.randn(M, 5000, device=cuda))
+    outs = []
+    old = C.get_variant(19)
+    try:
+        for v in (2, 0):
+            C.set_variant(19, v)
+            P = hip_ops.linear_fwd_partial(x, w, key=f"xg{v}").clone()
+            d = hip_ops.linear_dgrad(dz, w, h, 2.0).clone()
+            outs.append((P, d))
+    finally:
+        C.set_variant(19, old)
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    _close(outs[1][0].sum(0), x @ w.t(), rtol=1e-4, atol=1e-4)
