@@ -780,6 +780,8 @@ PYBIND11_MODULE(_C, m) {
   //   18 single-shard look-ahead step: 1 = fc1's epilogue inside fc2's split-K forward
   //   19 fc2 forward / dgrad: 2 = plain tile order (default: XCD-grouped, W2 rows stay in one
   //      XCD's L2 from the forward to the dgrad)
+  //   20 server head: 2 = grid (M, Q) with proportional column slices (default: grid (Q, M),
+  //      128-column slices on the fc2 forward's XCD groups)
   // The measurements behind each default are in the comment at the slot's use and docs/PERF.md.
   m.def("set_variant", [](int64_t slot, int64_t v) {
     TORCH_CHECK(slot >= 0 && slot < 24, "variant slot");

@@ -33,9 +33,32 @@ namespace sl {
 // Column slices of <= 32 float4 (128 columns) per workgroup; grid (M, Q) for both kernels.
 constexpr int HS = 32;
 
-__device__ __forceinline__ void head_slice(int n4, int Q, int q, int& a, int& b) {
-  a = (int)(((int64_t)n4 * q) / Q);
-  b = (int)(((int64_t)n4 * (q + 1)) / Q);
+// Head workgroup layout (hl = 0, the default): grid (Q, M), slice q = float4 columns
+// [32 q, 32 q + 32), so with Q = 8 dispatch slot L = q + 8 m runs on XCD q and slice q is
+// exactly the 128 fc2 outputs whose W2 rows the XCD-grouped fc2 forward / dgrad keep on XCD q
+// (csrc/linear.hip): the forward's slabs, h2 and dz2 of a slice stay in one XCD's L2 from the
+// forward through head_fwd and head_bwd to the dgrad.  hl = 1 (variant 20 = 2): the earlier
+// grid (M, Q) with proportional slices.
+__device__ __forceinline__ void head_wg(int hl, int& m, int& q, int& Q) {
+  if (hl == 0) {
+    q = blockIdx.x;
+    m = blockIdx.y;
+    Q = gridDim.x;
+  } else {
+    m = blockIdx.x;
+    q = blockIdx.y;
+    Q = gridDim.y;
+  }
+}
+
+__device__ __forceinline__ void head_slice(int n4, int Q, int q, int& a, int& b, int hl) {
+  if (hl == 0) {
+    a = min(n4, HS * q);
+    b = min(n4, HS * q + HS);
+  } else {
+    a = (int)(((int64_t)n4 * q) / Q);
+    b = (int)(((int64_t)n4 * (q + 1)) / Q);
+  }
 }
 
 // head_fwd_kernel: workgroup (m, q) reduces fc2's split-K slabs for its column slice of row
@@ -55,12 +78,15 @@ __device__ __forceinline__ void head_slice(int n4, int Q, int q, int& a, int& b)
 template <bool BF, bool IPC>
 __global__ void __launch_bounds__(256)
 head_fwd_kernel(const float* __restrict__ P2, int S2, int64_t slab2, Epi e2, const float* __restrict__ W3,
-                int ldw3, float* __restrict__ h2, float* __restrict__ plog, int M, int N2, int C, IpcStep ip) {
+                int ldw3, float* __restrict__ h2, float* __restrict__ plog, int M, int N2, int C, IpcStep ip,
+                int hl) {
   __shared__ f32x4 part[8][HS];
   __shared__ f32x4 hs[HS];
-  const int m = blockIdx.x, q = blockIdx.y, Q = gridDim.y, tid = threadIdx.x;
+  int m, q, Q;
+  head_wg(hl, m, q, Q);
+  const int tid = threadIdx.x;
   int qa, qb;
-  head_slice(N2 >> 2, Q, q, qa, qb);
+  head_slice(N2 >> 2, Q, q, qa, qb, hl);
   const int ncol = qb - qa;
   const int lane = tid & 63, wv = tid >> 6, half = lane >> 5, c = lane & 31;
   constexpr int JU = 13;
@@ -258,15 +284,17 @@ __global__ void __launch_bounds__(256)
 head_bwd_kernel(const float* __restrict__ plog, const float* __restrict__ b3, const float* __restrict__ W3,
                 int ldw3, const int64_t* __restrict__ y, int64_t ignore, float scale, float dscale,
                 const float* __restrict__ h2, float* __restrict__ dlog, float* __restrict__ dz2,
-                float* __restrict__ loss_rows, int M, int N2, int C, int Qp) {
+                float* __restrict__ loss_rows, int M, int N2, int C, int Qp, int hl) {
   // Qp: number of partial-logit slabs in plog (head_fwd: one per column slice = gridDim.y;
   // fc2_head_fwd: one per 8-column tile)
   extern __shared__ float lg[];   // C
   __shared__ f32x4 part[8][HS];
-  const int m = blockIdx.x, q = blockIdx.y, Q = gridDim.y, tid = threadIdx.x;
+  int m, q, Q;
+  head_wg(hl, m, q, Q);
+  const int tid = threadIdx.x;
   const int lane = tid & 63, wv = tid >> 6;
   int qa, qb;
-  head_slice(N2 >> 2, Q, q, qa, qb);
+  head_slice(N2 >> 2, Q, q, qa, qb, hl);
   const int ncol = qb - qa;
   const int c = tid & (HS - 1), g = tid >> 5;
   constexpr int JU = 13;
@@ -623,16 +651,20 @@ wgrad_group_mfma_kernel(WgGroup grp, int M, SlOpt o) {
 
 int head3_slices(int N2) { return max(1, (N2 / 4 + HS - 1) / HS); }
 
+static int head_layout() { return g_variant[20] == 2 ? 1 : 0; }
+static dim3 head_grid(int M, int Q, int hl) { return hl == 0 ? dim3(Q, M) : dim3(M, Q); }
+
 static void launch_head_bwd(const float* plog, const float* b3, const float* W3, int ldw3, const int64_t* y,
                             int64_t ignore, float scale, float dscale, const float* h2, float* dlog, float* dz2,
-                            float* loss_rows, int M, int N2, int C, int Q, int Qp, hipStream_t st) {
+                            float* loss_rows, int M, int N2, int C, int Q, int Qp, hipStream_t st, int hl) {
   const size_t sh = (size_t)C * sizeof(float);
+  const dim3 g = head_grid(M, Q, hl);
   if (g_bf16)
-    head_bwd_kernel<true><<<dim3(M, Q), 256, sh, st>>>(plog, b3, W3, ldw3, y, ignore, scale, dscale, h2, dlog, dz2,
-                                                        loss_rows, M, N2, C, Qp);
+    head_bwd_kernel<true><<<g, 256, sh, st>>>(plog, b3, W3, ldw3, y, ignore, scale, dscale, h2, dlog, dz2, loss_rows,
+                                              M, N2, C, Qp, hl);
   else
-    head_bwd_kernel<false><<<dim3(M, Q), 256, sh, st>>>(plog, b3, W3, ldw3, y, ignore, scale, dscale, h2, dlog, dz2,
-                                                         loss_rows, M, N2, C, Qp);
+    head_bwd_kernel<false><<<g, 256, sh, st>>>(plog, b3, W3, ldw3, y, ignore, scale, dscale, h2, dlog, dz2,
+                                               loss_rows, M, N2, C, Qp, hl);
 }
 
 hipError_t server_head3(const float* P2, int S2, int64_t slab2, Epi e2, const float* W3, int ldw3, const float* b3,
@@ -643,7 +675,8 @@ hipError_t server_head3(const float* P2, int S2, int64_t slab2, Epi e2, const fl
   if ((N2 & 3) || (ldw3 & 3)) return hipErrorInvalidValue;
   const int Q = head3_slices(N2);
   if (ws_elems < (int64_t)Q * M * C) return hipErrorInvalidValue;
-  const dim3 g(M, Q);
+  const int hl = head_layout();
+  const dim3 g = head_grid(M, Q, hl);
   if (ipc != nullptr) {
     // the fused all-reduce: one flag word per workgroup, one [M, N2] partial per slot; the
     // local partial may be S2 split-K slabs (summed before the push)
@@ -651,17 +684,17 @@ hipError_t server_head3(const float* P2, int S2, int64_t slab2, Epi e2, const fl
         ipc->T > kIpcMaxRanks)
       return hipErrorInvalidValue;
     if (g_bf16)
-      head_fwd_kernel<true, true><<<g, 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C, *ipc);
+      head_fwd_kernel<true, true><<<g, 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C, *ipc, hl);
     else
-      head_fwd_kernel<false, true><<<g, 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C, *ipc);
+      head_fwd_kernel<false, true><<<g, 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C, *ipc, hl);
   } else {
     const IpcStep none{};
     if (g_bf16)
-      head_fwd_kernel<true, false><<<g, 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C, none);
+      head_fwd_kernel<true, false><<<g, 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C, none, hl);
     else
-      head_fwd_kernel<false, false><<<g, 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C, none);
+      head_fwd_kernel<false, false><<<g, 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C, none, hl);
   }
-  launch_head_bwd(ws, b3, W3, ldw3, y, ignore, scale, e2.dscale, h2, dlog, dz2, loss_rows, M, N2, C, Q, Q, st);
+  launch_head_bwd(ws, b3, W3, ldw3, y, ignore, scale, e2.dscale, h2, dlog, dz2, loss_rows, M, N2, C, Q, Q, st, hl);
   return hipGetLastError();
 }
 
@@ -679,7 +712,8 @@ hipError_t server_fc2_head(const float* X, int ldx, const float* W2, int ldw2, E
   if (ws_elems < (int64_t)T * M * C) return hipErrorInvalidValue;
   fc2_head_fwd_kernel<8><<<dim3(T, (M + 15) / 16), 1024, 0, st>>>(X, ldx, W2, ldw2, e2, W3, ldw3, h2, ws, M, N2, K, C,
                                                                   g_bf16);
-  launch_head_bwd(ws, b3, W3, ldw3, y, ignore, scale, e2.dscale, h2, dlog, dz2, loss_rows, M, N2, C, Q, T, st);
+  launch_head_bwd(ws, b3, W3, ldw3, y, ignore, scale, e2.dscale, h2, dlog, dz2, loss_rows, M, N2, C, Q, T, st,
+                  head_layout());
   return hipGetLastError();
 }
 
