@@ -88,6 +88,10 @@ class Session:
         if self.is_bob:
             self._build_bob()
         self.bob_log.info("Bob Started Getting Tipsy")
+        if self.pl.bob_tp > 1:
+            kind = ("peer-mapped (one kernel, fused into the server head)" if getattr(self, "tp_ipc", None) is not None
+                    else "RCCL" if getattr(self, "tp_native_comm", None) is not None else "torch.distributed")
+            self.bob_log.info(f"[perf] Bob tensor-parallel over {self.pl.bob_tp} ranks; TP all-reduce: {kind}")
 
     # ------------------------------------------------------------------ construction
     def front_module(self):
