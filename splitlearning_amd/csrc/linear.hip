@@ -313,13 +313,15 @@ skinny_dgrad_kernel(const float* __restrict__ dZ, int ldz, const float* __restri
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
   if (xcd8) {
-    // XCD-grouped order (default; S = 8 slices of 128 rows): dispatch slot L goes to
-    // XCD L % 8 and takes N slice L % 8, i.e. the W rows the forward's XCD-grouped order
-    // left in that XCD's L2 (skinny_fwd_once_kernel).  Tile math and sums unchanged.
+    // XCD-grouped order (default; S = 8 xcd8 slices, xcd8 of them per 128-row group): dispatch
+    // slot L goes to XCD L % 8 and takes an N slice of row group L % 8, i.e. the W rows the
+    // forward's XCD-grouped order left in that XCD's L2 (skinny_fwd_once_kernel).  Tile math
+    // and sums unchanged.
     const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-    bz = L & 7;
-    bx = (L >> 3) % gridDim.x;
-    by = (L >> 3) / gridDim.x;
+    const int j = L >> 3;
+    bz = (L & 7) * xcd8 + j % xcd8;
+    bx = (j / xcd8) % gridDim.x;
+    by = (j / xcd8) / gridDim.x;
   }
   const int k0 = bx * 64, m0 = by * 16;
   const int S = gridDim.z, sidx = bz;
@@ -708,9 +710,10 @@ hipError_t linear_dgrad(const float* dZ, int ldz, const float* W, int ldw, const
     else
       skinny_dgrad_kernel<8><<<grid, 512, 0, st>>>(dZ, ldz, W, ldw, hprev, ldh, scale, dX, ldx, 0, M, N, K);
   } else {
-    // XCD-grouped order when the 8 N slices are 128 rows (the forward's groups; variant 19 = 2:
-    // plain order)
-    const int xg = (g_variant[19] != 2 && S == 8 && ((N + 4 * S - 1) / (4 * S)) * 4 == 128) ? 1 : 0;
+    // XCD-grouped order when S / 8 N slices make one 128-row group of the forward (S = 8 at
+    // TP = 1, S = 16 at a TP = 8 shard; variant 19 = 2: plain order)
+    const int nblk = ((N + 4 * S - 1) / (4 * S)) * 4;
+    const int xg = (g_variant[19] != 2 && S % 8 == 0 && nblk * (S / 8) == 128) ? S / 8 : 0;
     if (g_bf16)
       skinny_dgrad_kernel<8, true><<<grid, 512, 0, st>>>(dZ, ldz, W, ldw, nullptr, 0, 1.f, ws, 0, slab, M, N, K, xg);
     else

@@ -590,3 +590,22 @@ def test_xcd_grouped_order_is_bitwise_identical(cuda, M):
         C.set_variant(19, old)
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
     _close(outs[1][0].sum(0), x @ w.t(), rtol=1e-4, atol=1e-4)
+
+
+def test_xcd_grouped_dgrad_tp8_shard_is_bitwise_identical(cuda):
+    """The grouped dgrad order with two 64-row N slices per 128-row group (a TP = 8 shard:
+    K = 628, S = 16) is bitwise the plain order."""
+    C = hip_ops.C()
+    w = torch.randn(1000, 628, device=cuda) / 30.0
+    dz = torch.randn(16, 1000, device=cuda)
+    h = torch.relu(torch.randn(16, 628, device=cuda))
+    outs = []
+    old = C.get_variant(19)
+    try:
+        for v in (2, 0):
+            C.set_variant(19, v)
+            outs.append(hip_ops.linear_dgrad(dz, w, h, 2.0).clone())
+    finally:
+        C.set_variant(19, old)
+    assert torch.equal(outs[0], outs[1])
+    _close(outs[1], torch_ops.linear_dgrad(dz, w, h, 2.0), rtol=1e-4, atol=1e-4)
