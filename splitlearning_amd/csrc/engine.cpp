@@ -9,7 +9,8 @@
 // sequence for a whole epoch from C++:
 //
 //   [fc1 epilogue of the look-ahead slabs | fc1 forward]  -> h1
-//   fc2 forward (split-K slabs; row-parallel: unsplit product + native all-reduce)
+//   fc2 forward (split-K slabs; row-parallel: this shard's product, all-reduced by the
+//     peer-mapped all-reduce fused into head_fwd (ipc_ar.h), or by RCCL before the head)
 //   head_fwd + head_bwd  (fc2 epilogue, fc3, softmax-CE, fc3 dgrad, fc2 ReLU/dropout bwd)
 //   fc2 dgrad (+ fc1 ReLU/dropout mask)                     -> dz1
 //   wgrad_group: fc1/fc2/fc3 dW fused into Adam/SGD, plus fc1's product for the next
