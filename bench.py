@@ -77,6 +77,12 @@ def _phase_kind(mode: str, name: str):
     return None
 
 
+def _ipc_status():
+    """The peer-mapped TP all-reduce's set-up outcome on this process (parallel/rccl.py)."""
+    from splitlearning_amd.parallel.rccl import IPC_STATUS
+    return dict(IPC_STATUS) if IPC_STATUS else None
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -253,6 +259,7 @@ def main(argv=None):
                 "tp_allreduce": ("ipc" if getattr(sess, "tp_ipc", None) is not None else
                                  "rccl" if tpc is not None else "torch.distributed" if N > 1 else "none"),
                 "bytes_sent_per_rank_per_step": sent,
+                "tp_ipc_setup": _ipc_status(),
             },
         }
         line = json.dumps(out)

@@ -88,14 +88,8 @@ def main():
     n_ep = min(2048, shard.shape[0] // 16 * 16)
     order = torch.randperm(shard.shape[0], device=dev)[:n_ep]
 
-    def _epoch(v):
-        def run():
-            C.set_variant(6, v)
-            H.conv_local_epoch_(shard, ylab, order, 16, cw, cb, cfg, scw, scb, 2)
-            C.set_variant(6, 0)
-        return run
-    cases.append((f"conv_local_epoch[{n_ep // 16} steps, fused opt]", _epoch(0), 0))
-    cases.append((f"conv_local_epoch[{n_ep // 16} steps, 2 launches, 8 lanes/ch]", _epoch(1), 0))
+    cases.append((f"conv_local_epoch[{n_ep // 16} steps, fused opt]",
+                  lambda: H.conv_local_epoch_(shard, ylab, order, 16, cw, cb, cfg, scw, scb, 2), 0))
     y, am = H.conv_front_fwd(shard, idx, cw, cb)
     dy = torch.randn(M, 5408, device=dev)
     cases.append(("conv_bwd_step(2 kernels)", lambda: H.conv_front_bwd_step_(dy, y, am, shard, idx, cw, cb, cfg,
@@ -128,33 +122,17 @@ def main():
     cases.append(("fused:fc2_fwd_partial", lambda: H.linear_fwd_partial(h1f, L2.W), W2.numel() * 4))
     cases.append(("fused:head3", lambda: H.server_head3(P2, L2.b, True, 0.5, 3, L3.W, L3.b, yl, 1 / 16), 0))
     h2f, dlf, dz2f, _ = H.server_head3(P2, L2.b, True, 0.5, 3, L3.W, L3.b, yl, 1 / 16)
-    cases.append(("fused:fc2_dgrad_partial", lambda: H.linear_dgrad_partial(dz2f, L2.W), W2.numel() * 4))
-    dz1p = H.linear_dgrad_partial(dz2f, L2.W)
+    dz1f = H.linear_dgrad(dz2f, L2.W, h1f, 2.0)
     wst = [fslot.state(f"fc{i}.{n}", t) for i, L in ((1, L1), (2, L2), (3, L3)) for n, t in
            (("weight", L.W), ("bias", L.b))]
-    grp = [(None, dz1p, h1f, 2.0, x, L1.W, wst[0], L1.b, wst[1]), (dz2f, None, None, 1.0, h1f, L2.W, wst[2], L2.b,
-                                                                     wst[3]),
-           (dlf, None, None, 1.0, h2f, L3.W, wst[4], L3.b, wst[5])]
+    grp = [(dz1f, x, L1.W, wst[0], L1.b, wst[1]), (dz2f, h1f, L2.W, wst[2], L2.b, wst[3]),
+           (dlf, h2f, L3.W, wst[4], L3.b, wst[5])]
     cases.append(("fused:wgrad_group3", lambda: H.wgrad_group_(grp, M, cfg, 3), 32_146_100 * 24))
     cases.append(("fused:wgrad_fc1_only", lambda: H.wgrad_group_(grp[:1], M, cfg, 3), W1.numel() * 24))
     dz1r = torch.randn(M, N1, device=dev)
-    grp_plain = [(dz1r, None, None, 1.0, x, L1.W, wst[0], L1.b, wst[1])]
-    cases.append(("fused:wgrad_fc1_plain_dz", lambda: H.wgrad_group_(grp_plain, M, cfg, 3), W1.numel() * 24))
     pn = H.lookahead_slabs(dev, 5408, M, N1)
-    cases.append(("fused:wgrad_fc1_plain_dz_lookahead",
-                  lambda: H.wgrad_group_(grp_plain, M, cfg, 3, x_next=x, p_next=pn), W1.numel() * 24))
-    def _v1(fn):
-        def run():
-            C.set_variant(3, 1)
-            fn()
-            C.set_variant(3, 0)
-        return run
-    cases.append(("fused:wgrad_fc1_plain_dz[mfma]", _v1(lambda: H.wgrad_group_(grp_plain, M, cfg, 3)), W1.numel() * 24))
-    cases.append(("fused:wgrad_fc1_plain_dz_lookahead[mfma]",
-                  _v1(lambda: H.wgrad_group_(grp_plain, M, cfg, 3, x_next=x, p_next=pn)), W1.numel() * 24))
-    grp3_plain = [grp_plain[0], grp[1], grp[2]]
-    cases.append(("fused:wgrad_group3_plain_lookahead",
-                  lambda: H.wgrad_group_(grp3_plain, M, cfg, 3, x_next=x, p_next=pn), 32_146_100 * 24))
+    cases.append(("fused:wgrad_group3_lookahead",
+                  lambda: H.wgrad_group_(grp, M, cfg, 3, x_next=x, p_next=pn), 32_146_100 * 24))
     cases.append(("v3:wgrad_fc1_same_tensors", lambda: H.linear_wgrad_step_(dz1r, x, L1.W, L1.b, cfg, wst[0], wst[1], 3),
                   W1.numel() * 24))
 
@@ -186,8 +164,6 @@ def main():
     for _ in range(a.rounds):
         for name, fn, nb in cases:
             rec(name, timeit(fn, a.iters), nb)
-    for slot in range(8):
-        C.set_variant(slot, 0)
     table = []
     for name, ts in res.items():
         ts = sorted(ts)

@@ -28,7 +28,9 @@ from splitlearning_amd.ops import hip_ops as H  # noqa: E402
 
 
 def parse(v):
-    return {int(a): int(b) for a, b in (kv.split("=") for kv in v.split(","))}
+    """`SLOT=VALUE[,...]`; the key `fences` (0 / 1) toggles the peer-mapped all-reduce's
+    release / acquire fences (`--allreduce ipc`) instead of a kernel-variant slot."""
+    return {(a if a == "fences" else int(a)): int(b) for a, b in (kv.split("=") for kv in v.split(","))}
 
 
 def main():
@@ -45,12 +47,12 @@ def main():
     dev = torch.device("cuda", 0)
     ops.set_backend("hip")
     B, nb = 16, 64
-    slots = sorted({s for v in a.variants for s in parse(v)})
+    slots = sorted({s for v in a.variants for s in parse(v) if s != "fences"})
     for tp in a.tp:
         torch.manual_seed(0)
         acts = torch.rand(B * nb, 5408, device=dev) * 20
         labels = torch.randint(0, 10, (B * nb,), device=dev)
-        ar = None
+        ar = ipc = None
         if tp > 1:
             from splitlearning_amd.parallel.rccl import ipc_allreduce, native_allreduce, self_comm
             if a.allreduce == "ipc":
@@ -80,7 +82,11 @@ def main():
                 for s in slots:
                     C.set_variant(s, 0)
                 for s, val in parse(v).items():
-                    C.set_variant(s, val)
+                    if s == "fences":
+                        if ipc is not None:
+                            ipc.set_fences(bool(val))
+                    else:
+                        C.set_variant(s, val)
                 epochs(1)
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()

@@ -72,9 +72,9 @@ def main():
         W3, s3, b3, sb3 = layer(N3, N2)
         g1 = torch.randn_like(W1)
         pn = H.lookahead_slabs(dev, K1, M, n1)
-        L1 = (dz1, None, None, 1.0, x, W1, s1, b1, sb1)
-        L2 = (dz2, None, None, 1.0, h1, W2, s2, b2, sb2)
-        L3 = (dz3, None, None, 1.0, h2, W3, s3, b3, sb3)
+        L1 = (dz1, x, W1, s1, b1, sb1)
+        L2 = (dz2, h1, W2, s2, b2, sb2)
+        L3 = (dz3, h2, W3, s3, b3, sb3)
         st = {"m": s1["m"], "v": s1["v"]}
         n_par = W1.numel()
         res = {

@@ -46,13 +46,8 @@ hipError_t linear_dgrad(const float* dZ, int ldz, const float* W, int ldw, const
                         hipStream_t st);
 hipError_t linear_epilogue(const float* P, int ldp, float* Y, int ldy, int M, int N, Epi e, int S, int64_t slab,
                            hipStream_t st);
-int lookahead_fc2_slices(int N1);
-hipError_t lookahead_fc2_fwd(const float* pn, int S1, int64_t slab1, Epi e1, float* h1, const float* W2, float* P2,
-                             int64_t p2_elems, int M, int N1, int N2, int* S2_out, hipStream_t st);
 hipError_t linear_fwd_partial(const float* X, int ldx, const float* W, int ldw, int M, int N, int K, float* ws,
                               int64_t ws_elems, int max_split, int* S_out, hipStream_t st);
-hipError_t linear_dgrad_partial(const float* dZ, int ldz, const float* W, int ldw, int M, int N, int K, float* ws,
-                                int64_t ws_elems, int* S_out, hipStream_t st);
 hipError_t linear_wgrad_opt(const float* dZ, int ldz, const float* A, int lda, float* W, int ldw, float* s0,
                             float* s1, float* bias, float* sb0, float* sb1, int M, int N, int K, SlOpt o,
                             hipStream_t st);
@@ -220,7 +215,7 @@ SlOpt epoch_opt(void* ctx, int64_t t) {
 // A whole SISA local epoch: ceil(n/B) client steps over `order` (the last one partial, like
 // DataLoader(drop_last=False)), optimizer steps t0, t0+1, ...  One launch per step: each
 // step's kernel applies the previous step's optimizer update in its prologue
-// (conv.hip: conv_local_epoch); variant 6 = 1 runs the two-launch step instead (A/B).
+// (conv.hip: conv_local_epoch).
 void conv_local_epoch(const at::Tensor& x, const at::Tensor& order, const at::Tensor& labels, int64_t B,
                       at::Tensor& w, at::Tensor& b, at::Tensor& slab, at::Tensor& loss_rows, at::Tensor& s0w,
                       const OptT& s1w, at::Tensor& s0b, const OptT& s1b, int64_t kind, double lr, double beta1,
@@ -241,18 +236,6 @@ void conv_local_epoch(const at::Tensor& x, const at::Tensor& order, const at::Te
   TORCH_CHECK(ws.is_contiguous(), "ws contiguous");
   TORCH_CHECK(kind == 1 || kind == 2, "local epoch: SGD-momentum or Adam");
   const hipStream_t st = cur_stream();
-  if (sl::g_variant[6] == 1) {
-    for (int64_t s = 0, t = t0; s < n; s += B, ++t) {
-      const int bs = (int)std::min<int64_t>(B, n - s);
-      check(sl::conv_local_step(x.data_ptr(), x.scalar_type() == at::kByte, order.data_ptr<int64_t>() + s,
-                                labels.data_ptr<int64_t>(), bs, w.data_ptr<float>(), b.data_ptr<float>(),
-                                slab.data_ptr<float>(), loss_rows.data_ptr<float>() + s, s0w.data_ptr<float>(),
-                                fptr(s1w), s0b.data_ptr<float>(), fptr(s1b),
-                                make_opt(kind, lr, beta1, beta2, eps, wd, momentum, t, 0), st),
-            "conv_local_epoch");
-    }
-    return;
-  }
   EpochOpt ctx{kind, lr, beta1, beta2, eps, wd, momentum};
   check(sl::conv_local_epoch(x.data_ptr(), x.scalar_type() == at::kByte, order.data_ptr<int64_t>(), n, (int)B,
                              labels.data_ptr<int64_t>(), w.data_ptr<float>(), b.data_ptr<float>(),
@@ -556,47 +539,12 @@ int64_t linear_fwd_partial(const at::Tensor& X, const at::Tensor& W, at::Tensor&
   return S;
 }
 
-// fc1 look-ahead slabs P1 [S1, M, N1] -> h1 (fc1 epilogue) and fc2's split-K product slabs in
-// ws ([S2, M, N2], one per 64-wide k-slice of h1); returns S2
-int64_t lookahead_fc2_fwd(const at::Tensor& P1, const OptT& b1, double drop1, uint64_t seed1, int64_t col_off,
-                          int64_t dseed1, at::Tensor& h1, const at::Tensor& W2, at::Tensor& ws) {
-  need_f32(P1, "P1");
-  TORCH_CHECK(P1.dim() == 3 && P1.is_contiguous(), "P1 [S, M, N1] contiguous");
-  need_2d(h1, "h1");
-  need_rows(W2, "W2");
-  need_f32(ws, "ws");
-  const int64_t S1 = P1.size(0), M = P1.size(1), N1 = P1.size(2), N2 = W2.size(0);
-  TORCH_CHECK(h1.size(0) == M && h1.size(1) == N1 && h1.stride(0) == N1, "h1 [M, N1] dense");
-  TORCH_CHECK(W2.size(1) == N1 && W2.stride(0) == N1 && N1 % 4 == 0, "W2 [N2, N1] dense, N1 % 4 == 0");
-  TORCH_CHECK(ws.is_contiguous(), "ws contiguous");
-  if (b1.has_value() && b1->defined()) TORCH_CHECK(b1->numel() == N1, "b1 [N1]");
-  int S2 = 0;
-  check(sl::lookahead_fc2_fwd(P1.data_ptr<float>(), (int)S1, M * N1, make_epi(b1, true, drop1, seed1, col_off, dseed1),
-                              h1.data_ptr<float>(), W2.data_ptr<float>(), ws.data_ptr<float>(), ws.numel(), (int)M,
-                              (int)N1, (int)N2, &S2, cur_stream()),
-        "lookahead_fc2_fwd");
-  return S2;
-}
-
-int64_t linear_dgrad_partial(const at::Tensor& dZ, const at::Tensor& W, at::Tensor& ws) {
-  need_2d(dZ, "dZ");
-  need_rows(W, "W");
-  need_f32(ws, "ws");
-  TORCH_CHECK(ws.is_contiguous(), "ws contiguous");
-  const int64_t M = dZ.size(0), N = dZ.size(1), K = W.size(1);
-  TORCH_CHECK(W.size(0) == N && K % 4 == 0, "W must be [N,K]");
-  int S = 1;
-  check(sl::linear_dgrad_partial(dZ.data_ptr<float>(), (int)dZ.stride(0), W.data_ptr<float>(), (int)W.stride(0),
-                                 (int)M, (int)N, (int)K, ws.data_ptr<float>(), ws.numel(), &S, cur_stream()),
-        "linear_dgrad_partial");
-  return S;
-}
-
 // ---------------------------------------------------------------- fused server step
 // P2: fc2 partial sums, [S2, M, N2] split-K slabs or a reduced [M, N2] tensor.
 void server_head3(const at::Tensor& P2, const OptT& b2, bool relu2, double drop2, uint64_t seed2, int64_t dseed2,
                   const at::Tensor& W3, const OptT& b3, const at::Tensor& y, int64_t ignore, double scale,
-                  at::Tensor& h2, at::Tensor& dlog, at::Tensor& dz2, at::Tensor& loss_rows, at::Tensor& ws) {
+                  at::Tensor& h2, at::Tensor& dlog, at::Tensor& dz2, at::Tensor& loss_rows, at::Tensor& ws, int64_t G,
+                  const OptT& gscale) {
   need_f32(P2, "P2");
   TORCH_CHECK(P2.is_contiguous() && (P2.dim() == 2 || P2.dim() == 3), "P2 [S,M,N2] or [M,N2] contiguous");
   const int64_t S2 = P2.dim() == 3 ? P2.size(0) : 1;
@@ -607,7 +555,12 @@ void server_head3(const at::Tensor& P2, const OptT& b2, bool relu2, double drop2
   need_f32(ws, "ws");
   TORCH_CHECK(ws.is_contiguous() && ws.numel() >= (int64_t)sl::head3_slices((int)N2) * M * C, "head workspace");
   need_cuda(y, "labels");
-  TORCH_CHECK(y.scalar_type() == at::kLong && y.numel() == M && y.is_contiguous(), "labels int64 [M]");
+  TORCH_CHECK(G >= 1 && C % G == 0, "C % groups");
+  TORCH_CHECK(y.scalar_type() == at::kLong && y.numel() == M * G && y.is_contiguous(), "labels int64 [M, groups]");
+  if (gscale.has_value() && gscale->defined()) {
+    need_f32(*gscale, "gscale");
+    TORCH_CHECK(gscale->is_contiguous() && gscale->numel() == M * G, "gscale [M, groups]");
+  }
   for (auto* t : {&h2, &dz2}) {
     need_f32(*t, "h2/dz2");
     TORCH_CHECK(t->is_contiguous() && t->size(0) == M && t->size(1) == N2, "h2/dz2 [M,N2]");
@@ -615,52 +568,16 @@ void server_head3(const at::Tensor& P2, const OptT& b2, bool relu2, double drop2
   need_f32(dlog, "dlog");
   TORCH_CHECK(dlog.is_contiguous() && dlog.size(0) == M && dlog.size(1) == C, "dlog [M,C]");
   need_f32(loss_rows, "loss_rows");
-  TORCH_CHECK(loss_rows.numel() >= M, "loss_rows");
+  TORCH_CHECK(loss_rows.numel() >= M * G, "loss_rows [M, groups]");
   check(sl::server_head3(P2.data_ptr<float>(), (int)S2, M * N2, make_epi(b2, relu2, drop2, seed2, 0, dseed2),
                          W3.data_ptr<float>(), (int)W3.stride(0), fptr(b3), y.data_ptr<int64_t>(), ignore,
                          (float)scale, h2.data_ptr<float>(), dlog.data_ptr<float>(), dz2.data_ptr<float>(),
                          loss_rows.data_ptr<float>(), ws.data_ptr<float>(), ws.numel(), (int)M, (int)N2, (int)C,
-                         cur_stream()),
+                         cur_stream(), nullptr, (int)G, fptr(gscale)),
         "server_head3");
 }
 
-// Single-shard server head from fc1's output: fc2 forward (full K per workgroup) + fc2
-// epilogue + partial fc3 logits in one launch, then the softmax-CE / fc3-dgrad kernel
-// (fused.hip server_fc2_head).  Returns nothing; writes h2, dlog, dz2, loss_rows.
-void server_fc2_head(const at::Tensor& h1, const at::Tensor& W2, const OptT& b2, bool relu2, double drop2,
-                     uint64_t seed2, int64_t dseed2, const at::Tensor& W3, const OptT& b3, const at::Tensor& y,
-                     int64_t ignore, double scale, at::Tensor& h2, at::Tensor& dlog, at::Tensor& dz2,
-                     at::Tensor& loss_rows, at::Tensor& ws) {
-  need_rows(h1, "h1");
-  need_rows(W2, "W2");
-  const int64_t M = h1.size(0), K = h1.size(1), N2 = W2.size(0);
-  TORCH_CHECK(W2.size(1) == K && K % 4 == 0, "W2 [N2, K]");
-  need_rows(W3, "W3");
-  const int64_t C = W3.size(0);
-  TORCH_CHECK(W3.size(1) == N2 && N2 % 4 == 0 && C <= 4096, "W3 [C, N2], N2 % 4 == 0");
-  need_f32(ws, "ws");
-  TORCH_CHECK(ws.is_contiguous() && ws.numel() >= (int64_t)sl::fc2_head_tiles((int)N2) * M * C, "head workspace");
-  need_cuda(y, "labels");
-  TORCH_CHECK(y.scalar_type() == at::kLong && y.numel() == M && y.is_contiguous(), "labels int64 [M]");
-  for (auto* t : {&h2, &dz2}) {
-    need_f32(*t, "h2/dz2");
-    TORCH_CHECK(t->is_contiguous() && t->size(0) == M && t->size(1) == N2, "h2/dz2 [M,N2]");
-  }
-  need_f32(dlog, "dlog");
-  TORCH_CHECK(dlog.is_contiguous() && dlog.size(0) == M && dlog.size(1) == C, "dlog [M,C]");
-  need_f32(loss_rows, "loss_rows");
-  TORCH_CHECK(loss_rows.numel() >= M, "loss_rows");
-  if (b2.has_value() && b2->defined()) TORCH_CHECK(b2->numel() == N2, "b2 [N2]");
-  check(sl::server_fc2_head(h1.data_ptr<float>(), (int)h1.stride(0), W2.data_ptr<float>(), (int)W2.stride(0),
-                            make_epi(b2, relu2, drop2, seed2, 0, dseed2), W3.data_ptr<float>(), (int)W3.stride(0),
-                            fptr(b3), y.data_ptr<int64_t>(), ignore, (float)scale, h2.data_ptr<float>(),
-                            dlog.data_ptr<float>(), dz2.data_ptr<float>(), loss_rows.data_ptr<float>(),
-                            ws.data_ptr<float>(), ws.numel(), (int)M, (int)K, (int)N2, (int)C, cur_stream()),
-        "server_fc2_head");
-}
-
-// layers: up to 3 tuples (dz, dzp, hmask, mscale, A, W, s0, s1, bias, sb0, sb1); exactly one of dz / dzp
-// (dzp = [S, M, N] split-N partial slabs of the layer's output gradient, masked by hmask > 0).
+// layers: up to 3 tuples (dz, A, W, s0, s1, bias, sb0, sb1).
 // xn / pn (optional): next batch [mn, K0] -> its split-K partial pre-activations of layer 0
 // with the updated weights, pn = [ceil(K0/256), mn, N0].
 void wgrad_group(const std::vector<py::tuple>& layers, int64_t M, const OptT& xn, const OptT& pn, OPT_ARGS) {
@@ -669,40 +586,26 @@ void wgrad_group(const std::vector<py::tuple>& layers, int64_t M, const OptT& xn
   g.n = (int)layers.size();
   for (size_t i = 0; i < layers.size(); ++i) {
     const py::tuple& L = layers[i];
-    TORCH_CHECK(L.size() == 11, "layer tuple has 11 fields");
+    TORCH_CHECK(L.size() == 8, "layer tuple (dz, A, W, s0, s1, bias, sb0, sb1)");
     auto opt = [&](int j) -> OptT { return L[j].is_none() ? OptT() : OptT(L[j].cast<at::Tensor>()); };
-    const at::Tensor A = L[4].cast<at::Tensor>();
-    at::Tensor W = L[5].cast<at::Tensor>();
-    at::Tensor s0 = L[6].cast<at::Tensor>();
+    const at::Tensor dz = L[0].cast<at::Tensor>();
+    const at::Tensor A = L[1].cast<at::Tensor>();
+    at::Tensor W = L[2].cast<at::Tensor>();
+    at::Tensor s0 = L[3].cast<at::Tensor>();
     need_rows(A, "A");
     need_rows(W, "W");
     need_rows(s0, "s0");
     const int64_t N = W.size(0), K = W.size(1);
     TORCH_CHECK(A.size(0) == M && A.size(1) == K && K % 4 == 0, "A [M,K]");
     TORCH_CHECK(s0.sizes() == W.sizes() && s0.stride(0) == W.stride(0), "s0 like W");
-    OptT s1 = opt(7), bias = opt(8), sb0 = opt(9), sb1 = opt(10), dz = opt(0), dzp = opt(1), hm = opt(2);
+    OptT s1 = opt(4), bias = opt(5), sb0 = opt(6), sb1 = opt(7);
     if (kind == 2) TORCH_CHECK(s1.has_value() && s1->sizes() == W.sizes() && s1->stride(0) == W.stride(0), "s1");
     if (bias.has_value()) TORCH_CHECK(bias->numel() == N && sb0.has_value() && sb0->numel() == N, "bias state");
     sl::WgDesc& d = g.d[i];
-    TORCH_CHECK(dz.has_value() != dzp.has_value(), "exactly one of dz / dzp");
-    if (dz.has_value()) {
-      need_2d(*dz, "dz");
-      TORCH_CHECK(dz->size(0) == M && dz->size(1) == N, "dz [M,N]");
-      d.dz = dz->data_ptr<float>();
-      d.ldz = (int)dz->stride(0);
-    } else {
-      need_f32(*dzp, "dzp");
-      TORCH_CHECK(dzp->is_contiguous() && dzp->numel() % (M * N) == 0, "dzp [S,M,N]");
-      d.dzp = dzp->data_ptr<float>();
-      d.S = (int)(dzp->numel() / (M * N));
-      d.slab = M * N;
-      if (hm.has_value()) {
-        need_f32(*hm, "hmask");
-        TORCH_CHECK(hm->is_contiguous() && hm->numel() == M * N, "hmask [M,N]");
-        d.hmask = hm->data_ptr<float>();
-      }
-      d.mscale = L[3].cast<float>();
-    }
+    need_2d(dz, "dz");
+    TORCH_CHECK(dz.size(0) == M && dz.size(1) == N, "dz [M,N]");
+    d.dz = dz.data_ptr<float>();
+    d.ldz = (int)dz.stride(0);
     d.A = A.data_ptr<float>();
     d.lda = (int)A.stride(0);
     d.W = W.data_ptr<float>();
@@ -759,30 +662,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("relu_mask", &relu_mask);
   m.def("server_head3", &server_head3);
   m.def("head3_slices", [](int64_t n2) { return (int64_t)sl::head3_slices((int)n2); });
-  m.def("server_fc2_head", &server_fc2_head);
-  m.def("fc2_head_tiles", [](int64_t n2) { return (int64_t)sl::fc2_head_tiles((int)n2); });
   m.def("linear_fwd_partial", &linear_fwd_partial);
-  m.def("lookahead_fc2_fwd", &lookahead_fc2_fwd);
-  m.def("lookahead_fc2_slices", [](int64_t N1) { return (int64_t)sl::lookahead_fc2_slices((int)N1); });
-  m.def("linear_dgrad_partial", &linear_dgrad_partial);
   m.def("wgrad_group", &wgrad_group);
-  // Kernel-variant slots (0 = the measured default everywhere), for A/B scripts and tests:
-  //   1 look-ahead LDS layout (1 plain, 2 XOR)     2 wgrad grid (1 2-D, 2 1-D)
-  //   3 wgrad dW form (1 all-MFMA)                 4 wgrad stores (1 plain, not write-through)
-  //   5 dgrad split cap                            6 client local step (1 8-lane per-step launches)
-  //   7 wgrad tile walk (1 forward, 2 reversed)    8 dgrad form (2 full-N)
-  //   10 tiled GEMM tile form                      11 fp32 M > 128 product (1 in-tree GEMM)
-  //   12 single-shard fc2 + head (2 fused)         13 executor launch-skip probe (timing only)
-  //   14 skinny forward (2 k-loop form; 3 / 4: 4 / 16 waves per workgroup)
-  //   15 U-shape head step (1 per-thread FMA form)
-  //   16 TP server step: 1 = separate peer-mapped all-reduce launch instead of the one fused
-  //      into head_fwd
-  //   18 single-shard look-ahead step: 1 = fc1's epilogue inside fc2's split-K forward
-  //   19 fc2 forward / dgrad: 2 = plain tile order (default: XCD-grouped, W2 rows stay in one
-  //      XCD's L2 from the forward to the dgrad)
-  //   20 server head: 2 = grid (M, Q) with proportional column slices (default: grid (Q, M),
-  //      128-column slices on the fc2 forward's XCD groups)
-  // The measurements behind each default are in the comment at the slot's use and docs/PERF.md.
+  // Kernel-variant slots for A/B runs of work in progress (0 = the default everywhere).  A
+  // slot lives only while its alternative is being measured; the losers are removed with the
+  // numbers kept in docs/PERF.md.  In use:
+  //   11 fp32 products of M > 128 rows: 1 = the in-tree tiled GEMM instead of hipBLASLt
+  //   21 server head: 1 = head_fwd + head_bwd launches instead of the one-launch fused head
   m.def("set_variant", [](int64_t slot, int64_t v) {
     TORCH_CHECK(slot >= 0 && slot < 24, "variant slot");
     sl::g_variant[slot] = (int)v;

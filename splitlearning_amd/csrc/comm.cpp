@@ -38,7 +38,7 @@ TpComm::~TpComm() {
 }
 
 void TpComm::allreduce_sum_f32(float* p, size_t n, hipStream_t st) {
-  if (ipc_ != nullptr && (int64_t)n <= ipc_->cap() && n % 4 == 0) {
+  if (ipc_ != nullptr && ipc_->serves(p, n)) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     // a captured launch would freeze the flag generation into the graph: RCCL there
     if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
@@ -138,7 +138,10 @@ void sl_register_comm(py::module& m) {
         a.allreduce_sum_f32(t.data_ptr<float>(), (size_t)t.numel(), stream());
       })
       .def("error", &sl::IpcAllReduce::error)
+      .def("host_error", &sl::IpcAllReduce::host_error)
+      .def("set_fences", &sl::IpcAllReduce::set_fences)
       .def("set_timeout_s", &sl::IpcAllReduce::set_timeout_s)
+      .def_property_readonly("timeout_s", &sl::IpcAllReduce::timeout_s)
       .def_property_readonly("cap", &sl::IpcAllReduce::cap)
       .def_property_readonly("rank", &sl::IpcAllReduce::rank)
       .def_property_readonly("size", &sl::IpcAllReduce::size);

@@ -440,21 +440,12 @@ hipError_t conv_local_step(const void* x, bool x_u8, const int64_t* idx, const i
                            SlOpt o, hipStream_t st) {
   if (B <= 0) return hipSuccess;
   const float scale = 1.f / (float)B;
-  if (g_variant[6] == 1) {   // 8 lanes per channel (256 threads): A/B reference
-    if (x_u8)
-      conv_fwd_ce_wgrad_kernel<uint8_t, 8, false><<<B, 256, 0, st>>>((const uint8_t*)x, idx, labels, w, b, scale, slab,
-                                                              loss_rows);
-    else
-      conv_fwd_ce_wgrad_kernel<float, 8, false><<<B, 256, 0, st>>>((const float*)x, idx, labels, w, b, scale, slab,
-                                                            loss_rows);
-  } else {
-    if (x_u8)
-      conv_fwd_ce_wgrad_kernel<uint8_t, 32, false><<<B, 1024, 0, st>>>((const uint8_t*)x, idx, labels, w, b, scale, slab,
-                                                                loss_rows);
-    else
-      conv_fwd_ce_wgrad_kernel<float, 32, false><<<B, 1024, 0, st>>>((const float*)x, idx, labels, w, b, scale, slab,
-                                                              loss_rows);
-  }
+  if (x_u8)
+    conv_fwd_ce_wgrad_kernel<uint8_t, 32, false><<<B, 1024, 0, st>>>((const uint8_t*)x, idx, labels, w, b, scale, slab,
+                                                                      loss_rows);
+  else
+    conv_fwd_ce_wgrad_kernel<float, 32, false><<<B, 1024, 0, st>>>((const float*)x, idx, labels, w, b, scale, slab,
+                                                                    loss_rows);
   conv_opt_reduce_kernel<<<1, 320, 0, st>>>(slab, B, w, b, s0w, s1w, s0b, s1b, o);
   return hipGetLastError();
 }

@@ -40,9 +40,6 @@ hipError_t linear_epilogue(const float* P, int ldp, float* Y, int ldy, int M, in
                            hipStream_t st);
 hipError_t linear_fwd_partial(const float* X, int ldx, const float* W, int ldw, int M, int N, int K, float* ws,
                               int64_t ws_elems, int max_split, int* S_out, hipStream_t st);
-int lookahead_fc2_slices(int N1);
-hipError_t lookahead_fc2_fwd(const float* pn, int S1, int64_t slab1, Epi e1, float* h1, const float* W2, float* P2,
-                             int64_t p2_elems, int M, int N1, int N2, int* S2_out, hipStream_t st);
 }  // namespace sl
 
 namespace py = pybind11;
@@ -111,6 +108,10 @@ class ServerEpoch {
     emulate_ = cfg.contains("emulate_tp") && cfg["emulate_tp"].cast<bool>();
     TORCH_CHECK(!row2_ || comm_ != nullptr || ipc_ != nullptr || emulate_,
                 "a row-parallel fc2 needs the native communicator");
+    // grouped cross-entropy (SISA-concat's k heads, protocols/concat.py): labels [n, G], per-
+    // (row, group) loss scales [n, G] passed to run(), losses [n, G]
+    G_ = cfg.contains("groups") ? cfg["groups"].cast<int>() : 1;
+    TORCH_CHECK(G_ >= 1 && L_[2].N % G_ == 0, "fc3 width % groups");
     B_ = cfg["B"].cast<int>();
     TORCH_CHECK(B_ >= 1 && B_ <= 64, "batch 1..64 (look-ahead row chunks of the wgrad kernel)");
     pn_ = get(cfg, "pn");
@@ -128,21 +129,33 @@ class ServerEpoch {
     TORCH_CHECK(h1_.numel() >= (int64_t)B_ * L_[0].N && dz1_.numel() >= (int64_t)B_ * L_[0].N, "h1 / dz1");
     TORCH_CHECK(h2_.numel() >= (int64_t)B_ * L_[1].N && dz2_.numel() >= (int64_t)B_ * L_[1].N, "h2 / dz2");
     TORCH_CHECK(dlog_.numel() >= (int64_t)B_ * L_[2].N, "dlog");
-    TORCH_CHECK(p2ws_.numel() >= (int64_t)std::max(16, sl::lookahead_fc2_slices(L_[0].N)) * B_ * L_[1].N,
-                "fc2 slab workspace");
-    TORCH_CHECK(headws_.numel() >= (int64_t)std::max(sl::head3_slices(L_[1].N), sl::fc2_head_tiles(L_[1].N)) * B_ *
-                                        L_[2].N,
-                "head workspace");
+    TORCH_CHECK(p2ws_.numel() >= (int64_t)16 * B_ * L_[1].N, "fc2 slab workspace");
+    TORCH_CHECK(headws_.numel() >= (int64_t)sl::head3_slices(L_[1].N) * B_ * L_[2].N, "head workspace");
   }
 
   // One epoch over acts [n, K1] / labels [n] in batches of B.  `pre`: fc1's product for the
   // first batch is pending in pn (look-ahead prologue / previous step).  Returns the
   // updated (fwd_count, t, pre).
   py::tuple run(const at::Tensor& acts, const at::Tensor& labels, at::Tensor& loss_rows, int64_t seed_base,
-                int64_t fwd_count, int64_t t, bool pre, bool lookahead) {
+                int64_t fwd_count, int64_t t, bool pre, bool lookahead, const c10::optional<at::Tensor>& gscale) {
+    TORCH_CHECK(!emulate_, "an emulate_tp shard executor is driven by tp_emulate_epoch, not run()");
     check_batch(acts, labels, loss_rows);
+    gscale_ = nullptr;
+    if (G_ > 1) {
+      TORCH_CHECK(gscale.has_value() && gscale->is_cuda() && gscale->scalar_type() == at::kFloat &&
+                      gscale->is_contiguous() && gscale->numel() == acts.size(0) * G_,
+                  "grouped CE: gscale f32 [n, groups]");
+      gscale_ = gscale->data_ptr<float>();
+    }
     const int64_t n = acts.size(0);
-    for (int64_t s = 0; s < n; s += B_) {
+    const sl::IpcAllReduce* ipc = row2_ ? ipc_obj() : nullptr;
+    for (int64_t s = 0, i = 0; s < n; s += B_, ++i) {
+      // a peer-mapped wait that timed out (stalled / dead peer) raises the error word and
+      // every later wait gives up at once; its host-pinned mirror is read here without a
+      // device sync, so the epoch aborts within one timeout plus <= 64 queued steps
+      if (ipc != nullptr && (i & 63) == 63 && ipc->host_error() != 0)
+        TORCH_CHECK(false, "peer-mapped TP all-reduce: a flag wait timed out on this rank (a peer stalled or "
+                           "died); aborting the server epoch at step ", i);
       Step st = begin(acts, labels, s, seed_base, fwd_count, t, pre, lookahead);
       forward_product(st);
       if (row2_ && !ipc_head(st.M)) allreduce(p2ws_.data_ptr<float>(), (size_t)st.M * L_[1].N);
@@ -171,9 +184,11 @@ class ServerEpoch {
                     acts.size(1) == L_[0].K,
                 "acts [n, K1] contiguous f32");
     const int64_t n = acts.size(0);
-    TORCH_CHECK(labels.is_cuda() && labels.scalar_type() == at::kLong && labels.is_contiguous() && labels.numel() == n,
-                "labels int64 [n]");
-    TORCH_CHECK(loss_rows.is_cuda() && loss_rows.scalar_type() == at::kFloat && loss_rows.numel() >= n, "loss [n]");
+    TORCH_CHECK(labels.is_cuda() && labels.scalar_type() == at::kLong && labels.is_contiguous() &&
+                    labels.numel() == n * G_,
+                "labels int64 [n, groups]");
+    TORCH_CHECK(loss_rows.is_cuda() && loss_rows.scalar_type() == at::kFloat && loss_rows.numel() >= n * G_,
+                "loss [n, groups]");
   }
 
   Step begin(const at::Tensor& acts, const at::Tensor& labels, int64_t s, int64_t seed_base, int64_t fwd_count,
@@ -204,15 +219,7 @@ class ServerEpoch {
     float* h1 = h1_.data_ptr<float>();
     float* P2 = p2ws_.data_ptr<float>();
     const Epi e1 = sl::make_epi_raw(L_[0].b.data_ptr<float>(), true, p1_, st.sd0, col_off1_, nullptr);
-    if (lookahead_fc2(st)) {
-      // variant 18 = 1: the look-ahead epilogue inside fc2's split-K forward (one launch)
-      ck(sl::lookahead_fc2_fwd(pn_.data_ptr<float>(), (int)S1, (int64_t)M * N1, e1, h1, L_[1].W.data_ptr<float>(),
-                               P2, p2ws_.numel(), M, N1, N2, &S2_, sm),
-         "fc1 epilogue + fc2 forward");
-      return;
-    }
-    if (skip(1)) {
-    } else if (st.pre)
+    if (st.pre)
       ck(sl::linear_epilogue(pn_.data_ptr<float>(), N1, h1, N1, M, N1, e1, (int)S1, (int64_t)M * N1, sm),
          "fc1 epilogue");
     else
@@ -220,32 +227,22 @@ class ServerEpoch {
                         fwdws_.numel(), sm),
          "fc1 forward");
     S2_ = 1;
-    if (fuse_head()) return;              // fc2's product is formed by the fused head (finish)
-    if (skip(2)) {
-      S2_ = row2_ ? 1 : S2_probe_;
-    } else if (row2_) {
-      if (ipc_head(M) || emulate_) {
-        // the fused head sums this rank's split-K slabs before its push (no epilogue launch,
-        // and a split product at every shard width); the single-process emulation follows
-        // the same decomposition (tp_emulate_epoch sums each shard's slabs, then the shards)
-        ck(sl::linear_fwd_partial(h1, N1, L_[1].W.data_ptr<float>(), N1, M, N2, N1, P2, p2ws_.numel(), 16, &S2_, sm),
-           "fc2 forward");
-      } else if (N1 <= 1280) {
-        ck(sl::linear_fwd_partial(h1, N1, L_[1].W.data_ptr<float>(), N1, M, N2, N1, P2, p2ws_.numel(), 1, &S2_, sm),
-           "fc2 forward");
-      } else {
-        Epi plain{};
-        plain.dscale = 1.f;
-        ck(sl::linear_fwd(h1, N1, L_[1].W.data_ptr<float>(), N1, P2, N2, M, N2, N1, plain, fwdws_.data_ptr<float>(),
-                          fwdws_.numel(), sm),
-           "fc2 forward");
-        S2_ = 1;
-      }
-    } else {
-      ck(sl::linear_fwd_partial(h1, N1, L_[1].W.data_ptr<float>(), N1, M, N2, N1, P2, p2ws_.numel(), 16, &S2_, sm),
+    if (row2_ && !(ipc_head(M) || emulate_) && N1 > 1280) {
+      // row-parallel fc2 all-reduced by RCCL on a wide shard: one plain product
+      Epi plain{};
+      plain.dscale = 1.f;
+      ck(sl::linear_fwd(h1, N1, L_[1].W.data_ptr<float>(), N1, P2, N2, M, N2, N1, plain, fwdws_.data_ptr<float>(),
+                        fwdws_.numel(), sm),
          "fc2 forward");
-      S2_probe_ = S2_;
+      return;
     }
+    // split-K slabs, reduced by the head (single shard, the fused peer-mapped all-reduce, or the
+    // single-process emulation, which sums each shard's slabs then the shards), or one unsplit
+    // partial on a narrow RCCL-reduced shard (nothing to reduce before the collective)
+    const int max_split = (row2_ && !(ipc_head(M) || emulate_)) ? 1 : 16;
+    ck(sl::linear_fwd_partial(h1, N1, L_[1].W.data_ptr<float>(), N1, M, N2, N1, P2, p2ws_.numel(), max_split, &S2_,
+                              sm),
+       "fc2 forward");
   }
 
   // head (h2, dlogits, dz2, loss), fc1's dZ, and the grouped wgrad + optimizer step with the
@@ -264,32 +261,23 @@ class ServerEpoch {
     float* dlog = dlog_.data_ptr<float>();
     const double s1 = p1_ > 0 ? 1.0 / (1.0 - p1_) : 1.0;
     const Epi e2 = sl::make_epi_raw(L_[1].b.data_ptr<float>(), true, p2_, st.sd1, 0, nullptr);
-    if (skip(4)) {
-    } else if (fuse_head())
-      ck(sl::server_fc2_head(h1, N1, L_[1].W.data_ptr<float>(), N1, e2, L_[2].W.data_ptr<float>(), N2,
-                             L_[2].b.data_ptr<float>(), st.labels->data_ptr<int64_t>() + st.s, -100, (float)(1.0 / M),
-                             h2, dlog, dz2, loss_rows.data_ptr<float>() + st.s, headws_.data_ptr<float>(),
-                             headws_.numel(), M, N1, N2, C, sm),
-         "server fc2 + head");
-    else {
-      // tensor-parallel fc2 with a peer-mapped all-reduce: head_fwd performs it (run() issued
-      // no separate all-reduce for this step)
-      sl::IpcStep step;
-      const sl::IpcStep* ip = nullptr;
-      if (row2_ && ipc_head(M)) {
-        step = ipc_obj()->begin_step();
-        ip = &step;
-      }
-      ck(sl::server_head3(p2ws_.data_ptr<float>(), S2_, (int64_t)M * N2, e2, L_[2].W.data_ptr<float>(), N2,
-                          L_[2].b.data_ptr<float>(), st.labels->data_ptr<int64_t>() + st.s, -100, (float)(1.0 / M),
-                          h2, dlog, dz2, loss_rows.data_ptr<float>() + st.s, headws_.data_ptr<float>(),
-                          headws_.numel(), M, N2, C, sm, ip),
-         "server head");
+    // tensor-parallel fc2 with a peer-mapped all-reduce: head_fwd performs it (run() issued
+    // no separate all-reduce for this step)
+    sl::IpcStep step;
+    const sl::IpcStep* ip = nullptr;
+    if (row2_ && ipc_head(M)) {
+      step = ipc_obj()->begin_step();
+      ip = &step;
     }
-    if (!skip(8))
-      ck(sl::linear_dgrad(dz2, N2, L_[1].W.data_ptr<float>(), N1, h1, N1, (float)s1, dz1, N1, dgws_.data_ptr<float>(),
-                          dgws_.numel(), M, N2, N1, sm),
-         "fc2 dgrad");
+    ck(sl::server_head3(p2ws_.data_ptr<float>(), S2_, (int64_t)M * N2, e2, L_[2].W.data_ptr<float>(), N2,
+                        L_[2].b.data_ptr<float>(), st.labels->data_ptr<int64_t>() + st.s * G_, -100,
+                        G_ > 1 ? 1.f : (float)(1.0 / M), h2, dlog, dz2, loss_rows.data_ptr<float>() + st.s * G_,
+                        headws_.data_ptr<float>(), headws_.numel(), M, N2, C, sm, ip, G_,
+                        gscale_ != nullptr ? gscale_ + st.s * G_ : nullptr),
+       "server head");
+    ck(sl::linear_dgrad(dz2, N2, L_[1].W.data_ptr<float>(), N1, h1, N1, (float)s1, dz1, N1, dgws_.data_ptr<float>(),
+                        dgws_.numel(), M, N2, N1, sm),
+       "fc2 dgrad");
     ++st.t;
     sl::WgGroup g{};
     g.n = 3;
@@ -321,18 +309,18 @@ class ServerEpoch {
       g.pn = pn_.data_ptr<float>();
     }
     const SlOpt o = sl::make_opt_raw(kind_, lr_, beta1_, beta2_, eps_, wd_, mom_, st.t, nullptr);
-    if (!skip(16)) ck(sl::wgrad_group(g, M, o, sm), "wgrad_group");
+    ck(sl::wgrad_group(g, M, o, sm), "wgrad_group");
     st.next_pre = next_full;
   }
 
   // the peer-mapped all-reduce in use for this executor (attached to the RCCL communicator
   // or given bare), or null
   sl::IpcAllReduce* ipc_obj() const { return comm_ != nullptr ? comm_->ipc() : ipc_; }
-  // whether step rows M run the all-reduce inside head_fwd (variant 16 = 1: the separate
-  // all-reduce kernel; a stream being captured: RCCL, see TpComm::allreduce_sum_f32)
+  // whether step rows M run the all-reduce inside head_fwd (a stream being captured: RCCL, see
+  // TpComm::allreduce_sum_f32; a message the peer-mapped region cannot hold: the separate path)
   bool ipc_head(int M) const {
     const sl::IpcAllReduce* a = ipc_obj();
-    if (a == nullptr || sl::g_variant[16] == 1 || skip(2) || skip(4)) return false;
+    if (a == nullptr) return false;
     if ((int64_t)M * L_[1].N > a->cap() || (int64_t)M * sl::head3_slices(L_[1].N) > sl::kIpcFlags) return false;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     return hipStreamIsCapturing(stream(), &cs) == hipSuccess && cs == hipStreamCaptureStatusNone;
@@ -341,8 +329,10 @@ class ServerEpoch {
   void allreduce(float* p, size_t n) {
     if (comm_ != nullptr)
       comm_->allreduce_sum_f32(p, n, stream());   // the attached peer-mapped path or RCCL
-    else
+    else if (ipc_ != nullptr)
       ipc_->allreduce_sum_f32(p, n, stream());
+    else
+      TORCH_CHECK(false, "ServerEpoch: a row-parallel fc2 without a communicator");
   }
 
   at::Tensor product_view(int M) const { return p2ws_.narrow(0, 0, (int64_t)M * L_[1].N); }
@@ -358,21 +348,7 @@ class ServerEpoch {
     product_view(M).copy_(sum);
     S2_ = 1;
   }
-  // single-shard tail, variant 12 = 2: fc2's forward fused into the head (fused.hip
-  // fc2_head_fwd_kernel).  Measured slower (native executor, TP = 1: 250.9 vs 178.4 us per
-  // step; profiles/r2_fused_head_ab.txt): 125 workgroups that each reduce the whole K = 5000
-  // re-read all of h1 (320 KB) per 8 output columns and run 6 dependent load rounds per wave;
-  // the 1008-workgroup split-K forward + head_fwd pair stays the default.
-  bool fuse_head() const { return !row2_ && sl::g_variant[12] == 2; }
-  bool lookahead_fc2(const Step& st) const {
-    return st.pre && !row2_ && !fuse_head() && sl::g_variant[18] >= 1 && !skip(1) && !skip(2);
-  }
   bool row_parallel() const { return row2_; }
-  // Timing probe (variant 13, a bit mask; never set outside scripts/native_ab.py): skip
-  // launches to price each one in the real stream and cache state — 1 fc1 epilogue, 2 fc2
-  // forward, 4 head, 8 fc2 dgrad (+ reduce), 16 wgrad_group.  The numerics of a probed epoch
-  // are meaningless.
-  static bool skip(int bit) { return (sl::g_variant[13] & bit) != 0; }
   int batch() const { return B_; }
 
  private:
@@ -385,7 +361,9 @@ class ServerEpoch {
   sl::IpcAllReduce* ipc_ = nullptr;
   int B_ = 16;
   bool emulate_ = false;
-  int S2_ = 1, S2_probe_ = 1;
+  int S2_ = 1;
+  int G_ = 1;
+  const float* gscale_ = nullptr;
   at::Tensor pn_, p2ws_, fwdws_, dgws_, headws_, h1_, h2_, dz1_, dz2_, dlog_;
   static hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
 };
@@ -437,5 +415,6 @@ void sl_register_engine(py::module& m) {
   py::class_<ServerEpoch>(m, "ServerEpoch")
       .def(py::init<const py::dict&>())
       .def("run", &ServerEpoch::run, py::arg("acts"), py::arg("labels"), py::arg("loss_rows"), py::arg("seed_base"),
-           py::arg("fwd_count"), py::arg("t"), py::arg("pre"), py::arg("lookahead"));
+           py::arg("fwd_count"), py::arg("t"), py::arg("pre"), py::arg("lookahead"),
+           py::arg("gscale") = py::none());
 }

@@ -6,13 +6,8 @@
 namespace sl {
 
 struct WgDesc {
-  const float* dz;      // [M, N] (ld ldz), or nullptr when given as partial slabs:
+  const float* dz;      // [M, N] output gradient (ld ldz)
   int ldz;
-  const float* dzp;     // [S][M][N] split-N partial sums of dZ (before the mask)
-  int S;
-  int64_t slab;
-  const float* hmask;   // [M, N] post-activation of this layer: dz *= mscale * [hmask > 0]
-  float mscale;
   const float* A;       // [M, K] layer input
   int lda;
   float* W;
@@ -23,8 +18,8 @@ struct WgDesc {
   float* sb0;
   float* sb1;
   int N, K;
-  int yb0;              // first blockIdx.y of this layer (2-D grid: all-MFMA variant)
-  int wb0;              // first block of this layer (1-D grid: default kernel)
+  int yb0;              // first blockIdx.y of this layer (2-D grid)
+  int wb0;              // first block of this layer (1-D grid)
 };
 struct WgGroup {
   WgDesc d[3];
@@ -40,23 +35,19 @@ struct WgGroup {
   int nt0;              // layer 0's tile count (set by wgrad_group)
   int grid2d;           // 2-D grid (set by wgrad_group: when few of its workgroups are empty)
   int wt;               // write-through (sc1) W/m/v stores (set by wgrad_group)
-  int swz;              // look-ahead LDS tile layout: 0 padded, 1 plain, 2 XOR (set by wgrad_group)
   int bf16;             // bf16 compute: dZ / A / look-ahead operands rounded to bf16 (set by wgrad_group)
 };
 
 int head3_slices(int N2);
-// ipc (tensor-parallel fc2): P2 is this rank's unreduced [M, N2] partial; head_fwd pushes its
-// slice to every rank, waits for the T slices and sums them in rank order (the fc2 all-reduce
-// fused into the slab reduction: ipc_ar.h)
+// One launch (head_fused_kernel; variant 21 = 1: the head_fwd + head_bwd pair).  ipc
+// (tensor-parallel fc2): P2 is this rank's unreduced [M, N2] partial; the head pushes its slice
+// to every rank, waits for the T slices and sums them in rank order (the fc2 all-reduce fused
+// into the slab reduction: ipc_ar.h).  G > 1: the C logits are G cross-entropy groups (labels
+// y [M, G], per-(row, group) scales gscale [M, G] or `scale`, losses loss_rows [M, G]).
 hipError_t server_head3(const float* P2, int S2, int64_t slab2, Epi e2, const float* W3, int ldw3, const float* b3,
                         const int64_t* y, int64_t ignore, float scale, float* h2, float* dlog, float* dz2,
                         float* loss_rows, float* ws, int64_t ws_elems, int M, int N2, int C, hipStream_t st,
-                        const IpcStep* ipc = nullptr);
+                        const IpcStep* ipc = nullptr, int G = 1, const float* gscale = nullptr);
 hipError_t wgrad_group(const WgGroup& g, int M, SlOpt o, hipStream_t st);
-int fc2_head_tiles(int N2);
-hipError_t server_fc2_head(const float* X, int ldx, const float* W2, int ldw2, Epi e2, const float* W3, int ldw3,
-                           const float* b3, const int64_t* y, int64_t ignore, float scale, float* h2, float* dlog,
-                           float* dz2, float* loss_rows, float* ws, int64_t ws_elems, int M, int K, int N2, int C,
-                           hipStream_t st);
 
 }  // namespace sl

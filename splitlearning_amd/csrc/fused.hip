@@ -17,10 +17,9 @@
 //                400 KB fast enough, W3 has to be spread over many CUs.)
 //
 //  wgrad_group_kernel   the fused wgrad+optimizer (v3 layout) for up to 3 layers in one
-//                launch, plus (FWDN) fc1's look-ahead forward for the next batch.  A layer's
-//                dZ may also be given as un-reduced split-N slabs plus a ReLU/dropout mask
-//                (PART), reduced while staging into LDS; measured slower than a separate
-//                reduce launch at fc1's size, so the server step passes a plain dZ.
+//                launch, plus (FWDN) fc1's look-ahead forward for the next batch.  (dZ given
+//                as un-reduced split-N slabs, reduced while staging, measured slower than a
+//                separate reduce launch at fc1's size: removed, docs/PERF.md.)
 //
 // The look-ahead SISA step is 7 launches: slab epilogue (h1), fc2 forward (split-K),
 // head_fwd, head_bwd, fc2 dgrad (split-N) + reduce, wgrad_group.
@@ -33,32 +32,21 @@ namespace sl {
 // Column slices of <= 32 float4 (128 columns) per workgroup; grid (M, Q) for both kernels.
 constexpr int HS = 32;
 
-// Head workgroup layout (hl = 0, the default): grid (Q, M), slice q = float4 columns
-// [32 q, 32 q + 32), so with Q = 8 dispatch slot L = q + 8 m runs on XCD q and slice q is
-// exactly the 128 fc2 outputs whose W2 rows the XCD-grouped fc2 forward / dgrad keep on XCD q
-// (csrc/linear.hip): the forward's slabs, h2 and dz2 of a slice stay in one XCD's L2 from the
-// forward through head_fwd and head_bwd to the dgrad.  hl = 1 (variant 20 = 2): the earlier
-// grid (M, Q) with proportional slices.
-__device__ __forceinline__ void head_wg(int hl, int& m, int& q, int& Q) {
-  if (hl == 0) {
-    q = blockIdx.x;
-    m = blockIdx.y;
-    Q = gridDim.x;
-  } else {
-    m = blockIdx.x;
-    q = blockIdx.y;
-    Q = gridDim.y;
-  }
+// Head workgroup layout: grid (Q, M), slice q = float4 columns [32 q, 32 q + 32), so with
+// Q = 8 dispatch slot L = q + 8 m runs on XCD q and slice q is exactly the 128 fc2 outputs
+// whose W2 rows the XCD-grouped fc2 forward / dgrad keep on XCD q (csrc/linear.hip): the
+// forward's slabs, h2 and dz2 of a slice stay in one XCD's L2 from the forward through
+// head_fwd and head_bwd to the dgrad (L2 hit rate of the head kernels 66 -> 88 % against the
+// earlier grid (M, Q) with proportional slices, profiles/r2_pmc_xcd_l2_hits.txt).
+__device__ __forceinline__ void head_wg(int& m, int& q, int& Q) {
+  q = blockIdx.x;
+  m = blockIdx.y;
+  Q = gridDim.x;
 }
 
-__device__ __forceinline__ void head_slice(int n4, int Q, int q, int& a, int& b, int hl) {
-  if (hl == 0) {
-    a = min(n4, HS * q);
-    b = min(n4, HS * q + HS);
-  } else {
-    a = (int)(((int64_t)n4 * q) / Q);
-    b = (int)(((int64_t)n4 * (q + 1)) / Q);
-  }
+__device__ __forceinline__ void head_slice(int n4, int q, int& a, int& b) {
+  a = min(n4, HS * q);
+  b = min(n4, HS * q + HS);
 }
 
 // head_fwd_kernel: workgroup (m, q) reduces fc2's split-K slabs for its column slice of row
@@ -78,15 +66,14 @@ __device__ __forceinline__ void head_slice(int n4, int Q, int q, int& a, int& b,
 template <bool BF, bool IPC>
 __global__ void __launch_bounds__(256)
 head_fwd_kernel(const float* __restrict__ P2, int S2, int64_t slab2, Epi e2, const float* __restrict__ W3,
-                int ldw3, float* __restrict__ h2, float* __restrict__ plog, int M, int N2, int C, IpcStep ip,
-                int hl) {
+                int ldw3, float* __restrict__ h2, float* __restrict__ plog, int M, int N2, int C, IpcStep ip) {
   __shared__ f32x4 part[8][HS];
   __shared__ f32x4 hs[HS];
   int m, q, Q;
-  head_wg(hl, m, q, Q);
+  head_wg(m, q, Q);
   const int tid = threadIdx.x;
   int qa, qb;
-  head_slice(N2 >> 2, Q, q, qa, qb, hl);
+  head_slice(N2 >> 2, q, qa, qb);
   const int ncol = qb - qa;
   const int lane = tid & 63, wv = tid >> 6, half = lane >> 5, c = lane & 31;
   constexpr int JU = 13;
@@ -103,6 +90,7 @@ head_fwd_kernel(const float* __restrict__ P2, int S2, int64_t slab2, Epi e2, con
   };
   load_w(0);
   if constexpr (IPC) {
+    __shared__ int s_ok;
     if (wv == 0) {
       if (lane < ncol) {
         // this rank's split-K slabs (S2 >= 1) summed in slab order: the plain product the
@@ -110,15 +98,19 @@ head_fwd_kernel(const float* __restrict__ P2, int S2, int64_t slab2, Epi e2, con
         const f32x4* src = reinterpret_cast<const f32x4*>(P2 + (int64_t)m * N2) + qa + lane;
         f32x4 v = {0.f, 0.f, 0.f, 0.f};
         for (int s = 0; s < S2; ++s) v += src[s * (slab2 >> 2)];
-        const int64_t slot = ((int64_t)ip.par * ip.T + ip.me) * ip.cap + (int64_t)m * N2;
-        for (int r = 0; r < ip.T; ++r) ipc_st4(ip.P.data[r] + slot + 4 * (qa + lane), make_float4(v[0], v[1], v[2], v[3]));
+        const int64_t slot = ((int64_t)ip.par * ip.T + ip.me) * ip.cap + (int64_t)m * N2 + 4 * (qa + lane);
+        for (int r = 0; r < ip.T; ++r) ipc_st4(ipc_rsrc(ip.P.data[r]), slot, make_float4(v[0], v[1], v[2], v[3]));
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const int fi = m * Q + q;
-      if (lane < ip.T) ipc_raise_flag(ip.P.flags[lane] + ((int64_t)ip.par * ip.T + ip.me) * ip.nflags + fi, ip.gen);
-      ipc_wait_flags(ip, lane, fi);
+      if (lane < ip.T) ipc_raise_flag(ip.P.flags[lane] + ((int64_t)ip.par * ip.T + ip.me) * ip.nflags + fi, ip.gen, ip.fences);
+      const bool ok = ipc_wait_flags(ip, lane, fi);
+      if (lane == 0) s_ok = ok ? 1 : 0;
     }
     __syncthreads();
+    // a wait gave up (stalled / dead peer, error word raised): nothing sound to compute; the
+    // job aborts on the error word (ServerEpoch::run polls its host mirror)
+    if (!s_ok) return;
     P2 = ip.P.data[ip.me] + (int64_t)ip.par * ip.T * ip.cap;
     S2 = ip.T;
     slab2 = ip.cap;
@@ -131,8 +123,10 @@ head_fwd_kernel(const float* __restrict__ P2, int S2, int64_t slab2, Epi e2, con
       const f32x4* src = reinterpret_cast<const f32x4*>(P2 + (int64_t)m * N2) + qa + cc;
       if constexpr (IPC) {
         // the T slots of the peer-mapped region (S2 = T <= 8: one per slab group)
+        const __amdgpu_buffer_rsrc_t rs = ipc_rsrc(ip.P.data[ip.me]);
+        const int64_t o0 = (int64_t)ip.par * ip.T * ip.cap + (int64_t)m * N2 + 4 * (qa + cc);
         for (int s = sg; s < S2; s += 8) {
-          const float4 u = ipc_ld4(reinterpret_cast<const float*>(src + s * (slab2 >> 2)));
+          const float4 u = ipc_ld4(rs, o0 + (int64_t)s * slab2);
           v += f32x4{u.x, u.y, u.z, u.w};
         }
       } else {
@@ -176,105 +170,6 @@ head_fwd_kernel(const float* __restrict__ P2, int S2, int64_t slab2, Epi e2, con
   }
 }
 
-// fc2_head_fwd_kernel (single-shard tail, fc2 not row-parallel): fc2's forward WITHOUT
-// split-K — a workgroup owns NT = 8 output columns and reduces the whole K inside itself (16
-// waves x 1/16 of K, exact-fp32 MFMA, LDS sum) — so it can apply fc2's bias / ReLU /
-// dropout (-> h2) and form its columns' share of the fc3 logits (plog[tile][m][c]) itself.
-// Replaces the split-K fc2 forward + head_fwd pair (two launches and a slab round trip).
-// grid (ceil(N/8), ceil(M/16)), 1024 threads.  bf: bf16 compute (operands rounded).
-template <int NT>
-__global__ void __launch_bounds__(1024)
-fc2_head_fwd_kernel(const float* __restrict__ X, int ldx, const float* __restrict__ W, int ldw, Epi e,
-                    const float* __restrict__ W3, int ldw3, float* __restrict__ h2, float* __restrict__ plog, int M,
-                    int N, int K, int C, int bf) {
-  __shared__ f32x4 red[16][64];
-  __shared__ float sh[16][NT];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, tid = threadIdx.x;
-  const int n0 = blockIdx.x * NT, m0 = blockIdx.y * 16, tile = blockIdx.x;
-  const int li = lane & 15, q = lane >> 4;
-  const bool va = m0 + li < M, vb = li < NT && n0 + li < N;
-  const float* pa = X + (int64_t)(va ? m0 + li : 0) * ldx;
-  const float* pb = W + (int64_t)(vb ? n0 + li : 0) * ldw;
-  const int kper = ((K + 16 * 16 - 1) / (16 * 16)) * 16;
-  const int kb = wv * kper, ke = min(K, kb + kper);
-  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  constexpr int U = 8;
-  int k = kb;
-  for (; k + 16 * U <= ke; k += 16 * U) {
-    float4 a[U], w[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int kk = k + 16 * u + 4 * q;
-      a[u] = va ? *reinterpret_cast<const float4*>(pa + kk) : z4;
-      w[u] = vb ? *reinterpret_cast<const float4*>(pb + kk) : z4;
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (bf) {
-        a[u] = bfr4(a[u]);
-        w[u] = bfr4(w[u]);
-      }
-      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u].x, w[u].x, acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u].y, w[u].y, acc1, 0, 0, 0);
-      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u].z, w[u].z, acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u].w, w[u].w, acc1, 0, 0, 0);
-    }
-  }
-  for (; k < ke; k += 16) {
-    const int kk = k + 4 * q;
-    const bool in = kk < ke;
-    float4 a = (va && in) ? *reinterpret_cast<const float4*>(pa + kk) : z4;
-    float4 w = (vb && in) ? *reinterpret_cast<const float4*>(pb + kk) : z4;
-    if (bf) {
-      a = bfr4(a);
-      w = bfr4(w);
-    }
-    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, w.x, acc0, 0, 0, 0);
-    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, w.y, acc1, 0, 0, 0);
-    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, w.z, acc0, 0, 0, 0);
-    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, w.w, acc1, 0, 0, 0);
-  }
-  red[wv][lane] = acc0 + acc1;
-  __syncthreads();
-  // lane (li = column, q): rows 4q + r.  Waves are summed in order 0..15 (deterministic).
-  if (wv == 0) {
-    f32x4 sum = red[0][lane];
-#pragma unroll
-    for (int i = 1; i < 16; ++i) sum += red[i][lane];
-    if (li < NT) {
-      const int n = n0 + li;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + 4 * q + r;
-        float v = 0.f;
-        if (n < N && m < M) {
-          v = apply_epi(e, sum[r], m, n);
-          h2[(int64_t)m * N + n] = v;
-        }
-        sh[4 * q + r][li] = v;
-      }
-    }
-  }
-  __syncthreads();
-  // this tile's share of the fc3 logits: plog[tile][m][c] = sum_j h2[m][n0 + j] * W3[c][n0 + j]
-  for (int i = tid; i < 16 * C; i += 1024) {
-    const int mm = i / C, c = i - mm * C;
-    const int m = m0 + mm;
-    if (m >= M) continue;
-    float d = 0.f;
-#pragma unroll
-    for (int j = 0; j < NT; ++j) {
-      const int n = n0 + j;
-      if (n < N) {
-        const float w3 = W3[(int64_t)c * ldw3 + n];
-        d = fmaf(bf ? bfr(sh[mm][j]) : sh[mm][j], bf ? bfr(w3) : w3, d);
-      }
-    }
-    plog[((int64_t)tile * M + m) * C + c] = d;
-  }
-}
-
 // head_bwd_kernel: workgroup (m, q) sums row m's partial logits (+ b3), softmax-CE (loss and
 // dlogits written by q == 0), then dz2 = (dlogits . W3) * dscale * [h2 > 0] for its slice.
 // The softmax's two wave reductions run on DPP row moves + v_readlane, and each exponential
@@ -284,17 +179,16 @@ __global__ void __launch_bounds__(256)
 head_bwd_kernel(const float* __restrict__ plog, const float* __restrict__ b3, const float* __restrict__ W3,
                 int ldw3, const int64_t* __restrict__ y, int64_t ignore, float scale, float dscale,
                 const float* __restrict__ h2, float* __restrict__ dlog, float* __restrict__ dz2,
-                float* __restrict__ loss_rows, int M, int N2, int C, int Qp, int hl) {
-  // Qp: number of partial-logit slabs in plog (head_fwd: one per column slice = gridDim.y;
-  // fc2_head_fwd: one per 8-column tile)
+                float* __restrict__ loss_rows, int M, int N2, int C, int Qp) {
+  // Qp: number of partial-logit slabs in plog (head_fwd: one per column slice)
   extern __shared__ float lg[];   // C
   __shared__ f32x4 part[8][HS];
   int m, q, Q;
-  head_wg(hl, m, q, Q);
+  head_wg(m, q, Q);
   const int tid = threadIdx.x;
   const int lane = tid & 63, wv = tid >> 6;
   int qa, qb;
-  head_slice(N2 >> 2, Q, q, qa, qb, hl);
+  head_slice(N2 >> 2, q, qa, qb);
   const int ncol = qb - qa;
   const int c = tid & (HS - 1), g = tid >> 5;
   constexpr int JU = 13;
@@ -370,6 +264,213 @@ head_bwd_kernel(const float* __restrict__ plog, const float* __restrict__ b3, co
   }
 }
 
+// head_fused_kernel: head_fwd and head_bwd in ONE launch.  Workgroup (q, m) runs head_fwd's
+// phase (slab reduction [+ the fused peer-mapped all-reduce], fc2 epilogue -> h2, its slice's
+// partial fc3 logits), publishes the partial logits, and waits for the other Q - 1 slices of
+// row m inside the launch instead of at a kernel boundary; then head_bwd's phase (logits,
+// softmax-CE, dlogits, dz2 for its slice) reuses the W3 slice and the h2 mask still in its
+// registers (head_bwd re-loaded both).  Hand-off (MI355X_MICROARCH.md, "Valid forms", first
+// row of the sc1 table): the partial logits are written with sc1 (write-through) stores, every
+// storing wave drains `s_waitcnt vmcnt(0)`, a workgroup barrier, then ONE agent-scope atomic
+// add per workgroup on row m's counter; the waiting lane polls the counter with sc1 loads and
+// every read of the partials is an sc1 load after a workgroup barrier.  The counter is never
+// reset: a workgroup's ticket (the value its add returned) names its launch, so it waits for
+// (ticket / Q + 1) * Q arrivals.  Every row's Q workgroups are consecutive in dispatch order,
+// so a waiting workgroup only waits for workgroups already dispatched with it (no residency
+// deadlock); the poll is bounded anyway (a safety net, ~2 s).
+// G > 1: grouped cross-entropy (SISA-concat's k heads, protocols/concat.py): the C logits are G
+// groups of C / G, each with its own label y[m G + g], scale (gscale[m G + g], or `scale`) and
+// loss loss_rows[m G + g].
+template <bool BF, bool IPC>
+__global__ void __launch_bounds__(256)
+head_fused_kernel(const float* __restrict__ P2, int S2, int64_t slab2, Epi e2, const float* __restrict__ W3,
+                  int ldw3, const float* __restrict__ b3, const int64_t* __restrict__ y, int64_t ignore, float scale,
+                  const float* __restrict__ gscale, int G, float* __restrict__ h2, float* __restrict__ plog, int ldp,
+                  unsigned long long* __restrict__ cnt, float* __restrict__ dlog, float* __restrict__ dz2,
+                  float* __restrict__ loss_rows, int M, int N2, int C, IpcStep ip) {
+  extern __shared__ float lg[];   // C
+  __shared__ f32x4 part[8][HS];
+  __shared__ f32x4 hs[HS];
+  int m, q, Q;
+  head_wg(m, q, Q);
+  const int tid = threadIdx.x;
+  int qa, qb;
+  head_slice(N2 >> 2, q, qa, qb);
+  const int ncol = qb - qa;
+  const int lane = tid & 63, wv = tid >> 6, half = lane >> 5, c = lane & 31;
+  const int g8 = tid >> 5;             // = 2 wv + half: this thread's output group lane
+  constexpr int JU = 13;
+  // W3 loads of the first output group do not depend on anything: issue them first.  Thread
+  // (g8, c) holds W3[8 j + g8][slice column c] for both phases.
+  f32x4 w[JU];
+  auto load_w = [&](int j0) {
+#pragma unroll
+    for (int j = 0; j < JU; ++j) {
+      const int o = 8 * (j0 + j) + g8;
+      w[j] = (o < C && c < ncol) ? *reinterpret_cast<const f32x4*>(W3 + (int64_t)o * ldw3 + 4 * (qa + c))
+                                 : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  load_w(0);
+  bool peers = false;
+  if constexpr (IPC) {
+    __shared__ int s_ok;
+    if (wv == 0) {
+      if (lane < ncol) {
+        const f32x4* src = reinterpret_cast<const f32x4*>(P2 + (int64_t)m * N2) + qa + lane;
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        for (int s = 0; s < S2; ++s) v += src[s * (slab2 >> 2)];
+        const int64_t slot = ((int64_t)ip.par * ip.T + ip.me) * ip.cap + (int64_t)m * N2 + 4 * (qa + lane);
+        for (int r = 0; r < ip.T; ++r) ipc_st4(ipc_rsrc(ip.P.data[r]), slot, make_float4(v[0], v[1], v[2], v[3]));
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int fi = m * Q + q;
+      if (lane < ip.T) ipc_raise_flag(ip.P.flags[lane] + ((int64_t)ip.par * ip.T + ip.me) * ip.nflags + fi, ip.gen, ip.fences);
+      const bool ok = ipc_wait_flags(ip, lane, fi);
+      if (lane == 0) s_ok = ok ? 1 : 0;
+    }
+    __syncthreads();
+    // a wait that gave up (stalled / dead peer, error word raised) falls back to the local
+    // partial: the numbers are meaningless but the launch completes and every workgroup still
+    // arrives at the row counter below (the job aborts on the error word)
+    peers = s_ok != 0;
+  }
+  // 1. slab reduction: 32 columns x 8 slab groups
+  {
+    const int cc = tid & (HS - 1), sg = tid >> 5;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (cc < ncol) {
+      if (IPC && peers) {
+        const __amdgpu_buffer_rsrc_t rs = ipc_rsrc(ip.P.data[ip.me]);
+        const int64_t o0 = (int64_t)ip.par * ip.T * ip.cap + (int64_t)m * N2 + 4 * (qa + cc);
+        for (int s = sg; s < ip.T; s += 8) {
+          const float4 u = ipc_ld4(rs, o0 + (int64_t)s * ip.cap);
+          v += f32x4{u.x, u.y, u.z, u.w};
+        }
+      } else {
+        const f32x4* src = reinterpret_cast<const f32x4*>(P2 + (int64_t)m * N2) + qa + cc;
+#pragma unroll 4
+        for (int s = sg; s < S2; s += 8) v += src[s * (slab2 >> 2)];
+      }
+    }
+    part[sg][cc] = v;
+  }
+  __syncthreads();
+  f32x4 hh = {0.f, 0.f, 0.f, 0.f};      // this slice's h2 (threads 0..HS-1), kept for the mask
+  if (tid < HS) {
+    f32x4 v = part[0][tid];
+#pragma unroll
+    for (int g = 1; g < 8; ++g) v += part[g][tid];
+    if (tid < ncol) {
+      const int col = 4 * (qa + tid);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) hh[i] = apply_epi(e2, v[i], m, col + i);
+      reinterpret_cast<f32x4*>(h2 + (int64_t)m * N2)[qa + tid] = hh;
+    }
+    hs[tid] = hh;
+  }
+  __syncthreads();
+  // 2. partial logits: half-wave h (32 lanes = the slice's columns) owns output 8 j + 2 wv + h;
+  // published with sc1 stores (write-through) for the hand-off
+  {
+    const f32x4 h = BF ? bfr4(hs[c]) : hs[c];
+    float* dst = plog + ((int64_t)q * M + m) * ldp;
+    for (int j0 = 0; j0 * 8 < C; j0 += JU) {
+      if (j0) load_w(j0);
+#pragma unroll
+      for (int j = 0; j < JU; ++j) {
+        const f32x4 wj = BF ? bfr4(w[j]) : w[j];
+        const float d = sl_row16_sum(wj[0] * h[0] + wj[1] * h[1] + wj[2] * h[2] + wj[3] * h[3]);
+        const float s0 = sl_lane(d, 0) + sl_lane(d, 16), s1 = sl_lane(d, 32) + sl_lane(d, 48);
+        const int o = 8 * (j0 + j) + 2 * wv;
+        if (lane == 0) {
+          if (o < C) __hip_atomic_store(dst + o, s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (o + 1 < C) __hip_atomic_store(dst + o + 1, s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+    if (C > 8 * JU) load_w(0);           // phase 2 starts from the first output group again
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // 3. hand-off: arrive on row m's counter, wait for the row's other Q - 1 slices
+  if (tid == 0) {
+    const unsigned long long ticket = __hip_atomic_fetch_add(cnt + m, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long target = (ticket / (unsigned)Q + 1ull) * (unsigned)Q;
+    if (ticket + 1 < target) {
+      const uint64_t t0 = wall_clock64();
+      while (__hip_atomic_load(cnt + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(1);
+        if (wall_clock64() - t0 > 200000000ull) break;   // ~2 s at the 100 MHz wall clock: never hit
+      }
+    }
+  }
+  __syncthreads();
+  // 4. logits of row m (sc1 loads of the Q published partials, slice order) + b3
+  for (int o = tid; o < C; o += 256) {
+    float v = b3 ? b3[o] : 0.f;
+    for (int s = 0; s < Q; ++s)
+      v += __hip_atomic_load(plog + ((int64_t)s * M + m) * ldp + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    lg[o] = v;
+  }
+  __syncthreads();
+  // 5. softmax-CE per label group (wave g % 4 takes group g)
+  const int Cg = C / G;
+  for (int g = wv; g < G; g += 4) {
+    const int64_t lab = y[(int64_t)m * G + g];
+    float* lgg = lg + g * Cg;
+    const float sc = gscale ? gscale[(int64_t)m * G + g] : scale;
+    if (lab == ignore || lab < 0 || lab >= Cg) {
+      for (int cc = lane; cc < Cg; cc += 64) lgg[cc] = 0.f;
+      if (lane == 0 && q == 0) loss_rows[(int64_t)m * G + g] = 0.f;
+    } else {
+      const float zl = lgg[lab];
+      float mx = -INFINITY;
+      for (int cc = lane; cc < Cg; cc += 64) mx = fmaxf(mx, lgg[cc]);
+      mx = sl_wave_max_dpp(mx);
+      float se = 0.f;
+      for (int cc = lane; cc < Cg; cc += 64) {
+        const float e = expf(lgg[cc] - mx);
+        lgg[cc] = e;
+        se += e;
+      }
+      se = sl_wave_sum_dpp(se);
+      if (lane == 0 && q == 0) loss_rows[(int64_t)m * G + g] = mx + logf(se) - zl;
+      const float inv = 1.f / se;
+      for (int cc = lane; cc < Cg; cc += 64) {
+        float p = lgg[cc] * inv;
+        if (cc == lab) p -= 1.f;
+        lgg[cc] = p * sc;
+      }
+    }
+  }
+  __syncthreads();
+  if (q == 0)
+    for (int cc = tid; cc < C; cc += 256) dlog[(int64_t)m * C + cc] = lg[cc];
+  // 6. dz2 for this slice: (dlogits . W3[:, slice]) * dscale * [h2 > 0]
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int j0 = 0; j0 * 8 < C; j0 += JU) {
+    if (j0) load_w(j0);
+#pragma unroll
+    for (int j = 0; j < JU; ++j) {
+      const int o = 8 * (j0 + j) + g8;
+      const float l = o < C ? lg[o] : 0.f;
+      acc += BF ? bfr(l) * bfr4(w[j]) : l * w[j];
+    }
+  }
+  part[g8][c] = acc;
+  __syncthreads();
+  if (tid < ncol) {
+    f32x4 v = part[0][tid];
+#pragma unroll
+    for (int gg = 1; gg < 8; ++gg) v += part[gg][tid];
+    f32x4 out;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[i] = hh[i] > 0.f ? v[i] * e2.dscale : 0.f;
+    reinterpret_cast<f32x4*>(dz2 + (int64_t)m * N2)[qa + tid] = out;
+  }
+}
+
 // Traversal order.  Workgroups are dispatched in linear (x fastest) order, so the tile
 // order is the order in which fc1's W/m/v stream through the 256 MiB Infinity Cache.
 // With grp.rev0 set, layer 0's tiles are walked last-to-first (the other layers keep
@@ -418,15 +519,14 @@ __device__ __forceinline__ void st_wt(float* base, int N, int ld, int boff, f32x
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), rs, boff, 0, 16);
 }
 
-template <bool ADAM, int FWDC, bool PART>
+template <bool ADAM, int FWDC>
 __global__ void __launch_bounds__(1024)
 wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
   // FWDC: look-ahead row chunks of 16 (0 = no look-ahead; 1: next batch <= 16 rows; 4: <= 64)
   constexpr bool FWDN = FWDC > 0;
   __shared__ f32x4 sa[16][64];
   __shared__ float sdz[16][16];
-  // look-ahead: the updated W tile, rows padded to 65 float4 (variant 1 = 1: plain 64-float4
-  // rows; 2: XOR-swizzled columns, conflict-free for both the row write and the column read).
+  // look-ahead: the updated W tile, rows padded to 65 float4.
   // The MFMA B-layout read below takes 16 rows of one column: with a 1 KB row stride all
   // 16 hit the same LDS banks (rocprofv3 SQ_LDS_BANK_CONFLICT 3.96 M cycles per TP = 1
   // step, 0 without the look-ahead); one float4 of padding spreads them over all banks.
@@ -474,17 +574,7 @@ wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
       if (tid < 256) {
         const int mr = mc + (tid >> 4), nn = n0 + (tid & 15);
         float v = 0.f;
-        if (mr < M && nn < L.N) {
-          if (PART && L.dzp) {
-            // every slab load (and the mask load) in flight at once: bit-identical to
-            // dgrad_reduce_kernel's sum, one round trip instead of S dependent ones
-            const float hm = L.hmask ? L.hmask[(int64_t)mr * L.N + nn] : 1.f;
-            v = sum_slabs(L.dzp + (int64_t)mr * L.N + nn, L.S, L.slab);
-            if (L.hmask) v = hm > 0.f ? v * L.mscale : 0.f;
-          } else {
-            v = L.dz[(int64_t)mr * L.ldz + nn];
-          }
-        }
+        if (mr < M && nn < L.N) v = L.dz[(int64_t)mr * L.ldz + nn];
         sdz[tid >> 4][tid & 15] = grp.bf16 ? bfr(v) : v;
       }
     }
@@ -513,13 +603,10 @@ wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
     // next batch's partial pre-activations with the updated tile: stage W_new through LDS
     // into MFMA B layout; wave w covers columns [16w, 16w+16) with 4 exact-fp32 MFMAs
     // (B[k][n] = W_new[n][k]: lane (n = li, k-group lq) reads one float4 of the tile)
-    // layout: grp.swz 0 = rows padded to 65 float4, 1 = plain 64, 2 = column XOR (row & 15)
-    const int wcol = grp.swz == 2 ? (lane ^ r) : lane;
-    const int rcol = grp.swz == 2 ? ((4 * r + lq) ^ li) : 4 * r + lq;
-    const int rs = grp.swz == 0 ? 65 : 64;
-    sw[r * rs + wcol] = act ? p : zv;
+    // rows padded to 65 float4 (a plain 64 and an XOR-swizzled layout measured the same)
+    sw[r * 65 + lane] = act ? p : zv;
     __syncthreads();
-    f32x4 wv4 = sw[li * rs + rcol];
+    f32x4 wv4 = sw[li * 65 + 4 * r + lq];
     if (grp.bf16) wv4 = bfr4(wv4);
 #pragma unroll
     for (int c = 0; c < FWDC; ++c) {
@@ -550,187 +637,105 @@ wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
   }
 }
 
-// All-MFMA form of the grouped wgrad+optimizer (variant 1; NOT the default).  Workgroup = 16 waves over a
-// 16-row x 256-column tile of W; wave w owns columns [16w, 16w+16).  Per 16-row batch chunk
-// the wave forms its 16x16 tile of dW^T with 4 exact-fp32 v_mfma_f32_16x16x4f32:
-//   A[k][m] = X[m][k] (lane: k = lane&15, m = lane>>4), B[m][n] = dZ[m][n],
-// whose accumulator layout (lane: n = lane&15, k = 4*(lane>>4)+i) is exactly one float4 of
-// a W row -> the W / state streams are float4 loads and the batch operands come straight
-// from L2 (no LDS staging: the LDS version re-read the X tile once per wave, 16x).
-// Look-ahead (FWDN): with W_new in that same layout, 4 more MFMAs give the wave's share of
-// x_next @ W_new^T (A = x_next float4 component i, B = W_new component i); the 16 waves'
-// 16x16 partials are summed through LDS into one split-K slab per 256-column block.
-// Measured on MI355X (fc1, 5000x5408, Adam): 147 us vs 120 us for the LDS-staged kernel
-// below — each wave instruction here touches 16 rows x 64 B instead of 1 row x 1 KB, and
-// HBM streams the latter better; the X-tile LDS re-reads it avoids were not the limiter.
-template <bool ADAM, bool FWDN>
-__global__ void __launch_bounds__(1024)
-wgrad_group_mfma_kernel(WgGroup grp, int M, SlOpt o) {
-  __shared__ f32x4 red[FWDN ? 16 : 1][64];
-  const int by = (int)blockIdx.y;
-  const bool l0 = !(grp.n > 1 && by >= grp.d[1].yb0);
-  const WgDesc L = (grp.n > 2 && by >= grp.d[2].yb0) ? grp.d[2] : (l0 ? grp.d[0] : grp.d[1]);
-  const int kb = blockIdx.x * 256;
-  if (kb >= L.K) return;                 // uniform per workgroup
-  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, li = lane & 15, lq = lane >> 4;
-  const int n0 = (by - L.yb0) * 16;
-  const int kw = kb + wv * 16;
-  const int n = n0 + li, k4 = kw + 4 * lq;
-  const bool nin = n < L.N;
-  const bool act = nin && k4 < L.K;
-  const f32x4 zv = {0.f, 0.f, 0.f, 0.f};
-  const int64_t off = (int64_t)n * L.ldw + k4;
-  f32x4 p = zv, q0 = zv, q1 = zv;
-  if (act) {
-    p = *reinterpret_cast<const f32x4*>(L.W + off);
-    q0 = *reinterpret_cast<const f32x4*>(L.s0 + off);
-    if (ADAM) q1 = *reinterpret_cast<const f32x4*>(L.s1 + off);
-  }
-  f32x4 xv = zv;
-  if (FWDN && l0 && li < grp.mn && k4 < L.K) xv = *reinterpret_cast<const f32x4*>(grp.xn + (int64_t)li * grp.ldxn + k4);
-  const bool kin = kw + li < L.K;
-  f32x4 g = zv;
-  float gb = 0.f;
-  for (int mc = 0; mc < M; mc += 16) {
-    float a[4], b[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int m = mc + 4 * s + lq;
-      a[s] = (m < M && kin) ? L.A[(int64_t)m * L.lda + kw + li] : 0.f;
-      float v = 0.f;
-      if (m < M && nin) {
-        if (L.dzp) {
-          for (int z = 0; z < L.S; ++z) v += L.dzp[z * L.slab + (int64_t)m * L.N + n];
-          if (L.hmask) v = L.hmask[(int64_t)m * L.N + n] > 0.f ? v * L.mscale : 0.f;
-        } else {
-          v = L.dz[(int64_t)m * L.ldz + n];
-        }
-      }
-      b[s] = v;
-    }
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      g = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], g, 0, 0, 0);
-      gb += b[s];
-    }
-  }
-  if (act) {
-    sl_opt_update4<ADAM>(o, p, g, q0, q1);
-    if (o.kind != 0) *reinterpret_cast<f32x4*>(L.W + off) = p;
-    *reinterpret_cast<f32x4*>(L.s0 + off) = q0;
-    if (ADAM) *reinterpret_cast<f32x4*>(L.s1 + off) = q1;
-  } else {
-    p = zv;
-  }
-  if (FWDN && l0) {
-    f32x4 z = zv;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) z = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[i], p[i], z, 0, 0, 0);
-    red[wv][lane] = z;                    // z[j] = partial(m = 4*lq + j, n = n0 + li)
-    __syncthreads();
-    if (tid < 256) {
-      const int m = tid >> 4, nn = tid & 15;
-      float v = 0.f;
-#pragma unroll
-      for (int w = 0; w < 16; ++w) v += red[w][16 * (m >> 2) + nn][m & 3];
-      if (m < grp.mn && n0 + nn < L.N) grp.pn[((int64_t)blockIdx.x * grp.mn + m) * L.N + n0 + nn] = v;
-    }
-  }
-  if (L.bias && blockIdx.x == 0 && wv == 0) {
-    gb += __shfl_xor(gb, 16);
-    gb += __shfl_xor(gb, 32);
-    if (lq == 0 && nin) {
-      float pb = L.bias[n], b0 = L.sb0[n], b1 = L.sb1 ? L.sb1[n] : 0.f;
-      sl_opt_update(o, pb, gb, b0, b1);
-      if (o.kind != 0) L.bias[n] = pb;
-      L.sb0[n] = b0;
-      if (L.sb1) L.sb1[n] = b1;
-    }
-  }
-}
-
 int head3_slices(int N2) { return max(1, (N2 / 4 + HS - 1) / HS); }
 
-static int head_layout() { return g_variant[20] == 2 ? 1 : 0; }
-static dim3 head_grid(int M, int Q, int hl) { return hl == 0 ? dim3(Q, M) : dim3(M, Q); }
+static dim3 head_grid(int M, int Q) { return dim3(Q, M); }
 
 static void launch_head_bwd(const float* plog, const float* b3, const float* W3, int ldw3, const int64_t* y,
                             int64_t ignore, float scale, float dscale, const float* h2, float* dlog, float* dz2,
-                            float* loss_rows, int M, int N2, int C, int Q, int Qp, hipStream_t st, int hl) {
+                            float* loss_rows, int M, int N2, int C, int Q, int Qp, hipStream_t st) {
   const size_t sh = (size_t)C * sizeof(float);
-  const dim3 g = head_grid(M, Q, hl);
+  const dim3 g = head_grid(M, Q);
   if (g_bf16)
     head_bwd_kernel<true><<<g, 256, sh, st>>>(plog, b3, W3, ldw3, y, ignore, scale, dscale, h2, dlog, dz2, loss_rows,
-                                              M, N2, C, Qp, hl);
+                                              M, N2, C, Qp);
   else
     head_bwd_kernel<false><<<g, 256, sh, st>>>(plog, b3, W3, ldw3, y, ignore, scale, dscale, h2, dlog, dz2,
-                                               loss_rows, M, N2, C, Qp, hl);
+                                               loss_rows, M, N2, C, Qp);
+}
+
+// Row counters of the fused head's in-launch hand-off (head_fused_kernel), one per batch row,
+// per device, zero-initialised once and never freed (captured graphs hold the address).  The
+// head runs on one stream per process at a time (Bob's steps are a serial chain), which the
+// ticket arithmetic relies on.
+constexpr int kHeadRows = 1 << 16;
+
+static unsigned long long* head_counters() {
+  static unsigned long long* per_dev[64] = {nullptr};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (per_dev[dev] == nullptr) {
+    void* p = nullptr;
+    if (hipMalloc(&p, sizeof(unsigned long long) * kHeadRows) != hipSuccess) return nullptr;
+    if (hipMemset(p, 0, sizeof(unsigned long long) * kHeadRows) != hipSuccess) return nullptr;
+    if (hipDeviceSynchronize() != hipSuccess) return nullptr;
+    per_dev[dev] = static_cast<unsigned long long*>(p);
+  }
+  return per_dev[dev];
 }
 
 hipError_t server_head3(const float* P2, int S2, int64_t slab2, Epi e2, const float* W3, int ldw3, const float* b3,
                         const int64_t* y, int64_t ignore, float scale, float* h2, float* dlog, float* dz2,
                         float* loss_rows, float* ws, int64_t ws_elems, int M, int N2, int C, hipStream_t st,
-                        const IpcStep* ipc) {
+                        const IpcStep* ipc, int G, const float* gscale) {
   if (M <= 0) return hipSuccess;
-  if ((N2 & 3) || (ldw3 & 3)) return hipErrorInvalidValue;
+  if ((N2 & 3) || (ldw3 & 3) || G < 1 || C % G != 0) return hipErrorInvalidValue;
   const int Q = head3_slices(N2);
   if (ws_elems < (int64_t)Q * M * C) return hipErrorInvalidValue;
-  const int hl = head_layout();
-  const dim3 g = head_grid(M, Q, hl);
-  if (ipc != nullptr) {
-    // the fused all-reduce: one flag word per workgroup, one [M, N2] partial per slot; the
-    // local partial may be S2 split-K slabs (summed before the push)
-    if (S2 < 1 || (slab2 & 3) || (int64_t)M * Q > ipc->nflags || (int64_t)M * N2 > ipc->cap || ipc->T < 1 ||
-        ipc->T > kIpcMaxRanks)
-      return hipErrorInvalidValue;
-    if (g_bf16)
-      head_fwd_kernel<true, true><<<g, 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C, *ipc, hl);
-    else
-      head_fwd_kernel<false, true><<<g, 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C, *ipc, hl);
-  } else {
-    const IpcStep none{};
-    if (g_bf16)
-      head_fwd_kernel<true, false><<<g, 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C, none, hl);
-    else
-      head_fwd_kernel<false, false><<<g, 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C, none, hl);
+  const dim3 g = head_grid(M, Q);
+  if (ipc != nullptr && (S2 < 1 || (slab2 & 3) || (int64_t)M * Q > ipc->nflags || (int64_t)M * N2 > ipc->cap ||
+                         ipc->T < 1 || ipc->T > kIpcMaxRanks))
+    return hipErrorInvalidValue;
+  // one launch with the in-launch hand-off (default), unless the counters cannot be had (a
+  // first use inside a graph capture) or variant 21 = 1 asks for the two-kernel form
+  unsigned long long* cnt = nullptr;
+  if (g_variant[21] != 1 && M <= kHeadRows) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    static bool ready = false;
+    if (ready || (hipStreamIsCapturing(st, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone)) {
+      cnt = head_counters();
+      ready = cnt != nullptr;
+    }
   }
-  launch_head_bwd(ws, b3, W3, ldw3, y, ignore, scale, e2.dscale, h2, dlog, dz2, loss_rows, M, N2, C, Q, Q, st, hl);
-  return hipGetLastError();
-}
-
-int fc2_head_tiles(int N2) { return (N2 + 7) / 8; }
-
-// fc2 forward (full K per workgroup) + fc2 epilogue + partial fc3 logits in one launch, then
-// head_bwd: the single-shard server head in 2 launches instead of fc2 forward + 2.
-hipError_t server_fc2_head(const float* X, int ldx, const float* W2, int ldw2, Epi e2, const float* W3, int ldw3,
-                           const float* b3, const int64_t* y, int64_t ignore, float scale, float* h2, float* dlog,
-                           float* dz2, float* loss_rows, float* ws, int64_t ws_elems, int M, int K, int N2, int C,
-                           hipStream_t st) {
-  if (M <= 0) return hipSuccess;
-  if ((N2 & 3) || (ldw3 & 3) || (K & 3) || (ldx & 3) || (ldw2 & 3)) return hipErrorInvalidValue;
-  const int T = fc2_head_tiles(N2), Q = head3_slices(N2);
-  if (ws_elems < (int64_t)T * M * C) return hipErrorInvalidValue;
-  fc2_head_fwd_kernel<8><<<dim3(T, (M + 15) / 16), 1024, 0, st>>>(X, ldx, W2, ldw2, e2, W3, ldw3, h2, ws, M, N2, K, C,
-                                                                  g_bf16);
-  launch_head_bwd(ws, b3, W3, ldw3, y, ignore, scale, e2.dscale, h2, dlog, dz2, loss_rows, M, N2, C, Q, T, st,
-                  head_layout());
+  const IpcStep none{};
+  const IpcStep& ip = ipc ? *ipc : none;
+  if (cnt != nullptr) {
+    const size_t sh = (size_t)C * sizeof(float);
+#define SL_HF(BF, IP)                                                                                          \
+  head_fused_kernel<BF, IP><<<g, 256, sh, st>>>(P2, S2, slab2, e2, W3, ldw3, b3, y, ignore, scale, gscale, G, h2, \
+                                                ws, C, cnt, dlog, dz2, loss_rows, M, N2, C, ip)
+    if (g_bf16) { if (ipc) SL_HF(true, true); else SL_HF(true, false); }
+    else { if (ipc) SL_HF(false, true); else SL_HF(false, false); }
+#undef SL_HF
+    return hipGetLastError();
+  }
+  if (G != 1) return hipErrorInvalidValue;   // the grouped CE exists in the fused kernel only
+  if (ipc != nullptr) {
+    if (g_bf16)
+      head_fwd_kernel<true, true><<<g, 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C, ip);
+    else
+      head_fwd_kernel<false, true><<<g, 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C, ip);
+  } else {
+    if (g_bf16)
+      head_fwd_kernel<true, false><<<g, 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C, none);
+    else
+      head_fwd_kernel<false, false><<<g, 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C, none);
+  }
+  launch_head_bwd(ws, b3, W3, ldw3, y, ignore, scale, e2.dscale, h2, dlog, dz2, loss_rows, M, N2, C, Q, Q, st);
   return hipGetLastError();
 }
 
 // Per-launch traversal / store form.  The direction of layer 0's walk alternates from one
 // launch to the next (graph capture bakes the pattern in; every captured chunk has an even
-// number of steps).  Variant 7 (A/B and tests): 1 = always forward, 2 = always reversed.
-// W/m/v are stored write-through (32-bit byte offsets: layers under 2 GB only); variant
-// 4 = 1 selects plain stores.  Measured (scripts/cache_ab.py, one process, interleaved
+// number of steps).  W/m/v are stored write-through (32-bit byte offsets: layers under 2 GB
+// only; plain stores otherwise).  Measured (scripts/cache_ab.py, one process, interleaved
 // rounds, us per look-ahead server step at TP = 1 / 2 / 4 / 8): always-forward 183.4 /
 // 102.2 / 70.2 / 59.7, alternating 172.6 / 100.9 / 69.6 / 59.8, alternating +
 // write-through 171.8 / 100.9 / 68.7 / 59.5 (profiles/r1_cache_ab.txt).
 static void set_traversal(WgGroup& gg) {
   static unsigned flip = 0;
-  const int v7 = g_variant[7];
-  gg.rev0 = v7 == 1 ? 0 : (v7 == 2 ? 1 : (int)(flip++ & 1u));
-  gg.wt = g_variant[4] == 1 ? 0 : 1;
-  gg.swz = g_variant[1];
+  gg.rev0 = (int)(flip++ & 1u);
+  gg.wt = 1;
   gg.bf16 = g_bf16;
   for (int i = 0; i < gg.n; ++i)
     if ((int64_t)gg.d[i].N * gg.d[i].ldw * 4 > 2147483647LL) gg.wt = 0;
@@ -741,6 +746,7 @@ hipError_t wgrad_group(const WgGroup& g, int M, SlOpt o, hipStream_t st) {
   WgGroup gg = g;
   set_traversal(gg);
   for (int i = 0; i < gg.n; ++i) {
+    if (gg.d[i].dz == nullptr) return hipErrorInvalidValue;
     gg.d[i].yb0 = yb;
     gg.d[i].wb0 = wb;
     yb += (gg.d[i].N + 15) / 16;
@@ -749,39 +755,25 @@ hipError_t wgrad_group(const WgGroup& g, int M, SlOpt o, hipStream_t st) {
   }
   if (yb == 0 || kmax == 0) return hipSuccess;
   gg.nt0 = ((gg.d[0].N + 15) / 16) * ((gg.d[0].K + 255) / 256);
-  dim3 grid((kmax + 255) / 256, yb);     // 2-D grid of the all-MFMA variant
-  const dim3 grid1(wb);                  // 1-D grid over the real tiles (default kernel)
+  const dim3 grid((kmax + 255) / 256, yb);   // 2-D: (K blocks of the widest layer) x (row tiles)
+  const dim3 grid1(wb);                      // 1-D over the real tiles
   if (gg.xn && (gg.mn <= 0 || gg.mn > 64 || !gg.pn)) return hipErrorInvalidValue;
-  if (gg.xn && gg.mn > 16 && g_variant[3] == 1) return hipErrorInvalidValue;   // MFMA-dW variant: <= 16
   const bool fw = gg.xn != nullptr;
-  const bool fw4 = fw && gg.mn > 16;
-  bool part = false;
-  for (int i = 0; i < gg.n; ++i) part = part || gg.d[i].dzp != nullptr;
-  if (g_variant[3] != 1) {   // default: LDS-staged VALU dW (row-contiguous W streams)
+  const int fc = (fw && gg.mn > 16) ? 4 : (fw ? 1 : 0);
   // 2-D grid when it wastes < 10 % of its workgroups (TP = 1: 3 %, measured 1.4 us per step
-  // faster there), else the 1-D grid (TP = 2 / 4 / 8: 18-55 % empty, 0.3-1.2 us faster);
-  // variant 2: 1 = always 2-D, 2 = always 1-D (profiles/r1_cache_ab_grid.txt)
+  // faster there), else the 1-D grid (TP = 2 / 4 / 8: 18-55 % empty, 0.3-1.2 us faster;
+  // profiles/r1_cache_ab_grid.txt)
   const int64_t g2 = (int64_t)grid.x * grid.y;
-  gg.grid2d = g_variant[2] == 1 ? 1 : (g_variant[2] == 2 ? 0 : ((g2 - wb) * 10 < g2 ? 1 : 0));
-#define SL_WG(A, F, P) wgrad_group_kernel<A, F, P><<<gg.grid2d ? grid : grid1, 1024, 0, st>>>(gg, M, o)
-    const int fc = fw4 ? 4 : (fw ? 1 : 0);
-    if (part) {
-      if (o.kind == 2) { if (fc == 4) SL_WG(true, 4, true); else if (fc) SL_WG(true, 1, true); else SL_WG(true, 0, true); }
-      else { if (fc == 4) SL_WG(false, 4, true); else if (fc) SL_WG(false, 1, true); else SL_WG(false, 0, true); }
-    } else {
-      if (o.kind == 2) { if (fc == 4) SL_WG(true, 4, false); else if (fc) SL_WG(true, 1, false); else SL_WG(true, 0, false); }
-      else { if (fc == 4) SL_WG(false, 4, false); else if (fc) SL_WG(false, 1, false); else SL_WG(false, 0, false); }
-    }
-#undef SL_WG
-    return hipGetLastError();
-  }
-  // variant 1: all-MFMA form (64-byte row segments per wave: measured slower, see above)
+  gg.grid2d = (g2 - wb) * 10 < g2 ? 1 : 0;
+  const dim3 gr = gg.grid2d ? grid : grid1;
   if (o.kind == 2) {
-    if (fw) wgrad_group_mfma_kernel<true, true><<<grid, 1024, 0, st>>>(gg, M, o);
-    else wgrad_group_mfma_kernel<true, false><<<grid, 1024, 0, st>>>(gg, M, o);
+    if (fc == 4) wgrad_group_kernel<true, 4><<<gr, 1024, 0, st>>>(gg, M, o);
+    else if (fc) wgrad_group_kernel<true, 1><<<gr, 1024, 0, st>>>(gg, M, o);
+    else wgrad_group_kernel<true, 0><<<gr, 1024, 0, st>>>(gg, M, o);
   } else {
-    if (fw) wgrad_group_mfma_kernel<false, true><<<grid, 1024, 0, st>>>(gg, M, o);
-    else wgrad_group_mfma_kernel<false, false><<<grid, 1024, 0, st>>>(gg, M, o);
+    if (fc == 4) wgrad_group_kernel<false, 4><<<gr, 1024, 0, st>>>(gg, M, o);
+    else if (fc) wgrad_group_kernel<false, 1><<<gr, 1024, 0, st>>>(gg, M, o);
+    else wgrad_group_kernel<false, 0><<<gr, 1024, 0, st>>>(gg, M, o);
   }
   return hipGetLastError();
 }

@@ -161,35 +161,19 @@ static hipError_t launch_gemm(const float* X, int ldx, const float* W, int ldw, 
   return hipGetLastError();
 }
 
-// Tile form per dtype (variant 10 for A/B: 1..4 = (WM, BK) = (2, 16|32), (2, 32|64), (4, 16|32),
-// (4, 32|64) for fp32|bf16; 0 = the measured default).  Measured on MI355X (TFLOP/s at M 14000,
-// N 5000, K 5408 / 4096^3; profiles/r2_gemm_bench.txt): fp32 73.7 / 75.0 / 89.3 / 73.1 and
-// 84-101; bf16 144-162 (operands converted from fp32 in the staging).  The default is the best
-// of each.  All forms are one-stage-prefetch kernels whose stage compute (2048 cycles fp32,
-// 256-512 bf16) is shorter than a loaded memory round trip: latency-bound, well below
-// hipBLASLt's 141 TF fp32 on the same shapes, which is why the fp32 evaluation product is routed
-// to the library (linear.hip linear_fwd, variant 11) and this kernel serves --dtype bf16.
+// Tile form per dtype: (WM, BK) = (4, 16) fp32, (4, 64) bf16, the best of the four forms
+// measured on MI355X (TFLOP/s at M 14000, N 5000, K 5408 / 4096^3; profiles/r2_gemm_bench.txt):
+// fp32 73.7 / 75.0 / 89.3 / 73.1 and 84-101; bf16 144-162 (operands converted from fp32 in the
+// staging).  One-stage-prefetch kernels whose stage compute is shorter than a loaded memory
+// round trip: latency-bound, below hipBLASLt's 141 TF fp32 on the same shapes, which is why the
+// fp32 evaluation product is routed to the library (ops/hip_ops.py) and this kernel serves
+// --dtype bf16 and graph capture.
 hipError_t gemm_nt(const float* X, int ldx, const float* W, int ldw, float* Y, int ldy, int M, int N, int K, Epi e,
                    bool bf16, hipStream_t st) {
   if (M <= 0 || N <= 0) return hipSuccess;
   if ((K & 3) || (ldx & 3) || (ldw & 3)) return hipErrorInvalidValue;
-  const int v = g_variant[10];
-  if (bf16) {
-    switch (v) {
-      case 1: return launch_gemm<true, 2, 32>(X, ldx, W, ldw, Y, ldy, M, N, K, e, st);
-      case 2: return launch_gemm<true, 2, 64>(X, ldx, W, ldw, Y, ldy, M, N, K, e, st);
-      case 3: return launch_gemm<true, 4, 32>(X, ldx, W, ldw, Y, ldy, M, N, K, e, st);
-      case 4: return launch_gemm<true, 4, 64>(X, ldx, W, ldw, Y, ldy, M, N, K, e, st);
-      default: return launch_gemm<true, 4, 64>(X, ldx, W, ldw, Y, ldy, M, N, K, e, st);
-    }
-  }
-  switch (v) {
-    case 1: return launch_gemm<false, 2, 16>(X, ldx, W, ldw, Y, ldy, M, N, K, e, st);
-    case 2: return launch_gemm<false, 2, 32>(X, ldx, W, ldw, Y, ldy, M, N, K, e, st);
-    case 3: return launch_gemm<false, 4, 16>(X, ldx, W, ldw, Y, ldy, M, N, K, e, st);
-    case 4: return launch_gemm<false, 4, 32>(X, ldx, W, ldw, Y, ldy, M, N, K, e, st);
-    default: return launch_gemm<false, 4, 16>(X, ldx, W, ldw, Y, ldy, M, N, K, e, st);
-  }
+  if (bf16) return launch_gemm<true, 4, 64>(X, ldx, W, ldw, Y, ldy, M, N, K, e, st);
+  return launch_gemm<false, 4, 16>(X, ldx, W, ldw, Y, ldy, M, N, K, e, st);
 }
 
 }  // namespace sl

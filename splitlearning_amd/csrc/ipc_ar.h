@@ -10,7 +10,24 @@
 // sums the T slots in rank order 0..T-1 — so every rank computes bitwise the same sum, which
 // keeps the replicated fc3 and the fc2 epilogue identical across ranks.  Regions are
 // double-buffered by step parity and flags carry a monotonic generation, so no reset or
-// closing barrier is needed.  Waits are bounded (a timeout raises the error word).
+// closing barrier is needed.
+//
+// Memory ordering (HIP / AMDGPU memory model, system scope because the peers are other
+// devices):
+//   producer  payload: 16-B write-through stores at system scope (sc0 sc1) into the peer's
+//             uncached region -> every storing wave `s_waitcnt vmcnt(0)` -> (workgroup
+//             barrier when several waves stored) -> ONE lane: a system-scope RELEASE fence,
+//             `s_waitcnt vmcnt(0)` (inline: the compiler may drop its own wait after the
+//             write-back, MI355X_MICROARCH.md "Compiler hazard") -> relaxed flag store;
+//   consumer  relaxed polls of its own flag words (no acquire per poll: 2-3x slower per hop)
+//             -> ONE system-scope ACQUIRE fence once the flag matched -> workgroup barrier
+//             -> the slot reads (system-scope sc0 sc1 loads).
+// Failure: every wait is bounded (wall clock); a timeout raises the error word, and every
+// later wait (this kernel or any later step) that finds its flag missing sees the word and
+// gives up at once instead of waiting out the timeout again — so a dead peer costs one
+// timeout, not one per step.  The word is mirrored into host-pinned memory, which the native
+// executor reads every few steps without a device sync (engine.cpp ServerEpoch::run) and
+// raises on.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -42,58 +59,82 @@ struct IpcStep {
   uint32_t gen;
   int64_t cap;        // floats per slot
   int nflags;         // flag words per (parity, source)
-  int* err;
+  int* err;           // device error word (uncached)
+  int* herr;          // host-pinned mirror of it (read by the host without a sync)
   int64_t timeout;    // wall-clock ticks
+  int fences;         // 1: release / acquire fences around the flags (default); 0: the
+                      // measured-cost A/B only (set_fences(False), scripts/native_ab.py)
 };
 
 __device__ __forceinline__ uint32_t ipc_poll_flag(const uint32_t* f) {
   return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__device__ __forceinline__ void ipc_raise_flag(uint32_t* f, uint32_t v) {
+// Release, then the flag: the payload this lane's workgroup stored (drained and barriered by
+// the caller) is visible to any agent that observes the flag and acquires.
+__device__ __forceinline__ void ipc_raise_flag(uint32_t* f, uint32_t v, int fence = 1) {
+  if (fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Payload moves at system scope (each dword a relaxed system-scope atomic: global_store /
-// global_load with sc0 sc1), so the protocol follows the memory model whatever cache type
-// the driver gives a peer's mapping: a store leaves no dirty line in this GPU's L2 and is
-// complete at `s_waitcnt vmcnt(0)`; a load never hits a stale line of an earlier generation.
-__device__ __forceinline__ void ipc_st4(float* p, float4 v) {
-  uint32_t* q = reinterpret_cast<uint32_t*>(p);
-  __hip_atomic_store(q + 0, __float_as_uint(v.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  __hip_atomic_store(q + 1, __float_as_uint(v.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  __hip_atomic_store(q + 2, __float_as_uint(v.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  __hip_atomic_store(q + 3, __float_as_uint(v.w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+__device__ __forceinline__ void ipc_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); }
+
+// 16-B payload access at system scope through a buffer resource over a (wave-uniform) region
+// base: one write-through store / cache-bypassing load per float4 (sc0 sc1 = cache policy 17).
+typedef int ipc_i32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ipc_rsrc(const float* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, 0x7fffffff, 0x00020000);
 }
 
-__device__ __forceinline__ float4 ipc_ld4(const float* p) {
-  const uint32_t* q = reinterpret_cast<const uint32_t*>(p);
-  float4 v;
-  v.x = __uint_as_float(__hip_atomic_load(q + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-  v.y = __uint_as_float(__hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-  v.z = __uint_as_float(__hip_atomic_load(q + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-  v.w = __uint_as_float(__hip_atomic_load(q + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-  return v;
+__device__ __forceinline__ void ipc_st4(__amdgpu_buffer_rsrc_t rs, int64_t off_floats, float4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ipc_i32x4, v), rs, (int)(off_floats * 4), 0, 17);
+}
+
+__device__ __forceinline__ float4 ipc_ld4(__amdgpu_buffer_rsrc_t rs, int64_t off_floats) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off_floats * 4), 0, 17));
+}
+
+__device__ __forceinline__ bool ipc_failed(const IpcStep& s) {
+  return __hip_atomic_load(s.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+}
+
+__device__ __forceinline__ void ipc_fail(int* err, int* herr) {
+  __hip_atomic_fetch_or(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (herr) __hip_atomic_store(herr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Lanes 0..T-1 of the calling wave each wait for source rank `lane`'s flag word `idx` of this
-// generation (bounded: a timeout raises *err and gives up).
-__device__ __forceinline__ void ipc_wait_flags(const IpcStep& s, int lane, int idx) {
+// generation, then acquire.  Bounded: a missing flag with the error word already set (an
+// earlier timeout on this rank) gives up at once; otherwise the wall-clock timeout raises the
+// word.  Returns false (uniformly over the wave) when any wait gave up.
+__device__ __forceinline__ bool ipc_wait_flags(const IpcStep& s, int lane, int idx) {
+  bool ok = true;
   if (lane < s.T) {
     const uint32_t* f = s.P.flags[s.me] + ((int64_t)s.par * s.T + lane) * s.nflags + idx;
-    const uint64_t t0 = wall_clock64();
-    while ((int32_t)(ipc_poll_flag(f) - s.gen) < 0) {
-      __builtin_amdgcn_s_sleep(1);
-      if ((int64_t)(wall_clock64() - t0) > s.timeout) {
-        atomicOr(s.err, 1);
-        break;
+    if ((int32_t)(ipc_poll_flag(f) - s.gen) < 0) {
+      const uint64_t t0 = wall_clock64();
+      while ((int32_t)(ipc_poll_flag(f) - s.gen) < 0) {
+        if (ipc_failed(s)) {
+          ok = false;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        if ((int64_t)(wall_clock64() - t0) > s.timeout) {
+          ipc_fail(s.err, s.herr);
+          ok = false;
+          break;
+        }
       }
     }
   }
+  ok = __all(ok);
+  if (s.fences) ipc_acquire();
+  return ok;
 }
 
-hipError_t ipc_allreduce_launch(const IpcPeers& P, float* x, int64_t n, int T, int me, uint32_t gen, int64_t cap,
-                                int max_chunks, int* err, int64_t timeout_ticks, hipStream_t st);
+hipError_t ipc_allreduce_launch(const IpcStep& s, float* x, int64_t n, hipStream_t st);
 
 class IpcAllReduce {
  public:
@@ -106,8 +147,14 @@ class IpcAllReduce {
   std::string handle() const;
   // every rank's handle() in rank order; maps the peers' regions
   void open(const std::vector<std::string>& handles);
-  // in-place sum of n floats (n % 4 == 0; above cap: cap-sized pieces) over the ranks, on stream st (stream-ordered; NOT
-  // capturable: the flag generation is a launch argument, TpComm uses RCCL under capture)
+  // whether a buffer can go through the peer-mapped kernel: n % 4 == 0, n <= cap and a
+  // 16-B aligned address (float4 accesses); otherwise the caller uses RCCL
+  bool serves(const float* p, size_t n) const {
+    return (int64_t)n <= cap_ && n % 4 == 0 && (reinterpret_cast<uintptr_t>(p) & 15) == 0;
+  }
+  // in-place sum of n floats (n % 4 == 0, 16-B aligned; above cap: cap-sized pieces) over
+  // the ranks, on stream st (stream-ordered; NOT capturable: the flag generation is a launch
+  // argument, TpComm uses RCCL under capture)
   void allreduce_sum_f32(float* p, size_t n, hipStream_t st);
   // the next generation for a fused consumer (same sequence as allreduce_sum_f32's calls)
   IpcStep begin_step();
@@ -115,10 +162,14 @@ class IpcAllReduce {
   int rank() const { return rank_; }
   int size() const { return nranks_; }
   bool opened() const { return opened_; }
-  // device error word: nonzero after a wait timed out (synchronising read)
+  // error word: nonzero after a wait timed out.  error() synchronises; host_error() reads
+  // the host-pinned mirror without any device call (may lag the device by the work queued)
   int error() const;
+  int host_error() const { return __atomic_load_n(herr_, __ATOMIC_ACQUIRE); }
   // bound on every flag wait (default 30 s: far above any host skew between ranks)
   void set_timeout_s(double s) { timeout_ = (int64_t)(s * 1000.0 * clock_khz_); }
+  double timeout_s() const { return (double)timeout_ / (1000.0 * clock_khz_); }
+  void set_fences(bool on) { fences_ = on; }
 
  private:
   int nranks_, rank_;
@@ -127,12 +178,15 @@ class IpcAllReduce {
   float* data_ = nullptr;
   uint32_t* flags_ = nullptr;
   int* err_ = nullptr;
+  int* herr_ = nullptr;        // host-pinned (mapped) mirror of err_
+  int* herr_dev_ = nullptr;    // its device address
   IpcPeers peers_{};
   std::vector<void*> mapped_;
   uint32_t gen_ = 0;
   bool opened_ = false;
   int64_t timeout_ = 0;
   int clock_khz_ = 100000;
+  bool fences_ = true;
 };
 
 }  // namespace sl

@@ -1,12 +1,10 @@
-// One-kernel all-reduce over peer-mapped HBM for Bob's tensor-parallel step (see ipc_ar.h).
+// One-kernel all-reduce over peer-mapped HBM for Bob's tensor-parallel step (see ipc_ar.h for
+// the protocol and its memory ordering).
 //
-// Memory protocol (CDNA4, xGMI peers): the receive regions and flags are allocated
-// uncached, and every payload / flag access is a system-scope one (sc0 sc1: ipc_ar.h
-// ipc_st4 / ipc_ld4), so a peer's stores land in this GPU's HBM and no L2 line can go stale
-// between parity reuses whatever cache type a mapping gets.  A workgroup's payload stores
-// are drained (`s_waitcnt vmcnt(0)` in every wave) before the workgroup barrier, and only
-// then does one lane per destination raise that destination's flag; the reader polls its
-// own flag words with system-scope loads, then reads the slots after a workgroup barrier.
+// The receive regions and flags are allocated uncached (a peer's stores land in this GPU's
+// HBM, no L2 line can go stale between parity reuses whatever cache type a mapping gets);
+// payload moves as 16-B system-scope write-through stores and cache-bypassing loads; every
+// flag is raised behind a system-scope release and every wait ends in an acquire.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -25,48 +23,43 @@ namespace {
     if (e_ != hipSuccess) throw std::runtime_error(std::string(#cmd ": ") + hipGetErrorString(e_)); \
   } while (0)
 
-__global__ __launch_bounds__(kIpcThreads) void ipc_allreduce_kernel(IpcPeers P, float* __restrict__ x, int64_t n,
-                                                                    int T, int me, int par, uint32_t gen,
-                                                                    int64_t cap, int max_chunks, int* err,
-                                                                    int64_t timeout) {
+// Workgroup c owns floats [c * kIpcChunk, (c + 1) * kIpcChunk) of the message; flag word c.
+__global__ __launch_bounds__(kIpcThreads) void ipc_allreduce_kernel(IpcStep s, float* __restrict__ x, int64_t n) {
   const int c = blockIdx.x;
   const int64_t off = (int64_t)c * kIpcChunk + threadIdx.x * 4;
   const bool live = off < n;   // n % 4 == 0 (checked by the launcher)
   float4 v = {0.f, 0.f, 0.f, 0.f};
   if (live) v = *reinterpret_cast<const float4*>(x + off);
   // push: this chunk into slot [par][me] of every rank's region (this rank's own included)
-  const int64_t slot = ((int64_t)par * T + me) * cap + off;
+  const int64_t slot = ((int64_t)s.par * s.T + s.me) * s.cap + off;
   if (live)
-    for (int r = 0; r < T; ++r) ipc_st4(P.data[r] + slot, v);
+    for (int r = 0; r < s.T; ++r) ipc_st4(ipc_rsrc(s.P.data[r]), slot, v);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  const int64_t fme = ((int64_t)par * T + me) * max_chunks + c;
-  if (threadIdx.x < T) ipc_raise_flag(P.flags[threadIdx.x] + fme, gen);
-  // wait for every rank's chunk c of this generation (lane r polls source r)
-  if (threadIdx.x < T) {
-    const uint32_t* f = P.flags[me] + ((int64_t)par * T + threadIdx.x) * max_chunks + c;
-    const uint64_t t0 = wall_clock64();
-    while ((int32_t)(ipc_poll_flag(f) - gen) < 0) {
-      __builtin_amdgcn_s_sleep(1);
-      if ((int64_t)(wall_clock64() - t0) > timeout) {
-        atomicOr(err, 1);
-        break;
-      }
-    }
+  const int64_t fme = ((int64_t)s.par * s.T + s.me) * s.nflags + c;
+  __shared__ int s_ok;
+  if (threadIdx.x < 64) {
+    if (threadIdx.x < s.T) ipc_raise_flag(s.P.flags[threadIdx.x] + fme, s.gen, s.fences);
+    // wait for every rank's chunk c of this generation (lane r polls source r)
+    const bool ok = ipc_wait_flags(s, threadIdx.x, c);
+    if (threadIdx.x == 0) s_ok = ok ? 1 : 0;
   }
   __syncthreads();
-  if (!live) return;
+  // a wait gave up (dead / stalled peer): leave x as it was, write nothing derived from
+  // stale slots (the job aborts on the error word)
+  if (!s_ok || !live) return;
   // every slot's load in flight at once, then the fixed-order sum over ranks 0..T-1
   // (bitwise identical on every rank)
-  const float* base = P.data[me] + (int64_t)par * T * cap + off;
+  const __amdgpu_buffer_rsrc_t rs = ipc_rsrc(s.P.data[s.me]);
+  const int64_t base = (int64_t)s.par * s.T * s.cap + off;
   float4 u[kIpcMaxRanks];
 #pragma unroll
   for (int r = 0; r < kIpcMaxRanks; ++r)
-    if (r < T) u[r] = ipc_ld4(base + (int64_t)r * cap);
+    if (r < s.T) u[r] = ipc_ld4(rs, base + (int64_t)r * s.cap);
   float4 acc = u[0];
 #pragma unroll
   for (int r = 1; r < kIpcMaxRanks; ++r) {
-    if (r < T) {
+    if (r < s.T) {
       acc.x += u[r].x;
       acc.y += u[r].y;
       acc.z += u[r].z;
@@ -78,14 +71,14 @@ __global__ __launch_bounds__(kIpcThreads) void ipc_allreduce_kernel(IpcPeers P, 
 
 }  // namespace
 
-hipError_t ipc_allreduce_launch(const IpcPeers& P, float* x, int64_t n, int T, int me, uint32_t gen, int64_t cap,
-                                int max_chunks, int* err, int64_t timeout_ticks, hipStream_t st) {
+hipError_t ipc_allreduce_launch(const IpcStep& s, float* x, int64_t n, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  if (n > cap || n % 4 != 0 || T < 1 || T > kIpcMaxRanks || me < 0 || me >= T) return hipErrorInvalidValue;
+  if (n > s.cap || n % 4 != 0 || (reinterpret_cast<uintptr_t>(x) & 15) != 0 || s.T < 1 || s.T > kIpcMaxRanks ||
+      s.me < 0 || s.me >= s.T)
+    return hipErrorInvalidValue;
   const int chunks = (int)((n + kIpcChunk - 1) / kIpcChunk);
-  if (chunks > max_chunks) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(ipc_allreduce_kernel, dim3(chunks), dim3(kIpcThreads), 0, st, P, x, n, T, me,
-                     (int)(gen & 1u), gen, cap, max_chunks, err, timeout_ticks);
+  if (chunks > s.nflags) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(ipc_allreduce_kernel, dim3(chunks), dim3(kIpcThreads), 0, st, s, x, n);
   return hipGetLastError();
 }
 
@@ -97,11 +90,15 @@ IpcAllReduce::IpcAllReduce(int nranks, int rank, int64_t cap) : nranks_(nranks),
   max_chunks_ = std::max((int)(cap_ / kIpcChunk), kIpcFlags);
   const size_t dbytes = sizeof(float) * 2 * (size_t)nranks * (size_t)cap_;
   const size_t fbytes = sizeof(uint32_t) * 2 * (size_t)nranks * (size_t)max_chunks_;
+  if (dbytes / 4 > 0x7fffffff / 4) throw std::runtime_error("IpcAllReduce: region above 2 GB");
   SL_HIP_THROW(hipExtMallocWithFlags(reinterpret_cast<void**>(&data_), dbytes, hipDeviceMallocUncached));
   SL_HIP_THROW(hipExtMallocWithFlags(reinterpret_cast<void**>(&flags_), fbytes, hipDeviceMallocUncached));
   SL_HIP_THROW(hipMemset(flags_, 0, fbytes));
-  SL_HIP_THROW(hipMalloc(reinterpret_cast<void**>(&err_), sizeof(int)));
+  SL_HIP_THROW(hipExtMallocWithFlags(reinterpret_cast<void**>(&err_), sizeof(int), hipDeviceMallocUncached));
   SL_HIP_THROW(hipMemset(err_, 0, sizeof(int)));
+  SL_HIP_THROW(hipHostMalloc(reinterpret_cast<void**>(&herr_), sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
+  *herr_ = 0;
+  SL_HIP_THROW(hipHostGetDevicePointer(reinterpret_cast<void**>(&herr_dev_), herr_, 0));
   SL_HIP_THROW(hipDeviceSynchronize());
   int dev = 0, khz = 0;
   SL_HIP_THROW(hipGetDevice(&dev));
@@ -115,6 +112,7 @@ IpcAllReduce::~IpcAllReduce() {
   if (data_) hipFree(data_);
   if (flags_) hipFree(flags_);
   if (err_) hipFree(err_);
+  if (herr_) hipHostFree(herr_);
 }
 
 std::string IpcAllReduce::handle() const {
@@ -154,13 +152,14 @@ void IpcAllReduce::open(const std::vector<std::string>& handles) {
 
 void IpcAllReduce::allreduce_sum_f32(float* p, size_t n, hipStream_t st) {
   if (!opened_) throw std::runtime_error("IpcAllReduce: open() first");
-  if (n % 4 != 0) throw std::runtime_error("IpcAllReduce: n % 4 != 0");
+  if (n % 4 != 0 || (reinterpret_cast<uintptr_t>(p) & 15) != 0)
+    throw std::runtime_error("IpcAllReduce: n % 4 != 0 or a buffer not 16-B aligned");
   // a message above the capacity goes as consecutive cap-sized pieces (every rank issues
   // the same sequence, so the generations stay in step)
   for (size_t o = 0; o < n; o += (size_t)cap_) {
     const int64_t m = std::min<int64_t>(cap_, (int64_t)(n - o));
-    ++gen_;
-    SL_HIP_THROW(ipc_allreduce_launch(peers_, p + o, m, nranks_, rank_, gen_, cap_, max_chunks_, err_, timeout_, st));
+    const IpcStep s = begin_step();
+    SL_HIP_THROW(ipc_allreduce_launch(s, p + o, m, st));
   }
 }
 
@@ -176,14 +175,16 @@ IpcStep IpcAllReduce::begin_step() {
   s.cap = cap_;
   s.nflags = max_chunks_;
   s.err = err_;
+  s.herr = herr_dev_;
   s.timeout = timeout_;
+  s.fences = fences_ ? 1 : 0;
   return s;
 }
 
 int IpcAllReduce::error() const {
   int e = 0;
   SL_HIP_THROW(hipMemcpy(&e, err_, sizeof(int), hipMemcpyDeviceToHost));
-  return e;
+  return e | host_error();
 }
 
 }  // namespace sl

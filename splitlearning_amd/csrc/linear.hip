@@ -212,9 +212,8 @@ static bool fwd_once_plan(int M, int N, int K, int max_split, int64_t ws_elems, 
     S = 1;
     return true;
   }
-  // waves per workgroup (variant 14: 3 -> 4, 4 -> 16, for A/B; default 8)
-  const int nwt = g_variant[14] == 3 ? 4 : (g_variant[14] == 4 ? 16 : 8);
-  NW = std::min(waves, nwt);
+  // 8 waves per workgroup (4 and 16 measured no better, docs/PERF.md)
+  NW = std::min(waves, 8);
   S = (waves + NW - 1) / NW;
   if (S > smax) {
     S = smax;
@@ -404,101 +403,6 @@ skinny_dgrad_kernel(const float* __restrict__ dZ, int ldz, const float* __restri
   }
 }
 
-// Full-N dgrad: dX[M, K] = mask(dZ[M, N] . W[N, K]) with the WHOLE reduction over N inside
-// one workgroup, so the result is stored masked and final (no split-N slabs, no reduce
-// launch).  grid (ceil(K/32), ceil(M/16)), 1024 threads = 16 waves; wave w owns an N slice.
-// MFMA v_mfma_f32_16x16x4f32 with A = dZ (16 rows m x 4 n), B = W (4 n x 16 k): the 32
-// k-columns of the workgroup are two 16-column MFMA tiles fed by one float2 load per lane
-// (16 lanes x 8 B = one 128-B row segment of W per n).  Lane (m = lane&15, q = lane>>4) takes
-// n = n0 + 4q + s at sub-step s, so its four dZ values of a 16-n group are one float4 load.
-// The 16 waves' partial tiles are summed through LDS in a fixed order (deterministic).
-// At B = 16 this reads W once (fc2: 20 MB) from 157 workgroups; the split-N form it replaces
-// needed ~630 workgroups plus a reduce launch over the slabs.
-template <int NC>   // columns per lane: 2 (32-column tiles, float2 loads) or 1 (16-column tiles)
-__global__ void __launch_bounds__(1024)
-dgrad_fulln_kernel(const float* __restrict__ dZ, int ldz, const float* __restrict__ W, int ldw,
-                   const float* __restrict__ hprev, int ldh, float scale, float* __restrict__ out, int ldo,
-                   int M, int N, int K) {
-  __shared__ f32x4 red[16][NC][64];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int k0 = blockIdx.x * 16 * NC, m0 = blockIdx.y * 16;
-  const int j = lane & 15, q = lane >> 4;
-  const int kc = k0 + NC * j;                      // this lane's NC columns kc ..
-  const bool vk = kc + NC - 1 < K;                 // K % 4 == 0 (host check): never straddles K
-  const bool vm = (m0 + j) < M;
-  // N slice of this wave: multiples of 16
-  const int nper = ((N + 16 * 16 - 1) / (16 * 16)) * 16;
-  const int nb = wv * nper, ne = min(N, nb + nper);
-  const float* za = dZ + (int64_t)(vm ? m0 + j : 0) * ldz;
-  f32x4 acc[NC];
-#pragma unroll
-  for (int c = 0; c < NC; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto ldw_ = [&](int nn) {
-    float2 r = make_float2(0.f, 0.f);
-    if (NC == 2)
-      r = *reinterpret_cast<const float2*>(W + (int64_t)nn * ldw + kc);
-    else
-      r.x = W[(int64_t)nn * ldw + kc];
-    return r;
-  };
-  constexpr int U = 4;                             // 16-n groups in flight per lane
-  int n = nb;
-  for (; n + 16 * U <= ne; n += 16 * U) {
-    float4 a[U];
-    float2 w[U][4];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int nq = n + 16 * u + 4 * q;
-      a[u] = vm ? *reinterpret_cast<const float4*>(za + nq) : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-      for (int s = 0; s < 4; ++s) w[u][s] = vk ? ldw_(nq + s) : make_float2(0.f, 0.f);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const float av[4] = {a[u].x, a[u].y, a[u].z, a[u].w};
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        acc[0] = mfma4(av[s], w[u][s].x, acc[0]);
-        if (NC == 2) acc[NC - 1] = mfma4(av[s], w[u][s].y, acc[NC - 1]);
-      }
-    }
-  }
-  for (; n < ne; n += 16) {                        // tail groups (N % 16 handled per element)
-    const int nq = n + 4 * q;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int nn = nq + s;
-      const bool in = nn < ne;
-      const float av = (vm && in) ? za[nn] : 0.f;
-      const float2 wv2 = (vk && in) ? ldw_(nn) : make_float2(0.f, 0.f);
-      acc[0] = mfma4(av, wv2.x, acc[0]);
-      if (NC == 2) acc[NC - 1] = mfma4(av, wv2.y, acc[NC - 1]);
-    }
-  }
-#pragma unroll
-  for (int c = 0; c < NC; ++c) red[wv][c][lane] = acc[c];
-  __syncthreads();
-  // 256 NC outputs: thread t -> (column half h, lane l); D_h[row][col]: row = 4*(l>>4) + r, col j = l & 15
-  const int t = threadIdx.x;
-  if (t < 64 * NC) {
-    const int h = t >> 6, l = t & 63;
-    f32x4 sm = red[0][h][l];
-#pragma unroll
-    for (int v = 1; v < 16; ++v) sm += red[v][h][l];
-    const int kk = k0 + NC * (l & 15) + h;
-    if (kk < K) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + 4 * (l >> 4) + r;
-        if (m >= M) continue;
-        float v = sm[r];
-        if (hprev) v = (hprev[(int64_t)m * ldh + kk] > 0.f) ? v * scale : 0.f;
-        out[(int64_t)m * ldo + kk] = v;
-      }
-    }
-  }
-}
-
 __global__ void dgrad_reduce_kernel(const float* __restrict__ P, int S, int64_t slab,
                                     const float* __restrict__ hprev, int ldh, float scale,
                                     float* __restrict__ out, int ldo, int M, int K) {
@@ -624,7 +528,7 @@ hipError_t linear_fwd(const float* X, int ldx, const float* W, int ldw, float* Y
   if (M > 128) return gemm_nt(X, ldx, W, ldw, Y, ldy, M, N, K, e, g_bf16 != 0, st);
   dim3 grid((N + 15) / 16, (M + 15) / 16);
   int NW1, S1;
-  if (!g_bf16 && g_variant[14] != 2 && fwd_once_plan(M, N, K, 16, ws ? ws_elems : 0, NW1, S1)) {
+  if (!g_bf16 && fwd_once_plan(M, N, K, 16, ws ? ws_elems : 0, NW1, S1)) {
     skinny_fwd_once_kernel<4><<<dim3(grid.x, grid.y, S1), NW1 * 64, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e, ws,
                                                                           (int64_t)M * N);
     if (S1 > 1) {
@@ -667,38 +571,20 @@ hipError_t linear_dgrad(const float* dZ, int ldz, const float* W, int ldw, const
                         hipStream_t st) {
   if (M <= 0 || K <= 0) return hipSuccess;
   const int kt = (K + 63) / 64, mt = (M + 15) / 16;
-  // variant 8 = 2: the full-N form (reduction over N inside one workgroup, masked store, one
-  // launch).  Measured through the native executor it LOST to the split-N + reduce pair
-  // below at every TP shard (us per server step, TP = 1 / 2 / 4 / 8: 171.9 / 104.4 / 72.5 /
-  // 55.6 full-N vs 170.9 / 101.6 / 68.9 / 51.8 split; profiles/r2_dgrad_fulln_ab.txt): with
-  // the whole N per workgroup there are only K/32 workgroups (20 at a TP = 8 shard), each a
-  // chain of 1000-row strided reads, and the reduce launch is cheaper than that latency.
-  // variant 8 = 3: the same with 16-column tiles (twice the workgroups, one float per lane):
-  // also slower than the split pair, us per step at TP = 1 / 2 / 4 / 8: 179.2 / 103.2 / 70.8 /
-  // 54.6 vs 176.8 / 101.0 / 68.5 / 51.8 (profiles/r2_dgrad_fulln16_ab.txt).
-  if ((g_variant[8] == 2 || g_variant[8] == 3) && !g_bf16 && M <= 64 && (K & 3) == 0 && (ldw & 1) == 0 &&
-      (ldz & 3) == 0) {
-    if (g_variant[8] == 3) {
-      dgrad_fulln_kernel<1><<<dim3((K + 15) / 16, mt), 1024, 0, st>>>(dZ, ldz, W, ldw, hprev, ldh, scale, dX, ldx, M,
-                                                                       N, K);
-    } else {
-      dgrad_fulln_kernel<2><<<dim3((K + 31) / 32, mt), 1024, 0, st>>>(dZ, ldz, W, ldw, hprev, ldh, scale, dX, ldx, M,
-                                                                       N, K);
-    }
-    return hipGetLastError();
-  }
+  // A full-N form (the whole reduction over N in one workgroup, masked store, one launch)
+  // LOST to this split-N + reduce pair at every TP shard (us per server step, TP = 1 / 2 / 4 /
+  // 8: 171.9 / 104.4 / 72.5 / 55.6 vs 170.9 / 101.6 / 68.9 / 51.8; profiles/r2_dgrad_fulln_ab.txt):
+  // only K/32 workgroups, each a chain of strided reads.  Removed in round 3 (git history).
   int S = 1;
   // aim for >= ~256 workgroups on the 256-CU part; split N when there are few K tiles.
-  // Variant 5, for A/B: 1 = never split, >1 = max split with N slices down to 16 rows.
-  // Both measured slower or equal at every TP shard (at TP = 8: 57.6 us per native-executor
-  // server step unsplit vs 51.8 us split; profiles/r1_dgrad_split_ab.txt).
-  const int v5 = g_variant[5];
-  const int smax = v5 > 0 ? v5 : 16;
+  // Never splitting measured slower at every TP shard (TP = 8: 57.6 vs 51.8 us per native
+  // server step; profiles/r1_dgrad_split_ab.txt).
+  const int smax = 16;
   // few K tiles over a long N (a TP shard's fc2: K = 628, N = 1000 at TP = 8): N slices down
   // to 32 rows (S = 16): 3.1 vs 3.7 us per launch in the graph-replay probe
   // (scripts/probe/dgrad_probe.hip).  Short N (the U-shape fc2, N = 100) stays unsplit: one
   // launch with the mask fused beats a split plus a reduce launch.
-  const int rmin = v5 > 1 ? 16 : ((kt * mt <= 64 && N >= 512) ? 32 : 64);
+  const int rmin = (kt * mt <= 64 && N >= 512) ? 32 : 64;
   while (S < smax && kt * mt * S < 768 && N / (S * 2) >= rmin) S *= 2;
   const int64_t slab = (int64_t)M * K;
   if (ws == nullptr) S = 1;
@@ -711,122 +597,15 @@ hipError_t linear_dgrad(const float* dZ, int ldz, const float* W, int ldw, const
       skinny_dgrad_kernel<8><<<grid, 512, 0, st>>>(dZ, ldz, W, ldw, hprev, ldh, scale, dX, ldx, 0, M, N, K);
   } else {
     // XCD-grouped order when S / 8 N slices make one 128-row group of the forward (S = 8 at
-    // TP = 1, S = 16 at a TP = 8 shard; variant 19 = 2: plain order)
+    // TP = 1, S = 16 at a TP = 8 shard)
     const int nblk = ((N + 4 * S - 1) / (4 * S)) * 4;
-    const int xg = (g_variant[19] != 2 && S % 8 == 0 && nblk * (S / 8) == 128) ? S / 8 : 0;
+    const int xg = (S % 8 == 0 && nblk * (S / 8) == 128) ? S / 8 : 0;
     if (g_bf16)
       skinny_dgrad_kernel<8, true><<<grid, 512, 0, st>>>(dZ, ldz, W, ldw, nullptr, 0, 1.f, ws, 0, slab, M, N, K, xg);
     else
       skinny_dgrad_kernel<8><<<grid, 512, 0, st>>>(dZ, ldz, W, ldw, nullptr, 0, 1.f, ws, 0, slab, M, N, K, xg);
     launch_dgrad_reduce(ws, S, slab, hprev, ldh, scale, dX, ldx, M, K, st);
   }
-  return hipGetLastError();
-}
-
-// fc1's look-ahead epilogue fused into fc2's split-K forward (single-shard tail, variant 18
-// = 1).  Workgroup (ks, nr, mt) owns the 64-wide k-slice ks of h1 for 16 rows: it reduces
-// the S1 look-ahead slabs of that slice in slab order (bitwise the epilogue kernel's sum),
-// applies fc1's bias / ReLU / dropout (writing h1 when nr == 0), stages the tile in LDS and
-// forms the slice's partial product with fc2's 128 output columns nr on exact-fp32 MFMA;
-// P2 gets one slab per k-slice for the head to reduce.  The W2 loads are issued first, so
-// they overlap the slab reduction.  The k-slice runs fastest in the grid, padded to a
-// multiple of 8, so the 8 column ranges of one slice share an XCD (and its L2 copy of the
-// slabs).  Removes the epilogue launch — and measured slower through the native executor
-// (us per TP = 1 step, profiles/r2_lookahead_fc2_fused_ab.txt): 173.0 (64-wide slices) and
-// 176.5 (128-wide) vs 170.8 for the epilogue + split-K forward pair.  The slab round trip now
-// sits in front of every workgroup's MFMAs, and the head reduces 79 / 40 product slabs
-// instead of the forward's 16: more latency than the launch boundary it saves.  Opt-in.
-template <int LKS>
-__global__ void __launch_bounds__(256)
-lookahead_fc2_fwd_kernel(const float* __restrict__ pn, int S1, int64_t slab1, Epi e1, float* __restrict__ h1,
-                         const float* __restrict__ W2, float* __restrict__ P2, int64_t slab2, int M, int N1, int N2,
-                         int nks) {
-  __shared__ float At[16][LKS + 4];
-  const int ks = blockIdx.x;
-  if (ks >= nks) return;                                 // grid padding (XCD grouping)
-  const int nr = blockIdx.y, m0 = blockIdx.z * 16, k0 = ks * LKS;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int q4 = (lane >> 4) * 4, j = lane & 15;
-  constexpr int U = LKS / 16;
-  // W2 rows of this wave's two 16-column tiles: every load before anything else
-  float4 w[2][U];
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int n = (nr * 8 + 2 * wv + t) * 16 + j;
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int kk = k0 + 16 * u + q4;
-      w[t][u] = (n < N2 && kk < N1) ? ld4(W2 + (int64_t)n * N1 + kk) : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-  }
-  // h1 tile: thread -> (row r, float4 columns c4, c4 + 16, ...); the slabs summed in order
-  // from 0
-  const int r = tid >> 4;
-#pragma unroll
-  for (int c4 = tid & 15; c4 < LKS / 4; c4 += 16) {
-    const int m = m0 + r, k = k0 + 4 * c4;
-    f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if (m < M && k < N1) {
-      const float* p = pn + (int64_t)m * N1 + k;
-      constexpr int SU = 32;
-      for (int s0 = 0; s0 < S1; s0 += SU) {
-        float4 rr[SU];
-#pragma unroll
-        for (int i = 0; i < SU; ++i)
-          rr[i] = (s0 + i < S1) ? ld4(p + (int64_t)(s0 + i) * slab1) : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-        for (int i = 0; i < SU; ++i) v += f32x4{rr[i].x, rr[i].y, rr[i].z, rr[i].w};
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = apply_epi(e1, v[i], m, k + i);
-      if (nr == 0) *reinterpret_cast<f32x4*>(h1 + (int64_t)m * N1 + k) = v;
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) At[r][4 * c4 + i] = v[i];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int n0 = (nr * 8 + 2 * wv + t) * 16;
-    if (n0 >= N2) break;
-    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const float* ar = &At[j][16 * u + q4];
-      acc0 = mfma4(ar[0], w[t][u].x, acc0);
-      acc1 = mfma4(ar[1], w[t][u].y, acc1);
-      acc0 = mfma4(ar[2], w[t][u].z, acc0);
-      acc1 = mfma4(ar[3], w[t][u].w, acc1);
-    }
-    const f32x4 sm = acc0 + acc1;
-    const int n = n0 + j;
-    if (n < N2) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + q4 + r;
-        if (m < M) P2[(int64_t)ks * slab2 + (int64_t)m * N2 + n] = sm[r];
-      }
-    }
-  }
-}
-
-// k-slice width: variant 18 = 1 -> 64, = 2 -> 128
-static int lookahead_ks() { return g_variant[18] == 2 ? 128 : 64; }
-int lookahead_fc2_slices(int N1) { return (N1 + 63) / 64; }   // capacity bound (the narrower slice)
-
-hipError_t lookahead_fc2_fwd(const float* pn, int S1, int64_t slab1, Epi e1, float* h1, const float* W2, float* P2,
-                             int64_t p2_elems, int M, int N1, int N2, int* S2_out, hipStream_t st) {
-  *S2_out = 0;
-  if (M <= 0) return hipSuccess;
-  const int ks = lookahead_ks();
-  const int nks = (N1 + ks - 1) / ks;
-  if ((N1 & 3) || S1 < 1 || (int64_t)nks * M * N2 > p2_elems) return hipErrorInvalidValue;
-  const dim3 g((nks + 7) / 8 * 8, (N2 + 127) / 128, (M + 15) / 16);
-  if (ks == 128)
-    lookahead_fc2_fwd_kernel<128><<<g, 256, 0, st>>>(pn, S1, slab1, e1, h1, W2, P2, (int64_t)M * N2, M, N1, N2, nks);
-  else
-    lookahead_fc2_fwd_kernel<64><<<g, 256, 0, st>>>(pn, S1, slab1, e1, h1, W2, P2, (int64_t)M * N2, M, N1, N2, nks);
-  *S2_out = nks;
   return hipGetLastError();
 }
 
@@ -845,13 +624,13 @@ hipError_t linear_fwd_partial(const float* X, int ldx, const float* W, int ldw, 
   if (ws_elems < slab * S) S = 1;
   if (ws_elems < slab) return hipErrorInvalidValue;
   int NW1, S1;
-  if (!g_bf16 && g_variant[14] != 2 && fwd_once_plan(M, N, K, max_split, ws_elems, NW1, S1)) {
+  if (!g_bf16 && fwd_once_plan(M, N, K, max_split, ws_elems, NW1, S1)) {
     Epi e1{};
     e1.dscale = 1.f;
-    // XCD-grouped tile order (at most 64 column tiles: grid padded to 64); variant 19 = 2:
-    // plain order.  Native executor, us per TP = 1 step: 174.4 vs 175.5 and 176.9 vs 178.1 in
-    // two interleaved runs (profiles/r2_xcd_grouped_fc2_ab.txt); bitwise the same products.
-    const bool xg = g_variant[19] != 2 && grid.x <= 64;
+    // XCD-grouped tile order (at most 64 column tiles: grid padded to 64).  Native executor,
+    // us per TP = 1 step against the plain order: 174.4 vs 175.5 and 176.9 vs 178.1 in two
+    // interleaved runs (profiles/r2_xcd_grouped_fc2_ab.txt); bitwise the same products.
+    const bool xg = grid.x <= 64;
     skinny_fwd_once_kernel<4><<<dim3(xg ? 64 : grid.x, grid.y, S1), NW1 * 64, 0, st>>>(
         X, ldx, W, ldw, ws, N, M, N, K, e1, ws, slab, xg ? (int)grid.x : 0);
     *S_out = S1;

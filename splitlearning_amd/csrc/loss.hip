@@ -400,7 +400,7 @@ hipError_t head_step(const float* X, float* W, float* b, const int64_t* y, int64
   if (M <= 0) return hipSuccess;
   if (M * K > 4096 || C * K > 4096 || M * C > 1024) return hipErrorInvalidValue;
   const bool al = ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(W)) & 15) == 0;
-  if (M <= 16 && C <= 16 && K <= 128 && (K & 3) == 0 && C * K <= 2048 && al && g_variant[15] != 1) {
+  if (M <= 16 && C <= 16 && K <= 128 && (K & 3) == 0 && C * K <= 2048 && al) {
     if (g_bf16)
       head_step_mfma_kernel<true><<<1, 256, 0, st>>>(X, W, b, y, ignore, scale, loss_rows, dX, W, b, s0w, s1w, s0b,
                                                      s1b, M, K, C, o, mask_dx ? 1 : 0);

@@ -88,6 +88,9 @@ class TailEngine:
         self.dz: list[torch.Tensor] = []
         self._train_fwd = False
         self._pre = None          # pending look-ahead fc1 partial slabs (see fused_step)
+        # cross-entropy groups of the last layer's outputs (SISA-concat: one 100-way head per
+        # client, protocols/concat.py); 1 = one softmax over all outputs
+        self.ce_groups = 1
 
     # ------------------------------------------------------------------ forward
     def forward(self, x: torch.Tensor, train: bool | None = None, dseeds=None, pre: bool = False) -> torch.Tensor:
@@ -122,6 +125,32 @@ class TailEngine:
         return h
 
     __call__ = forward
+
+    def forward_block(self, x: torch.Tensor, k_off: int, out_off: int, out_len: int) -> torch.Tensor:
+        """Inference (no dropout) of the tail on an input that is non-zero only in layer 0's
+        input columns [k_off, k_off + x.shape[1]), returning only the last layer's outputs
+        [out_off, out_off + out_len): layer 0 multiplies just that column block of its weight
+        and the last layer just those rows.  SISA-concat evaluation (protocols/concat.py):
+        Alice j's activation in slot j, zeros elsewhere, read head j — without forming the
+        zero-padded [rows, 5408 k] input or the other k - 1 heads."""
+        self.fwd_count += 1
+        h = x
+        n = len(self.layers)
+        for i, L in enumerate(self.layers):
+            ls = L.spec
+            W, b = L.W, L.b
+            if i == 0:
+                W = W[:, k_off:k_off + x.shape[1]]
+            if i == n - 1:
+                W, b = W[out_off:out_off + out_len], b[out_off:out_off + out_len]
+            if L.style == "row":
+                part = self.ops.linear_fwd(h, W, None, False, 0.0, 0, 0)
+                self.allreduce(part)
+                h = self.ops.linear_epilogue(part, b, ls.relu, 0.0, 0, 0)
+            else:
+                h = self.ops.linear_fwd(h, W, b, ls.relu, 0.0, 0, L.col_off)
+        self.acts = []
+        return h
 
     # ------------------------------------------------------------------ backward
     def backward_dgrad(self, dout: torch.Tensor, need_dx: bool, premasked: bool = False):
@@ -178,7 +207,7 @@ class TailEngine:
         `backward_dgrad`.  `x_next`: also form the next batch's layer-0 product with the updated
         weights, consumed by `forward(x_next, pre=True)` (no separate read of W0)."""
         t = slot.tick() if t is None else t
-        layers = [(self.dz[i], None, None, 1.0, self.acts[i], L.W, slot.state(f"{prefix}{L.spec.name}.weight", L.W),
+        layers = [(self.dz[i], self.acts[i], L.W, slot.state(f"{prefix}{L.spec.name}.weight", L.W),
                    L.b, slot.state(f"{prefix}{L.spec.name}.bias", L.b)) for i, L in enumerate(self.layers)]
         pn = None
         if x_next is not None:
@@ -261,20 +290,11 @@ class TailEngine:
             P1 = self._pre
             assert P1 is not None and P1.shape[1] == M, "no pending look-ahead for this batch"
             self._pre = None
-            if self._lookahead_fc2():
-                # variant 18 = 1: the epilogue inside fc2's split-K forward (as the native
-                # executor does: csrc/engine.cpp lookahead_fc2)
-                h1, P2 = ops.lookahead_fc2_fwd(P1, L1.b, p1, seeds[0], L1.col_off, L2.W, **ds(0))
-            else:
-                h1 = ops.linear_epilogue(P1, L1.b, True, p1, seeds[0], L1.col_off, **ds(0))
+            h1 = ops.linear_epilogue(P1, L1.b, True, p1, seeds[0], L1.col_off, **ds(0))
         else:
             self._pre = None
             h1 = ops.linear_fwd(x, L1.W, L1.b, True, p1, seeds[0], L1.col_off, **ds(0))
-        if L2.style != "row" and hasattr(ops, "server_fc2_head") and ops.C().get_variant(12) == 2:
-            # variant 12 = 2: fc2's forward fused into the head (measured slower: csrc/engine.cpp)
-            h2, dlog, dz2, loss = ops.server_fc2_head(h1, L2.W, L2.b, True, p2, seeds[1], L3.W, L3.b, labels,
-                                                      1.0 / M, **ds(1))
-        elif L2.style == "row":
+        if L2.style == "row":
             if L2.W.shape[1] <= 1280:
                 # small K shard (TP >= 4): one unsplit product, all-reduced as is — no
                 # split-K reduce launch before the collective
@@ -282,11 +302,9 @@ class TailEngine:
             else:
                 P2 = ops.linear_fwd(h1, L2.W, None, False, 0.0, 0, 0)
             self.allreduce(P2)
-        elif P2 is None:
+        else:
             P2 = ops.linear_fwd_partial(h1, L2.W)
-        if L2.style == "row" or not hasattr(ops, "server_fc2_head") or ops.C().get_variant(12) != 2:
-            h2, dlog, dz2, loss = ops.server_head3(P2, L2.b, True, p2, seeds[1], L3.W, L3.b, labels, 1.0 / M,
-                                                   **ds(1))
+        h2, dlog, dz2, loss = ops.server_head3(P2, L2.b, True, p2, seeds[1], L3.W, L3.b, labels, 1.0 / M, **ds(1))
         s1 = 1.0 / (1.0 - p1) if p1 else 1.0
         dx = None
         # dz1 is materialised (split-N dgrad + reduce/mask kernel): reducing the split-N
@@ -297,18 +315,10 @@ class TailEngine:
         dz1 = ops.linear_dgrad(dz2, L2.W, h1, s1)
         if need_dx:
             dx = ops.linear_dgrad(dz1, L1.W, None, 1.0)
-        src1 = (dz1, None, None, 1.0)
         self.acts = [x, h1, h2]
-        self._wg = [src1 + (x,), (dz2, None, None, 1.0, h1), (dlog, None, None, 1.0, h2)]
+        self._wg = [(dz1, x), (dz2, h1), (dlog, h2)]
         self._train_fwd = True
         return loss, dx
-
-    def _lookahead_fc2(self) -> bool:
-        """Single-shard tail with the fused look-ahead epilogue + fc2 forward (variant 18 = 1)."""
-        ops = self.ops
-        L2 = self.layers[1]
-        return (L2.style != "row" and hasattr(ops, "lookahead_fc2_fwd") and ops.C().get_variant(18) >= 1
-                and ops.C().get_variant(12) != 2)
 
     def fused_step(self, slot: OptSlot, t: int | None = None, dyn=None, prefix: str = "", x_next=None):
         """Optimizer step of all three layers in one launch.  `x_next`: the next batch's
@@ -317,8 +327,8 @@ class TailEngine:
         of twice (fc1's 108 MB forward read disappears; train_fwd_bwd3(pre=True) consumes)."""
         t = slot.tick() if t is None else t
         layers = []
-        for (dz, dzp, hm, ms, A), L in zip(self._wg, self.layers):
-            layers.append((dz, dzp, hm, ms, A, L.W, slot.state(f"{prefix}{L.spec.name}.weight", L.W), L.b,
+        for (dz, A), L in zip(self._wg, self.layers):
+            layers.append((dz, A, L.W, slot.state(f"{prefix}{L.spec.name}.weight", L.W), L.b,
                            slot.state(f"{prefix}{L.spec.name}.bias", L.b)))
         pn = None
         if x_next is not None:
@@ -340,19 +350,22 @@ class TailEngine:
         return self.tp_size == 1
 
     def run_native_epoch(self, acts: torch.Tensor, labels: torch.Tensor, slot: OptSlot, B: int, pre: bool,
-                         lookahead: bool = True) -> torch.Tensor:
+                         lookahead: bool = True, gscale: torch.Tensor | None = None) -> torch.Tensor:
         """One epoch of fused server steps over `acts`/`labels` (batches of B, last one
         partial) issued from C++ (`_C.ServerEpoch`, csrc/engine.cpp): the same launches,
         seeds and step counts as looping `train_fwd_bwd3` + `fused_step`, without a
         Python round trip per step.  `pre`: the first batch's fc1 product is pending
-        (`lookahead_prologue`).  Returns the per-row losses."""
+        (`lookahead_prologue`).  With `ce_groups` = G > 1 (SISA-concat), labels and `gscale`
+        (each row-and-group's loss scale) are [n, G].  Returns the per-row losses ([n, G])."""
         ex = self._native_executor(slot, B)
         d = self._native[3]
         if pre:
             assert self._pre is not None and self._pre.data_ptr() == d["pn"].data_ptr(), \
                 "pending look-ahead is not in the executor's slab buffer"
-        loss = torch.empty(acts.shape[0], device=self.device)
-        fc, t, pre = ex.run(acts, labels, loss, self.seed_base, self.fwd_count, slot.t, pre, lookahead)
+        G = self.ce_groups
+        loss = torch.empty((acts.shape[0], G) if G > 1 else acts.shape[0], device=self.device)
+        fc, t, pre = ex.run(acts, labels.reshape(-1), loss, self.seed_base, self.fwd_count, slot.t, pre, lookahead,
+                            gscale.reshape(-1).contiguous() if gscale is not None else None)
         self.fwd_count, slot.t = int(fc), int(t)
         # the executor's own slab buffer holds the pending product (not a re-fetched one)
         self._pre = d["pn"] if pre else None
@@ -362,7 +375,7 @@ class TailEngine:
         cached = getattr(self, "_native", None)
         # the executor holds raw workspace addresses: rebuild it when a workspace it uses
         # has been replaced (grown) since it was built
-        if (cached is not None and cached[0] is slot and cached[1] == B
+        if (cached is not None and cached[0] is slot and cached[1] == B and cached[3]["groups"] == self.ce_groups
                 and cached[3]["pn"].data_ptr() == self.lookahead_slabs(B).data_ptr()):
             return cached[2]
         ops, dev = self.ops, self.device
@@ -382,13 +395,13 @@ class TailEngine:
              "p1": L1.spec.dropout, "p2": L2.spec.dropout, "col_off1": L1.col_off, "row2": L2.style == "row",
              "comm": getattr(self.allreduce, "comm", None) if L2.style == "row" else None,
              "ipc": getattr(self.allreduce, "ipc", None) if L2.style == "row" else None, "B": B,
+             "groups": self.ce_groups,
              "emulate_tp": L2.style == "row" and self.allreduce is None,
              "pn": self.lookahead_slabs(B),
-             "p2ws": ops._workspace(dev, max(16, ops.C().lookahead_fc2_slices(N1)) * B * N2, "fc2p" + tg),
+             "p2ws": ops._workspace(dev, 16 * B * N2, "fc2p" + tg),
              "fwdws": ops._workspace(dev, 16 * B * nmax, "fwd" + tg),
              "dgws": ops._workspace(dev, 16 * B * kmax, "dgrad" + tg),
-             "headws": ops._workspace(dev, max(ops.C().head3_slices(N2), ops.C().fc2_head_tiles(N2)) * B * C,
-                                      "head" + tg),
+             "headws": ops._workspace(dev, ops.C().head3_slices(N2) * B * C, "head" + tg),
              "h1": torch.empty(B, N1, device=dev), "h2": torch.empty(B, N2, device=dev),
              "dz1": torch.empty(B, N1, device=dev), "dz2": torch.empty(B, N2, device=dev),
              "dlog": torch.empty(B, C, device=dev)}

@@ -300,58 +300,23 @@ def linear_fwd_partial(x, w, max_split: int = 16, key: str = "fc2p"):
     return ws[:S * M * N].view(S, M, N)
 
 
-def lookahead_fc2_fwd(P1, b1, drop_p: float, seed: int, col_offset: int, w2, dseed=None, key: str = "fc2p"):
-    """fc1's look-ahead slabs P1 [S1, M, N1] -> (h1 [M, N1], fc2's split-K product slabs
-    [S2, M, N2]) in one launch (csrc/linear.hip lookahead_fc2_fwd_kernel, variant 18 = 1)."""
-    S1, M, N1 = P1.shape
-    N2 = w2.shape[0]
-    c = C()
-    ws = _workspace(P1.device, max(16, c.lookahead_fc2_slices(N1)) * M * N2, key)
-    h1 = torch.empty(M, N1, device=P1.device, dtype=torch.float32)
-    S2 = c.lookahead_fc2_fwd(P1, b1.detach() if b1 is not None else None, float(drop_p), seed & M64, col_offset,
-                             _ptr(dseed), h1, w2.detach(), ws)
-    return h1, ws[:S2 * M * N2].view(S2, M, N2)   # S2 = ceil(N1 / k-slice width)
-
-
-def linear_dgrad_partial(dz, w, key: str = "dz1p"):
-    """dz @ w as un-reduced split-N slabs [S, M, K] (no mask)."""
-    M, K = dz.shape[0], w.shape[1]
-    ws = _workspace(dz.device, 16 * M * K, key)
-    S = C().linear_dgrad_partial(dz, w.detach(), ws)
-    return ws[:S * M * K].view(S, M, K)
-
-
 def server_head3(P2, b2, relu2: bool, drop2: float, seed2: int, W3, b3, labels, scale: float,
-                 ignore_index: int = -100, dseed=None):
-    """fc2 epilogue + fc3 + softmax-CE + fc3 dgrad + fc2 ReLU/dropout backward, one kernel.
-    Returns (h2, dlogits, dz2, loss_rows)."""
+                 ignore_index: int = -100, dseed=None, groups: int = 1, gscale=None):
+    """fc2 epilogue + fc3 + softmax-CE + fc3 dgrad + fc2 ReLU/dropout backward in one launch.
+    `groups` > 1: the logits are that many cross-entropy groups (SISA-concat's heads) with
+    labels [M, groups] and per-(row, group) scales `gscale` (else `scale`).
+    Returns (h2, dlogits, dz2, loss_rows [M] or [M, groups])."""
     M, N2 = P2.shape[-2], P2.shape[-1]
     dev = P2.device
     h2 = torch.empty(M, N2, device=dev)
     dz2 = torch.empty(M, N2, device=dev)
     dlog = torch.empty(M, W3.shape[0], device=dev)
-    loss = torch.empty(M, device=dev)
+    loss = torch.empty(M, groups, device=dev) if groups > 1 else torch.empty(M, device=dev)
     ws = _workspace(dev, C().head3_slices(N2) * M * W3.shape[0], "head")
     C().server_head3(P2, b2.detach() if b2 is not None else None, relu2, float(drop2), seed2 & M64, _ptr(dseed),
-                     W3.detach(), b3.detach() if b3 is not None else None, labels, int(ignore_index), float(scale),
-                     h2, dlog, dz2, loss, ws)
-    return h2, dlog, dz2, loss
-
-
-def server_fc2_head(h1, W2, b2, relu2: bool, drop2: float, seed2: int, W3, b3, labels, scale: float,
-                    ignore_index: int = -100, dseed=None):
-    """Single-shard server head from fc1's output: fc2 forward + epilogue + fc3 + softmax-CE +
-    fc3 dgrad + fc2 ReLU/dropout backward in two launches.  Returns (h2, dlogits, dz2, loss_rows)."""
-    M, N2 = h1.shape[0], W2.shape[0]
-    dev = h1.device
-    h2 = torch.empty(M, N2, device=dev)
-    dz2 = torch.empty(M, N2, device=dev)
-    dlog = torch.empty(M, W3.shape[0], device=dev)
-    loss = torch.empty(M, device=dev)
-    ws = _workspace(dev, max(C().head3_slices(N2), C().fc2_head_tiles(N2)) * M * W3.shape[0], "head")
-    C().server_fc2_head(h1, W2.detach(), b2.detach() if b2 is not None else None, relu2, float(drop2), seed2 & M64,
-                        _ptr(dseed), W3.detach(), b3.detach() if b3 is not None else None, labels, int(ignore_index),
-                        float(scale), h2, dlog, dz2, loss, ws)
+                     W3.detach(), b3.detach() if b3 is not None else None, labels.reshape(-1), int(ignore_index),
+                     float(scale), h2, dlog, dz2, loss, ws, int(groups),
+                     gscale.reshape(-1).contiguous() if gscale is not None else None)
     return h2, dlog, dz2, loss
 
 
@@ -363,14 +328,13 @@ def lookahead_slabs(device, K0: int, mn: int, N0: int, tag: str = ""):
 
 def wgrad_group_(layers, M: int, cfg, t: int, dyn=None, x_next=None, p_next=None):
     """Fused wgrad+optimizer of up to 3 layers in one launch.  Each layer:
-    (dz, dzp, hmask, mscale, A, W, st_w, b, st_b) — exactly one of dz / dzp.
-    With `x_next` (<= 64 rows), also writes layer 0's split-K partial pre-activations of
-    the next batch under the *updated* weights into `p_next` (see lookahead_slabs)."""
+    (dz, A, W, st_w, b, st_b).  With `x_next` (<= 64 rows), also writes layer 0's split-K
+    partial pre-activations of the next batch under the *updated* weights into `p_next`
+    (see lookahead_slabs)."""
     tup = []
-    for dz, dzp, hm, ms, A, W, st_w, b, st_b in layers:
-        tup.append((dz, dzp, hm, float(ms), A, W.detach(), _s0(st_w), _s1(st_w),
-                    b.detach() if b is not None else None, _s0(st_b) if b is not None else None,
-                    _s1(st_b) if b is not None else None))
+    for dz, A, W, st_w, b, st_b in layers:
+        tup.append((dz, A, W.detach(), _s0(st_w), _s1(st_w), b.detach() if b is not None else None,
+                    _s0(st_b) if b is not None else None, _s1(st_b) if b is not None else None))
     C().wgrad_group(tup, int(M), x_next, p_next, *_opt_args(cfg, t, dyn))
 
 

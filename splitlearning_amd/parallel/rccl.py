@@ -111,6 +111,12 @@ def ipc_self_test(ipc, iters: int = 24) -> bool:
         ipc.set_timeout_s(old)
 
 
+# Outcome of the last peer-mapped set-up on this process (bench.py reports it): "setup" is
+# "ok" or the failure, "self_test" True / False / None (not reached), "fallback" the
+# all-reduce the job keeps when the peer-mapped path is refused.
+IPC_STATUS: dict = {}
+
+
 def make_ipc_allreduce(ranks: list[int], my_rank: int, cap: int = IPC_AR_CAP, group=None):
     """Collective over every process: a peer-mapped all-reduce (`_C.IpcAllReduce`, csrc/ipc_ar.h)
     among `ranks`, returned on members after set-up (IPC handle exchange, peer mapping) AND a
@@ -140,9 +146,14 @@ def make_ipc_allreduce(ranks: list[int], my_rank: int, cap: int = IPC_AR_CAP, gr
                 ipc.open(mine)
             except RuntimeError as e:
                 err = e
+    IPC_STATUS.clear()
+    IPC_STATUS.update({"ranks": len(ranks), "setup": "ok" if err is None else str(err)[:200], "self_test": None,
+                       "fallback": None})
     if not _agree(err is None, group):
         import warnings
         warnings.warn(f"peer-mapped all-reduce unavailable ({err or 'failed on another rank'}); using RCCL")
+        IPC_STATUS.update({"setup": IPC_STATUS["setup"] if err is not None else "failed on another rank",
+                           "fallback": "rccl"})
         return None
     ok = True
     if member:
@@ -150,8 +161,11 @@ def make_ipc_allreduce(ranks: list[int], my_rank: int, cap: int = IPC_AR_CAP, gr
             ok = ipc_self_test(ipc)
         except RuntimeError:
             ok = False
-    if not _agree(ok, group):
+    agreed = _agree(ok, group)
+    IPC_STATUS.update({"self_test": bool(ok and agreed)})
+    if not agreed:
         import warnings
         warnings.warn("peer-mapped all-reduce failed its self-test on some rank; using RCCL")
+        IPC_STATUS["fallback"] = "rccl"
         return None
     return ipc if member else None

@@ -37,6 +37,10 @@ class ConcatSession(SisaSession):
         return (self.make_bob_module(ServerTailSisaConcat, self.k),
                 sisa_server_spec(self.k, concat=True))
 
+    def _build_bob(self):
+        super()._build_bob()
+        self.tail.ce_groups = self.k         # one 100-way cross-entropy head per client
+
     def cut_width_in(self) -> int:
         return CUT_FEATURES
 
@@ -44,15 +48,12 @@ class ConcatSession(SisaSession):
         return 100
 
     def bob_infer(self, act, cid):
-        """Eval: Alice_cid's activation in slot cid, zeros elsewhere; returns head cid."""
+        """Eval: Alice_cid's activation in slot cid, zeros elsewhere; returns head cid.  Only
+        fc1's column block of slot cid and fc3's head-cid rows are multiplied
+        (`TailEngine.forward_block`): the zero blocks of the padded input add nothing, so this is
+        the same function at 1/k of fc1's work."""
         j = cid - 1
-        outs = []
-        for s in range(0, act.shape[0], 2048):
-            a = act[s:s + 2048]
-            X = torch.zeros(a.shape[0], CUT_FEATURES * self.k, device=self.device)
-            X[:, j * CUT_FEATURES:(j + 1) * CUT_FEATURES] = a
-            outs.append(self.tail.forward(X)[:, 100 * j:100 * (j + 1)].contiguous())
-        return torch.cat(outs, 0) if len(outs) > 1 else outs[0]
+        return self.tail.forward_block(act, j * CUT_FEATURES, 100 * j, 100)
 
     def concat_step(self, caches, t: int):
         k, B = self.k, self.B
@@ -100,6 +101,15 @@ class ConcatSession(SisaSession):
             scale[:, j] = sc.to(dev) * (Y[:, j] != -100)
         Ms = [max(r) for r in rows]
         tail = self.tail
+        if getattr(self.args, "native_epoch", True) and tail.native_epoch_ok(B):
+            # the fused server step on the concatenated rows (csrc/engine.cpp with the grouped
+            # cross-entropy head): every step takes B rows; rows past a step's M_t are zero
+            # with every label ignored, so they add nothing to any gradient — the same step
+            # as on M_t rows
+            tail.lookahead_prologue(X[:B])
+            tail.run_native_epoch(X, Y, self.bob_slot, B, True, gscale=scale)
+            self.comm.progress()
+            return sum(sum(r) for r in rows)
         grouped = tail.grouped_ok()
         pre = False
         for t in range(T):

@@ -80,7 +80,7 @@ def test_conv_bwd(cuda, kind):
 @pytest.mark.parametrize("gemm", [0, 1])
 def test_linear_fwd(cuda, M, N, K, relu, drop, gemm):
     """M <= 128: the skinny split-K kernels; M > 128: hipBLASLt + the fused epilogue (gemm 0)
-    or the in-tree LDS-tiled MFMA GEMM (gemm 1: variant 11, every tile form of slot 10)."""
+    or the in-tree LDS-tiled MFMA GEMM (gemm 1: variant 11)."""
     if gemm and M <= 128:
         pytest.skip("the tiled GEMM serves M > 128")
     x = torch.randn(M, K, device=cuda)
@@ -91,59 +91,47 @@ def test_linear_fwd(cuda, M, N, K, relu, drop, gemm):
     C = hip_ops.C()
     C.set_variant(11, gemm)
     try:
-        for tile in ((0, 1, 2, 3, 4) if gemm else (0,)):
-            C.set_variant(10, tile)
-            for once in ((0,) if gemm else (0, 2)):      # variant 14: 2 = the k-loop skinny form
-                C.set_variant(14, once)
-                y = hip_ops.linear_fwd(x, w, b, relu, drop, seed, col_offset=3)
-                _close(y, yr, rtol=1e-4, atol=1e-4)
+        y = hip_ops.linear_fwd(x, w, b, relu, drop, seed, col_offset=3)
+        _close(y, yr, rtol=1e-4, atol=1e-4)
     finally:
         C.set_variant(11, 0)
-        C.set_variant(10, 0)
-        C.set_variant(14, 0)
 
 
 @pytest.mark.parametrize("M,N,K,max_split", [(16, 1000, 5000, 16), (16, 1000, 628, 1), (16, 1000, 1000, 1),
                                               (64, 1000, 5000, 16), (16, 100, 1000, 16), (5, 37, 52, 16),
                                               (16, 1000, 1252, 2)])
-@pytest.mark.parametrize("once", [0, 2])
-def test_linear_fwd_partial(cuda, M, N, K, max_split, once):
+def test_linear_fwd_partial(cuda, M, N, K, max_split):
     """Un-reduced split-K slabs of x @ w.T (fc2 forward of the server step; max_split 1 = the
-    row-parallel TP shard's plain partial product) in both skinny forms (variant 14 = 2: the
-    k-loop form)."""
-    C = hip_ops.C()
-    C.set_variant(14, once)
-    try:
-        x = torch.randn(M, K, device=cuda)
-        w = torch.randn(N, K, device=cuda) / K ** 0.5
-        P = hip_ops.linear_fwd_partial(x, w, max_split=max_split, key=f"t{once}")
-        assert 1 <= P.shape[0] <= max_split
-        _close(P.sum(0), x @ w.t(), rtol=1e-4, atol=1e-4)
-    finally:
-        C.set_variant(14, 0)
+    row-parallel TP shard's plain partial product)."""
+    x = torch.randn(M, K, device=cuda)
+    w = torch.randn(N, K, device=cuda) / K ** 0.5
+    P = hip_ops.linear_fwd_partial(x, w, max_split=max_split, key="tpart")
+    assert 1 <= P.shape[0] <= max_split
+    _close(P.sum(0), x @ w.t(), rtol=1e-4, atol=1e-4)
+
+
+def test_linear_fwd_wide_k_uses_the_k_loop_form(cuda):
+    """K past the one-round-trip form's reach (the concat fc1 at k = 8: K = 43264) runs the
+    k-loop skinny kernel (csrc/linear.hip skinny_fwd_kernel)."""
+    x = torch.randn(16, 43264, device=cuda)
+    w = torch.randn(200, 43264, device=cuda) / 43264 ** 0.5
+    b = torch.randn(200, device=cuda)
+    y = hip_ops.linear_fwd(x, w, b, True, 0.0, 1)
+    _close(y, torch.relu(x @ w.t() + b), rtol=1e-4, atol=1e-4)
 
 
 @pytest.mark.parametrize("M,N,K", [(16, 5000, 5408), (16, 1000, 5000), (16, 100, 1000), (16, 10, 100),
                                     (3, 37, 52), (16, 1000, 628), (64, 1000, 5000), (40, 1000, 604),
                                     (16, 12, 8), (200, 1000, 5000), (1000, 100, 1000)])
 @pytest.mark.parametrize("masked", [False, True])
-@pytest.mark.parametrize("variant", [0, 2, 3])
-def test_linear_dgrad(cuda, M, N, K, masked, variant):
-    """variant 0: the split-N + reduce pair (default); 2 / 3: the full-N kernel (whole
-    reduction in one workgroup, masked store; 32- / 16-column tiles) where it applies
-    (N % 4 == 0, M <= 64)."""
-    C = hip_ops.C()
-    old = C.get_variant(8)
-    C.set_variant(8, variant)
-    try:
-        dz = torch.randn(M, N, device=cuda)
-        w = torch.randn(N, K, device=cuda) / N ** 0.5
-        h = torch.relu(torch.randn(M, K, device=cuda)) if masked else None
-        dx = hip_ops.linear_dgrad(dz, w, h, 2.0)
-        dxr = torch_ops.linear_dgrad(dz, w, h, 2.0)
-        _close(dx, dxr, rtol=1e-4, atol=1e-4)
-    finally:
-        C.set_variant(8, old)
+def test_linear_dgrad(cuda, M, N, K, masked):
+    """The split-N + reduce pair (the mask fused into the reduce), or one masked launch."""
+    dz = torch.randn(M, N, device=cuda)
+    w = torch.randn(N, K, device=cuda) / N ** 0.5
+    h = torch.relu(torch.randn(M, K, device=cuda)) if masked else None
+    dx = hip_ops.linear_dgrad(dz, w, h, 2.0)
+    dxr = torch_ops.linear_dgrad(dz, w, h, 2.0)
+    _close(dx, dxr, rtol=1e-4, atol=1e-4)
 
 
 @pytest.mark.parametrize("M,N,K", [(16, 5000, 5408), (16, 100, 1000), (7, 10, 100), (40, 33, 20)])
@@ -232,16 +220,12 @@ def test_conv_local_step(cuda, kind, B):
     _close(b1, b2, rtol=1e-3, atol=3e-4 if kind == "adam" else 1e-6)
 
 
-@pytest.mark.parametrize("variant", [0, 1])          # 0 = LDS-staged (default), 1 = all-MFMA
 @pytest.mark.parametrize("kind", ["sgd", "adam"])
 @pytest.mark.parametrize("M,shapes,mn", [(16, [(5000, 5408), (1000, 5000)], 16), (20, [(100, 1000), (33, 20)], 5),
                                          (7, [(10, 100)], 0), (64, [(1000, 5408), (100, 1000)], 64),
                                          (48, [(300, 1000)], 37)])
-def test_wgrad_group(cuda, variant, kind, M, shapes, mn):
+def test_wgrad_group(cuda, kind, M, shapes, mn):
     """Grouped wgrad+optimizer (+ layer-0 look-ahead forward, up to 64 rows) == per-layer fp32 reference."""
-    if variant == 1 and mn > 16:
-        pytest.skip("the all-MFMA dW variant's look-ahead covers <= 16 rows")
-    C = hip_ops.C()
     cfg = OptimCfg("adam", 1e-3, weight_decay=1e-5) if kind == "adam" else OptimCfg("sgd", 1e-2, momentum=0.9)
 
     def st(p):
@@ -254,34 +238,29 @@ def test_wgrad_group(cuda, variant, kind, M, shapes, mn):
         sw, sb = st(w), st(b)
         refs.append((dz, a, w.clone(), b.clone(), {k: v.clone() for k, v in sw.items()},
                      {k: v.clone() for k, v in sb.items()}))
-        layers.append((dz, None, None, 1.0, a, w, sw, b, sb))
+        layers.append((dz, a, w, sw, b, sb))
     kw = {}
     if mn:
         xn = torch.randn(mn, shapes[0][1], device=cuda)
         kw = {"x_next": xn, "p_next": hip_ops.lookahead_slabs(cuda, shapes[0][1], mn, shapes[0][0])}
-    try:
-        C.set_variant(3, variant)
-        hip_ops.wgrad_group_(layers, M, cfg, 4, **kw)
-    finally:
-        C.set_variant(3, 0)
+    hip_ops.wgrad_group_(layers, M, cfg, 4, **kw)
     for (dz, a, w2, b2, sw2, sb2), L in zip(refs, layers):
         torch_ops.linear_wgrad_step_(dz, a, w2, b2, cfg, sw2, sb2, 4)
-        _close(L[5], w2, rtol=1e-4, atol=1e-5)
-        _close(L[7], b2, rtol=1e-4, atol=1e-5)
+        _close(L[2], w2, rtol=1e-4, atol=1e-5)
+        _close(L[4], b2, rtol=1e-4, atol=1e-5)
         for k in sw2:
-            _close(L[6][k], sw2[k], rtol=1e-4, atol=1e-5)
-            _close(L[8][k], sb2[k], rtol=1e-4, atol=1e-5)
+            _close(L[3][k], sw2[k], rtol=1e-4, atol=1e-5)
+            _close(L[5][k], sb2[k], rtol=1e-4, atol=1e-5)
     if mn:
-        _close(kw["p_next"].sum(0), kw["x_next"] @ layers[0][5].t(), rtol=1e-4, atol=2e-3)
+        _close(kw["p_next"].sum(0), kw["x_next"] @ layers[0][2].t(), rtol=1e-4, atol=2e-3)
 
 
 @pytest.mark.parametrize("kind", ["sgd", "adam"])
-def test_wgrad_group_traversal_and_store_form_are_bit_identical(cuda, kind):
-    """The tile walk direction (variant 7: forward / reversed / alternating), the store form
-    (variant 4: write-through / plain) and the grid form (variant 2: auto / 2-D / 1-D) only
-    change where and when bytes move: every output, the look-ahead slabs included, is
-    bitwise the same."""
-    C = hip_ops.C()
+def test_wgrad_group_alternating_walk_is_bit_identical(cuda, kind):
+    """Consecutive launches walk fc1's tiles in opposite directions (the Infinity Cache reuse
+    order, csrc/fused.hip set_traversal): the walk only changes where and when bytes move, so
+    two launches on the same inputs (one forward, one reversed) give bitwise the same outputs,
+    the look-ahead slabs included."""
     cfg = OptimCfg("adam", 1e-3, weight_decay=1e-5) if kind == "adam" else OptimCfg("sgd", 1e-2, momentum=0.9)
     g = torch.Generator().manual_seed(3)
     M, shapes = 16, [(1000, 5408), (200, 1000), (100, 200)]
@@ -289,35 +268,25 @@ def test_wgrad_group_traversal_and_store_form_are_bit_identical(cuda, kind):
              torch.randn(N, generator=g)) for N, K in shapes]
     xn = torch.randn(M, shapes[0][1], generator=g).to(cuda)
     outs = []
-    try:
-        for v7, v4, v2 in ((1, 0, 0), (2, 0, 0), (0, 0, 0), (0, 0, 0), (1, 1, 0), (2, 1, 0), (2, 0, 1),
-                           (1, 0, 2), (2, 1, 1), (2, 1, 2)):
-            layers = []
-            for dz, a, w, b in base:
-                w, b = w.to(cuda), b.to(cuda)
-                sw = {"m": torch.full_like(w, 0.01), "v": torch.full_like(w, 0.02)} if kind == "adam" else \
-                    {"buf": torch.full_like(w, 0.01)}
-                sb = {k: torch.full_like(b, 0.01) for k in sw}
-                layers.append((dz.to(cuda), None, None, 1.0, a.to(cuda), w, sw, b, sb))
-            pn = hip_ops.lookahead_slabs(cuda, shapes[0][1], M, shapes[0][0])
-            C.set_variant(7, v7)
-            C.set_variant(4, v4)
-            C.set_variant(2, v2)
-            hip_ops.wgrad_group_(layers, M, cfg, 3, x_next=xn, p_next=pn)
-            torch.cuda.synchronize()
-            outs.append([t.clone() for L in layers for t in (L[5], L[7], *L[6].values(), *L[8].values())]
-                        + [pn.clone()])
-    finally:
-        for slot in (2, 4, 7):
-            C.set_variant(slot, 0)
+    for _ in range(3):
+        layers = []
+        for dz, a, w, b in base:
+            w, b = w.to(cuda), b.to(cuda)
+            sw = {"m": torch.full_like(w, 0.01), "v": torch.full_like(w, 0.02)} if kind == "adam" else \
+                {"buf": torch.full_like(w, 0.01)}
+            sb = {k: torch.full_like(b, 0.01) for k in sw}
+            layers.append((dz.to(cuda), a.to(cuda), w, sw, b, sb))
+        pn = hip_ops.lookahead_slabs(cuda, shapes[0][1], M, shapes[0][0])
+        hip_ops.wgrad_group_(layers, M, cfg, 3, x_next=xn, p_next=pn)
+        torch.cuda.synchronize()
+        outs.append([t.clone() for L in layers for t in (L[2], L[4], *L[3].values(), *L[5].values())] + [pn.clone()])
     for o in outs[1:]:
         for x, y in zip(outs[0], o):
             assert torch.equal(x, y)
 
 
-@pytest.mark.parametrize("variant", [0, 1])   # 0: optimizer folded into the next step, 1: 2 launches/step
 @pytest.mark.parametrize("kind", ["sgd", "adam"])
-def test_conv_local_epoch_matches_steps(cuda, kind, variant):
+def test_conv_local_epoch_matches_steps(cuda, kind):
     """The C++-looped epoch == the per-step calls (bitwise), incl. a partial last batch."""
     x = _shard(300, cuda)
     y_all = torch.randint(0, 10, (300,), device=cuda)
@@ -330,14 +299,9 @@ def test_conv_local_epoch_matches_steps(cuda, kind, variant):
             {"buf": torch.zeros_like(p)}
     w1, b1, w2, b2 = w.clone(), b.clone(), w.clone(), b.clone()
     s = [st(w), st(b), st(w), st(b)]
-    C = hip_ops.C()
-    C.set_variant(6, variant)      # also selects the per-step kernel's lane layout
-    try:
-        l1 = hip_ops.conv_local_epoch_(x, y_all, order, 16, w1, b1, cfg, s[0], s[1], 3)
-        l2 = torch.cat([hip_ops.conv_local_step_(x, y_all, order[i:i + 16], w2, b2, cfg, s[2], s[3], 3 + j)
-                        for j, i in enumerate(range(0, 109, 16))])
-    finally:
-        C.set_variant(6, 0)
+    l1 = hip_ops.conv_local_epoch_(x, y_all, order, 16, w1, b1, cfg, s[0], s[1], 3)
+    l2 = torch.cat([hip_ops.conv_local_step_(x, y_all, order[i:i + 16], w2, b2, cfg, s[2], s[3], 3 + j)
+                    for j, i in enumerate(range(0, 109, 16))])
     torch.cuda.synchronize()
     assert torch.equal(l1, l2) and torch.equal(w1, w2) and torch.equal(b1, b2)
     for k in s[0]:
@@ -368,28 +332,56 @@ def test_server_head3(cuda, M, S2, N2, C):
     _close(dz2, dz2r, rtol=1e-4, atol=1e-6)
 
 
-@pytest.mark.parametrize("M,K,N2,C", [(16, 5000, 1000, 100), (7, 628, 1000, 100), (64, 5000, 1000, 100),
-                                       (20, 132, 36, 7)])
-def test_server_fc2_head(cuda, M, K, N2, C):
-    """fc2 forward (whole K per workgroup) + epilogue + partial fc3 logits, then softmax-CE,
-    fc3 dgrad and fc2 ReLU/dropout backward, against the eager composition."""
-    g = torch.Generator().manual_seed(9)
-    h1 = torch.relu(torch.randn(M, K, generator=g)).to(cuda)
-    W2 = (torch.randn(N2, K, generator=g) / K ** 0.5).to(cuda)
+@pytest.mark.parametrize("M,S2,N2,C", [(16, 4, 1000, 100), (7, 1, 1000, 100), (16, 8, 1000, 10), (64, 16, 1000, 100),
+                                       (16, 1, 628, 100), (16, 2, 100, 10), (5, 3, 1000, 300)])
+def test_server_head_one_launch_is_bitwise_the_two_kernel_head(cuda, M, S2, N2, C):
+    """The one-launch head (head_fused_kernel: the row's slices hand their partial logits over
+    inside the launch) gives bitwise the outputs of the head_fwd + head_bwd pair (variant 21 = 1),
+    run twice back to back (the row counters carry across launches)."""
+    g = torch.Generator().manual_seed(M * 7 + C)
+    P2 = (torch.randn(S2, M, N2, generator=g) * 0.5).to(cuda)
     b2 = (torch.randn(N2, generator=g) * 0.1).to(cuda)
     W3 = (torch.randn(C, N2, generator=g) * 0.05).to(cuda)
     b3 = (torch.randn(C, generator=g) * 0.1).to(cuda)
     y = torch.randint(0, min(C, 10), (M,), generator=g).to(cuda)
-    y[0] = -100                                        # ignored row
-    seed = 7654321
-    h2, dlog, dz2, loss = hip_ops.server_fc2_head(h1, W2, b2, True, 0.5, seed, W3, b3, y, 1.0 / M)
-    h2r = torch_ops.linear_fwd(h1.cpu(), W2.cpu(), b2.cpu(), True, 0.5, seed)
-    logits = h2r @ W3.cpu().t() + b3.cpu()
-    lossr, dlogr = torch_ops.softmax_ce(logits, y.cpu(), 1.0 / M)
-    dz2r = (dlogr @ W3.cpu()) * (h2r > 0) * 2.0
-    _close(h2, h2r, rtol=1e-4, atol=1e-4)
-    _close(loss, lossr, rtol=1e-4, atol=1e-4)
-    _close(dlog, dlogr, rtol=1e-4, atol=1e-6)
+    y[M // 2] = -100
+    Cx = hip_ops.C()
+    outs = []
+    for v in (1, 0, 0, 1):
+        Cx.set_variant(21, v)
+        try:
+            outs.append([t.clone() for t in hip_ops.server_head3(P2, b2, True, 0.5, 99, W3, b3, y, 1.0 / M)])
+        finally:
+            Cx.set_variant(21, 0)
+    torch.cuda.synchronize()
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("M,G", [(16, 2), (16, 4), (9, 8)])
+def test_server_head_grouped_cross_entropy(cuda, M, G):
+    """G cross-entropy groups of 100 logits (SISA-concat's k heads): per-(row, group) label,
+    scale and loss; ignored (row, group) pairs give zero loss and zero dlogits."""
+    g = torch.Generator().manual_seed(G)
+    N2, C = 1000, 100 * G
+    P2 = (torch.randn(4, M, N2, generator=g) * 0.5).to(cuda)
+    b2 = (torch.randn(N2, generator=g) * 0.1).to(cuda)
+    W3 = (torch.randn(C, N2, generator=g) * 0.05).to(cuda)
+    b3 = (torch.randn(C, generator=g) * 0.1).to(cuda)
+    y = torch.randint(0, 10, (M, G), generator=g).to(cuda)
+    y[M - 1, 0] = -100
+    y[0, G - 1] = -100
+    sc = (1.0 / torch.randint(1, M + 1, (M, G), generator=g).float()).to(cuda)
+    h2, dlog, dz2, loss = hip_ops.server_head3(P2, b2, True, 0.5, 7, W3, b3, y, 1.0, groups=G, gscale=sc)
+    h2r = torch_ops.linear_epilogue(P2.sum(0).cpu(), b2.cpu(), True, 0.5, 7)
+    logits = (h2r @ W3.cpu().t() + b3.cpu()).view(M * G, 100)
+    lossr, dr = torch_ops.softmax_ce(logits, y.cpu().view(-1), 1.0)
+    dr = (dr.view(M, G, 100) * sc.cpu().view(M, G, 1)).view(M, C)
+    dz2r = (dr @ W3.cpu()) * (h2r > 0) * 2.0
+    _close(h2, h2r)
+    _close(loss.view(-1), lossr, rtol=1e-4, atol=1e-5)
+    _close(dlog, dr, rtol=1e-4, atol=1e-6)
     _close(dz2, dz2r, rtol=1e-4, atol=1e-6)
 
 
@@ -401,16 +393,11 @@ def test_relu_mask(cuda):
 
 @pytest.mark.parametrize("kind", ["sgd", "adam"])
 @pytest.mark.parametrize("M", [16, 7, 32])
-@pytest.mark.parametrize("form", [0, 1])
-def test_head_step_matches_torch(cuda, kind, M, form):
+def test_head_step_matches_torch(cuda, kind, M):
     """_C.head_step (the U-shape head's forward + CE + dgrad + optimizer in one launch) ==
-    the fp32 torch reference of the same step.  form 0: the MFMA kernel (<= 16 rows; more
-    rows take the FMA kernel), 1: the FMA kernel (variant 15 = 1)."""
-    hip_ops.C().set_variant(15, form)
-    try:
-        _head_step_check(cuda, kind, M)
-    finally:
-        hip_ops.C().set_variant(15, 0)
+    the fp32 torch reference of the same step (the MFMA kernel up to 16 rows, the FMA kernel
+    beyond)."""
+    _head_step_check(cuda, kind, M)
 
 
 def _head_step_check(cuda, kind, M):
@@ -547,65 +534,16 @@ def test_linear_fwd_bf16_compute(cuda, M, N, K):
     assert (y - torch.relu(x @ w.t() + b)).abs().max().item() > 1e-3
 
 
-@pytest.mark.parametrize("M,N1,N2,S1", [(16, 5000, 1000, 22), (64, 5000, 1000, 22), (16, 628, 1000, 22),
-                                        (5, 100, 37, 3), (16, 1000, 100, 7)])
-@pytest.mark.parametrize("ks", [1, 2])
-def test_lookahead_fc2_fwd(cuda, M, N1, N2, S1, ks):
-    """fc1's look-ahead epilogue inside fc2's split-K forward: h1 bitwise the epilogue kernel
-    (same slab order, same bias / ReLU / dropout), the product slabs sum to h1 @ W2^T."""
-    C = hip_ops.C()
-    old = C.get_variant(18)
-    C.set_variant(18, ks)                 # k-slice width 64 / 128
-    P1 = torch.randn(S1, M, N1, device=cuda)
-    b1 = torch.randn(N1, device=cuda)
-    W2 = torch.randn(N2, N1, device=cuda) / N1 ** 0.5
-    try:
-        h1, P2 = hip_ops.lookahead_fc2_fwd(P1, b1, 0.5, 77, 8, W2)
-    finally:
-        C.set_variant(18, old)
-    ref = hip_ops.linear_epilogue(P1, b1, True, 0.5, 77, 8)
-    assert torch.equal(h1, ref)
-    assert P2.shape[1:] == (M, N2) and P2.shape[0] <= hip_ops.C().lookahead_fc2_slices(N1)
-    _close(P2.sum(0), h1 @ W2.t(), rtol=1e-4, atol=1e-4)
-
-
 @pytest.mark.parametrize("M", [16, 64])
-def test_xcd_grouped_order_is_bitwise_identical(cuda, M):
-    """The XCD-grouped workgroup order of the fc2 forward / dgrad (default; variant 19 = 2 is
-    the plain order) only permutes which dispatch slot runs which tile: bitwise the same."""
-    C = hip_ops.C()
+def test_xcd_grouped_fc2_products(cuda, M):
+    """The XCD-grouped workgroup order of the fc2 forward / dgrad (a permutation of which
+    dispatch slot runs which tile) gives the fp32 products: split-K slabs summing to x @ w.T,
+    and the masked data gradient, at the full width and at a TP = 8 shard (K = 628, S = 16)."""
     x = torch.randn(M, 5000, device=cuda)
     w = torch.randn(1000, 5000, device=cuda) / 70.0
     dz = torch.randn(M, 1000, device=cuda)
     h = torch.relu(torch.randn(M, 5000, device=cuda))
-    outs = []
-    old = C.get_variant(19)
-    try:
-        for v in (2, 0):
-            C.set_variant(19, v)
-            P = hip_ops.linear_fwd_partial(x, w, key=f"xg{v}").clone()
-            d = hip_ops.linear_dgrad(dz, w, h, 2.0).clone()
-            outs.append((P, d))
-    finally:
-        C.set_variant(19, old)
-    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
-    _close(outs[1][0].sum(0), x @ w.t(), rtol=1e-4, atol=1e-4)
-
-
-def test_xcd_grouped_dgrad_tp8_shard_is_bitwise_identical(cuda):
-    """The grouped dgrad order with two 64-row N slices per 128-row group (a TP = 8 shard:
-    K = 628, S = 16) is bitwise the plain order."""
-    C = hip_ops.C()
-    w = torch.randn(1000, 628, device=cuda) / 30.0
-    dz = torch.randn(16, 1000, device=cuda)
-    h = torch.relu(torch.randn(16, 628, device=cuda))
-    outs = []
-    old = C.get_variant(19)
-    try:
-        for v in (2, 0):
-            C.set_variant(19, v)
-            outs.append(hip_ops.linear_dgrad(dz, w, h, 2.0).clone())
-    finally:
-        C.set_variant(19, old)
-    assert torch.equal(outs[0], outs[1])
-    _close(outs[1], torch_ops.linear_dgrad(dz, w, h, 2.0), rtol=1e-4, atol=1e-4)
+    _close(hip_ops.linear_fwd_partial(x, w, key="xg").sum(0), x @ w.t(), rtol=1e-4, atol=1e-4)
+    _close(hip_ops.linear_dgrad(dz, w, h, 2.0), torch_ops.linear_dgrad(dz, w, h, 2.0), rtol=1e-4, atol=1e-4)
+    w8, h8 = w[:, :628].contiguous(), h[:, :628].contiguous()
+    _close(hip_ops.linear_dgrad(dz, w8, h8, 2.0), torch_ops.linear_dgrad(dz, w8, h8, 2.0), rtol=1e-4, atol=1e-4)

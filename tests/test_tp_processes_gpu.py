@@ -46,3 +46,16 @@ def test_bench_full_schedule_with_ranks_sharing_the_gpu(tmp_path):
     assert c["ranks_share_gpu"] is True and d["value"] > 0
     assert set(c["phase_seconds"]) >= {"local_training", "server_training", "eval_breakdown", "unlearn_local",
                                        "server_retraining"}
+
+
+def test_stalled_tp_peer_aborts_every_survivor_within_one_timeout():
+    """A Bob TP rank that stops issuing mid-epoch: every surviving rank's fused head times out
+    once on its flags, every later wait gives up at once, and the native executor raises from
+    the host-pinned error mirror, so each survivor exits non-zero within 2x the wait timeout
+    (scripts/tp_peer_failure_one_gpu.py; reference: a child failure ends the job,
+    split_nn.py:183-186)."""
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "tp_peer_failure_one_gpu.py"), "3", "2.0"],
+                         capture_output=True, text=True, timeout=115, cwd=ROOT)
+    text = out.stdout + out.stderr
+    assert out.returncode == 0, text[-3000:]
+    assert out.stdout.count("aborted ") == 2 and "PASS" in out.stdout, text[-3000:]
