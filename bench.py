@@ -186,6 +186,17 @@ def main(argv=None):
             raise SystemExit("--schedule round is a SISA-mode schedule")
         steps = [(n, f) for n, f in steps if n in ("local_training", "server_training")]
 
+    calib = None
+    if N > 1:
+        # measured link costs on this job's ranks and transport (not timed): the split modes'
+        # per-batch act / cut-gradient message and Bob's TP all-reduce (parallel/calibrate.py)
+        from splitlearning_amd.parallel.calibrate import measure
+        tail = getattr(sess, "tail", None)
+        calib = measure(comm, dev, a.batch_size, allreduce=tail.allreduce if tail is not None else None,
+                        tp_ranks=pl.bob_ranks if pl.bob_tp > 1 else ())
+        if calib and calib.get("msg_us") is not None:
+            calib["bob_tp_policy"] = {m: choose_bob_tp(m, N, calib["msg_us"]) for m in ("vanilla", "ushape")}
+
     def step():
         # a fresh repetition of the schedule: fronts trainable, Bob's cut-layer cache empty
         # (the fronts change every repetition); weights and optimizer state carry on
@@ -260,6 +271,7 @@ def main(argv=None):
                                  "rccl" if tpc is not None else "torch.distributed" if N > 1 else "none"),
                 "bytes_sent_per_rank_per_step": sent,
                 "tp_ipc_setup": _ipc_status(),
+                "calib": calib,
             },
         }
         line = json.dumps(out)

@@ -57,6 +57,10 @@ def build_parser() -> argparse.ArgumentParser:
                    help="number of OS processes (0 = #GPUs on GPU, world_size on CPU)")
     g.add_argument("--bob_tp", type=int, default=0,
                    help="tensor-parallel degree of Bob's server tail (0 = all processes on GPU, 1 on CPU)")
+    g.add_argument("--calibrate", action="store_true",
+                   help="with --bob_tp 0 on several GPUs: measure the per-batch message cost over the "
+                        "job's own links at start-up (parallel/calibrate.py) and pick Bob's TP degree "
+                        "from it instead of the assumed MSG_US (or SL_MSG_US)")
     g.add_argument("--backend", choices=("auto", "nccl", "gloo"), default="auto")
     g.add_argument("--act_dtype", choices=("fp32", "bf16"), default="fp32",
                    help="wire dtype of every cut-layer activation transfer (per-batch vanilla / U-shape "

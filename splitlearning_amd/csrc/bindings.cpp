@@ -668,7 +668,6 @@ PYBIND11_MODULE(_C, m) {
   // slot lives only while its alternative is being measured; the losers are removed with the
   // numbers kept in docs/PERF.md.  In use:
   //   11 fp32 products of M > 128 rows: 1 = the in-tree tiled GEMM instead of hipBLASLt
-  //   21 server head: 1 = head_fwd + head_bwd launches instead of the one-launch fused head
   m.def("set_variant", [](int64_t slot, int64_t v) {
     TORCH_CHECK(slot >= 0 && slot < 24, "variant slot");
     sl::g_variant[slot] = (int)v;

@@ -205,6 +205,7 @@ __device__ __forceinline__ void sl_opt_update4(const SlOpt& o, f32x4& p, f32x4 g
 // _C.set_variant; 0 = the shipped default everywhere).
 namespace sl {
 extern int g_variant[24];
+
 extern int g_bf16;      // compute dtype of the GEMM-shaped kernels: 0 = exact fp32, 1 = bf16 operands
 }
 

@@ -39,8 +39,8 @@ struct WgGroup {
 };
 
 int head3_slices(int N2);
-// One launch (head_fused_kernel; variant 21 = 1: the head_fwd + head_bwd pair).  ipc
-// (tensor-parallel fc2): P2 is this rank's unreduced [M, N2] partial; the head pushes its slice
+// head_fwd + head_bwd (fused.hip).  ipc (tensor-parallel fc2): P2 is this rank's unreduced
+// [M, N2] partial; the head pushes its slice
 // to every rank, waits for the T slices and sums them in rank order (the fc2 all-reduce fused
 // into the slab reduction: ipc_ar.h).  G > 1: the C logits are G cross-entropy groups (labels
 // y [M, G], per-(row, group) scales gscale [M, G] or `scale`, losses loss_rows [M, G]).

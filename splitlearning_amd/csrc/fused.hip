@@ -179,8 +179,11 @@ __global__ void __launch_bounds__(256)
 head_bwd_kernel(const float* __restrict__ plog, const float* __restrict__ b3, const float* __restrict__ W3,
                 int ldw3, const int64_t* __restrict__ y, int64_t ignore, float scale, float dscale,
                 const float* __restrict__ h2, float* __restrict__ dlog, float* __restrict__ dz2,
-                float* __restrict__ loss_rows, int M, int N2, int C, int Qp) {
+                float* __restrict__ loss_rows, int M, int N2, int C, int Qp, int G, const float* __restrict__ gscale) {
   // Qp: number of partial-logit slabs in plog (head_fwd: one per column slice)
+  // G > 1: grouped cross-entropy (SISA-concat's k heads, protocols/concat.py): the C logits are
+  // G groups of C / G, each with its own label y[m G + g], scale (gscale[m G + g] or `scale`) and
+  // loss loss_rows[m G + g]; wave g % 4 takes group g
   extern __shared__ float lg[];   // C
   __shared__ f32x4 part[8][HS];
   int m, q, Q;
@@ -212,29 +215,32 @@ head_bwd_kernel(const float* __restrict__ plog, const float* __restrict__ b3, co
     lg[o] = v;
   }
   __syncthreads();
-  const int64_t lab = y[m];
-  if (wv == 0) {
-    if (lab == ignore) {
-      for (int cc = lane; cc < C; cc += 64) lg[cc] = 0.f;
-      if (lane == 0 && q == 0) loss_rows[m] = 0.f;
+  const int Cg = C / G;
+  for (int gr = wv; gr < G; gr += 4) {
+    const int64_t lab = y[(int64_t)m * G + gr];
+    float* lgg = lg + gr * Cg;
+    const float sc = gscale ? gscale[(int64_t)m * G + gr] : scale;
+    if (lab == ignore || lab < 0 || lab >= Cg) {
+      for (int cc = lane; cc < Cg; cc += 64) lgg[cc] = 0.f;
+      if (lane == 0 && q == 0) loss_rows[(int64_t)m * G + gr] = 0.f;
     } else {
-      const float zl = lg[lab];
+      const float zl = lgg[lab];
       float mx = -INFINITY;
-      for (int cc = lane; cc < C; cc += 64) mx = fmaxf(mx, lg[cc]);
+      for (int cc = lane; cc < Cg; cc += 64) mx = fmaxf(mx, lgg[cc]);
       mx = sl_wave_max_dpp(mx);
       float se = 0.f;
-      for (int cc = lane; cc < C; cc += 64) {
-        const float e = expf(lg[cc] - mx);
-        lg[cc] = e;
+      for (int cc = lane; cc < Cg; cc += 64) {
+        const float e = expf(lgg[cc] - mx);
+        lgg[cc] = e;
         se += e;
       }
       se = sl_wave_sum_dpp(se);
-      if (lane == 0 && q == 0) loss_rows[m] = mx + logf(se) - zl;
+      if (lane == 0 && q == 0) loss_rows[(int64_t)m * G + gr] = mx + logf(se) - zl;
       const float inv = 1.f / se;
-      for (int cc = lane; cc < C; cc += 64) {
-        float p = lg[cc] * inv;
+      for (int cc = lane; cc < Cg; cc += 64) {
+        float p = lgg[cc] * inv;
         if (cc == lab) p -= 1.f;
-        lg[cc] = p * scale;
+        lgg[cc] = p * sc;
       }
     }
   }
@@ -260,213 +266,6 @@ head_bwd_kernel(const float* __restrict__ plog, const float* __restrict__ b3, co
     f32x4 out;
 #pragma unroll
     for (int i = 0; i < 4; ++i) out[i] = hh[i] > 0.f ? v[i] * dscale : 0.f;
-    reinterpret_cast<f32x4*>(dz2 + (int64_t)m * N2)[qa + tid] = out;
-  }
-}
-
-// head_fused_kernel: head_fwd and head_bwd in ONE launch.  Workgroup (q, m) runs head_fwd's
-// phase (slab reduction [+ the fused peer-mapped all-reduce], fc2 epilogue -> h2, its slice's
-// partial fc3 logits), publishes the partial logits, and waits for the other Q - 1 slices of
-// row m inside the launch instead of at a kernel boundary; then head_bwd's phase (logits,
-// softmax-CE, dlogits, dz2 for its slice) reuses the W3 slice and the h2 mask still in its
-// registers (head_bwd re-loaded both).  Hand-off (MI355X_MICROARCH.md, "Valid forms", first
-// row of the sc1 table): the partial logits are written with sc1 (write-through) stores, every
-// storing wave drains `s_waitcnt vmcnt(0)`, a workgroup barrier, then ONE agent-scope atomic
-// add per workgroup on row m's counter; the waiting lane polls the counter with sc1 loads and
-// every read of the partials is an sc1 load after a workgroup barrier.  The counter is never
-// reset: a workgroup's ticket (the value its add returned) names its launch, so it waits for
-// (ticket / Q + 1) * Q arrivals.  Every row's Q workgroups are consecutive in dispatch order,
-// so a waiting workgroup only waits for workgroups already dispatched with it (no residency
-// deadlock); the poll is bounded anyway (a safety net, ~2 s).
-// G > 1: grouped cross-entropy (SISA-concat's k heads, protocols/concat.py): the C logits are G
-// groups of C / G, each with its own label y[m G + g], scale (gscale[m G + g], or `scale`) and
-// loss loss_rows[m G + g].
-template <bool BF, bool IPC>
-__global__ void __launch_bounds__(256)
-head_fused_kernel(const float* __restrict__ P2, int S2, int64_t slab2, Epi e2, const float* __restrict__ W3,
-                  int ldw3, const float* __restrict__ b3, const int64_t* __restrict__ y, int64_t ignore, float scale,
-                  const float* __restrict__ gscale, int G, float* __restrict__ h2, float* __restrict__ plog, int ldp,
-                  unsigned long long* __restrict__ cnt, float* __restrict__ dlog, float* __restrict__ dz2,
-                  float* __restrict__ loss_rows, int M, int N2, int C, IpcStep ip) {
-  extern __shared__ float lg[];   // C
-  __shared__ f32x4 part[8][HS];
-  __shared__ f32x4 hs[HS];
-  int m, q, Q;
-  head_wg(m, q, Q);
-  const int tid = threadIdx.x;
-  int qa, qb;
-  head_slice(N2 >> 2, q, qa, qb);
-  const int ncol = qb - qa;
-  const int lane = tid & 63, wv = tid >> 6, half = lane >> 5, c = lane & 31;
-  const int g8 = tid >> 5;             // = 2 wv + half: this thread's output group lane
-  constexpr int JU = 13;
-  // W3 loads of the first output group do not depend on anything: issue them first.  Thread
-  // (g8, c) holds W3[8 j + g8][slice column c] for both phases.
-  f32x4 w[JU];
-  auto load_w = [&](int j0) {
-#pragma unroll
-    for (int j = 0; j < JU; ++j) {
-      const int o = 8 * (j0 + j) + g8;
-      w[j] = (o < C && c < ncol) ? *reinterpret_cast<const f32x4*>(W3 + (int64_t)o * ldw3 + 4 * (qa + c))
-                                 : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  };
-  load_w(0);
-  bool peers = false;
-  if constexpr (IPC) {
-    __shared__ int s_ok;
-    if (wv == 0) {
-      if (lane < ncol) {
-        const f32x4* src = reinterpret_cast<const f32x4*>(P2 + (int64_t)m * N2) + qa + lane;
-        f32x4 v = {0.f, 0.f, 0.f, 0.f};
-        for (int s = 0; s < S2; ++s) v += src[s * (slab2 >> 2)];
-        const int64_t slot = ((int64_t)ip.par * ip.T + ip.me) * ip.cap + (int64_t)m * N2 + 4 * (qa + lane);
-        for (int r = 0; r < ip.T; ++r) ipc_st4(ipc_rsrc(ip.P.data[r]), slot, make_float4(v[0], v[1], v[2], v[3]));
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const int fi = m * Q + q;
-      if (lane < ip.T) ipc_raise_flag(ip.P.flags[lane] + ((int64_t)ip.par * ip.T + ip.me) * ip.nflags + fi, ip.gen, ip.fences);
-      const bool ok = ipc_wait_flags(ip, lane, fi);
-      if (lane == 0) s_ok = ok ? 1 : 0;
-    }
-    __syncthreads();
-    // a wait that gave up (stalled / dead peer, error word raised) falls back to the local
-    // partial: the numbers are meaningless but the launch completes and every workgroup still
-    // arrives at the row counter below (the job aborts on the error word)
-    peers = s_ok != 0;
-  }
-  // 1. slab reduction: 32 columns x 8 slab groups
-  {
-    const int cc = tid & (HS - 1), sg = tid >> 5;
-    f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if (cc < ncol) {
-      if (IPC && peers) {
-        const __amdgpu_buffer_rsrc_t rs = ipc_rsrc(ip.P.data[ip.me]);
-        const int64_t o0 = (int64_t)ip.par * ip.T * ip.cap + (int64_t)m * N2 + 4 * (qa + cc);
-        for (int s = sg; s < ip.T; s += 8) {
-          const float4 u = ipc_ld4(rs, o0 + (int64_t)s * ip.cap);
-          v += f32x4{u.x, u.y, u.z, u.w};
-        }
-      } else {
-        const f32x4* src = reinterpret_cast<const f32x4*>(P2 + (int64_t)m * N2) + qa + cc;
-#pragma unroll 4
-        for (int s = sg; s < S2; s += 8) v += src[s * (slab2 >> 2)];
-      }
-    }
-    part[sg][cc] = v;
-  }
-  __syncthreads();
-  f32x4 hh = {0.f, 0.f, 0.f, 0.f};      // this slice's h2 (threads 0..HS-1), kept for the mask
-  if (tid < HS) {
-    f32x4 v = part[0][tid];
-#pragma unroll
-    for (int g = 1; g < 8; ++g) v += part[g][tid];
-    if (tid < ncol) {
-      const int col = 4 * (qa + tid);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) hh[i] = apply_epi(e2, v[i], m, col + i);
-      reinterpret_cast<f32x4*>(h2 + (int64_t)m * N2)[qa + tid] = hh;
-    }
-    hs[tid] = hh;
-  }
-  __syncthreads();
-  // 2. partial logits: half-wave h (32 lanes = the slice's columns) owns output 8 j + 2 wv + h;
-  // published with sc1 stores (write-through) for the hand-off
-  {
-    const f32x4 h = BF ? bfr4(hs[c]) : hs[c];
-    float* dst = plog + ((int64_t)q * M + m) * ldp;
-    for (int j0 = 0; j0 * 8 < C; j0 += JU) {
-      if (j0) load_w(j0);
-#pragma unroll
-      for (int j = 0; j < JU; ++j) {
-        const f32x4 wj = BF ? bfr4(w[j]) : w[j];
-        const float d = sl_row16_sum(wj[0] * h[0] + wj[1] * h[1] + wj[2] * h[2] + wj[3] * h[3]);
-        const float s0 = sl_lane(d, 0) + sl_lane(d, 16), s1 = sl_lane(d, 32) + sl_lane(d, 48);
-        const int o = 8 * (j0 + j) + 2 * wv;
-        if (lane == 0) {
-          if (o < C) __hip_atomic_store(dst + o, s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (o + 1 < C) __hip_atomic_store(dst + o + 1, s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-    }
-    if (C > 8 * JU) load_w(0);           // phase 2 starts from the first output group again
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  // 3. hand-off: arrive on row m's counter, wait for the row's other Q - 1 slices
-  if (tid == 0) {
-    const unsigned long long ticket = __hip_atomic_fetch_add(cnt + m, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned long long target = (ticket / (unsigned)Q + 1ull) * (unsigned)Q;
-    if (ticket + 1 < target) {
-      const uint64_t t0 = wall_clock64();
-      while (__hip_atomic_load(cnt + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-        __builtin_amdgcn_s_sleep(1);
-        if (wall_clock64() - t0 > 200000000ull) break;   // ~2 s at the 100 MHz wall clock: never hit
-      }
-    }
-  }
-  __syncthreads();
-  // 4. logits of row m (sc1 loads of the Q published partials, slice order) + b3
-  for (int o = tid; o < C; o += 256) {
-    float v = b3 ? b3[o] : 0.f;
-    for (int s = 0; s < Q; ++s)
-      v += __hip_atomic_load(plog + ((int64_t)s * M + m) * ldp + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    lg[o] = v;
-  }
-  __syncthreads();
-  // 5. softmax-CE per label group (wave g % 4 takes group g)
-  const int Cg = C / G;
-  for (int g = wv; g < G; g += 4) {
-    const int64_t lab = y[(int64_t)m * G + g];
-    float* lgg = lg + g * Cg;
-    const float sc = gscale ? gscale[(int64_t)m * G + g] : scale;
-    if (lab == ignore || lab < 0 || lab >= Cg) {
-      for (int cc = lane; cc < Cg; cc += 64) lgg[cc] = 0.f;
-      if (lane == 0 && q == 0) loss_rows[(int64_t)m * G + g] = 0.f;
-    } else {
-      const float zl = lgg[lab];
-      float mx = -INFINITY;
-      for (int cc = lane; cc < Cg; cc += 64) mx = fmaxf(mx, lgg[cc]);
-      mx = sl_wave_max_dpp(mx);
-      float se = 0.f;
-      for (int cc = lane; cc < Cg; cc += 64) {
-        const float e = expf(lgg[cc] - mx);
-        lgg[cc] = e;
-        se += e;
-      }
-      se = sl_wave_sum_dpp(se);
-      if (lane == 0 && q == 0) loss_rows[(int64_t)m * G + g] = mx + logf(se) - zl;
-      const float inv = 1.f / se;
-      for (int cc = lane; cc < Cg; cc += 64) {
-        float p = lgg[cc] * inv;
-        if (cc == lab) p -= 1.f;
-        lgg[cc] = p * sc;
-      }
-    }
-  }
-  __syncthreads();
-  if (q == 0)
-    for (int cc = tid; cc < C; cc += 256) dlog[(int64_t)m * C + cc] = lg[cc];
-  // 6. dz2 for this slice: (dlogits . W3[:, slice]) * dscale * [h2 > 0]
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  for (int j0 = 0; j0 * 8 < C; j0 += JU) {
-    if (j0) load_w(j0);
-#pragma unroll
-    for (int j = 0; j < JU; ++j) {
-      const int o = 8 * (j0 + j) + g8;
-      const float l = o < C ? lg[o] : 0.f;
-      acc += BF ? bfr(l) * bfr4(w[j]) : l * w[j];
-    }
-  }
-  part[g8][c] = acc;
-  __syncthreads();
-  if (tid < ncol) {
-    f32x4 v = part[0][tid];
-#pragma unroll
-    for (int gg = 1; gg < 8; ++gg) v += part[gg][tid];
-    f32x4 out;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) out[i] = hh[i] > 0.f ? v[i] * e2.dscale : 0.f;
     reinterpret_cast<f32x4*>(dz2 + (int64_t)m * N2)[qa + tid] = out;
   }
 }
@@ -643,35 +442,16 @@ static dim3 head_grid(int M, int Q) { return dim3(Q, M); }
 
 static void launch_head_bwd(const float* plog, const float* b3, const float* W3, int ldw3, const int64_t* y,
                             int64_t ignore, float scale, float dscale, const float* h2, float* dlog, float* dz2,
-                            float* loss_rows, int M, int N2, int C, int Q, int Qp, hipStream_t st) {
+                            float* loss_rows, int M, int N2, int C, int Q, int Qp, hipStream_t st, int G,
+                            const float* gscale) {
   const size_t sh = (size_t)C * sizeof(float);
   const dim3 g = head_grid(M, Q);
   if (g_bf16)
     head_bwd_kernel<true><<<g, 256, sh, st>>>(plog, b3, W3, ldw3, y, ignore, scale, dscale, h2, dlog, dz2, loss_rows,
-                                              M, N2, C, Qp);
+                                              M, N2, C, Qp, G, gscale);
   else
     head_bwd_kernel<false><<<g, 256, sh, st>>>(plog, b3, W3, ldw3, y, ignore, scale, dscale, h2, dlog, dz2,
-                                               loss_rows, M, N2, C, Qp);
-}
-
-// Row counters of the fused head's in-launch hand-off (head_fused_kernel), one per batch row,
-// per device, zero-initialised once and never freed (captured graphs hold the address).  The
-// head runs on one stream per process at a time (Bob's steps are a serial chain), which the
-// ticket arithmetic relies on.
-constexpr int kHeadRows = 1 << 16;
-
-static unsigned long long* head_counters() {
-  static unsigned long long* per_dev[64] = {nullptr};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  if (per_dev[dev] == nullptr) {
-    void* p = nullptr;
-    if (hipMalloc(&p, sizeof(unsigned long long) * kHeadRows) != hipSuccess) return nullptr;
-    if (hipMemset(p, 0, sizeof(unsigned long long) * kHeadRows) != hipSuccess) return nullptr;
-    if (hipDeviceSynchronize() != hipSuccess) return nullptr;
-    per_dev[dev] = static_cast<unsigned long long*>(p);
-  }
-  return per_dev[dev];
+                                               loss_rows, M, N2, C, Qp, G, gscale);
 }
 
 hipError_t server_head3(const float* P2, int S2, int64_t slab2, Epi e2, const float* W3, int ldw3, const float* b3,
@@ -686,30 +466,8 @@ hipError_t server_head3(const float* P2, int S2, int64_t slab2, Epi e2, const fl
   if (ipc != nullptr && (S2 < 1 || (slab2 & 3) || (int64_t)M * Q > ipc->nflags || (int64_t)M * N2 > ipc->cap ||
                          ipc->T < 1 || ipc->T > kIpcMaxRanks))
     return hipErrorInvalidValue;
-  // one launch with the in-launch hand-off (default), unless the counters cannot be had (a
-  // first use inside a graph capture) or variant 21 = 1 asks for the two-kernel form
-  unsigned long long* cnt = nullptr;
-  if (g_variant[21] != 1 && M <= kHeadRows) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    static bool ready = false;
-    if (ready || (hipStreamIsCapturing(st, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone)) {
-      cnt = head_counters();
-      ready = cnt != nullptr;
-    }
-  }
   const IpcStep none{};
   const IpcStep& ip = ipc ? *ipc : none;
-  if (cnt != nullptr) {
-    const size_t sh = (size_t)C * sizeof(float);
-#define SL_HF(BF, IP)                                                                                          \
-  head_fused_kernel<BF, IP><<<g, 256, sh, st>>>(P2, S2, slab2, e2, W3, ldw3, b3, y, ignore, scale, gscale, G, h2, \
-                                                ws, C, cnt, dlog, dz2, loss_rows, M, N2, C, ip)
-    if (g_bf16) { if (ipc) SL_HF(true, true); else SL_HF(true, false); }
-    else { if (ipc) SL_HF(false, true); else SL_HF(false, false); }
-#undef SL_HF
-    return hipGetLastError();
-  }
-  if (G != 1) return hipErrorInvalidValue;   // the grouped CE exists in the fused kernel only
   if (ipc != nullptr) {
     if (g_bf16)
       head_fwd_kernel<true, true><<<g, 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C, ip);
@@ -721,7 +479,8 @@ hipError_t server_head3(const float* P2, int S2, int64_t slab2, Epi e2, const fl
     else
       head_fwd_kernel<false, false><<<g, 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C, none);
   }
-  launch_head_bwd(ws, b3, W3, ldw3, y, ignore, scale, e2.dscale, h2, dlog, dz2, loss_rows, M, N2, C, Q, Q, st);
+  launch_head_bwd(ws, b3, W3, ldw3, y, ignore, scale, e2.dscale, h2, dlog, dz2, loss_rows, M, N2, C, Q, Q, st, G,
+                  gscale);
   return hipGetLastError();
 }
 

@@ -351,17 +351,33 @@ HBM_BPS = 5.5e12
 _SERIAL = {"vanilla": (32.146e6, 20, 2, 3), "ushape": (5.509e6, 28, 4, 5)}   # params, B/param, rounds T=1, T>1
 
 
-def choose_bob_tp(mode: str, nprocs: int) -> int:
-    """Bob's tensor-parallel degree for `mode` on `nprocs` GPUs (see the cost model above)."""
+def measured_msg_us() -> float | None:
+    """A recorded per-message cost (us): `SL_MSG_US`, e.g. the `msg_us` a calibration run
+    (`parallel/calibrate.py`, bench.py's `calib` field, `split_nn.py --calibrate`) measured."""
+    v = os.environ.get("SL_MSG_US", "")
+    try:
+        return float(v) if v else None
+    except ValueError:
+        return None
+
+
+def choose_bob_tp(mode: str, nprocs: int, msg_us: float | None = None) -> int:
+    """Bob's tensor-parallel degree for `mode` on `nprocs` GPUs (see the cost model above).
+    `msg_us`: the measured per-message cost; default a recorded one (`measured_msg_us`), else
+    the MSG_US assumption."""
     if nprocs <= 1:
         return 1
     if mode not in _SERIAL:
         return nprocs
+    if msg_us is None:
+        msg_us = measured_msg_us()
+    if msg_us is None:
+        msg_us = MSG_US
     params, bpp, r1, rt = _SERIAL[mode]
     remote = (nprocs - 1) / nprocs                 # Alices round-robin over the GPUs; Bob on rank 0
 
     def cost(T):
-        return bpp * params / T / HBM_BPS * 1e6 + (rt if T > 1 else r1 * remote) * MSG_US
+        return bpp * params / T / HBM_BPS * 1e6 + (rt if T > 1 else r1 * remote) * msg_us
     cands = [T for T in (1, 2, 4, 8, 16) if T <= nprocs and nprocs % T == 0] or [1]
     return min(cands, key=lambda T: (cost(T), T))
 

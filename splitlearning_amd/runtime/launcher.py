@@ -47,6 +47,7 @@ def resolve(args):
         args.backend = "nccl" if use_gpu else "gloo"
     if args.bob_tp <= 0:
         from ..parallel.dist import choose_bob_tp
+        args.bob_tp_auto = True
         args.bob_tp = choose_bob_tp(args.mode, args.nprocs) if use_gpu else 1
     if args.kernels == "torch":
         from .. import ops
@@ -101,6 +102,19 @@ def worker(rank: int, nprocs: int, args, result_q=None):
     if nprocs > 1:
         init_process(rank, nprocs, args.backend, args.master_addr, args.master_port, args.timeout_s, dev)
         tp_group = make_tp_group(pl, args.backend)
+    if nprocs > 1 and getattr(args, "calibrate", False) and getattr(args, "bob_tp_auto", False) and args.use_gpu:
+        # measured link cost -> Bob's TP degree (every rank gets rank 0's measurement, so the
+        # placement agrees); the group for the policy's first guess is rebuilt
+        from ..parallel.calibrate import measure
+        from ..parallel.dist import choose_bob_tp
+        cal = measure(Comm(rank, nprocs, dev, pl, None), dev, args.batch_size)
+        args.calib = cal
+        if cal.get("msg_us") is not None:
+            tp = choose_bob_tp(args.mode, nprocs, cal["msg_us"])
+            if tp != pl.bob_tp:
+                args.bob_tp = tp
+                pl = Placement.make(args.world_size, nprocs, tp)
+                tp_group = make_tp_group(pl, args.backend)
     comm = Comm(rank, nprocs, dev, pl, tp_group)
     if getattr(args, "msg_log", False):
         comm.msg_log = []
@@ -133,7 +147,7 @@ def worker(rank: int, nprocs: int, args, result_q=None):
     if rank == 0:
         extra = {"mode": args.mode, "world_size": args.world_size, "nprocs": nprocs, "bob_tp": pl.bob_tp,
                  "device": str(dev), "kernels": ops.get_backend() if dev.type == "cuda" else "torch",
-                 "last_eval": getattr(sess, "last_eval", None)}
+                 "last_eval": getattr(sess, "last_eval", None), "calib": getattr(args, "calib", None)}
         sess.timer.dump(os.path.join(args.log_dir, "metrics.json"), extra)
         if result_q is not None:
             result_q.put({"phases": out["phases"], **extra})

@@ -172,6 +172,10 @@ def test_bench_multi_rank_gloo(tmp_path, nranks):
         assert p in c["phase_seconds"], p
     # the SISA dump crossed ranks (Alices on ranks 1.. multicast to every Bob TP rank)
     assert sum(c["bytes_sent_per_rank_per_step"]) > 0
+    # self-calibration: the per-batch message cost to every peer and the TP all-reduce cost
+    cal = c["calib"]
+    assert cal["msg_us"] > 0 and sorted(cal["per_peer_us"]) == [str(r) for r in range(1, nranks)]
+    assert cal["tp_allreduce_us"] > 0 and set(cal["bob_tp_policy"]) == {"vanilla", "ushape"}
 
 
 @pytest.mark.slow

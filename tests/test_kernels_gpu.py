@@ -332,33 +332,6 @@ def test_server_head3(cuda, M, S2, N2, C):
     _close(dz2, dz2r, rtol=1e-4, atol=1e-6)
 
 
-@pytest.mark.parametrize("M,S2,N2,C", [(16, 4, 1000, 100), (7, 1, 1000, 100), (16, 8, 1000, 10), (64, 16, 1000, 100),
-                                       (16, 1, 628, 100), (16, 2, 100, 10), (5, 3, 1000, 300)])
-def test_server_head_one_launch_is_bitwise_the_two_kernel_head(cuda, M, S2, N2, C):
-    """The one-launch head (head_fused_kernel: the row's slices hand their partial logits over
-    inside the launch) gives bitwise the outputs of the head_fwd + head_bwd pair (variant 21 = 1),
-    run twice back to back (the row counters carry across launches)."""
-    g = torch.Generator().manual_seed(M * 7 + C)
-    P2 = (torch.randn(S2, M, N2, generator=g) * 0.5).to(cuda)
-    b2 = (torch.randn(N2, generator=g) * 0.1).to(cuda)
-    W3 = (torch.randn(C, N2, generator=g) * 0.05).to(cuda)
-    b3 = (torch.randn(C, generator=g) * 0.1).to(cuda)
-    y = torch.randint(0, min(C, 10), (M,), generator=g).to(cuda)
-    y[M // 2] = -100
-    Cx = hip_ops.C()
-    outs = []
-    for v in (1, 0, 0, 1):
-        Cx.set_variant(21, v)
-        try:
-            outs.append([t.clone() for t in hip_ops.server_head3(P2, b2, True, 0.5, 99, W3, b3, y, 1.0 / M)])
-        finally:
-            Cx.set_variant(21, 0)
-    torch.cuda.synchronize()
-    for o in outs[1:]:
-        for a, b in zip(outs[0], o):
-            assert torch.equal(a, b)
-
-
 @pytest.mark.parametrize("M,G", [(16, 2), (16, 4), (9, 8)])
 def test_server_head_grouped_cross_entropy(cuda, M, G):
     """G cross-entropy groups of 100 logits (SISA-concat's k heads): per-(row, group) label,
