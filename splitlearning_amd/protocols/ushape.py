@@ -22,6 +22,7 @@ from ..engine.slots import OptSlot, adam
 from ..engine.tail import TailEngine
 from ..models import ClientFront, Head, ServerTailUShape, head_spec, ushape_server_spec
 from .base import AliceState, Session, _progress
+from .split_native import native_split_ok, run_native_split_epoch
 
 
 class UShapeSession(Session):
@@ -138,6 +139,9 @@ class UShapeSession(Session):
         host = self.host(cid)
         spans = [(s, min(s + B, n)) for s in range(0, n, B)]
         if not spans:
+            return
+        if order is not None and native_split_ok(self, cid, "ushape"):
+            run_native_split_epoch(self, cid, order, "ushape")   # the same launches, issued from C++
             return
         grouped = self.is_bob and self.tail.grouped_ok()
         la = self.split_lookahead(cid)

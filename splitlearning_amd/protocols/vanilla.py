@@ -19,6 +19,7 @@ from ..config import CUT_FEATURES
 from ..engine.slots import OptSlot, sgd_momentum
 from ..models import ServerTailSisa, sisa_server_spec
 from .base import Session, _progress
+from .split_native import native_split_ok, run_native_split_epoch
 
 
 class VanillaSession(Session):
@@ -88,6 +89,9 @@ class VanillaSession(Session):
         host = self.host(cid)
         spans = [(s, min(s + B, n)) for s in range(0, n, B)]
         if not spans:
+            return
+        if order is not None and native_split_ok(self, cid, "vanilla"):
+            run_native_split_epoch(self, cid, order, "vanilla")   # the same launches, issued from C++
             return
         ahead = self.split_lookahead(cid)        # False: Alice remote from every Bob shard
         la = self.is_bob and self.tail.fused3_ok() and self.tail.lookahead_ok(B) and ahead
