@@ -110,6 +110,8 @@ def main(argv=None):
     ap.add_argument("--dtype", choices=("fp32", "bf16"), default="fp32", help="compute dtype")
     ap.add_argument("--concat_unlearn", action="store_true", default=True,
                     help="concat: add the unlearning retrain (BASELINE config 5)")
+    ap.add_argument("--python_epoch", action="store_true",
+                    help="A/B: epochs as Python loops instead of the native executors")
     ap.add_argument("--json_out", type=str, default="")
     ap.add_argument("--ranks_share_gpu", action="store_true",
                     help="rehearsal of the N > 1 path on a one-GPU box: every rank on cuda:0, gloo "
@@ -160,6 +162,8 @@ def main(argv=None):
         "--log_dir", log_dir, "--watchdog", "off"]
     if a.mode == "concat" and a.concat_unlearn:
         argv_s.append("--concat_unlearn")
+    if a.python_epoch:
+        argv_s.append("--python_epoch")
     sargs = parse_args(argv_s)
     pl = Placement.make(ws, N, a.bob_tp if a.bob_tp > 0 else (choose_bob_tp(sargs.mode, N) if use_gpu else N))
     comm = Comm(rank, N, dev, pl, make_tp_group(pl, backend) if N > 1 else None)

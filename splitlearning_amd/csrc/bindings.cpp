@@ -36,6 +36,7 @@ hipError_t conv_local_epoch_multi(const MultiAlice* al, int k, int B, SlOpt (*op
                                   void* table, int64_t table_bytes, hipStream_t st);
 size_t alice_step_desc_bytes();
 hipError_t conv_apply(const ConvPending& p, float* w, float* b, hipStream_t st);
+hipError_t conv_fwd_multi(const FrontFwdSet& set, int64_t chunk, hipStream_t st);
 hipError_t head_step(const float* X, float* W, float* b, const int64_t* y, int64_t ignore, float scale,
                      float* loss_rows, float* dX, float* s0w, float* s1w, float* s0b, float* s1b, int M, int K, int C,
                      SlOpt o, bool mask_dx, hipStream_t st);
@@ -294,6 +295,41 @@ void conv_local_epoch_multi(py::list alices, int64_t B, int64_t kind, double lr,
   check(sl::conv_local_epoch_multi(al.data(), k, (int)B, &epoch_opt, &ctx, table.data_ptr(), table.numel(),
                                    cur_stream()),
         "conv_local_epoch_multi");
+}
+
+// Frozen-front forwards of up to 16 co-located Alices, one launch per `chunk` rows for all of
+// them (conv.hip: conv_fwd_multi).  alices: [(x uint8 [N, 784], idx int64 [n] or None (rows
+// 0 .. n), n, w, b, y [n, 5408])].
+void conv_fwd_multi(py::list alices, int64_t chunk) {
+  const int k = (int)alices.size();
+  TORCH_CHECK(k >= 1 && k <= kFrontFwdMax, "1..16 Alices per launch");
+  TORCH_CHECK(chunk >= 1 && chunk <= 65535, "chunk rows");
+  FrontFwdSet set{};
+  set.k = k;
+  for (int a = 0; a < k; ++a) {
+    auto t = alices[a].cast<py::tuple>();
+    TORCH_CHECK(t.size() == 6, "alice tuple (x, idx, n, w, b, y)");
+    auto x = t[0].cast<at::Tensor>();
+    auto idx = t[1].cast<OptT>();
+    const int64_t n = t[2].cast<int64_t>();
+    auto w = t[3].cast<at::Tensor>();
+    auto b = t[4].cast<at::Tensor>();
+    auto y = t[5].cast<at::Tensor>();
+    check_x(x);
+    TORCH_CHECK(x.scalar_type() == at::kByte, "uint8 shards");
+    check_params(w, b);
+    TORCH_CHECK(n >= 0, "n");
+    if (idx.has_value()) {
+      check_idx(*idx, n);
+    } else {
+      TORCH_CHECK(n <= x.numel() / 784, "rows beyond the shard");
+    }
+    need_f32(y, "y");
+    TORCH_CHECK(y.is_contiguous() && y.numel() >= n * 5408, "y [n, 5408]");
+    set.d[a] = FrontFwdDesc{x.data_ptr<uint8_t>(), idx.has_value() ? idx->data_ptr<int64_t>() : nullptr, n,
+                            w.data_ptr<float>(), b.data_ptr<float>(), y.data_ptr<float>()};
+  }
+  check(sl::conv_fwd_multi(set, chunk, cur_stream()), "conv_fwd_multi");
 }
 
 // Split-mode client backward: dW partials from the cut gradient, then reduce+optimizer.
@@ -653,6 +689,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("head_step", &head_step);
   m.def("conv_local_epoch", &conv_local_epoch);
   m.def("conv_local_epoch_multi", &conv_local_epoch_multi);
+  m.def("conv_fwd_multi", &conv_fwd_multi);
   m.def("alice_step_desc_bytes", []() { return (int64_t)sl::alice_step_desc_bytes(); });
   m.def("linear_fwd", &linear_fwd);
   m.def("linear_epilogue", &linear_epilogue);

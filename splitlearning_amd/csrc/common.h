@@ -154,6 +154,22 @@ struct ConvPending {
   SlOpt o;
 };
 
+// One co-located Alice's frozen-front forward, for conv_fwd_multi (conv.hip): rows
+// idx[0 .. n) (or 0 .. n when idx is null) of her uint8 shard x -> y [n, 5408].
+struct FrontFwdDesc {
+  const uint8_t* x;
+  const int64_t* idx;
+  int64_t n;
+  const float* w;
+  const float* b;
+  float* y;
+};
+constexpr int kFrontFwdMax = 16;
+struct FrontFwdSet {
+  FrontFwdDesc d[kFrontFwdMax];
+  int k;
+};
+
 // One co-located Alice's local epoch, for conv_local_epoch_multi (conv.hip).
 struct MultiAlice {
   const uint8_t* x;        // shard pixels [N, 784]

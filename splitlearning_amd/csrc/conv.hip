@@ -76,22 +76,21 @@ __device__ __forceinline__ float conv_pending_param(const float* w, const float*
 // outputs, 5-6 per thread), so a batch of 16 runs 64 workgroups instead of 16 and each
 // thread's serial chain is a quarter as long (the per-sample 256-thread form measured
 // 11 us per batch of 16 in the split modes, where this kernel is on the critical path).
+// One (sample s = shard row src, channel group q) of the forward; am == nullptr: no argmax
+// (frozen-front forwards: evaluation, activation dumps).
 template <typename XT>
-__global__ void __launch_bounds__(256)
-conv_relu_pool_fwd_kernel(const XT* __restrict__ x, const int64_t* __restrict__ idx, int64_t row0,
-                          const float* __restrict__ w, const float* __restrict__ b,
-                          float* __restrict__ y, uint8_t* __restrict__ am,
-                          const int64_t* __restrict__ lab_in = nullptr, int64_t* __restrict__ lab_out = nullptr,
-                          const float* __restrict__ pslab = nullptr, int pB = 0, const float* __restrict__ s0w = nullptr,
-                          const float* __restrict__ s1w = nullptr, const float* __restrict__ s0b = nullptr,
-                          const float* __restrict__ s1b = nullptr, SlOpt o = SlOpt{}) {
+__device__ __forceinline__ void conv_fwd_sample(const XT* __restrict__ x, int64_t src, int s, int q,
+                                                const float* __restrict__ w, const float* __restrict__ b,
+                                                float* __restrict__ y, uint8_t* __restrict__ am,
+                                                const int64_t* __restrict__ lab_in, int64_t* __restrict__ lab_out,
+                                                const float* __restrict__ pslab, int pB, const float* __restrict__ s0w,
+                                                const float* __restrict__ s1w, const float* __restrict__ s0b,
+                                                const float* __restrict__ s1b, const SlOpt& o) {
   constexpr int CH = 8, NO = CH * 169, PER = (NO + 255) / 256;
   __shared__ float img[IMG_LDS];
   __shared__ float sw[CH * 9];
   __shared__ float sb[CH];
-  const int s = blockIdx.x, q = blockIdx.y;
   const int tid = threadIdx.x;
-  const int64_t src = idx ? idx[s] : row0 + s;
   // every independent load goes out before anything is consumed
   const XT* xr = x + src * 784;
   const float p0 = (float)xr[tid], p1 = (float)xr[256 + tid], p2 = (float)xr[512 + tid];
@@ -118,7 +117,7 @@ conv_relu_pool_fwd_kernel(const XT* __restrict__ x, const int64_t* __restrict__ 
   if (tid < 784 - 768) img[img_idx((768 + tid) / 28, (768 + tid) % 28)] = p3;
   __syncthreads();
   float* yo = y + (int64_t)s * 5408 + q * NO;
-  uint8_t* ao = am + (int64_t)s * 5408 + q * NO;
+  uint8_t* ao = am ? am + (int64_t)s * 5408 + q * NO : nullptr;
 #pragma unroll
   for (int u = 0; u < PER; ++u) {
     const int o = tid + 256 * u;
@@ -131,9 +130,34 @@ conv_relu_pool_fwd_kernel(const XT* __restrict__ x, const int64_t* __restrict__ 
       int arg;
       conv_pool_at(img, sw + oc * 9, sb[oc], ph, pw, yv, arg);
       yo[o] = yv;
-      ao[o] = (uint8_t)arg;
+      if (ao) ao[o] = (uint8_t)arg;
     }
   }
+}
+
+template <typename XT>
+__global__ void __launch_bounds__(256)
+conv_relu_pool_fwd_kernel(const XT* __restrict__ x, const int64_t* __restrict__ idx, int64_t row0,
+                          const float* __restrict__ w, const float* __restrict__ b,
+                          float* __restrict__ y, uint8_t* __restrict__ am,
+                          const int64_t* __restrict__ lab_in = nullptr, int64_t* __restrict__ lab_out = nullptr,
+                          const float* __restrict__ pslab = nullptr, int pB = 0, const float* __restrict__ s0w = nullptr,
+                          const float* __restrict__ s1w = nullptr, const float* __restrict__ s0b = nullptr,
+                          const float* __restrict__ s1b = nullptr, SlOpt o = SlOpt{}) {
+  const int s = blockIdx.x;
+  conv_fwd_sample<XT>(x, idx ? idx[s] : row0 + s, s, (int)blockIdx.y, w, b, y, am, lab_in, lab_out, pslab, pB, s0w,
+                      s1w, s0b, s1b, o);
+}
+
+// Frozen-front forward of several co-located Alices in one launch (evaluation and the SISA
+// activation dump, reference data_entities_vanilla_sisa.py:196-211,370-371): grid (rows,
+// 4, Alices); Alice a's rows [r0, r0 + gridDim.x) of her order, clipped to her n.  No argmax.
+__global__ void __launch_bounds__(256) conv_fwd_multi_kernel(FrontFwdSet set, int64_t r0) {
+  const FrontFwdDesc& d = set.d[blockIdx.z];
+  const int64_t r = r0 + blockIdx.x;
+  if (r >= d.n) return;                  // uniform per workgroup
+  conv_fwd_sample<uint8_t>(d.x, d.idx ? d.idx[r] : r, (int)r, (int)blockIdx.y, d.w, d.b, d.y, nullptr, nullptr,
+                           nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr, SlOpt{});
 }
 
 // ---------------------------------------------------------------------------------------
@@ -632,6 +656,19 @@ hipError_t conv_fwd(const void* x, bool x_u8, const int64_t* idx, int64_t row0, 
     conv_relu_pool_fwd_kernel<float><<<dim3(B, 4), 256, 0, st>>>((const float*)x, idx, row0, w, b, y, am, lab_in,
                                                                  lab_out, p.slab, p.B, p.s0w, p.s1w, p.s0b, p.s1b,
                                                                  p.o);
+  return hipGetLastError();
+}
+
+// Frozen-front forwards of set.k Alices (uint8 shards), chunk rows per launch: one launch per
+// chunk for all of them instead of one per Alice and chunk.
+hipError_t conv_fwd_multi(const FrontFwdSet& set, int64_t chunk, hipStream_t st) {
+  if (set.k <= 0 || set.k > kFrontFwdMax || chunk <= 0) return set.k == 0 ? hipSuccess : hipErrorInvalidValue;
+  int64_t nmax = 0;
+  for (int a = 0; a < set.k; ++a) nmax = std::max<int64_t>(nmax, set.d[a].n);
+  for (int64_t r0 = 0; r0 < nmax; r0 += chunk) {
+    const int rows = (int)std::min<int64_t>(chunk, nmax - r0);
+    conv_fwd_multi_kernel<<<dim3(rows, 4, set.k), 256, 0, st>>>(set, r0);
+  }
   return hipGetLastError();
 }
 

@@ -9,7 +9,7 @@
 // protocols/ushape.py `split_epoch`, look-ahead order) issues ~10 launches per batch from
 // Python; this class issues the SAME launches with the same arguments, seeds, workspace sizes
 // and optimizer step counts from C++, so the results are bit-identical
-// (tests/test_graphs_gpu.py::test_native_split_epoch_matches_python):
+// (tests/test_split_native_gpu.py):
 //
 //   Alice   conv forward of batch i (gathers its labels; applies her pending update in-kernel)
 //   Bob     [fc1 epilogue of the look-ahead slabs | fc1 forward] -> fc2 ...
@@ -20,6 +20,10 @@
 //   Alice   conv forward of batch i+1 (the update of batch i applied in-kernel)
 //   Bob     grouped wgrad + optimizer of every layer, with batch i+1's fc1 product (look-ahead)
 //   end     the last pending Alice update is stored
+//
+// (Running fc2 / fc3's update on a side stream beside the Alice's backward + next forward, fc1
+// alone on the main stream, measured slower: 87-88 k vs 92-94 k samples/s at vanilla ws = 2,
+// profiles/r3_vanilla_side_stream_ab.txt.)
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 

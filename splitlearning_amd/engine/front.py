@@ -75,6 +75,23 @@ class FrontEngine:
             return torch.empty(0, 5408, device=self.device)
         return outs[0] if len(outs) == 1 else torch.cat(outs, 0)
 
+    @staticmethod
+    def forward_multi(fronts: list, shards: list, orders: list, chunk: int = 8192) -> list:
+        """`forward_chunked` of several co-located Alices at once (evaluation, SISA activation
+        dumps): one launch per chunk of rows for all of them, bitwise each Alice's own
+        forward.  `orders[i]` None: the shard's rows in order.  Falls back to one Alice after
+        another on the torch backend or float shards."""
+        ops_ = fronts[0].ops if fronts else None
+        if not fronts or not hasattr(ops_, "conv_front_fwd_multi") or \
+                any(sh.x.dtype != torch.uint8 for sh in shards):
+            return [f.forward_chunked(sh, o if o is not None else sh.sequential_order(), chunk)
+                    for f, sh, o in zip(fronts, shards, orders)]
+        items = []
+        for f, sh, o in zip(fronts, shards, orders):
+            w, b = f.params
+            items.append((sh.x, o, sh.n if o is None else int(o.numel()), w, b))
+        return ops_.conv_front_fwd_multi(items, chunk)
+
     def backward_step(self, dy, y, am, shard: DeviceShard, idx, slot: OptSlot, t: int | None = None,
                       prefix: str = "", defer: bool = False):
         """Backward + optimizer step.  `defer` (split-mode epochs, HIP path): launch only the

@@ -68,6 +68,16 @@ def conv_front_fwd(x_u8, idx, w, b, y=None, am=None, labels=None):
     return (y, am) if labels is None else (y, am, lab)
 
 
+def conv_front_fwd_multi(items, chunk: int = 8192):
+    """Frozen-front forwards (no argmax) of several Alices, one launch per `chunk` rows for
+    up to 16 of them: items [(x_u8, idx or None (rows 0 .. n), n, w, b)] -> [y [n, 5408]]."""
+    outs = [torch.empty(int(n), CUT, device=x.device, dtype=torch.float32) for x, _, n, _, _ in items]
+    for g in range(0, len(items), 16):
+        C().conv_fwd_multi([(x, idx, int(n), w.detach(), b.detach(), y)
+                            for (x, idx, n, w, b), y in zip(items[g:g + 16], outs[g:g + 16])], int(chunk))
+    return outs
+
+
 def conv_front_bwd(dy, y, am, x_u8, idx, w, b):
     """dW, db only (kind 0 writes the gradient into the state slot)."""
     B = int(idx.numel())

@@ -400,11 +400,13 @@ class Session:
     def _eval_counts(self, omit_label: int):
         """counters[k+1, 6] summed over ranks (row c = Alice_c)."""
         counts = torch.zeros(self.k + 1, 6, dtype=torch.int64, device=self.device)
+        # every hosted Alice's test activations from one launch per chunk (frozen fronts)
+        hosted = [cid for cid in range(1, self.k + 1) if self.hosts(cid)]
+        acts = dict(zip(hosted, FrontEngine.forward_multi([self.alices[c].front for c in hosted],
+                                                          [self.alices[c].test for c in hosted],
+                                                          [None] * len(hosted))))
         for cid in range(1, self.k + 1):
-            act = None
-            if self.hosts(cid):
-                a = self.alices[cid]
-                act = a.front.forward_chunked(a.test, a.test.sequential_order())
+            act = acts.pop(cid, None)
             logits = self._bob_logits_for(cid, act)
             if self.hosts(cid):
                 a = self.alices[cid]

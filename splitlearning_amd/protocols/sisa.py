@@ -137,19 +137,31 @@ class SisaSession(Session):
     def give_activation_and_labels(self, cid: int, unlearned: bool = False):
         """Alice side of the dump: (activations [n,5408], labels [n]) over the train loader
         (fresh shuffle) or the unlearn loader (fixed order)."""
-        a = self.alices[cid]
-        if unlearned:
-            if a.unlearn_order is None:
-                raise RuntimeError(f"Alice-{cid} has no unlearn dataloader (unlearn/train_control first)")
-            order = a.unlearn_order
-        else:
-            order = a.train.shuffled_order(a.gen)
-        acts = a.front.forward_chunked(a.train, order)
-        if self.act_dtype != torch.float32:
-            acts = acts.to(self.act_dtype)
-        return acts, a.train.y[order]
+        return self._give_many([(cid, unlearned)])[cid]
 
-    def get_activation_and_labels(self, client_id: int, unlearned: bool = False, unlearn_id=None):
+    def _give_many(self, reqs) -> dict:
+        """`give_activation_and_labels` of several hosted Alices [(cid, unlearned)]: their
+        frozen fronts run together, one launch per chunk of rows (FrontEngine.forward_multi)."""
+        fronts, shards, orders = [], [], []
+        for cid, unlearned in reqs:
+            a = self.alices[cid]
+            if unlearned:
+                if a.unlearn_order is None:
+                    raise RuntimeError(f"Alice-{cid} has no unlearn dataloader (unlearn/train_control first)")
+                order = a.unlearn_order
+            else:
+                order = a.train.shuffled_order(a.gen)
+            fronts.append(a.front)
+            shards.append(a.train)
+            orders.append(order)
+        out = {}
+        for (cid, _), acts, order in zip(reqs, FrontEngine.forward_multi(fronts, shards, orders), orders):
+            if self.act_dtype != torch.float32:
+                acts = acts.to(self.act_dtype)
+            out[cid] = (acts, self.alices[cid].train.y[order])
+        return out
+
+    def get_activation_and_labels(self, client_id: int, unlearned: bool = False, unlearn_id=None, dumped=None):
         key = (client_id, unlearned, unlearn_id)
         hit = self.activation_and_labels_cache.get(key) if self.is_bob else None
         # every rank must agree on hit/miss: the cache is replicated on all Bob ranks and
@@ -160,7 +172,7 @@ class SisaSession(Session):
             return hit
         acts = labels = None
         if self.hosts(client_id):
-            acts, labels = self.give_activation_and_labels(client_id, unlearned)
+            acts, labels = dumped if dumped is not None else self.give_activation_and_labels(client_id, unlearned)
         acts = self.to_bob_var(client_id, acts, (CUT_FEATURES,), self.act_dtype)
         labels = self.to_bob_var(client_id, labels, (), torch.int64)
         self._cache_keys.add(key)
@@ -186,17 +198,16 @@ class SisaSession(Session):
                 keys.append(key)
         if not keys:
             return
+        dumps = self._give_many([(cid, unl) for cid, unl, _ in keys if self.hosts(cid)])
         if not self.comm.distributed:
             for cid, unl, uid in keys:
-                self.get_activation_and_labels(cid, unlearned=unl, unlearn_id=uid)
+                self.get_activation_and_labels(cid, unlearned=unl, unlearn_id=uid, dumped=dumps.get(cid))
             return
         local = {}
         counts = torch.zeros(self.k + 1, dtype=torch.int64, device=self.device)
-        for cid, unl, _ in keys:
-            if self.hosts(cid):
-                acts, labels = self.give_activation_and_labels(cid, unl)
-                local[cid] = self.pack(acts, labels)
-                counts[cid] = labels.numel()
+        for cid, (acts, labels) in dumps.items():
+            local[cid] = self.pack(acts, labels)
+            counts[cid] = labels.numel()
         self.comm.allreduce_sum_(counts)
         counts = counts.tolist()
         sends, recvs, got = [], [], {}

@@ -5,7 +5,7 @@ process — the one-GPU BASELINE point (ws = 2) and every co-located placement.
 The executor issues the same launches, with the same arguments, dropout seeds, workspaces
 and optimizer step counts, as `VanillaSession.split_epoch` / `UShapeSession.split_epoch` in
 their look-ahead order, so the parameters it produces are bit-identical to the Python
-loop's (tests/test_graphs_gpu.py::test_native_split_epoch_matches_python); the Python loop
+loop's (tests/test_split_native_gpu.py); the Python loop
 stays the path for every other placement and for `--python_epoch`.
 
 Reference hot loops: data_entities_vanilla.py:66-76 and data_entities.py:65-81.
