@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--tp", type=int, default=1, help="simulate a TP shard (rank 0 of tp, 1-rank all-reduce)")
     ap.add_argument("--time", action="store_true", help="print wall-clock us/step (second half of the run)")
     ap.add_argument("--variant", action="append", default=[], help="slot=value kernel variant (A/B)")
+    ap.add_argument("--allreduce", choices=("rccl", "ipc"), default="rccl",
+                    help="TP shard's all-reduce stand-in: 1-rank RCCL or the 1-rank peer-mapped kernel")
     a = ap.parse_args()
     for kv in a.variant:
         slot, val = (int(v) for v in kv.split("="))
@@ -38,8 +40,14 @@ def main():
     labels = torch.randint(0, 10, (n,), device=dev)
     ar = None
     if a.tp > 1:
-        from splitlearning_amd.parallel.rccl import native_allreduce, self_comm
-        ar = native_allreduce(self_comm())
+        from splitlearning_amd.parallel.rccl import ipc_allreduce, native_allreduce, self_comm
+        if a.allreduce == "ipc":
+            # the peer-mapped all-reduce fused into head_fwd, one rank (no peer to wait for)
+            ipc = H.C().IpcAllReduce(1, 0, 64 * 1024)
+            ipc.open([ipc.handle()])
+            ar = ipc_allreduce(ipc)
+        else:
+            ar = native_allreduce(self_comm())
     tail = TailEngine(ServerTailSisa(), sisa_server_spec(), dev, tp_rank=0, tp_size=a.tp, allreduce=ar)
     slot = OptSlot(adam(1e-3, 1e-5))
     if a.path == "local":

@@ -271,11 +271,12 @@ class TailEngine:
         p[0].copy_(self.ops.linear_fwd(x0, L1.W, None, False, 0.0, 0, 0))
         self._pre = p
 
-    def train_fwd_bwd3(self, x, labels, need_dx: bool, dseeds=None, pre: bool = False):
+    def train_fwd_bwd3(self, x, labels, need_dx: bool, dseeds=None, pre: bool = False, gscale=None):
         """Training forward + softmax-CE + all data gradients of the 3-layer tail.
         Returns (per-row loss, dL/dx or None); `fused_step` then applies the optimizer.
         `pre`: fc1's product for `x` was already computed by the previous step's
-        `fused_step(x_next=x)` (or `lookahead_prologue(x)`); only its epilogue runs here."""
+        `fused_step(x_next=x)` (or `lookahead_prologue(x)`); only its epilogue runs here.
+        With `ce_groups` = G > 1 (SISA-concat), labels and `gscale` are [M, G]."""
         ops = self.ops
         L1, L2, L3 = self.layers
         M = x.shape[0]
@@ -304,7 +305,9 @@ class TailEngine:
             self.allreduce(P2)
         else:
             P2 = ops.linear_fwd_partial(h1, L2.W)
-        h2, dlog, dz2, loss = ops.server_head3(P2, L2.b, True, p2, seeds[1], L3.W, L3.b, labels, 1.0 / M, **ds(1))
+        G = self.ce_groups
+        kw = ds(1) if G == 1 else dict(ds(1), groups=G, gscale=gscale)
+        h2, dlog, dz2, loss = ops.server_head3(P2, L2.b, True, p2, seeds[1], L3.W, L3.b, labels, 1.0 / M, **kw)
         s1 = 1.0 / (1.0 - p1) if p1 else 1.0
         dx = None
         # dz1 is materialised (split-N dgrad + reduce/mask kernel): reducing the split-N

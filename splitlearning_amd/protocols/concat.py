@@ -101,13 +101,21 @@ class ConcatSession(SisaSession):
             scale[:, j] = sc.to(dev) * (Y[:, j] != -100)
         Ms = [max(r) for r in rows]
         tail = self.tail
-        if getattr(self.args, "native_epoch", True) and tail.native_epoch_ok(B):
-            # the fused server step on the concatenated rows (csrc/engine.cpp with the grouped
-            # cross-entropy head): every step takes B rows; rows past a step's M_t are zero
-            # with every label ignored, so they add nothing to any gradient — the same step
-            # as on M_t rows
+        if tail.native_epoch_ok(B):
+            # the fused server step on the concatenated rows (the grouped cross-entropy head):
+            # every step takes B rows; rows past a step's M_t are zero with every label
+            # ignored, so they add nothing to any gradient — the same step as on M_t rows.
+            # Issued from C++ (csrc/engine.cpp), or step by step from here with the same
+            # launches (`--python_epoch`; bitwise equal, tests/test_split_native_gpu.py)
             tail.lookahead_prologue(X[:B])
-            tail.run_native_epoch(X, Y, self.bob_slot, B, True, gscale=scale)
+            if getattr(self.args, "native_epoch", True):
+                tail.run_native_epoch(X, Y, self.bob_slot, B, True, gscale=scale)
+            else:
+                for t in range(T):
+                    sl = slice(t * B, (t + 1) * B)
+                    tail.train_fwd_bwd3(X[sl], Y[sl].reshape(-1), need_dx=False, pre=True, gscale=scale[sl])
+                    tail.fused_step(self.bob_slot, x_next=X[(t + 1) * B:(t + 2) * B] if t + 1 < T else None)
+                    self.comm.progress()
             self.comm.progress()
             return sum(sum(r) for r in rows)
         grouped = tail.grouped_ok()

@@ -77,3 +77,38 @@ def test_native_split_ushape_large_batch_uses_python(cuda, tmp_path):
     from splitlearning_amd.protocols.split_native import native_split_ok
     assert not native_split_ok(_session("ushape", tmp_path, True, cuda, 64), 1, "ushape")
     assert native_split_ok(_session("vanilla", tmp_path, True, cuda, 64), 1, "vanilla")
+
+
+@pytest.mark.parametrize("k", [2, 4])
+def test_native_concat_epoch_matches_python(cuda, tmp_path, k):
+    """SISA-concat server epochs (k-head grouped CE, uneven shards): `_C.ServerEpoch` with the
+    grouped head against the same launches issued step by step from Python (`--python_epoch`):
+    bitwise equal parameters, Adam moments and counters."""
+    from splitlearning_amd.parallel.dist import Comm, Placement
+    from splitlearning_amd.protocols import ConcatSession
+
+    def session(native):
+        flags = [] if native else ["--python_epoch"]
+        args = parse_args(["--sisa", "--concat", "--world_size", str(k + 1), "--seed", "11", "--num_samples",
+                           "1500", "--no_tqdm", "--datapath", str(tmp_path / "d"),
+                           "--log_dir", str(tmp_path / ("ln" if native else "lp"))] + flags)
+        if not (tmp_path / "d").exists():
+            write_shards(args, verbose=False)
+        return ConcatSession(args, Comm(0, 1, cuda, Placement.make(k + 1, 1, 1)), cuda)
+
+    sp, sn = session(False), session(True)
+    B = sn.B
+    g = torch.Generator().manual_seed(k)
+    ns = [B * 5 + 3, B * 3 + 11, B * 6, B * 2 + 1][:k]
+    caches = [((torch.rand(n, 5408, generator=g) * 10).to(cuda), torch.randint(0, 10, (n,), generator=g).to(cuda))
+              for n in ns]
+    for _ in range(2):
+        for s in (sp, sn):
+            s.concat_epoch(caches)
+    torch.cuda.synchronize()
+    for La, Lb in zip(sp.tail.layers, sn.tail.layers):
+        assert torch.equal(La.W, Lb.W) and torch.equal(La.b, Lb.b), La.spec.name
+    for name, st in sp.bob_slot.states.items():
+        for key, v in st.items():
+            assert torch.equal(v, sn.bob_slot.states[name][key]), (name, key)
+    assert sp.bob_slot.t == sn.bob_slot.t and sp.tail.fwd_count == sn.tail.fwd_count
