@@ -20,11 +20,25 @@
 // different banks.  Requires K % 4 == 0 and 16-byte aligned rows (host checks).
 #include "common.h"
 
+#include <algorithm>
 #include <type_traits>
 
 namespace sl {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+// Operand loads are buffer loads with 32-bit byte offsets (operands < 2 GB: gemm_nt splits
+// taller X by rows); an out-of-range tile element gets an offset past the buffer and reads as
+// 0.  (`cond ? *p : zero` was turned into a load through a select of the global pointer and
+// the address of a private zero: flat loads, the staging registers demoted to scratch, and
+// every LDS wait also waiting for the prefetch.)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t gemm_rsrc(const float* base, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ float4 gemm_ld(__amdgpu_buffer_rsrc_t rs, bool in, int64_t elem) {
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  const int off = in ? (int)(elem * 4) : 0x7ffffff0;
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+}
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ bf16x4 to_bf16x4(float4 v) {
@@ -58,17 +72,17 @@ gemm_nt_kernel(const float* __restrict__ X, int ldx, const float* __restrict__ W
   const int tm = blockIdx.x % tilesM, tn = blockIdx.x / tilesM;
   const int m0 = tm * BM, n0 = tn * BN;
   float4 ra[APER], rb[BPER];
-  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  const __amdgpu_buffer_rsrc_t rX = gemm_rsrc(X, (int64_t)M * ldx * 4), rW = gemm_rsrc(W, (int64_t)N * ldw * 4);
   auto gload = [&](int k0) {
 #pragma unroll
     for (int p = 0; p < APER; ++p) {
       const int i = tid + p * NT, r = i / F4R, k = k0 + (i % F4R) * 4, gm = m0 + r;
-      ra[p] = (gm < M && k < K) ? *reinterpret_cast<const float4*>(X + (int64_t)gm * ldx + k) : z4;
+      ra[p] = gemm_ld(rX, gm < M && k < K, (int64_t)gm * ldx + k);
     }
 #pragma unroll
     for (int p = 0; p < BPER; ++p) {
       const int i = tid + p * NT, r = i / F4R, k = k0 + (i % F4R) * 4, gn = n0 + r;
-      rb[p] = (gn < N && k < K) ? *reinterpret_cast<const float4*>(W + (int64_t)gn * ldw + k) : z4;
+      rb[p] = gemm_ld(rW, gn < N && k < K, (int64_t)gn * ldw + k);
     }
   };
   auto sstore = [&](int buf) {
@@ -98,7 +112,10 @@ gemm_nt_kernel(const float* __restrict__ X, int ldx, const float* __restrict__ W
   __syncthreads();
   for (int s = 0; s < nk; ++s) {
     const int buf = s & 1;
-    if (s + 1 < nk) gload((s + 1) * BK);        // next stage's loads in flight during the MFMAs
+    // next stage's loads in flight during the MFMAs (unconditional: the last stage reloads
+    // its own block, unused; a conditional load keeps ra / rb out of registers)
+    gload((s + 1 < nk ? s + 1 : s) * BK);
+    __builtin_amdgcn_sched_barrier(0);          // the loads go out before the MFMAs
     if constexpr (BF16) {
 #pragma unroll
       for (int kk = 0; kk < BK; kk += 32) {
@@ -132,10 +149,13 @@ gemm_nt_kernel(const float* __restrict__ X, int ldx, const float* __restrict__ W
               acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][c], b[j][c], acc[i][j], 0, 0, 0);
       }
     }
-    if (s + 1 < nk) {
-      sstore(buf ^ 1);    // the other buffer: its last readers finished before the previous barrier
-      __syncthreads();
-    }
+    // keep the staging stores (and so the wait for the prefetched data) after this stage's
+    // MFMAs: scheduled above them, they expose the whole load latency every stage
+    __builtin_amdgcn_sched_barrier(0);
+    // the other buffer (its last readers finished before the previous barrier); at the last
+    // stage an unused write, kept unconditional so the loads are not sunk below the MFMAs
+    sstore(buf ^ 1);
+    __syncthreads();
   }
   // epilogue: lane (li, lq) of block (i, j) holds rows 4 lq + r, column li
 #pragma unroll
@@ -150,6 +170,132 @@ gemm_nt_kernel(const float* __restrict__ X, int ldx, const float* __restrict__ W
         if (m < M) Y[(int64_t)m * ldy + n] = apply_epi(e, acc[i][j][r], m, n);
       }
     }
+}
+
+// fp32 on the 32 x 32 x 2 MFMA: each wave a 64 x 64 tile as 2 x 2 blocks of 32 x 32
+// (4 accumulators of 16 floats).  Lane half h = lane >> 5 holds k = 2 s + h of a step; the
+// k order inside a 16-wide stage is permuted so a lane's operands for 8 consecutive steps are
+// two contiguous float4s (logical k of step s, half h: 8 h + s), one ds_read_b128 each.
+// Split-K (gridDim.y = S > 1, for grids of few tiles): slice z = blockIdx.y covers k in
+// [z kc, z kc + kc) and stores its raw partial sums into slab z of P ([S][M][N]); the slabs are
+// then reduced with the epilogue applied (linear_epilogue).
+template <int WM, int BK>
+__global__ void __launch_bounds__(128 * WM)
+gemm_nt_f32x32_kernel(const float* __restrict__ X, int ldx, const float* __restrict__ W, int ldw,
+                      float* __restrict__ Y, int ldy, int M, int N, int K, Epi e, int kc, float* __restrict__ P) {
+  constexpr int BM = 64 * WM, BN = 128, NT = 128 * WM;
+  constexpr int LD = BK + 4;
+  constexpr int F4R = BK / 4;
+  constexpr int APER = BM * F4R / NT, BPER = BN * F4R / NT;
+  static_assert(APER * NT == BM * F4R && BPER * NT == BN * F4R, "tile / thread split");
+  static_assert(BK % 16 == 0, "16-wide k groups");
+  typedef float f32x16 __attribute__((ext_vector_type(16)));
+  __shared__ __attribute__((aligned(16))) float As[2][BM][LD];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BN][LD];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int tilesM = (M + BM - 1) / BM;
+  const int tm = blockIdx.x % tilesM, tn = blockIdx.x / tilesM;
+  const int m0 = tm * BM, n0 = tn * BN;
+  float4 ra[APER], rb[BPER];
+  const __amdgpu_buffer_rsrc_t rX = gemm_rsrc(X, (int64_t)M * ldx * 4), rW = gemm_rsrc(W, (int64_t)N * ldw * 4);
+  const int kb = (int)blockIdx.y * kc, ke = min(K, kb + kc);
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int p = 0; p < APER; ++p) {
+      const int i = tid + p * NT, r = i / F4R, k = k0 + (i % F4R) * 4, gm = m0 + r;
+      ra[p] = gemm_ld(rX, gm < M && k < ke, (int64_t)gm * ldx + k);
+    }
+#pragma unroll
+    for (int p = 0; p < BPER; ++p) {
+      const int i = tid + p * NT, r = i / F4R, k = k0 + (i % F4R) * 4, gn = n0 + r;
+      rb[p] = gemm_ld(rW, gn < N && k < ke, (int64_t)gn * ldw + k);
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int p = 0; p < APER; ++p) {
+      const int i = tid + p * NT, r = i / F4R, k = (i % F4R) * 4;
+      *reinterpret_cast<float4*>(&As[buf][r][k]) = ra[p];
+    }
+#pragma unroll
+    for (int p = 0; p < BPER; ++p) {
+      const int i = tid + p * NT, r = i / F4R, k = (i % F4R) * 4;
+      *reinterpret_cast<float4*>(&Bs[buf][r][k]) = rb[p];
+    }
+  };
+  const int wm = (wv % WM) * 64, wn = (wv / WM) * 64;
+  const int lr = lane & 31, h = lane >> 5;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const int nk = (ke - kb + BK - 1) / BK;
+  gload(kb);
+  sstore(0);
+  __syncthreads();
+  for (int s = 0; s < nk; ++s) {
+    const int buf = s & 1;
+    gload(kb + (s + 1 < nk ? s + 1 : s) * BK);
+    __builtin_amdgcn_sched_barrier(0);          // the loads go out before the MFMAs
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 16) {
+      f32x4 a[2][2], b[2][2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          a[i][q] = *reinterpret_cast<const f32x4*>(&As[buf][wm + 32 * i + lr][kk + 8 * h + 4 * q]);
+          b[i][q] = *reinterpret_cast<const f32x4*>(&Bs[buf][wn + 32 * i + lr][kk + 8 * h + 4 * q]);
+        }
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][q][c], b[j][q][c], acc[i][j], 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    sstore(buf ^ 1);
+    __syncthreads();
+  }
+  // C / D: lane l of block (i, j), register r: row 32 i + (r & 3) + 8 (r >> 2) + 4 h, column 32 j + l & 31
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + wn + 32 * j + lr;
+      if (n >= N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (m >= M) continue;
+        if (P) P[((int64_t)blockIdx.y * M + m) * N + n] = acc[i][j][r];
+        else Y[(int64_t)m * ldy + n] = apply_epi(e, acc[i][j][r], m, n);
+      }
+    }
+}
+
+hipError_t linear_epilogue(const float* P, int ldp, float* Y, int ldy, int M, int N, Epi e, int S, int64_t slab,
+                           hipStream_t st);
+
+// S > 1: split-K over S slices into ws ([S][M][N], >= S M N floats), then one reduce +
+// epilogue launch.
+template <int WM, int BK>
+static hipError_t launch_gemm_f32x32(const float* X, int ldx, const float* W, int ldw, float* Y, int ldy, int M, int N,
+                                     int K, Epi e, int S, float* ws, hipStream_t st) {
+  const int64_t tiles = (int64_t)((M + 64 * WM - 1) / (64 * WM)) * ((N + 127) / 128);
+  if (tiles > 0x7fffffff) return hipErrorInvalidValue;
+  const int kc = S > 1 ? ((K + S - 1) / S + BK - 1) / BK * BK : K;
+  gemm_nt_f32x32_kernel<WM, BK><<<dim3((unsigned)tiles, S), 128 * WM, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e,
+                                                                             kc, S > 1 ? ws : nullptr);
+  if (S > 1) return linear_epilogue(ws, N, Y, ldy, M, N, e, S, (int64_t)M * N, st);
+  return hipGetLastError();
 }
 
 template <bool BF16, int WM, int BK>
@@ -168,12 +314,46 @@ static hipError_t launch_gemm(const float* X, int ldx, const float* W, int ldw, 
 // round trip: latency-bound, below hipBLASLt's 141 TF fp32 on the same shapes, which is why the
 // fp32 evaluation product is routed to the library (ops/hip_ops.py) and this kernel serves
 // --dtype bf16 and graph capture.
+static hipError_t gemm_nt_rows(const float* X, int ldx, const float* W, int ldw, float* Y, int ldy, int M, int N,
+                               int K, Epi e, bool bf16, float* ws, int64_t ws_elems, hipStream_t st);
+
 hipError_t gemm_nt(const float* X, int ldx, const float* W, int ldw, float* Y, int ldy, int M, int N, int K, Epi e,
-                   bool bf16, hipStream_t st) {
+                   bool bf16, float* ws, int64_t ws_elems, hipStream_t st) {
   if (M <= 0 || N <= 0) return hipSuccess;
   if ((K & 3) || (ldx & 3) || (ldw & 3)) return hipErrorInvalidValue;
+  constexpr int64_t kMax = 0x7fff0000;            // buffer-load byte offsets (gemm_ld)
+  if ((int64_t)N * ldw * 4 > kMax || (int64_t)ldx * 4 * 256 > kMax) return hipErrorInvalidValue;
+  const int rows = (int)std::min<int64_t>(M, kMax / ((int64_t)ldx * 4) / 256 * 256);
+  // the dropout hash takes the row index: a chunked product would restart it (inference only)
+  if (rows < M && e.thresh) return hipErrorInvalidValue;
+  for (int m = 0; m < M; m += rows) {
+    const hipError_t r = gemm_nt_rows(X + (int64_t)m * ldx, ldx, W, ldw, Y + (int64_t)m * ldy, ldy,
+                                      std::min(rows, M - m), N, K, e, bf16, ws, ws_elems, st);
+    if (r != hipSuccess) return r;
+  }
+  return hipSuccess;
+}
+
+static hipError_t gemm_nt_rows(const float* X, int ldx, const float* W, int ldw, float* Y, int ldy, int M, int N,
+                               int K, Epi e, bool bf16, float* ws, int64_t ws_elems, hipStream_t st) {
+  if (!ws) ws_elems = 0;
   if (bf16) return launch_gemm<true, 4, 64>(X, ldx, W, ldw, Y, ldy, M, N, K, e, st);
-  return launch_gemm<false, 4, 16>(X, ldx, W, ldw, Y, ldy, M, N, K, e, st);
+  switch (g_variant[10]) {   // A/B of the fp32 forms (scripts/gemm_bench.py)
+    case 1: return launch_gemm_f32x32<2, 16>(X, ldx, W, ldw, Y, ldy, M, N, K, e, 1, nullptr, st);
+    case 2: return launch_gemm_f32x32<4, 16>(X, ldx, W, ldw, Y, ldy, M, N, K, e, 1, nullptr, st);
+    case 3: return launch_gemm_f32x32<2, 32>(X, ldx, W, ldw, Y, ldy, M, N, K, e, 1, nullptr, st);
+    case 4: return launch_gemm_f32x32<4, 32>(X, ldx, W, ldw, Y, ldy, M, N, K, e, 1, nullptr, st);
+    case 5: return launch_gemm<false, 4, 16>(X, ldx, W, ldw, Y, ldy, M, N, K, e, st);
+    default: break;
+  }
+  // fp32: the 32 x 32 x 2 form.  256 x 128 tiles when they fill the chip (>= 2 per CU), else
+  // 128 x 128 tiles, split over K until ~2 workgroups per CU (slices >= 512 deep, <= 8)
+  const int64_t t4 = (int64_t)((M + 255) / 256) * ((N + 127) / 128);
+  if (t4 >= 512) return launch_gemm_f32x32<4, 16>(X, ldx, W, ldw, Y, ldy, M, N, K, e, 1, nullptr, st);
+  const int64_t t2 = (int64_t)((M + 127) / 128) * ((N + 127) / 128);
+  int S = 1;
+  while (S < 8 && t2 * S * 2 <= 640 && K / (S * 2) >= 512 && (int64_t)S * 2 * M * N <= ws_elems) S *= 2;
+  return launch_gemm_f32x32<2, 16>(X, ldx, W, ldw, Y, ldy, M, N, K, e, S, ws, st);
 }
 
 }  // namespace sl

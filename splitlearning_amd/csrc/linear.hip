@@ -30,7 +30,7 @@ int g_variant[24] = {0};
 int g_bf16 = 0;
 
 hipError_t gemm_nt(const float* X, int ldx, const float* W, int ldw, float* Y, int ldy, int M, int N, int K, Epi e,
-                   bool bf16, hipStream_t st);
+                   bool bf16, float* ws, int64_t ws_elems, hipStream_t st);
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -525,7 +525,7 @@ hipError_t linear_fwd(const float* X, int ldx, const float* W, int ldw, float* Y
   // many rows (evaluation over a whole test set, large batches): the LDS-tiled MFMA GEMM.
   // In fp32 the caller (hip_ops.linear_fwd) hands plain products to hipBLASLt and only the
   // epilogue runs here, except inside a HIP graph capture or under variant 11 = 1.
-  if (M > 128) return gemm_nt(X, ldx, W, ldw, Y, ldy, M, N, K, e, g_bf16 != 0, st);
+  if (M > 128) return gemm_nt(X, ldx, W, ldw, Y, ldy, M, N, K, e, g_bf16 != 0, ws, ws_elems, st);
   dim3 grid((N + 15) / 16, (M + 15) / 16);
   int NW1, S1;
   if (!g_bf16 && fwd_once_plan(M, N, K, 16, ws ? ws_elems : 0, NW1, S1)) {

@@ -220,7 +220,12 @@ def linear_fwd(x, w, b, relu: bool, drop_p: float, seed: int, col_offset: int = 
         P = torch.mm(x, w.t())
         C().linear_epilogue(P, bias, out, relu, float(drop_p), seed & M64, col_offset, _ptr(dseed))
         return out
-    ws = _fwd_workspace(x.device, 16 * M * N) if M <= LARGE_M else None
+    if M <= LARGE_M:
+        ws = _fwd_workspace(x.device, 16 * M * N)
+    elif ((M + 255) // 256) * ((N + 127) // 128) < 512:
+        ws = _workspace(x.device, 8 * M * N, "gemm")     # split-K slabs of the tiled GEMM (csrc/gemm.hip)
+    else:
+        ws = None
     C().linear_fwd(x, w, bias, out, relu, float(drop_p), seed & M64, col_offset, _ptr(dseed), ws)
     return out
 
