@@ -674,12 +674,14 @@ void wgrad_group(const std::vector<py::tuple>& layers, int64_t M, const OptT& xn
 void sl_register_comm(pybind11::module& m);
 void sl_register_engine(pybind11::module& m);
 void sl_register_split(pybind11::module& m);
+void sl_register_resident(pybind11::module& m);
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "splitlearning_amd gfx950 (MI355X) HIP kernels";
   sl_register_comm(m);
   sl_register_engine(m);
   sl_register_split(m);
+  sl_register_resident(m);
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_local_step", &conv_local_step);
   m.def("conv_bwd_step", &conv_bwd_step);

@@ -158,6 +158,10 @@ class IpcAllReduce {
   void allreduce_sum_f32(float* p, size_t n, hipStream_t st);
   // the next generation for a fused consumer (same sequence as allreduce_sum_f32's calls)
   IpcStep begin_step();
+  // S consecutive generations for a persistent consumer (csrc/resident.hip: step i of the
+  // launch uses gen + i, parity (gen + i) & 1); every rank reserves the same S
+  IpcStep begin_steps(int64_t S);
+  int flag_words() const { return max_chunks_; }
   int64_t cap() const { return cap_; }
   int rank() const { return rank_; }
   int size() const { return nranks_; }

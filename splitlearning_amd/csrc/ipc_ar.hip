@@ -163,6 +163,12 @@ void IpcAllReduce::allreduce_sum_f32(float* p, size_t n, hipStream_t st) {
   }
 }
 
+IpcStep IpcAllReduce::begin_steps(int64_t S) {
+  IpcStep s = begin_step();
+  if (S > 1) gen_ += (uint32_t)(S - 1);
+  return s;
+}
+
 IpcStep IpcAllReduce::begin_step() {
   if (!opened_) throw std::runtime_error("IpcAllReduce: open() first");
   ++gen_;

@@ -412,6 +412,60 @@ class TailEngine:
         self._native = (slot, B, ex, d)      # d keeps the workspaces alive
         return ex
 
+    # ------------------------------------------------------------------ register-resident epoch
+    def resident_ok(self, slot: OptSlot, B: int) -> bool:
+        """Whether `run_resident_epoch` can drive this shard (`_C.ResidentEpoch`,
+        csrc/resident.hip): the fused 3-layer tail with one cross-entropy group, <= 16 rows
+        per step, an fc1 shard of <= 768 rows (a TP >= 7 shard of model2_sisa) whose state
+        fits the chip's registers and LDS, and, tensor-parallel, the peer-mapped region."""
+        if (self.device.type != "cuda" or not self.fused3_ok() or not hasattr(self.ops, "C")
+                or self.ce_groups != 1 or not 1 <= B <= 16 or self.layers[0].W.shape[0] > 768):
+            return False
+        if self.layers[1].style == "row" and getattr(self.allreduce, "ipc", None) is None:
+            return False
+        return self._resident_executor(slot, B).ok()
+
+    def run_resident_epoch(self, acts: torch.Tensor, labels: torch.Tensor, slot: OptSlot, B: int) -> torch.Tensor:
+        """One epoch over `acts` / `labels` with every full batch in ONE persistent launch that
+        keeps this shard's weights and optimizer state on-chip (csrc/resident.hip); a trailing
+        partial batch runs on the launch-per-stage executor.  Same step / seed / Adam-count
+        bookkeeping as `run_native_epoch`; the sums run in another order, so results agree
+        with it to fp32 rounding, not bitwise.  Returns the per-row losses."""
+        ex = self._resident_executor(slot, B)
+        n = acts.shape[0]
+        loss = torch.empty(n, device=self.device)
+        fc, t, done = ex.run(acts, labels, loss, self.seed_base, self.fwd_count, slot.t)
+        self.fwd_count, slot.t = int(fc), int(t)
+        self._pre = None
+        if done < n:
+            rest_a, rest_y = acts[done:], labels[done:]
+            if self.native_epoch_ok(B):
+                loss[done:] = self.run_native_epoch(rest_a, rest_y, slot, B, False)
+            else:
+                loss[done:], _ = self.train_fwd_bwd3(rest_a, rest_y, need_dx=False)
+                self.fused_step(slot)
+        return loss
+
+    def _resident_executor(self, slot: OptSlot, B: int):
+        cached = getattr(self, "_resident", None)
+        if cached is not None and cached[0] is slot and cached[1] == B:
+            return cached[2]
+        L1, L2, _ = self.layers
+        layers = []
+        for L in self.layers:
+            sw, sb = slot.state(f"{L.spec.name}.weight", L.W), slot.state(f"{L.spec.name}.bias", L.b)
+            layers.append({"W": L.W, "b": L.b, "s0": sw.get("m", sw.get("buf")), "s1": sw.get("v"),
+                           "sb0": sb.get("m", sb.get("buf")), "sb1": sb.get("v")})
+        cfg = slot.cfg
+        d = {"layers": layers, "kind": {"sgd": 1, "adam": 2}[cfg.kind], "lr": cfg.lr, "beta1": cfg.beta1,
+             "beta2": cfg.beta2, "eps": cfg.eps, "wd": cfg.weight_decay, "momentum": cfg.momentum,
+             "p1": L1.spec.dropout, "p2": L2.spec.dropout, "col_off1": L1.col_off, "B": B,
+             "ipc": getattr(self.allreduce, "ipc", None) if L2.style == "row" else None,
+             "timeout_s": float(getattr(self, "resident_timeout_s", 10.0))}
+        ex = self.ops.C().ResidentEpoch(d)
+        self._resident = (slot, B, ex, d)
+        return ex
+
     # ------------------------------------------------------------------ TP emulation
     @staticmethod
     def emulate_tp_epoch(shards: list, slots: list, acts: torch.Tensor, labels: torch.Tensor, B: int,
