@@ -126,6 +126,12 @@ def build_parser() -> argparse.ArgumentParser:
                    help="GPU: move data-plane messages with torch.distributed isend/irecv instead of "
                         "the native RCCL communicators (per-batch p2p on the compute stream, TP "
                         "all-reduce inside the server step)")
+    g.add_argument("--resident", choices=("auto", "off"), default="auto",
+                   help="SISA server epochs of a narrow Bob shard (fc1 <= 768 rows: TP >= 7) as ONE "
+                        "persistent launch per client epoch with the shard's weights and Adam state "
+                        "held on-chip (csrc/resident.hip); 'auto' uses it where it fits and, "
+                        "tensor-parallel, after a cross-rank self-test passed; 'off' = the "
+                        "launch-per-stage executor")
     g.add_argument("--tp_allreduce", choices=("auto", "rccl"), default="auto",
                    help="Bob's per-step TP all-reduce: 'auto' = one kernel over peer-mapped HBM "
                         "(csrc/ipc_ar.h) when every Bob rank sets it up and passes its self-test, "

@@ -13,8 +13,10 @@ constexpr int kResTiles = 4;        // fc1 tiles (16 rows x 256 columns) per wor
 constexpr int kResGroups = 6;       // fc1 column groups (workgroups per 16-row block)
 constexpr int kResRows2 = 4;        // fc2 rows (and fc3 columns) per workgroup
 constexpr int kResMaxC = 128;       // fc3 width bound (classes)
-constexpr int kResSeams = 4;        // A: fc1 look-ahead, B: logit partials, C: dlogits, D: dz2 + W2
+constexpr int kResSeams = 4;        // A: h1 rows, B: logit partials, C: dlogits, D: dz2 + W2
 constexpr int kResShardStride = 32; // counter shards 128 B apart
+constexpr int kResMaxRB = 48;       // fc1 row blocks (16 rows; shard width <= 768)
+constexpr int kResCounters = kResSeams * 8 + kResMaxRB;   // seam shards, then one per row block
 
 struct ResLayer {
   float *W, *m, *v;       // [N, K] (v unused for SGD)
@@ -42,12 +44,12 @@ struct ResArgs {
   int lookahead_last;     // 1: the last step also forms the next batch's fc1 product (unused: 0)
   // hand-off buffers (zeroed once by the host; double-buffered by step parity)
   float* LA;              // [2][ngrp][16][N1p] fc1 look-ahead partial pre-activations
-  float* B1x;             // [2][N1p] fc1 bias after the step that produced the look-ahead
+  float* H1;              // [2][16][N1p] h1 rows published by each row block's group-0 workgroup
   float* LP;              // [2][G][16][C4] logit partials of each workgroup's fc2 rows
   float* DL;              // [2][16][C4] dlogits
-  float* DZ2;             // [2][16][N2] fc2 output gradient
-  float* W2B;             // [2][nrb][N2 / 4][16][4] W2 after each step, in the fc1 tiles' layout
-  unsigned* cnt;          // [kResSeams][8 shards][kResShardStride] arrival counters (zeroed per launch)
+  float* DZ2;             // [2][16][G][4] fc2 output gradient, dz2[m][w + G ii] at [m][w][ii]
+  float* W2B;             // [2][nrb][G][16][4] W2 after each step: W2[w + G ii][16 rb + jj] at [rb][w][jj][ii]
+  unsigned* cnt;          // [kResCounters][kResShardStride] arrival counters (zeroed per launch)
   const int* shard_n;     // [kResSeams][8] arrivals per shard and step
   int* err;               // nonzero after a wait gave up (timeout or a peer's error)
   int64_t timeout;        // wall-clock ticks per wait

@@ -58,6 +58,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rs_of(const void* base) {
 __device__ __forceinline__ f32x4 hld4(__amdgpu_buffer_rsrc_t rs, int boff) {
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, boff, 0, 16));
 }
+__device__ __forceinline__ float hld1(__amdgpu_buffer_rsrc_t rs, int boff) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, boff, 0, 16));
+}
 __device__ __forceinline__ void hst4(__amdgpu_buffer_rsrc_t rs, int boff, f32x4 v) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(res_i32x4, v), rs, boff, 0, 16);
 }
@@ -80,6 +83,18 @@ __device__ __forceinline__ void arrive(unsigned* cnt, int seam, int w) {
   if (threadIdx.x == 0)
     __hip_atomic_fetch_add(cnt + (seam * 8 + (w & 7)) * kResShardStride, 1u, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Row-block hand-off (fc1 look-ahead partials of one 16-row block's column groups to its
+// group-0 workgroup): one counter per row block after the seam shards.
+__device__ __forceinline__ unsigned* rb_counter(unsigned* cnt, int rb) {
+  return cnt + (kResSeams * 8 + rb) * kResShardStride;
+}
+__device__ __forceinline__ void arrive_rb(unsigned* cnt, int rb) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_fetch_add(rb_counter(cnt, rb), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Wait until every shard of `seam` holds `mult` arrivals per producer of that shard (lanes
@@ -116,11 +131,75 @@ __device__ __forceinline__ bool seam_wait(const ResArgs& a, int seam, unsigned m
   return *s_ok != 0;
 }
 
+// Wait until the row-block counter reaches `tgt` (thread 0 polls); false on give-up.
+__device__ __forceinline__ bool rb_wait(const ResArgs& a, int rb, unsigned tgt, int* s_ok) {
+  if (threadIdx.x == 0) {
+    bool ok = true;
+    const unsigned* p = rb_counter(a.cnt, rb);
+    if (poll(p) < tgt) {
+      const uint64_t t0 = wall_clock64();
+      while (poll(p) < tgt) {
+        if (failed(a.err)) {
+          ok = false;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        if ((int64_t)(wall_clock64() - t0) > a.timeout) {
+          __hip_atomic_fetch_or(a.err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok = false;
+          break;
+        }
+      }
+    }
+    *s_ok = ok ? 1 : 0;
+  }
+  __syncthreads();
+  return *s_ok != 0;
+}
+
 __device__ __forceinline__ float drop_relu(float v, uint32_t lo, uint32_t hi, uint32_t row, uint32_t col,
                                            uint32_t thr, float dsc) {
   v = fmaxf(v, 0.f);
   if (thr) v = sl_hash_keep(lo, hi, row, col, thr) ? v * dsc : 0.f;
   return v;
+}
+
+// The optimizer step of one element: sl_opt_update's arithmetic (common.h) for SGD-momentum /
+// Adam, with the step's Adam scalars passed in VGPRs (ss = lr / (1 - beta1^t), ib = 1 /
+// sqrt(1 - beta2^t); as SGPR operands they pushed the kernel's scalar registers into spills)
+// and the hardware square root and reciprocal (v_sqrt_f32 / v_rcp_f32, 1 ulp) in place of the
+// correctly rounded sqrtf and division: with the state on-chip the update is VALU-bound (a TP
+// = 8 shard's 16 K elements per CU took 4-5 us of the step with the IEEE sequences, ~25
+// instructions each), and 1 ulp of the update is ~1e-10 absolute at lr 1e-3, far inside the
+// torch comparison (tests/test_resident_gpu.py).
+template <bool ADAM>
+__device__ __forceinline__ void res_update(const SlOpt& o, float ss, float ib, float& p, float g, float& s0,
+                                           float& s1) {
+  if (o.wd != 0.f) g = fmaf(o.wd, p, g);
+  if (!ADAM) {
+    const float b = (o.momentum != 0.f) ? fmaf(o.momentum, s0, g) : g;
+    s0 = b;
+    p = fmaf(-o.lr, b, p);
+  } else {
+    const float m = fmaf(o.beta1, s0, (1.f - o.beta1) * g);
+    const float v = fmaf(o.beta2, s1, (1.f - o.beta2) * g * g);
+    s0 = m;
+    s1 = v;
+    const float denom = __builtin_amdgcn_sqrtf(v) * ib + o.eps;
+    p = p - ss * (m * __builtin_amdgcn_rcpf(denom));
+  }
+}
+template <bool ADAM>
+__device__ __forceinline__ void res_update4(const SlOpt& o, float ss, float ib, f32x4& p, f32x4 g, f32x4& s0,
+                                            f32x4& s1) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    float pp = p[c], a0 = s0[c], a1 = s1[c];
+    res_update<ADAM>(o, ss, ib, pp, g[c], a0, a1);
+    p[c] = pp;
+    s0[c] = a0;
+    s1[c] = a1;
+  }
 }
 
 // LDS carve (bytes; every offset a multiple of 16)
@@ -138,7 +217,8 @@ constexpr int OFF_W3 = OFF_RED2 + 16 * 16 * 4;        // W3 columns {W, m, v}[4]
 constexpr int OFF_B3 = OFF_W3 + 3 * 4 * kResMaxC * 4; // b3 {W, m, v}[kResMaxC]
 constexpr int OFF_B2 = OFF_B3 + 3 * kResMaxC * 4;     // b2 {W, m, v}[4]
 constexpr int OFF_B1 = OFF_B2 + 3 * 4 * 4;            // b1 {W, m, v}[16]
-constexpr int OFF_OK = OFF_B1 + 3 * 16 * 4;
+constexpr int OFF_W2N = OFF_B1 + 3 * 16 * 4;         // W2 after the step, [4 rows][kSh1Max] (publication)
+constexpr int OFF_OK = OFF_W2N + 4 * kSh1Max * 4;
 constexpr int kResLds = OFF_OK + 16;
 
 }  // namespace
@@ -181,6 +261,7 @@ __global__ void __launch_bounds__(kResThreads) resident_epoch_kernel(ResArgs a) 
   float* sb3 = reinterpret_cast<float*>(smem + OFF_B3);
   float* sb2 = reinterpret_cast<float*>(smem + OFF_B2);
   float* sb1 = reinterpret_cast<float*>(smem + OFF_B1);
+  float* sW2n = reinterpret_cast<float*>(smem + OFF_W2N);
   int* s_ok = reinterpret_cast<int*>(smem + OFF_OK);
   constexpr int NW = kResThreads / 64;                      // 8 waves
   constexpr int XS = kResTiles * 64;                        // sx row pitch (f32x4)
@@ -198,9 +279,8 @@ __global__ void __launch_bounds__(kResThreads) resident_epoch_kernel(ResArgs a) 
   const int grp = fc1 ? w - rb * a.ngrp : 0;
   const int n0 = rb * 16, cb0 = grp * kResTiles;
   const int nct = fc1 ? min(kResTiles, a.ncb - cb0) : 0;
-  const __amdgpu_buffer_rsrc_t rLA = rs_of(a.LA), rB1 = rs_of(a.B1x), rLP = rs_of(a.LP), rDL = rs_of(a.DL),
+  const __amdgpu_buffer_rsrc_t rLA = rs_of(a.LA), rH1 = rs_of(a.H1), rLP = rs_of(a.LP), rDL = rs_of(a.DL),
                                rDZ = rs_of(a.DZ2), rW2B = rs_of(a.W2B);
-  const int nq2 = N2 >> 2;
 
   // ---- load the state: fc1 rows n1 + 8 h of tile ct in p / s0 / s1[ct][h]
   f32x4 p[kResTiles][2], s0[kResTiles][2], s1[kResTiles][2];
@@ -264,10 +344,11 @@ __global__ void __launch_bounds__(kResThreads) resident_epoch_kernel(ResArgs a) 
 
   // a batch's input slice in MFMA A layout: lane (li, lq) of wave r holds, for column group
   // h, x[row li][kb + 16 (r + 8 h) + 4 lq .. +3] of tile ct (rows >= M read as 0)
-  auto load_x = [&](int batch, f32x4 (&xv)[kResTiles][2]) {
+  auto load_x = [&](int batch, f32x4 (&xv)[kResTiles][2], int ct0 = 0, int ct1 = kResTiles) {
     RES_IDX();
 #pragma unroll
     for (int ct = 0; ct < kResTiles; ++ct)
+      if (ct >= ct0 && ct < ct1)
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int k = (cb0 + ct) * 256 + 16 * (r + 8 * h) + 4 * lq;
@@ -287,8 +368,9 @@ __global__ void __launch_bounds__(kResThreads) resident_epoch_kernel(ResArgs a) 
   // the look-ahead: pre[m][n0 + nn] = sum over this workgroup's columns of x[m] . W1[n0 + nn]
   // (exact-fp32 MFMA 16x16x4; the updated tile staged through LDS into B layout, rows padded
   // to 65 float4, as wgrad_group_kernel; wave r covers the tile's 16-column groups r and
-  // r + 8) -> LA[par][grp], and b1 -> B1x[par]
-  auto lookahead = [&](const f32x4 (&xv)[kResTiles][2], int par) {
+  // r + 8) -> LA[par][grp]; the row block's group-0 workgroup turns the groups' partials into
+  // h1 rows (H1[par]) for step `step` and publishes them (seam A).  False: a wait gave up.
+  auto lookahead = [&](const f32x4 (&xv)[kResTiles][2], int par, int step, unsigned mult) -> bool {
     RES_IDX();
     f32x4 z = zv;
 #pragma unroll
@@ -309,42 +391,74 @@ __global__ void __launch_bounds__(kResThreads) resident_epoch_kernel(ResArgs a) 
     }
     red[r * 64 + lane] = z;   // z[j] = partial(m = 4 lq + j, n = n0 + li)
     __syncthreads();
+    float own = 0.f;
     if (tid < 256) {
       const int m = tid >> 4, nn = tid & 15;
-      float v = 0.f;
 #pragma unroll
-      for (int ww = 0; ww < NW; ++ww) v += red[ww * 64 + 16 * (m >> 2) + nn][m & 3];
-      if (m < M && n0 + nn < N1) hst1(rLA, ((((par * a.ngrp + grp) * 16) + m) * N1p + n0 + nn) * 4, v);
+      for (int ww = 0; ww < NW; ++ww) own += red[ww * 64 + 16 * (m >> 2) + nn][m & 3];
+      if (grp != 0 && m < M && n0 + nn < N1) hst1(rLA, ((((par * a.ngrp + grp) * 16) + m) * N1p + n0 + nn) * 4, own);
     }
-    if (grp == 0 && tid < 16 && n0 + tid < N1) hst1(rB1, (par * N1p + n0 + tid) * 4, sb1[tid]);
-  };
-  // W2 after a step, in the fc1 tiles' layout W2B[par][rb(j)][n / 4][j % 16][n % 4]
-  auto publish_w2 = [&](int par) {
-    RES_IDX();
+    if (grp != 0) {
+      arrive_rb(a.cnt, rb);          // this column group's partial is published to the row block
+      return true;
+    }
+    // group 0: wait for the row block's other column groups, sum the partials in group order,
+    // bias, ReLU, dropout (the consuming step's seed) -> h1 rows [n0, n0 + 16) -> seam A
+    if (!rb_wait(a, rb, (unsigned)(a.ngrp - 1) * mult, s_ok)) return false;
+    if (tid < 256) {
+      const int m = tid >> 4, nn = tid & 15, n = n0 + nn;
+      if (m < M && n < N1) {
+        float parts[kResGroups];
 #pragma unroll
-    for (int s = 0; s < S2; ++s) {
-      const int j = q2 + 128 * s;
-      if (own2 && j < N1)
-        hst1(rW2B, ((((par * a.nrb + (j >> 4)) * nq2 + (n2 >> 2)) * 16 + (j & 15)) * 4 + (n2 & 3)) * 4, w2[s]);
+        for (int g = 1; g < kResGroups; ++g)
+          parts[g] = g < a.ngrp ? hld1(rLA, ((((par * a.ngrp + g) * 16) + m) * N1p + n) * 4) : 0.f;
+        float v = own;
+#pragma unroll
+        for (int g = 1; g < kResGroups; ++g) v += parts[g];
+        v = drop_relu(v + sb1[nn], a.seeds[4 * step], a.seeds[4 * step + 1], m, a.col_off1 + n, a.thr1, a.dsc1);
+        hst1(rH1, ((par * 16 + m) * N1p + n) * 4, v);
+      }
+    }
+    arrive(a.cnt, 0, w);
+    return true;
+  };
+  // W2 after a step, in the fc1 tiles' layout W2B[par][rb(j)][w][j % 16][ii] (this workgroup's
+  // four rows n = w + G ii side by side: gathered through LDS, one float4 store per column)
+  auto publish_w2 = [&](int par) {
+    {
+      RES_IDX();
+#pragma unroll
+      for (int s = 0; s < S2; ++s) {
+        const int j = q2 + 128 * s;
+        if (j < N1) sW2n[i2 * kSh1Max + j] = own2 ? w2[s] : 0.f;
+      }
+    }
+    __syncthreads();
+    {
+      RES_IDX();
+      for (int j = tid; j < N1; j += kResThreads) {
+        const f32x4 v = {sW2n[j], sW2n[kSh1Max + j], sW2n[2 * kSh1Max + j], sW2n[3 * kSh1Max + j]};
+        hst4(rW2B, ((((par * a.nrb + (j >> 4)) * G + w) * 16 + (j & 15)) * 4) * 4, v);
+      }
     }
   };
 
   // ---- prologue: W2_0 for the first step's dz1; the first batch's look-ahead -> seam A (step 0)
   publish_w2(0);
+  bool fc1_failed = false;
   if (fc1) {
     f32x4 xv[kResTiles][2];
     load_x(0, xv);
     stash_x(xv);
-    lookahead(xv, 0);
-    arrive(a.cnt, 0, w);
+    if (!lookahead(xv, 0, 0, 1u)) fc1_failed = true;
   }
 
-  for (int i = 0; i < a.S; ++i) {
+  for (int i = 0; i < a.S && !fc1_failed; ++i) {
     const int par = i & 1, nxt = par ^ 1;
-    const uint32_t sd0 = a.seeds[4 * i], sd1 = a.seeds[4 * i + 1], sd2 = a.seeds[4 * i + 2],
-                   sd3 = a.seeds[4 * i + 3];
-    SlOpt o = a.o;
-    o.dyn = ADAM ? a.adam + 2 * i : nullptr;
+    const uint32_t sd2 = a.seeds[4 * i + 2], sd3 = a.seeds[4 * i + 3];
+    const SlOpt o = a.o;
+    float ss = ADAM ? a.adam[2 * i] : 0.f, ib = ADAM ? a.adam[2 * i + 1] : 0.f;
+    asm volatile("" : "+v"(ss), "+v"(ib));   // held in VGPRs (res_update)
 
     // ================= A: h1_t, fc2 rows, logit partials
     RES_MARK(0);
@@ -352,23 +466,21 @@ __global__ void __launch_bounds__(kResThreads) resident_epoch_kernel(ResArgs a) 
     RES_MARK(1);
     {
       RES_IDX();
+      // h1_t rows as published by each row block's group-0 workgroup (rows >= M are zero)
       const int q4 = N1p >> 2;
-      for (int e = tid; e < 16 * q4; e += kResThreads) {
+      constexpr int U = (16 * kSh1Max / 4 + kResThreads - 1) / kResThreads;   // float4 per thread
+      f32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = tid + u * kResThreads;
         const int m = e / q4, j = 4 * (e - m * q4);
-        f32x4 v = zv;
-        if (m < M) {
-          f32x4 parts[kResGroups];
+        v[u] = (e < 16 * q4 && m < M) ? hld4(rH1, ((par * 16 + m) * N1p + j) * 4) : zv;
+      }
 #pragma unroll
-          for (int g = 0; g < kResGroups; ++g)
-            parts[g] = g < a.ngrp ? hld4(rLA, ((((par * a.ngrp + g) * 16) + m) * N1p + j) * 4) : zv;
-          const f32x4 bb = hld4(rB1, (par * N1p + j) * 4);
-#pragma unroll
-          for (int g = 0; g < kResGroups; ++g) v += parts[g];
-          v += bb;
-#pragma unroll
-          for (int c = 0; c < 4; ++c) v[c] = drop_relu(v[c], sd0, sd1, m, a.col_off1 + j + c, a.thr1, a.dsc1);
-        }
-        *reinterpret_cast<f32x4*>(sh1 + m * SH1P + j) = v;
+      for (int u = 0; u < U; ++u) {
+        const int e = tid + u * kResThreads;
+        const int m = e / q4, j = 4 * (e - m * q4);
+        if (e < 16 * q4) *reinterpret_cast<f32x4*>(sh1 + m * SH1P + j) = v[u];
       }
     }
     __syncthreads();
@@ -486,17 +598,14 @@ __global__ void __launch_bounds__(kResThreads) resident_epoch_kernel(ResArgs a) 
         const int c4 = tid & 31, gq = tid >> 5;
         f32x4 v = zv;
         if (c4 < nc4) {
+          f32x4 parts[256 / NG];
 #pragma unroll
-          for (int h = 0; h < 256 / NG; h += 4) {
-            f32x4 parts[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              const int src = gq + NG * (h + k);
-              parts[k] = src < G ? hld4(rLP, (((par * G + src) * 16 + m) * C4 + 4 * c4) * 4) : zv;
-            }
-#pragma unroll
-            for (int k = 0; k < 4; ++k) v += parts[k];
+          for (int k = 0; k < 256 / NG; ++k) {
+            const int src = gq + NG * k;
+            parts[k] = src < G ? hld4(rLP, (((par * G + src) * 16 + m) * C4 + 4 * c4) * 4) : zv;
           }
+#pragma unroll
+          for (int k = 0; k < 256 / NG; ++k) v += parts[k];
         }
         red[gq * 32 + c4] = v;
       }
@@ -566,7 +675,11 @@ __global__ void __launch_bounds__(kResThreads) resident_epoch_kernel(ResArgs a) 
         const int oi = oi0 + (tid >> 4), part = tid & 15;
         const int m = oi >> 2, ii = oi & 3;
         float s = 0.f;
-        for (int c = part; c < C; c += 16) s = fmaf(sdl[m * MC + c], sW3[ii * MC + c], s);
+#pragma unroll
+        for (int c0 = 0; c0 < MC; c0 += 16) {   // classes >= C hold zeros
+          const int c = c0 + part;
+          s = fmaf(sdl[m * MC + c], sW3[ii * MC + c], s);
+        }
         s = sl_row16_sum(s);
         if (part == 0) {
           const float h = sh2[m * 4 + ii];
@@ -580,61 +693,71 @@ __global__ void __launch_bounds__(kResThreads) resident_epoch_kernel(ResArgs a) 
       if (tid < C) {
         // b3: identical on every workgroup
         float g = 0.f;
-        for (int m = 0; m < M; ++m) g += sdl[m * MC + tid];
-        sl_opt_update(o, sb3[tid], g, sb3[MC + tid], sb3[2 * MC + tid]);
+#pragma unroll
+        for (int m = 0; m < 16; ++m) g += sdl[m * MC + tid];   // rows >= M are zero
+        res_update<ADAM>(o, ss, ib, sb3[tid], g, sb3[MC + tid], sb3[2 * MC + tid]);
       }
       for (int e = tid; e < 4 * MC; e += kResThreads) {
         const int ii = e / MC, c = e - ii * MC;
         if (c < C && w + G * ii < N2) {
           float g = 0.f;
-          for (int m = 0; m < M; ++m) g = fmaf(sdl[m * MC + c], sh2[m * 4 + ii], g);
-          sl_opt_update(o, sW3[ii * MC + c], g, sW3[(4 + ii) * MC + c], sW3[(8 + ii) * MC + c]);
+#pragma unroll
+          for (int m = 0; m < 16; ++m) g = fmaf(sdl[m * MC + c], sh2[m * 4 + ii], g);
+          res_update<ADAM>(o, ss, ib, sW3[ii * MC + c], g, sW3[(4 + ii) * MC + c], sW3[(8 + ii) * MC + c]);
         }
       }
       if (tid < 4 && w + G * tid < N2) {
         float g = 0.f;
-        for (int m = 0; m < M; ++m) g += sdz2[m * 4 + tid];
-        sl_opt_update(o, sb2[tid], g, sb2[4 + tid], sb2[8 + tid]);
+#pragma unroll
+        for (int m = 0; m < 16; ++m) g += sdz2[m * 4 + tid];
+        res_update<ADAM>(o, ss, ib, sb2[tid], g, sb2[4 + tid], sb2[8 + tid]);
       }
 #pragma unroll
       for (int s = 0; s < S2; ++s) {
         const int j = q2 + 128 * s;
         if (own2 && j < N1) {
           float g = 0.f;
-          for (int m = 0; m < M; ++m) g = fmaf(sdz2[m * 4 + i2], sh1[m * SH1P + j], g);
-          sl_opt_update(o, w2[s], g, w2m[s], w2v[s]);
+#pragma unroll
+          for (int m = 0; m < 16; ++m) g = fmaf(sdz2[m * 4 + i2], sh1[m * SH1P + j], g);
+          res_update<ADAM>(o, ss, ib, w2[s], g, w2m[s], w2v[s]);
         }
       }
-      if (tid < 64) {
-        const int m = tid >> 2, ii = tid & 3, n = w + G * ii;
-        if (m < M && n < N2) hst1(rDZ, ((par * 16 + m) * N2 + n) * 4, sdz2[m * 4 + ii]);
-      }
+      if (tid < M)   // DZ2[par][m][w][ii] = dz2[m][n = w + G ii]
+        hst4(rDZ, (((par * 16 + tid) * G + w) * 4) * 4, *reinterpret_cast<const f32x4*>(sdz2 + tid * 4));
     }
-    publish_w2(nxt);
     arrive(a.cnt, 3, w);
     RES_MARK(9);
+    // W2_{t+1} for the next step's dz1: off this seam's critical path (the next step's seam-B
+    // arrival drains these stores, long before its seam D releases the readers)
+    publish_w2(nxt);
 
     // ================= D: fc1 rows' dz1, b1 / W1 steps, next batch's look-ahead
     if (fc1) {
       const bool more = i + 1 < a.S;
+      // dz1[m][nn] = sum_n dz2[m][n] W2_t[n][n0 + nn]; fc2 rows in the publishers' order: block
+      // b = 4 workgroups w' = 4 b + lq, MFMA k index c = ii, i.e. n = w' + G c.  W2_t was
+      // published a step ago, so its operands load before the wait; dz2's after it.
+      constexpr int KB = 256 / 4 / NW;                       // blocks per wave (G <= 256)
+      f32x4 B4[KB];
+      {
+        RES_IDX();
+#pragma unroll
+        for (int k = 0; k < KB; ++k) {
+          const int wp = 4 * (r + NW * k) + lq;
+          B4[k] = (wp < G && n0 + li < N1) ? hld4(rW2B, ((((par * a.nrb + rb) * G + wp) * 16 + li) * 4) * 4) : zv;
+        }
+      }
       if (!seam_wait(a, 3, (unsigned)(i + 1), s_ok)) break;
       RES_MARK(10);
       {
-        // dz1[m][nn] = sum_n dz2[m][n] W2_t[n][n0 + nn]: wave r takes the 16-row blocks
-        // b = r + 8 k of fc2; MFMA k index = n = 16 b + 4 lq + c (c = the float4 component)
         RES_IDX();
-        constexpr int KB = 1024 / 16 / NW;                   // blocks per wave (fc2 <= 1024 rows)
-        f32x4 A4[KB], B4[KB];
+        f32x4 acc = zv;
+        f32x4 A4[KB];
 #pragma unroll
         for (int k = 0; k < KB; ++k) {
-          const int b = r + NW * k;
-          const int nb = 16 * b + 4 * lq;
-          A4[k] = (nb < N2 && li < M) ? hld4(rDZ, ((par * 16 + li) * N2 + nb) * 4) : zv;
-          B4[k] = (nb < N2 && n0 + li < N1)
-                      ? hld4(rW2B, ((((par * a.nrb + rb) * nq2 + 4 * b + lq) * 16 + li) * 4) * 4)
-                      : zv;
+          const int wp = 4 * (r + NW * k) + lq;
+          A4[k] = (wp < G && li < M) ? hld4(rDZ, (((par * 16 + li) * G + wp) * 4) * 4) : zv;
         }
-        f32x4 acc = zv;
 #pragma unroll
         for (int k = 0; k < KB; ++k)
 #pragma unroll
@@ -656,12 +779,17 @@ __global__ void __launch_bounds__(kResThreads) resident_epoch_kernel(ResArgs a) 
       }
       __syncthreads();
       RES_MARK(11);
+      // the next batch's inputs: the first two tiles' loads issued under the dW / Adam work
+      // below, the rest after it (all four up front spill the state registers)
+      f32x4 xv[kResTiles][2];
+      if (more) load_x(i + 1, xv, 0, 2);
       {
         RES_IDX();
         if (grp == 0 && tid < 16 && n0 + tid < N1) {
           float g = 0.f;
-          for (int m = 0; m < M; ++m) g += sdz[m * 16 + tid];
-          sl_opt_update(o, sb1[tid], g, sb1[16 + tid], sb1[32 + tid]);
+#pragma unroll
+          for (int m = 0; m < 16; ++m) g += sdz[m * 16 + tid];
+          res_update<ADAM>(o, ss, ib, sb1[tid], g, sb1[16 + tid], sb1[32 + tid]);
         }
 #pragma unroll
         for (int ct = 0; ct < kResTiles; ++ct) {
@@ -676,19 +804,20 @@ __global__ void __launch_bounds__(kResThreads) resident_epoch_kernel(ResArgs a) 
               g0 += sdz[m * 16 + r] * xm;
               g1 += sdz[m * 16 + r + 8] * xm;
             }
-            if (n1 < N1) sl_opt_update4<ADAM>(o, p[ct][0], g0, s0[ct][0], s1[ct][0]);
-            if (n1 + 8 < N1) sl_opt_update4<ADAM>(o, p[ct][1], g1, s0[ct][1], s1[ct][1]);
+            if (n1 < N1) res_update4<ADAM>(o, ss, ib, p[ct][0], g0, s0[ct][0], s1[ct][0]);
+            if (n1 + 8 < N1) res_update4<ADAM>(o, ss, ib, p[ct][1], g1, s0[ct][1], s1[ct][1]);
           }
+          __builtin_amdgcn_sched_barrier(0);   // one tile's update live at a time
         }
       }
       RES_MARK(12);
       if (more) {
-        f32x4 xv[kResTiles][2];
-        load_x(i + 1, xv);
-        __syncthreads();   // every wave is done with x_t (sx) and with h1 (sh1: sw aliases it)
+        // the LDS copy of the next batch's inputs for the next step's dW goes in after the
+        // look-ahead (its barriers also order every wave's dW reads of x_t before the overwrite)
+        load_x(i + 1, xv, 2, kResTiles);
+        const bool ok = lookahead(xv, nxt, i + 1, (unsigned)(i + 2));
         stash_x(xv);
-        lookahead(xv, nxt);
-        arrive(a.cnt, 0, w);
+        if (!ok) break;
         RES_MARK(13);
       }
     }
@@ -763,7 +892,7 @@ static std::string check_shape(const ResArgs& a) {
   if (a.K1 % 4) return "fc1 input width % 4";
   if (a.N2 % 4 || a.N2 > kResRows2 * a.G || a.N2 > 1024) return "fc2 width % 4 and <= 4 G, <= 1024";
   if (a.C < 1 || a.C > kResMaxC || a.C4 % 4) return "classes <= 128";
-  if (a.nfc1 > a.G || a.ngrp > kResGroups) return "fc1 tiles per workgroup";
+  if (a.nfc1 > a.G || a.ngrp > kResGroups || a.nrb > kResMaxRB) return "fc1 tiles per workgroup";
   if (a.G > 256 || a.G < a.M) return "workgroups";
   if (a.ipc.T > 0 && ((int64_t)a.G * 64 > a.ipc.cap || a.G > a.ipc.nflags || a.ipc.T > kIpcMaxRanks))
     return "peer-mapped exchange region";
@@ -801,7 +930,7 @@ hipError_t resident_epoch_launch(const ResArgs& a, hipStream_t st) {
     if (e != hipSuccess) return e;
     attr = true;
   }
-  hipError_t e = hipMemsetAsync(a.cnt, 0, (size_t)kResSeams * 8 * kResShardStride * sizeof(unsigned), st);
+  hipError_t e = hipMemsetAsync(a.cnt, 0, (size_t)kResCounters * kResShardStride * sizeof(unsigned), st);
   if (e != hipSuccess) return e;
   if (a.o.kind == 2)
     resident_epoch_kernel<true><<<a.G, kResThreads, kResLds, st>>>(a);

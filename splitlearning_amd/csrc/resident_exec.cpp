@@ -100,24 +100,24 @@ class ResidentEpoch {
     a.col_off1 = col_off1_;
     auto opt = at::TensorOptions().dtype(at::kFloat).device(dev);
     LA_ = at::zeros({2LL * a.ngrp * 16 * a.N1p}, opt);
-    B1x_ = at::zeros({2LL * a.N1p}, opt);
+    H1_ = at::zeros({2LL * 16 * a.N1p}, opt);
     LP_ = at::zeros({2LL * a.G * 16 * a.C4}, opt);
     DL_ = at::zeros({2LL * 16 * a.C4}, opt);
-    DZ2_ = at::zeros({2LL * 16 * a.N2}, opt);
-    W2B_ = at::zeros({2LL * a.nrb * (a.N2 / 4 > 0 ? a.N2 / 4 : 1) * 64}, opt);
-    cnt_ = at::zeros({(int64_t)sl::kResSeams * 8 * sl::kResShardStride}, opt.dtype(at::kInt));
+    DZ2_ = at::zeros({2LL * 16 * a.G * 4}, opt);
+    W2B_ = at::zeros({2LL * a.nrb * a.G * 64}, opt);
+    cnt_ = at::zeros({(int64_t)sl::kResCounters * sl::kResShardStride}, opt.dtype(at::kInt));
     err_ = at::zeros({1}, opt.dtype(at::kInt));
     // arrivals per counter shard (producer workgroup w lands on shard w % 8)
     std::vector<int> sn(sl::kResSeams * 8, 0);
     for (int w = 0; w < a.G; ++w) {
-      if (w < a.nfc1) ++sn[0 * 8 + (w & 7)];
+      if (w < a.nfc1 && w % a.ngrp == 0) ++sn[0 * 8 + (w & 7)];   // row blocks' group-0 workgroups
       ++sn[1 * 8 + (w & 7)];
       if (w < a.M) ++sn[2 * 8 + (w & 7)];
       ++sn[3 * 8 + (w & 7)];
     }
     shard_n_ = at::tensor(sn, at::TensorOptions().dtype(at::kInt)).to(dev);
     a.LA = LA_.data_ptr<float>();
-    a.B1x = B1x_.data_ptr<float>();
+    a.H1 = H1_.data_ptr<float>();
     a.LP = LP_.data_ptr<float>();
     a.DL = DL_.data_ptr<float>();
     a.DZ2 = DZ2_.data_ptr<float>();
@@ -220,7 +220,7 @@ class ResidentEpoch {
   sl::ResArgs a_{};
   bool ok_ = false;
   std::string why_;
-  at::Tensor LA_, B1x_, LP_, DL_, DZ2_, W2B_, cnt_, err_, shard_n_, adam_, seeds_;
+  at::Tensor LA_, H1_, LP_, DL_, DZ2_, W2B_, cnt_, err_, shard_n_, adam_, seeds_;
 };
 
 }  // namespace

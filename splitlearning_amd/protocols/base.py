@@ -87,6 +87,7 @@ class Session:
         self.activation_and_labels_cache: dict = {}
         if self.is_bob:
             self._build_bob()
+        self._resident_ok = self._decide_resident()       # collective over all ranks
         self.bob_log.info("Bob Started Getting Tipsy")
         if self.pl.bob_tp > 1:
             kind = ("peer-mapped (one kernel, fused into the server head)" if getattr(self, "tp_ipc", None) is not None
@@ -94,6 +95,11 @@ class Session:
             self.bob_log.info(f"[perf] Bob tensor-parallel over {self.pl.bob_tp} ranks; TP all-reduce: {kind}")
 
     # ------------------------------------------------------------------ construction
+    def _decide_resident(self) -> bool:
+        """Whether Bob's epochs run on the register-resident executor (SISA overrides; a
+        collective when it does, so every rank calls it)."""
+        return False
+
     def front_module(self):
         from ..models import ClientFrontSisa
         return ClientFrontSisa()
@@ -187,7 +193,12 @@ class Session:
                 self.tp_ipc = make_ipc_allreduce(self.pl.bob_ranks, self.rank)
                 if self.tp_ipc is not None:
                     return ipc_allreduce(self.tp_ipc)
-            return native_allreduce(tpc) if tpc is not None else self.comm.tp_allreduce
+            if tpc is None:
+                return self.comm.tp_allreduce
+            ar = native_allreduce(tpc)
+            if self.tp_ipc is not None:
+                ar.ipc = self.tp_ipc     # the register-resident epoch exchanges through it in-launch
+            return ar
         return self.comm.tp_allreduce
 
     def _check_transport(self):

@@ -33,6 +33,10 @@ from .sisa import SisaSession
 class ConcatSession(SisaSession):
     mode = "concat"
 
+    def _decide_resident(self) -> bool:
+        # k cross-entropy groups (SISA-concat's heads): the resident executor serves one
+        return False
+
     def bob_module_and_spec(self):
         return (self.make_bob_module(ServerTailSisaConcat, self.k),
                 sisa_server_spec(self.k, concat=True))
