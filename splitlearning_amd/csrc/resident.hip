@@ -189,16 +189,42 @@ __device__ __forceinline__ void res_update(const SlOpt& o, float ss, float ib, f
     p = p - ss * (m * __builtin_amdgcn_rcpf(denom));
   }
 }
+// Four elements as two packed pairs (v_pk_fma_f32 / v_pk_mul_f32; the square root and the
+// reciprocal per element): the same operations as res_update, half the VALU issue slots.
+typedef float res_f32x2 __attribute__((ext_vector_type(2)));
+template <bool ADAM>
+__device__ __forceinline__ void res_update2(const SlOpt& o, float ss, float ib, res_f32x2& p, res_f32x2 g,
+                                            res_f32x2& s0, res_f32x2& s1) {
+  if (o.wd != 0.f) g = __builtin_elementwise_fma(res_f32x2{o.wd, o.wd}, p, g);
+  if (!ADAM) {
+    const res_f32x2 b = (o.momentum != 0.f) ? __builtin_elementwise_fma(res_f32x2{o.momentum, o.momentum}, s0, g) : g;
+    s0 = b;
+    p = __builtin_elementwise_fma(res_f32x2{-o.lr, -o.lr}, b, p);
+  } else {
+    const float c1 = 1.f - o.beta1, c2 = 1.f - o.beta2;
+    const res_f32x2 m = __builtin_elementwise_fma(res_f32x2{o.beta1, o.beta1}, s0, res_f32x2{c1, c1} * g);
+    const res_f32x2 v = __builtin_elementwise_fma(res_f32x2{o.beta2, o.beta2}, s1, (res_f32x2{c2, c2} * g) * g);
+    s0 = m;
+    s1 = v;
+    const res_f32x2 sq = {__builtin_amdgcn_sqrtf(v[0]), __builtin_amdgcn_sqrtf(v[1])};
+    const res_f32x2 den = __builtin_elementwise_fma(sq, res_f32x2{ib, ib}, res_f32x2{o.eps, o.eps});
+    const res_f32x2 rc = {__builtin_amdgcn_rcpf(den[0]), __builtin_amdgcn_rcpf(den[1])};
+    p = p - res_f32x2{ss, ss} * (m * rc);
+  }
+}
 template <bool ADAM>
 __device__ __forceinline__ void res_update4(const SlOpt& o, float ss, float ib, f32x4& p, f32x4 g, f32x4& s0,
                                             f32x4& s1) {
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    float pp = p[c], a0 = s0[c], a1 = s1[c];
-    res_update<ADAM>(o, ss, ib, pp, g[c], a0, a1);
-    p[c] = pp;
-    s0[c] = a0;
-    s1[c] = a1;
+  for (int h = 0; h < 2; ++h) {
+    res_f32x2 pp = {p[2 * h], p[2 * h + 1]}, a0 = {s0[2 * h], s0[2 * h + 1]}, a1 = {s1[2 * h], s1[2 * h + 1]};
+    res_update2<ADAM>(o, ss, ib, pp, res_f32x2{g[2 * h], g[2 * h + 1]}, a0, a1);
+    p[2 * h] = pp[0];
+    p[2 * h + 1] = pp[1];
+    s0[2 * h] = a0[0];
+    s0[2 * h + 1] = a0[1];
+    s1[2 * h] = a1[0];
+    s1[2 * h + 1] = a1[1];
   }
 }
 
@@ -208,6 +234,7 @@ constexpr int kSh1Max = 768;                         // N1p bound (6 W2 slots of
 constexpr int OFF_SX = 0;
 constexpr int OFF_SH1 = OFF_SX + kSxBytes;            // h1 [16][N1p]; look-ahead staging aliases it
 constexpr int OFF_RED = OFF_SH1 + 16 * kSh1Max * 4;   // [8][64] f32x4 / logits [16][32] f32x4
+static_assert(2 * 16 * 65 * 16 <= 16 * kSh1Max * 4, "two staged look-ahead tiles fit the h1 region");
 constexpr int OFF_SDZ = OFF_RED + 8 * 64 * 16;        // dz1 [16][16]
 constexpr int OFF_SDL = OFF_SDZ + 16 * 16 * 4;        // dlogits [16][kResMaxC]
 constexpr int OFF_SH2 = OFF_SDL + 16 * kResMaxC * 4;  // h2 [16][4]
@@ -374,17 +401,28 @@ __global__ void __launch_bounds__(kResThreads) resident_epoch_kernel(ResArgs a) 
     RES_IDX();
     f32x4 z = zv;
 #pragma unroll
-    for (int ct = 0; ct < kResTiles; ++ct) {
-      if (ct < nct) {
-        const int k = (cb0 + ct) * 256 + 4 * lane;
+    for (int ct0 = 0; ct0 < kResTiles; ct0 += 2) {       // two tiles staged per barrier pair
+      if (ct0 < nct) {
 #pragma unroll
-        for (int h = 0; h < 2; ++h) sw[(r + 8 * h) * 65 + lane] = (n1 + 8 * h < N1 && k < K1) ? p[ct][h] : zv;
+        for (int u = 0; u < 2; ++u) {
+          const int ct = ct0 + u, k = (cb0 + ct) * 256 + 4 * lane;
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+            sw[u * 16 * 65 + (r + 8 * h) * 65 + lane] = (ct < nct && n1 + 8 * h < N1 && k < K1) ? p[ct][h] : zv;
+        }
         __syncthreads();
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const f32x4 wv4 = sw[li * 65 + 4 * (r + 8 * h) + lq];
+        for (int u = 0; u < 2; ++u) {
+          const int ct = ct0 + u;
+          if (ct < nct) {
 #pragma unroll
-          for (int c = 0; c < 4; ++c) z = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[ct][h][c], wv4[c], z, 0, 0, 0);
+            for (int h = 0; h < 2; ++h) {
+              const f32x4 wv4 = sw[u * 16 * 65 + li * 65 + 4 * (r + 8 * h) + lq];
+#pragma unroll
+              for (int c = 0; c < 4; ++c)
+                z = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[ct][h][c], wv4[c], z, 0, 0, 0);
+            }
+          }
         }
         __syncthreads();
       }
@@ -514,27 +552,30 @@ __global__ void __launch_bounds__(kResThreads) resident_epoch_kernel(ResArgs a) 
         const int m = tid >> 2, ii = tid & 3;
         float pv = red2[(2 * ii) * 16 + m] + red2[(2 * ii + 1) * 16 + m];
         if (a.ipc.T > 0) {
-          // tensor-parallel fc2: this workgroup's 16 x 4 product block to every rank's slot
-          // [me] (system-scope stores over the peer mapping), one flag per (source, workgroup),
-          // then the T blocks summed in rank order (bitwise the same sum on every rank)
+          // tensor-parallel fc2: this workgroup's 16 x 4 product block to every rank as 8-byte
+          // granules {tag = step generation, value} (one untorn system-scope store each: the
+          // data is its own flag, no flag word and no fences), polled by the receiving lane
+          // until every source's tag matches, then summed in rank order (bitwise the same sum
+          // on every rank).  Region reuse is ordered by the exchange itself: a rank sends step
+          // i only after it received every rank's step i - 1, i.e. after each receiver finished
+          // reading the slot's previous use (step i - 2, same parity).
           const uint32_t gen = a.ipc.gen + (uint32_t)i;
           const int ipar = (int)(gen & 1u), T = a.ipc.T, me = a.ipc.me;
+          const int64_t half = a.ipc.cap >> 1;                   // granules per (parity, source)
           const int64_t slot = (int64_t)w * 64 + tid;
+          const uint64_t gr = ((uint64_t)gen << 32) | (uint64_t)__builtin_bit_cast(uint32_t, pv);
           for (int rr = 0; rr < T; ++rr)
-            __hip_atomic_store(a.ipc.P.data[rr] + (int64_t)(ipar * T + me) * a.ipc.cap + slot, pv,
+            __hip_atomic_store(reinterpret_cast<uint64_t*>(a.ipc.P.data[rr]) + (ipar * T + me) * half + slot, gr,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          if (tid == 0)
-            for (int rr = 0; rr < T; ++rr)
-              ipc_raise_flag(a.ipc.P.flags[rr] + (int64_t)(ipar * T + me) * a.ipc.nflags + w, gen, a.ipc.fences);
-          // lanes 0..T-1 wait for source `lane`'s flag (bounded; gives up at once once the
-          // error word is set), then one system-scope acquire
+          const uint64_t* mine = reinterpret_cast<const uint64_t*>(a.ipc.P.data[me]);
           bool ok = true;
-          if (tid < T) {
-            const uint32_t* f = a.ipc.P.flags[me] + (int64_t)(ipar * T + tid) * a.ipc.nflags + w;
-            if ((int32_t)(ipc_poll_flag(f) - gen) < 0) {
+          float sum = 0.f;
+          for (int src = 0; src < T && ok; ++src) {
+            const uint64_t* g = mine + (ipar * T + src) * half + slot;
+            uint64_t x = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if ((uint32_t)(x >> 32) != gen) {
               const uint64_t t0 = wall_clock64();
-              while ((int32_t)(ipc_poll_flag(f) - gen) < 0) {
+              while ((uint32_t)((x = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) >> 32) != gen) {
                 if (__hip_atomic_load(a.ipc.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) {
                   ok = false;
                   break;
@@ -547,16 +588,10 @@ __global__ void __launch_bounds__(kResThreads) resident_epoch_kernel(ResArgs a) 
                 }
               }
             }
+            sum += __builtin_bit_cast(float, (uint32_t)(x & 0xffffffffull));
           }
           ok = __all(ok);
-          if (a.ipc.fences) ipc_acquire();
-          float sum = 0.f;
-          if (ok)
-            for (int src = 0; src < T; ++src)
-              sum += __hip_atomic_load(a.ipc.P.data[me] + (int64_t)(ipar * T + src) * a.ipc.cap + slot,
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          else if (tid == 0)
-            __hip_atomic_fetch_or(a.err, 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (!ok && tid == 0) __hip_atomic_fetch_or(a.err, 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           pv = sum;
           if (tid == 0) *s_ok = ok ? 1 : 0;
         }
@@ -690,6 +725,17 @@ __global__ void __launch_bounds__(kResThreads) resident_epoch_kernel(ResArgs a) 
     __syncthreads();
     {
       RES_IDX();
+      if (tid < M)   // DZ2[par][m][w][ii] = dz2[m][n = w + G ii]
+        hst4(rDZ, (((par * 16 + tid) * G + w) * 4) * 4, *reinterpret_cast<const f32x4*>(sdz2 + tid * 4));
+    }
+    arrive(a.cnt, 3, w);
+    RES_MARK(9);
+    // the optimizer steps of b3, W3, b2 and W2 and W2_{t+1}'s publication (for the next step's
+    // dz1) after the seam: only dz2 is on its critical path; they fill this workgroup's wait
+    // for the other workgroups' dz2 (the next step's seam-B arrival drains the W2 stores, long
+    // before its seam D releases their readers)
+    {
+      RES_IDX();
       if (tid < C) {
         // b3: identical on every workgroup
         float g = 0.f;
@@ -722,13 +768,7 @@ __global__ void __launch_bounds__(kResThreads) resident_epoch_kernel(ResArgs a) 
           res_update<ADAM>(o, ss, ib, w2[s], g, w2m[s], w2v[s]);
         }
       }
-      if (tid < M)   // DZ2[par][m][w][ii] = dz2[m][n = w + G ii]
-        hst4(rDZ, (((par * 16 + tid) * G + w) * 4) * 4, *reinterpret_cast<const f32x4*>(sdz2 + tid * 4));
     }
-    arrive(a.cnt, 3, w);
-    RES_MARK(9);
-    // W2_{t+1} for the next step's dz1: off this seam's critical path (the next step's seam-B
-    // arrival drains these stores, long before its seam D releases the readers)
     publish_w2(nxt);
 
     // ================= D: fc1 rows' dz1, b1 / W1 steps, next batch's look-ahead
@@ -894,7 +934,7 @@ static std::string check_shape(const ResArgs& a) {
   if (a.C < 1 || a.C > kResMaxC || a.C4 % 4) return "classes <= 128";
   if (a.nfc1 > a.G || a.ngrp > kResGroups || a.nrb > kResMaxRB) return "fc1 tiles per workgroup";
   if (a.G > 256 || a.G < a.M) return "workgroups";
-  if (a.ipc.T > 0 && ((int64_t)a.G * 64 > a.ipc.cap || a.G > a.ipc.nflags || a.ipc.T > kIpcMaxRanks))
+  if (a.ipc.T > 0 && ((int64_t)a.G * 64 * 2 > a.ipc.cap || a.ipc.T > kIpcMaxRanks))
     return "peer-mapped exchange region";
   return "";
 }

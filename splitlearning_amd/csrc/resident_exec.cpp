@@ -86,7 +86,10 @@ class ResidentEpoch {
     a.N1p = (a.N1 + 3) & ~3;
     a.C4 = (a.C + 3) & ~3;
     a.M = B_;
-    a.G = std::min(256, cus);
+    // workgroups: one per CU (up to 256); a smaller count lets several ranks' persistent
+    // launches share one GPU (the multi-process test, scripts/resident_tp_one_gpu.py)
+    const int wg = cfg.contains("workgroups") ? cfg["workgroups"].cast<int>() : 0;
+    a.G = wg > 0 ? std::min(wg, std::min(256, cus)) : std::min(256, cus);
     a.nrb = (a.N1 + 15) / 16;
     a.ncb = (a.K1 + 255) / 256;
     a.ngrp = (a.ncb + sl::kResTiles - 1) / sl::kResTiles;
@@ -140,7 +143,7 @@ class ResidentEpoch {
     a.o = sl::make_opt_raw(kind_, lr_, beta1_, beta2_, eps_, wd_, mom_, 0, nullptr);
     if (ipc_ != nullptr) {
       TORCH_CHECK(ipc_->opened(), "ResidentEpoch: the peer-mapped region is not open");
-      TORCH_CHECK((int64_t)a.G * 64 <= ipc_->cap() && a.G <= ipc_->flag_words(),
+      TORCH_CHECK((int64_t)a.G * 64 * 2 <= ipc_->cap(),
                   "ResidentEpoch: peer-mapped region too small for the fc2 exchange");
     }
     std::string why;

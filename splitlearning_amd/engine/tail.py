@@ -461,7 +461,8 @@ class TailEngine:
              "beta2": cfg.beta2, "eps": cfg.eps, "wd": cfg.weight_decay, "momentum": cfg.momentum,
              "p1": L1.spec.dropout, "p2": L2.spec.dropout, "col_off1": L1.col_off, "B": B,
              "ipc": getattr(self.allreduce, "ipc", None) if L2.style == "row" else None,
-             "timeout_s": float(getattr(self, "resident_timeout_s", 10.0))}
+             "timeout_s": float(getattr(self, "resident_timeout_s", 10.0)),
+             "workgroups": int(getattr(self, "resident_workgroups", 0))}
         ex = self.ops.C().ResidentEpoch(d)
         self._resident = (slot, B, ex, d)
         return ex

@@ -169,3 +169,18 @@ def test_resident_rejects_a_wide_shard(cuda):
     te = TailEngine(ServerTailSisa(), sisa_server_spec(), cuda, ws_tag="#res4")
     slot = OptSlot(adam(1e-3, 1e-5))
     assert not te.resident_ok(slot, 16)          # fc1 5000 rows: the launch-per-stage executor
+
+
+def test_resident_tensor_parallel_across_processes_on_one_gpu():
+    """T = 2 real processes, each a persistent launch of 128 workgroups on the one GPU, the fc2
+    exchange through the peer-mapped region in-launch: replicated state and losses bitwise
+    equal across ranks and close to torch (scripts/resident_tp_one_gpu.py)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, os.path.join(root, "scripts", "resident_tp_one_gpu.py"), "2"],
+                         capture_output=True, text=True, timeout=110, cwd=root)
+    text = out.stdout + out.stderr
+    assert out.returncode == 0, text[-3000:]
+    assert out.stdout.count("PASS") == 2, text[-3000:]
