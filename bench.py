@@ -104,6 +104,9 @@ def main(argv=None):
     ap.add_argument("--bob_tp", type=int, default=0,
                     help="0 = the policy (parallel/dist.py choose_bob_tp: all GPUs for the SISA modes)")
     ap.add_argument("--graphs", choices=("auto", "on", "off"), default="auto")
+    ap.add_argument("--resident", choices=("auto", "off"), default="auto",
+                    help="SISA server epochs of a narrow Bob shard (TP >= 7) on the register-resident "
+                         "persistent executor (csrc/resident.hip) after its cross-rank self-test")
     ap.add_argument("--tp_allreduce", choices=("auto", "rccl"), default="auto",
                     help="Bob's TP all-reduce: peer-mapped one-kernel path when it passes set-up (auto) or RCCL")
     ap.add_argument("--act_dtype", choices=("fp32", "bf16"), default="fp32")
@@ -158,7 +161,7 @@ def main(argv=None):
         "--batch_size", str(a.batch_size), "--partition_alpha", str(a.partition_alpha),
         "--server_epochs", str(a.server_epochs), "--seed", str(a.seed), "--num_samples", str(a.num_samples),
         "--kernels", a.kernels, "--graphs", a.graphs, "--act_dtype", a.act_dtype, "--dtype", a.dtype, "--no_tqdm",
-        "--tp_allreduce", a.tp_allreduce,
+        "--tp_allreduce", a.tp_allreduce, "--resident", a.resident,
         "--log_dir", log_dir, "--watchdog", "off"]
     if a.mode == "concat" and a.concat_unlearn:
         argv_s.append("--concat_unlearn")
@@ -275,6 +278,10 @@ def main(argv=None):
                                  "rccl" if tpc is not None else "torch.distributed" if N > 1 else "none"),
                 "bytes_sent_per_rank_per_step": sent,
                 "tp_ipc_setup": _ipc_status(),
+                # Bob's server-epoch executor: the register-resident persistent launch (a shard
+                # narrow enough to keep on-chip, its self-test passed) or the launch-per-stage one
+                "server_executor": ("resident" if getattr(sess, "_resident_ok", False) else
+                                    "launch_per_stage") if sargs.mode in ("sisa", "control") else None,
                 "calib": calib,
             },
         }

@@ -184,3 +184,50 @@ def test_resident_tensor_parallel_across_processes_on_one_gpu():
     text = out.stdout + out.stderr
     assert out.returncode == 0, text[-3000:]
     assert out.stdout.count("PASS") == 2, text[-3000:]
+
+
+def test_sisa_session_runs_its_server_epochs_on_the_resident_executor(cuda, tmp_path):
+    """The production SISA protocol (local training -> frozen-front dump -> server epochs) with a
+    Bob tail as narrow as a TP = 8 shard (fc1 5408 -> 628): `_decide_resident` adopts the
+    resident executor, every server epoch runs on it (the launch-per-stage executor is never
+    called), and the run matches the same session on the launch-per-stage executor
+    (`--resident off`) to fp32-rounding-level divergence over one server epoch."""
+    from splitlearning_amd.config import parse_args
+    from splitlearning_amd.data.mnist import write_shards
+    from splitlearning_amd.parallel.dist import Comm, Placement
+    from splitlearning_amd.protocols import SisaSession
+    from splitlearning_amd.protocols.schedule import build_steps
+
+    class Narrow(SisaSession):
+        def bob_module_and_spec(self):   # a TP = 8 shard's width (shards are multiples of 4 wide)
+            return self.make_bob_module(_MLP, _spec(n1=628)), _spec(n1=628)
+
+    runs = {}
+    for res in ("auto", "off"):
+        args = parse_args(["--sisa", "--world_size", "2", "--seed", "5", "--num_samples", "1400", "--no_tqdm",
+                           "--server_epochs", "1", "--resident", res,
+                           "--datapath", str(tmp_path / f"d{res}"), "--log_dir", str(tmp_path / f"l{res}")])
+        write_shards(args, verbose=False)
+        sess = Narrow(args, Comm(0, 1, cuda, Placement.make(2, 1, 1)), cuda)
+        assert sess._resident_ok == (res == "auto")
+        calls = {"native": 0}
+        orig = sess.tail.run_native_epoch
+
+        def counted(*a, **k):
+            calls["native"] += 1
+            return orig(*a, **k)
+        sess.tail.run_native_epoch = counted
+        steps = dict(build_steps(sess, args))
+        steps["local_training"]()
+        steps["server_training"]()
+        torch.cuda.synchronize()
+        runs[res] = (sess, calls["native"])
+    sa, na = runs["auto"]
+    so, no = runs["off"]
+    n_train = sum(sa.n_train.values())
+    assert sa.bob_slot.t == so.bob_slot.t == -(-n_train // 16)
+    # the resident run issues the trailing partial batch (if any) on the launch-per-stage executor only
+    assert na <= 1 and no >= 1
+    for La, Lb in zip(sa.tail.layers, so.tail.layers):
+        d = (La.W - Lb.W).abs()
+        assert torch.isfinite(La.W).all() and d.max().item() < 2e-3 * sa.bob_slot.t, d.max().item()
