@@ -318,7 +318,7 @@ __device__ __forceinline__ void st_wt(float* base, int N, int ld, int boff, f32x
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), rs, boff, 0, 16);
 }
 
-template <bool ADAM, int FWDC>
+template <bool ADAM, int FWDC, bool BF = false>
 __global__ void __launch_bounds__(1024)
 wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
   // FWDC: look-ahead row chunks of 16 (0 = no look-ahead; 1: next batch <= 16 rows; 4: <= 64)
@@ -364,6 +364,7 @@ wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
   }
   f32x4 g = zv;
   float gb = 0.f;
+  f32x4 dacc = zv;   // bf16 form: dW[n0 + 4 lq + j][kb + 16 r + li] (MFMA accumulator layout)
   for (int mc = 0; mc < M; mc += 16) {
     if (mc) __syncthreads();
     {
@@ -378,12 +379,38 @@ wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
       }
     }
     __syncthreads();
+    if (BF) {
+      // `--dtype bf16`: the tile's dW = dZ^T A on bf16 MFMA (v_mfma_f32_16x16x16_bf16, k = the
+      // 16 batch rows of this chunk): wave r forms the 16 x 16 block of columns [16 r, 16 r + 16);
+      // lane (li, lq) supplies dZ[4 lq .. 4 lq + 3][n0 + li] and A[4 lq .. 4 lq + 3][16 r + li]
+      typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+      bf16x4_t av4, bv4;
+      const int col = 16 * r + li;
 #pragma unroll
-    for (int mm = 0; mm < 16; ++mm) {
-      const float d = sdz[mm][r];
-      g += d * sa[mm][lane];
-      gb += d;
+      for (int t = 0; t < 4; ++t) {
+        av4[t] = (__bf16)sdz[4 * lq + t][li];
+        bv4[t] = (__bf16)sa[4 * lq + t][col >> 2][col & 3];
+      }
+      dacc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(av4, bv4, dacc, 0, 0, 0);
+#pragma unroll
+      for (int mm = 0; mm < 16; ++mm) gb += sdz[mm][r];
+    } else {
+#pragma unroll
+      for (int mm = 0; mm < 16; ++mm) {
+        const float d = sdz[mm][r];
+        g += d * sa[mm][lane];
+        gb += d;
+      }
     }
+  }
+  if (BF) {
+    // back to the update's layout (row r, float4 column lane) through the A tile's LDS
+    __syncthreads();
+    float* dws = reinterpret_cast<float*>(&sa[0][0]);   // [16][256]
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dws[(4 * lq + j) * 256 + 16 * r + li] = dacc[j];
+    __syncthreads();
+    g = sa[r][lane];
   }
   if (act) {
     sl_opt_update4<ADAM>(o, p, g, q0, q1);
@@ -525,15 +552,23 @@ hipError_t wgrad_group(const WgGroup& g, int M, SlOpt o, hipStream_t st) {
   const int64_t g2 = (int64_t)grid.x * grid.y;
   gg.grid2d = (g2 - wb) * 10 < g2 ? 1 : 0;
   const dim3 gr = gg.grid2d ? grid : grid1;
+  // bf16 compute: a separate instantiation (dW on bf16 MFMA), so the fp32 kernels' registers
+  // and schedule are untouched
+#define SL_WG_LAUNCH(A, F)                                                          \
+  do {                                                                              \
+    if (gg.bf16) wgrad_group_kernel<A, F, true><<<gr, 1024, 0, st>>>(gg, M, o);      \
+    else wgrad_group_kernel<A, F, false><<<gr, 1024, 0, st>>>(gg, M, o);            \
+  } while (0)
   if (o.kind == 2) {
-    if (fc == 4) wgrad_group_kernel<true, 4><<<gr, 1024, 0, st>>>(gg, M, o);
-    else if (fc) wgrad_group_kernel<true, 1><<<gr, 1024, 0, st>>>(gg, M, o);
-    else wgrad_group_kernel<true, 0><<<gr, 1024, 0, st>>>(gg, M, o);
+    if (fc == 4) SL_WG_LAUNCH(true, 4);
+    else if (fc) SL_WG_LAUNCH(true, 1);
+    else SL_WG_LAUNCH(true, 0);
   } else {
-    if (fc == 4) wgrad_group_kernel<false, 4><<<gr, 1024, 0, st>>>(gg, M, o);
-    else if (fc) wgrad_group_kernel<false, 1><<<gr, 1024, 0, st>>>(gg, M, o);
-    else wgrad_group_kernel<false, 0><<<gr, 1024, 0, st>>>(gg, M, o);
+    if (fc == 4) SL_WG_LAUNCH(false, 4);
+    else if (fc) SL_WG_LAUNCH(false, 1);
+    else SL_WG_LAUNCH(false, 0);
   }
+#undef SL_WG_LAUNCH
   return hipGetLastError();
 }
 

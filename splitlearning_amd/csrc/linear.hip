@@ -131,7 +131,18 @@ skinny_fwd_kernel(const float* __restrict__ X, int ldx, const float* __restrict_
 // 5000 in 16 slices of 320 k over 2 waves, 4 round trips per wave).  Native executor, us per
 // server step (profiles/r2_chain_probe.txt): TP = 1 177.8 vs 178.1 and 174.9 vs 175.3, TP = 8
 // 52.3 vs 53.0 and 53.2 vs 53.9 — small, but the same sign in both interleaved runs.
-template <int U>
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ bf16x8_t pack_bf16x8(float4 lo, float4 hi) {
+  bf16x8_t v;
+  v[0] = (__bf16)lo.x; v[1] = (__bf16)lo.y; v[2] = (__bf16)lo.z; v[3] = (__bf16)lo.w;
+  v[4] = (__bf16)hi.x; v[5] = (__bf16)hi.y; v[6] = (__bf16)hi.z; v[7] = (__bf16)hi.w;
+  return v;
+}
+
+// BF: `--dtype bf16` form — lane group q stages k = 8q .. 8q + 7 of each 32-k step (two float4 of
+// its X row and W row, the fp32 form's bytes) for one v_mfma_f32_16x16x32_bf16 per step.
+template <int U, bool BF = false>
 __global__ void __launch_bounds__(1024)
 skinny_fwd_once_kernel(const float* __restrict__ X, int ldx, const float* __restrict__ W, int ldw,
                        float* __restrict__ Y, int ldy, int M, int N, int K, Epi e, float* __restrict__ P,
@@ -163,18 +174,26 @@ skinny_fwd_once_kernel(const float* __restrict__ X, int ldx, const float* __rest
   float4 a[U], w[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    const int kk = kb + 16 * u + kq;
+    // fp32: 16-k steps, lane group q at k = 4q; bf16: 32-k steps, lane group q at k = 8q, 8q + 4
+    const int kk = BF ? kb + 32 * (u >> 1) + 2 * kq + 4 * (u & 1) : kb + 16 * u + kq;
     const bool in = kk < K;                      // K % 4 == 0: a float4 never straddles K
     a[u] = (va && in) ? ld4(pa + kk) : z4;
     w[u] = (vb && in) ? ld4(pb + kk) : z4;
   }
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  if (BF) {
 #pragma unroll
-  for (int u = 0; u < U; ++u) {
-    acc0 = mfma4(a[u].x, w[u].x, acc0);
-    acc1 = mfma4(a[u].y, w[u].y, acc1);
-    acc0 = mfma4(a[u].z, w[u].z, acc0);
-    acc1 = mfma4(a[u].w, w[u].w, acc1);
+    for (int u = 0; u < U; u += 2)
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pack_bf16x8(a[u], a[u + 1]), pack_bf16x8(w[u], w[u + 1]), acc0,
+                                                     0, 0, 0);
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      acc0 = mfma4(a[u].x, w[u].x, acc0);
+      acc1 = mfma4(a[u].y, w[u].y, acc1);
+      acc0 = mfma4(a[u].z, w[u].z, acc0);
+      acc1 = mfma4(a[u].w, w[u].w, acc1);
+    }
   }
   red[wv][lane] = acc0 + acc1;
   __syncthreads();
@@ -226,15 +245,6 @@ static bool fwd_once_plan(int M, int N, int K, int max_split, int64_t ws_elems, 
 // each lane stages 8 consecutive k of its X row and W row (two float4 loads each), rounds
 // them to bf16 and issues one v_mfma_f32_16x16x32_bf16 (lane group q covers k = 8q..8q+7 of
 // a 32-k step); fp32 accumulation.  K slices are 32-aligned.
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-
-__device__ __forceinline__ bf16x8_t pack_bf16x8(float4 lo, float4 hi) {
-  bf16x8_t v;
-  v[0] = (__bf16)lo.x; v[1] = (__bf16)lo.y; v[2] = (__bf16)lo.z; v[3] = (__bf16)lo.w;
-  v[4] = (__bf16)hi.x; v[5] = (__bf16)hi.y; v[6] = (__bf16)hi.z; v[7] = (__bf16)hi.w;
-  return v;
-}
-
 template <int NW, int U>
 __global__ void __launch_bounds__(NW * 64)
 skinny_fwd_bf16_kernel(const float* __restrict__ X, int ldx, const float* __restrict__ W, int ldw,
@@ -340,6 +350,29 @@ skinny_dgrad_kernel(const float* __restrict__ dZ, int ldz, const float* __restri
   for (int c = 0; c < 4; ++c) acc[c] = {0.f, 0.f, 0.f, 0.f};
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
   int n = nb;
+  if (BF) {
+    // bf16 MFMA (v_mfma_f32_16x16x16_bf16), k index = n: lane (i, q) supplies dZ[m0 + i][n + 4q ..
+    // n + 4q + 3] (one float4) and, per column c of its float4, W[n + 4q .. n + 4q + 3][kcol + c]
+    // (four row loads: the fp32 form's bytes per 16 rows), so one MFMA per column group
+    // replaces four exact-fp32 ones; the accumulator layout is the fp32 form's.
+    typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+    for (; n + 16 <= ne; n += 16) {
+      const int nq = n + 4 * q;
+      const float4 a4 = vm ? ld4(za + nq) : z4;
+      float4 wr[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) wr[r] = vk ? ld4(W + (int64_t)(nq + r) * ldw + kcol) : z4;
+      const bf16x4_t A = {(__bf16)a4.x, (__bf16)a4.y, (__bf16)a4.z, (__bf16)a4.w};
+      const bf16x4_t B0 = {(__bf16)wr[0].x, (__bf16)wr[1].x, (__bf16)wr[2].x, (__bf16)wr[3].x};
+      const bf16x4_t B1 = {(__bf16)wr[0].y, (__bf16)wr[1].y, (__bf16)wr[2].y, (__bf16)wr[3].y};
+      const bf16x4_t B2 = {(__bf16)wr[0].z, (__bf16)wr[1].z, (__bf16)wr[2].z, (__bf16)wr[3].z};
+      const bf16x4_t B3 = {(__bf16)wr[0].w, (__bf16)wr[1].w, (__bf16)wr[2].w, (__bf16)wr[3].w};
+      acc[0] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(A, B0, acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(A, B1, acc[1], 0, 0, 0);
+      acc[2] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(A, B2, acc[2], 0, 0, 0);
+      acc[3] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(A, B3, acc[3], 0, 0, 0);
+    }
+  }
   for (; n + 16 <= ne; n += 16) {
     float a[4];
     float4 w[4];
@@ -528,9 +561,13 @@ hipError_t linear_fwd(const float* X, int ldx, const float* W, int ldw, float* Y
   if (M > 128) return gemm_nt(X, ldx, W, ldw, Y, ldy, M, N, K, e, g_bf16 != 0, ws, ws_elems, st);
   dim3 grid((N + 15) / 16, (M + 15) / 16);
   int NW1, S1;
-  if (!g_bf16 && fwd_once_plan(M, N, K, 16, ws ? ws_elems : 0, NW1, S1)) {
-    skinny_fwd_once_kernel<4><<<dim3(grid.x, grid.y, S1), NW1 * 64, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e, ws,
-                                                                          (int64_t)M * N);
+  if (fwd_once_plan(M, N, K, 16, ws ? ws_elems : 0, NW1, S1)) {
+    if (g_bf16)
+      skinny_fwd_once_kernel<4, true><<<dim3(grid.x, grid.y, S1), NW1 * 64, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K,
+                                                                                  e, ws, (int64_t)M * N);
+    else
+      skinny_fwd_once_kernel<4><<<dim3(grid.x, grid.y, S1), NW1 * 64, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e,
+                                                                            ws, (int64_t)M * N);
     if (S1 > 1) {
       launch_epilogue(ws, N, Y, ldy, M, N, e, S1, (int64_t)M * N, st);
     }
@@ -624,15 +661,19 @@ hipError_t linear_fwd_partial(const float* X, int ldx, const float* W, int ldw, 
   if (ws_elems < slab * S) S = 1;
   if (ws_elems < slab) return hipErrorInvalidValue;
   int NW1, S1;
-  if (!g_bf16 && fwd_once_plan(M, N, K, max_split, ws_elems, NW1, S1)) {
+  if (fwd_once_plan(M, N, K, max_split, ws_elems, NW1, S1)) {
     Epi e1{};
     e1.dscale = 1.f;
     // XCD-grouped tile order (at most 64 column tiles: grid padded to 64).  Native executor,
     // us per TP = 1 step against the plain order: 174.4 vs 175.5 and 176.9 vs 178.1 in two
     // interleaved runs (profiles/r2_xcd_grouped_fc2_ab.txt); bitwise the same products.
     const bool xg = grid.x <= 64;
-    skinny_fwd_once_kernel<4><<<dim3(xg ? 64 : grid.x, grid.y, S1), NW1 * 64, 0, st>>>(
-        X, ldx, W, ldw, ws, N, M, N, K, e1, ws, slab, xg ? (int)grid.x : 0);
+    if (g_bf16)
+      skinny_fwd_once_kernel<4, true><<<dim3(xg ? 64 : grid.x, grid.y, S1), NW1 * 64, 0, st>>>(
+          X, ldx, W, ldw, ws, N, M, N, K, e1, ws, slab, xg ? (int)grid.x : 0);
+    else
+      skinny_fwd_once_kernel<4><<<dim3(xg ? 64 : grid.x, grid.y, S1), NW1 * 64, 0, st>>>(
+          X, ldx, W, ldw, ws, N, M, N, K, e1, ws, slab, xg ? (int)grid.x : 0);
     *S_out = S1;
     return hipGetLastError();
   }

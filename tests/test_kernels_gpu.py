@@ -507,6 +507,25 @@ def test_linear_fwd_bf16_compute(cuda, M, N, K):
     assert (y - torch.relu(x @ w.t() + b)).abs().max().item() > 1e-3
 
 
+@pytest.mark.parametrize("M,N,K", [(16, 1000, 5000), (16, 1000, 628), (16, 100, 1000), (64, 1000, 5000), (5, 40, 64)])
+def test_linear_dgrad_bf16_mfma(cuda, M, N, K):
+    """--dtype bf16 data gradient on bf16 MFMA (v_mfma_f32_16x16x32_bf16 over 32-row steps of
+    W, the split-N tails on rounded operands): equals the fp32 product of the bf16-rounded
+    operands (exact products, fp32 accumulation) up to summation order, with the ReLU mask."""
+    C = hip_ops.C()
+    dz = torch.randn(M, N, device=cuda)
+    w = torch.randn(N, K, device=cuda) / N ** 0.5
+    h = torch.relu(torch.randn(M, K, device=cuda))
+    C.set_compute_dtype("bf16")
+    try:
+        got = hip_ops.linear_dgrad(dz, w, h, 2.0)
+    finally:
+        C.set_compute_dtype("fp32")
+    ref = (dz.bfloat16().float() @ w.bfloat16().float()) * (h > 0).float() * 2.0
+    _close(got, ref, rtol=1e-4, atol=2e-4)
+    assert (got - torch_ops.linear_dgrad(dz, w, h, 2.0)).abs().max().item() > 1e-4   # really bf16
+
+
 @pytest.mark.parametrize("M", [16, 64])
 def test_xcd_grouped_fc2_products(cuda, M):
     """The XCD-grouped workgroup order of the fc2 forward / dgrad (a permutation of which
