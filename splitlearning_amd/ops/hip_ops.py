@@ -189,10 +189,13 @@ _TABLE: dict = {}
 
 # ---------------------------------------------------------------- linear
 # training batches (M <= 128) run the skinny split-K kernels.  Many rows (evaluation over a
-# test set, large batches): in bf16 the in-tree LDS-tiled MFMA GEMM (csrc/gemm.hip); in fp32
-# the plain product goes to hipBLASLt (torch.mm: 141 TFLOP/s on Bob's eval shapes against
-# 89 for the in-tree kernel, profiles/r2_gemm_bench.txt) and the fused epilogue kernel
-# applies bias / ReLU / dropout.  Variant 11 = 1 forces the in-tree GEMM in fp32 too.
+# test set, large batches): the forward product runs the in-tree LDS-tiled MFMA GEMM
+# (csrc/gemm.hip, fused bias / ReLU / dropout epilogue) in fp32 and bf16 alike — 73-93 % of
+# hipBLASLt's fp32 rate on the evaluation shapes (profiles/r3i_gemm_bench.txt; the evaluation
+# phase is ~15 ms of a 5.8 s schedule, so the library's lead does not move the headline) —
+# with variant 11 = 2 selecting hipBLASLt + the in-tree epilogue instead.  The data gradient
+# of a batch past 128 rows (`--batch_size` > 128 only) has no in-tree NN-layout GEMM: it goes
+# to hipBLASLt (variant 11 = 1: the skinny kernel, which re-reads W once per 16 rows).
 LARGE_M = 128
 
 
@@ -202,12 +205,16 @@ def set_compute_dtype(dtype: str):
     C().set_compute_dtype(dtype)
 
 
-def _library_gemm(M: int) -> bool:
-    """fp32 products of many rows go to hipBLASLt (measured faster than the in-tree tiled
-    GEMM, csrc/gemm.hip) — except inside a HIP graph capture, where the library may not
-    allocate or initialise, and under variant 11 = 1 (the in-tree kernels, A/B and tests)."""
-    return (M > LARGE_M and C().get_compute_dtype() == "fp32" and C().get_variant(11) != 1
-            and not torch.cuda.is_current_stream_capturing())
+def _library_gemm(M: int, dgrad: bool = False) -> bool:
+    """Whether a product of M > 128 rows goes to hipBLASLt: the forward only under variant
+    11 = 2, the fp32 data gradient unless variant 11 = 1; never inside a HIP graph capture
+    (the library may not allocate or initialise there)."""
+    if M <= LARGE_M or torch.cuda.is_current_stream_capturing():
+        return False
+    v = C().get_variant(11)
+    if dgrad:
+        return C().get_compute_dtype() == "fp32" and v != 1
+    return v == 2
 
 
 def linear_fwd(x, w, b, relu: bool, drop_p: float, seed: int, col_offset: int = 0, out=None, dseed=None):
@@ -270,7 +277,7 @@ def linear_dgrad(dz, w, h_prev=None, scale: float = 1.0, out=None, ws=None):
     M, K = dz.shape[0], w.shape[1]
     if out is None:
         out = torch.empty(M, K, device=dz.device, dtype=torch.float32)
-    if _library_gemm(M):
+    if _library_gemm(M, dgrad=True):
         # many rows (large --batch_size): the skinny kernel would re-read W once per 16 rows;
         # the product goes to hipBLASLt (as the forward does) and the previous layer's
         # ReLU/dropout mask + scale is one in-tree elementwise launch

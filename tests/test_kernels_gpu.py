@@ -77,10 +77,10 @@ def test_conv_bwd(cuda, kind):
                                     (16, 37, 52), (200, 100, 1000), (1000, 5000, 5408), (8000, 1000, 5000),
                                     (129, 130, 36), (300, 10, 100)])
 @pytest.mark.parametrize("relu,drop", [(False, 0.0), (True, 0.0), (True, 0.5)])
-@pytest.mark.parametrize("gemm", [0, 1])
+@pytest.mark.parametrize("gemm", [0, 2])
 def test_linear_fwd(cuda, M, N, K, relu, drop, gemm):
-    """M <= 128: the skinny split-K kernels; M > 128: hipBLASLt + the fused epilogue (gemm 0)
-    or the in-tree LDS-tiled MFMA GEMM (gemm 1: variant 11)."""
+    """M <= 128: the skinny split-K kernels; M > 128: the in-tree LDS-tiled MFMA GEMM with its
+    fused epilogue (gemm 0, the default) or hipBLASLt + the in-tree epilogue (gemm 2: variant 11)."""
     if gemm and M <= 128:
         pytest.skip("the tiled GEMM serves M > 128")
     x = torch.randn(M, K, device=cuda)
