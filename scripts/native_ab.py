@@ -29,8 +29,9 @@ from splitlearning_amd.ops import hip_ops as H  # noqa: E402
 
 def parse(v):
     """`SLOT=VALUE[,...]`; the key `fences` (0 / 1) toggles the peer-mapped all-reduce's
-    release / acquire fences (`--allreduce ipc`) instead of a kernel-variant slot."""
-    return {(a if a == "fences" else int(a)): int(b) for a, b in (kv.split("=") for kv in v.split(","))}
+    release / acquire fences (`--allreduce ipc`) instead of a kernel-variant slot, the key
+    `chain` (0 / 1) the executor's persistent chain launch (csrc/chain.hip)."""
+    return {(a if a in ("fences", "chain") else int(a)): int(b) for a, b in (kv.split("=") for kv in v.split(","))}
 
 
 def main():
@@ -42,12 +43,13 @@ def main():
     ap.add_argument("--allreduce", choices=("rccl", "ipc"), default="rccl",
                     help="TP > 1 stand-in all-reduce: a 1-rank RCCL communicator or a 1-rank peer-mapped "
                          "all-reduce (csrc/ipc_ar.h: its kernel runs, with no peer to wait for)")
+    ap.add_argument("--trace", action="store_true", help="print the last chain launch's phase stamps")
     a = ap.parse_args()
     C = H.C()
     dev = torch.device("cuda", 0)
     ops.set_backend("hip")
     B, nb = 16, 64
-    slots = sorted({s for v in a.variants for s in parse(v) if s != "fences"})
+    slots = sorted({s for v in a.variants for s in parse(v) if s not in ("fences", "chain")})
     for tp in a.tp:
         torch.manual_seed(0)
         acts = torch.rand(B * nb, 5408, device=dev) * 20
@@ -62,6 +64,7 @@ def main():
             else:
                 ar = native_allreduce(self_comm())
         tail = TailEngine(ServerTailSisa(), sisa_server_spec(), dev, tp_rank=0, tp_size=tp, allreduce=ar)
+        tail.chain_trace = a.trace
         slot = OptSlot(adam(1e-3, 1e-5))
         assert tail.native_epoch_ok(B)
         tail.lookahead_prologue(acts[:B])
@@ -81,7 +84,14 @@ def main():
             for v in a.variants:
                 for s in slots:
                     C.set_variant(s, 0)
+                ch = bool(parse(v).get("chain", 0))
+                if getattr(tail, "server_chain", False) != ch or getattr(tail, "_native", None) is None:
+                    tail.server_chain = ch
+                    tail._native = None           # rebuilt with / without the chain launch
+                    pre = False
                 for s, val in parse(v).items():
+                    if s == "chain":
+                        continue
                     if s == "fences":
                         if ipc is not None:
                             ipc.set_fences(bool(val))
@@ -93,6 +103,12 @@ def main():
                 epochs(a.epochs)
                 torch.cuda.synchronize()
                 res[v].append((time.perf_counter() - t0) / (a.epochs * nb) * 1e6)
+                if a.trace and ch:
+                    tr = tail._native[2].chain_trace().cpu()
+                    t0w = int(tr[0])
+                    print(f"tp={tp} chain phases (us after wg 0 start) wg0: "
+                          + " ".join(f"{(int(x) - t0w) / 100:.2f}" for x in tr[:15])
+                          + " | wg last: " + " ".join(f"{(int(x) - t0w) / 100:.2f}" for x in tr[16:31]), flush=True)
         for s in slots:
             C.set_variant(s, 0)
         for v, xs in res.items():

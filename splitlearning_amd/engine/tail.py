@@ -400,6 +400,13 @@ class TailEngine:
              "ipc": getattr(self.allreduce, "ipc", None) if L2.style == "row" else None, "B": B,
              "groups": self.ce_groups,
              "emulate_tp": L2.style == "row" and self.allreduce is None,
+             # the step's forward / backward as one persistent launch (csrc/chain.hip) where it
+             # fits (opt-in: slower than the six kernels except at TP = 2, docs/PERF.md); off:
+             # the six-kernel chain, bitwise the Python path's launches
+             "chain": bool(getattr(self, "server_chain", False)),
+             "chain_timeout_s": float(getattr(self, "chain_timeout_s", 10.0)),
+             "chain_workgroups": int(getattr(self, "chain_workgroups", 0)),
+             "chain_trace": bool(getattr(self, "chain_trace", False)),
              "pn": self.lookahead_slabs(B),
              "p2ws": ops._workspace(dev, 16 * B * N2, "fc2p" + tg),
              "fwdws": ops._workspace(dev, 16 * B * nmax, "fwd" + tg),
