@@ -49,6 +49,7 @@ def worker(rank, world, port):
         base = _MLP(spec)
         mine = TailEngine(copy.deepcopy(base), spec, dev, tp_rank=rank, tp_size=world, allreduce=ipc_allreduce(ipc),
                           seed_base=seed_base)
+        mine.server_chain = True
         mine.chain_workgroups = 256 // world
         mine.chain_timeout_s = 5.0
         slot = OptSlot(adam(1e-3, 1e-5))

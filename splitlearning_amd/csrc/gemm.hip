@@ -346,13 +346,16 @@ static hipError_t gemm_nt_rows(const float* X, int ldx, const float* W, int ldw,
     case 5: return launch_gemm<false, 4, 16>(X, ldx, W, ldw, Y, ldy, M, N, K, e, st);
     default: break;
   }
-  // fp32: the 32 x 32 x 2 form.  256 x 128 tiles when they fill the chip (>= 2 per CU), else
-  // 128 x 128 tiles, split over K until ~2 workgroups per CU (slices >= 512 deep, <= 8)
+  // fp32: the 32 x 32 x 2 form.  256 x 128 tiles when they fill the chip (>= 1.5 per CU:
+  // M 14000, N 1000 measured 108.8 vs 104.4 TF/s against 128 x 128 tiles), else 128 x 128
+  // tiles, split over K until ~2 workgroups per CU (slices >= 512 deep, >= 256 when fewer
+  // tiles than CUs: M 14000, N 100, K 1000 ran 110 workgroups; <= 8 slices)
   const int64_t t4 = (int64_t)((M + 255) / 256) * ((N + 127) / 128);
-  if (t4 >= 512) return launch_gemm_f32x32<4, 16>(X, ldx, W, ldw, Y, ldy, M, N, K, e, 1, nullptr, st);
+  if (t4 >= 384) return launch_gemm_f32x32<4, 16>(X, ldx, W, ldw, Y, ldy, M, N, K, e, 1, nullptr, st);
   const int64_t t2 = (int64_t)((M + 127) / 128) * ((N + 127) / 128);
+  const int kmin = t2 < 256 ? 256 : 512;
   int S = 1;
-  while (S < 8 && t2 * S * 2 <= 640 && K / (S * 2) >= 512 && (int64_t)S * 2 * M * N <= ws_elems) S *= 2;
+  while (S < 8 && t2 * S * 2 <= 640 && K / (S * 2) >= kmin && (int64_t)S * 2 * M * N <= ws_elems) S *= 2;
   return launch_gemm_f32x32<2, 16>(X, ldx, W, ldw, Y, ldy, M, N, K, e, S, ws, st);
 }
 

@@ -27,6 +27,17 @@ def test_reference_flags_and_defaults():
         assert f in flags
 
 
+def test_server_executor_flags():
+    """Bob's server-epoch executors beyond the reference's flags: the register-resident epoch
+    (default where it fits) and the persistent chain launch (opt-in)."""
+    a = parse_args(["--sisa"])
+    assert a.resident == "auto" and a.server_chain == "off"
+    a = parse_args(["--sisa", "--resident", "off", "--server_chain", "on"])
+    assert a.resident == "off" and a.server_chain == "on"
+    with pytest.raises(SystemExit):
+        parse_args(["--server_chain", "auto"])
+
+
 @pytest.mark.parametrize("argv,msg", [
     (["--concat"], "--concat option can only be used with the --sisa"),
     (["--vanilla", "--sisa"], "--vanilla option cannot be used"),
