@@ -62,6 +62,13 @@ def main():
             ok = (a0 > 0) & (a1 > 0)
             if ok.any():
                 print(f"  {k:2d}->{k + 1:2d} {NAMES[k]:34s} {(a1 - a0)[ok].mean().item():6.2f} us")
+        # inside "wait D": the parameter updates (9 -> 14), W2's publication (14 -> 15), the wait (15 -> 10)
+        for k0, k1, nm in ((9, 14, "b3 / W3 / b2 / W2 updates"), (14, 15, "W2 publication"),
+                           (15, 10, "B4 loads + wait D")):
+            a0, a1 = x[:, k0], x[:, k1]
+            ok = (a0 > 0) & (a1 > 0)
+            if ok.any():
+                print(f"  {k0:2d}->{k1:2d} {nm:34s} {(a1 - a0)[ok].mean().item():6.2f} us")
         # fc2-only workgroups: wait D is skipped; stamp 9 -> next step's stamp 0
         nxt = (x[1:, 0] - x[:-1, 9]).mean().item()
         print(f"  9 -> next 0 (rest of step)                {nxt:6.2f} us")

@@ -769,33 +769,31 @@ __global__ void __launch_bounds__(kResThreads) resident_epoch_kernel(ResArgs a) 
         }
       }
     }
-    publish_w2(nxt);
+    RES_MARK(14);
+    // W2_{t+1}'s publication: fc1 workgroups issue it after their dz1 (its write-through stores
+    // ahead of seam D's poll held the poll until they were acknowledged: 2.7 us measured)
+    if (!fc1) publish_w2(nxt);
+    RES_MARK(15);
 
     // ================= D: fc1 rows' dz1, b1 / W1 steps, next batch's look-ahead
     if (fc1) {
       const bool more = i + 1 < a.S;
       // dz1[m][nn] = sum_n dz2[m][n] W2_t[n][n0 + nn]; fc2 rows in the publishers' order: block
-      // b = 4 workgroups w' = 4 b + lq, MFMA k index c = ii, i.e. n = w' + G c.  W2_t was
-      // published a step ago, so its operands load before the wait; dz2's after it.
+      // b = 4 workgroups w' = 4 b + lq, MFMA k index c = ii, i.e. n = w' + G c.  The seam is
+      // polled with no loads in flight (the updates above have filled the wait, so it passes in
+      // one poll: issued behind W2_t's operand loads it waited for them, measured 4.3 us from
+      // the publication to the release), then both operands load in one round trip.
       constexpr int KB = 256 / 4 / NW;                       // blocks per wave (G <= 256)
-      f32x4 B4[KB];
-      {
-        RES_IDX();
-#pragma unroll
-        for (int k = 0; k < KB; ++k) {
-          const int wp = 4 * (r + NW * k) + lq;
-          B4[k] = (wp < G && n0 + li < N1) ? hld4(rW2B, ((((par * a.nrb + rb) * G + wp) * 16 + li) * 4) * 4) : zv;
-        }
-      }
       if (!seam_wait(a, 3, (unsigned)(i + 1), s_ok)) break;
       RES_MARK(10);
       {
         RES_IDX();
         f32x4 acc = zv;
-        f32x4 A4[KB];
+        f32x4 A4[KB], B4[KB];
 #pragma unroll
         for (int k = 0; k < KB; ++k) {
           const int wp = 4 * (r + NW * k) + lq;
+          B4[k] = (wp < G && n0 + li < N1) ? hld4(rW2B, ((((par * a.nrb + rb) * G + wp) * 16 + li) * 4) * 4) : zv;
           A4[k] = (wp < G && li < M) ? hld4(rDZ, (((par * 16 + li) * G + wp) * 4) * 4) : zv;
         }
 #pragma unroll
@@ -818,6 +816,7 @@ __global__ void __launch_bounds__(kResThreads) resident_epoch_kernel(ResArgs a) 
         }
       }
       __syncthreads();
+      publish_w2(nxt);
       RES_MARK(11);
       // the next batch's inputs: the first two tiles' loads issued under the dW / Adam work
       // below, the rest after it (all four up front spill the state registers)
