@@ -19,7 +19,7 @@ constexpr int kChMaxWC4 = 40;        // tile columns / 4
 constexpr int kChMaxC = 128;         // classes
 constexpr int kChSeams = 4;          // 0: fc2 partials, 1: logit partials, 2: dlogits, 3: dz2
 constexpr int kChStride = 32;        // counter words between counters (128 B)
-constexpr int kChCounters = kChSeams * 8 + 2 * kChMaxCB;   // seam shards, then 2 sets of column-group counters
+constexpr int kChCounters = kChSeams * 8 + kChMaxCB;   // seam shards, then one dz1 counter per column group
 
 struct ChainArgs {
   int M, N1, N2, C, C4;

@@ -32,7 +32,7 @@
 //                                                                                -> seam 2
 //   head (again): dh2 = dlogits . W3[:, rows], then dz2 via the ReLU / dropout mask
 //                                                                                -> seam 3
-//   tile (again): dz1 partial over its rows, DP[rb][m][slice] (MFMA).  Group counter 1, then
+//   tile (again): dz1 partial over its rows, DP[rb][m][slice] (MFMA).  The column group's counter, then
 //        rows {rb, rb + 8} of the slice: the 8 partials in order, h1 > 0 mask, dropout scale
 //        -> dz1.
 // Summation orders are fixed, so a launch is deterministic.  They differ from the six-kernel
@@ -93,8 +93,8 @@ __device__ __forceinline__ bool ch_spin(const ChainArgs& a, const unsigned* p, u
 __device__ __forceinline__ unsigned* ch_seam(const ChainArgs& a, int seam, int shard) {
   return a.cnt + (seam * 8 + shard) * kChStride;
 }
-__device__ __forceinline__ unsigned* ch_group(const ChainArgs& a, int set, int cb) {
-  return a.cnt + (kChSeams * 8 + set * kChMaxCB + cb) * kChStride;
+__device__ __forceinline__ unsigned* ch_group(const ChainArgs& a, int cb) {
+  return a.cnt + (kChSeams * 8 + cb) * kChStride;
 }
 
 // every shard of `seam` holds this launch's arrivals (lanes 0..7 of wave 0 poll one shard
@@ -114,8 +114,8 @@ __device__ __forceinline__ bool ch_seam_wait(const ChainArgs& a, int seam, int* 
   return *s_ok != 0;
 }
 
-__device__ __forceinline__ bool ch_group_wait(const ChainArgs& a, int set, int cb, int* s_ok) {
-  if (threadIdx.x == 0) *s_ok = ch_spin(a, ch_group(a, set, cb), a.gen * (unsigned)kChRB) ? 1 : 0;
+__device__ __forceinline__ bool ch_group_wait(const ChainArgs& a, int cb, int* s_ok) {
+  if (threadIdx.x == 0) *s_ok = ch_spin(a, ch_group(a, cb), a.gen * (unsigned)kChRB) ? 1 : 0;
   __syncthreads();
   return *s_ok != 0;
 }
@@ -222,8 +222,7 @@ __global__ void __launch_bounds__(kChThreads) chain_step_kernel(ChainArgs a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) sh1[m * kPW + 4 * q + i] = o[i];
     }
-    CH_MARK(1);
-    CH_MARK(2);
+    CH_MARK(1);   // (mark 2 was the column group's h1 exchange, replaced by the formation above)
     // F3: the W2 block -> LDS
 #pragma unroll
     for (int u = 0; u < U2; ++u) {
@@ -501,9 +500,9 @@ __global__ void __launch_bounds__(kChThreads) chain_step_kernel(ChainArgs a) {
         }
       }
     }
-    ch_arrive(ch_group(a, 1, cb));
+    ch_arrive(ch_group(a, cb));
     CH_MARK(12);
-    if (!ch_group_wait(a, 1, cb, s_ok)) return;
+    if (!ch_group_wait(a, cb, s_ok)) return;
     CH_MARK(13);
     if (tid < 2 * WC4) {
       const int k = tid / WC4, q = tid - k * WC4;
