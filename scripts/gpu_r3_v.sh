@@ -3,7 +3,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export PYTHONUNBUFFERED=1
-timeout -k 10 300 python -u scripts/gemm_bench.py --forms 2 4 3 --shapes all --reps 16 > gpurun_out/r3v_gemm_forms.txt 2>&1
+timeout -k 10 300 python -u scripts/gemm_bench.py --forms 0 2 --shapes all --reps 16 > gpurun_out/r3v_gemm_forms.txt 2>&1
 rc=$?
 grep -v amdgpu.ids gpurun_out/r3v_gemm_forms.txt
 exit $rc
