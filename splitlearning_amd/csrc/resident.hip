@@ -537,11 +537,21 @@ __global__ void __launch_bounds__(kResThreads) resident_epoch_kernel(ResArgs a) 
           for (int m = 0; m < 16; ++m) acc[m] = fmaf(sh1[m * SH1P + j], w2[s], acc[m]);
         }
       }
+      // the 16 wave sums as one reduce-scatter: each exchange halves the values a lane holds
+      // (17 lane exchanges instead of 16 x 6); lane L ends with row m = L[5:2]
 #pragma unroll
-      for (int m = 0; m < 16; ++m) {
-        const float t = sl_wave_sum(acc[m]);
-        if (lane == 0) red2[r * 16 + m] = t;
+      for (int h = 8, bit = 32; h >= 1; h >>= 1, bit >>= 1) {
+        const bool up = (lane & bit) != 0;
+#pragma unroll
+        for (int u = 0; u < h; ++u) {
+          const float keep = up ? acc[h + u] : acc[u], send = up ? acc[u] : acc[h + u];
+          acc[u] = keep + __shfl_xor(send, bit);
+        }
       }
+      float t = acc[0];
+      t += __shfl_xor(t, 2);
+      t += __shfl_xor(t, 1);
+      if ((lane & 3) == 0) red2[r * 16 + (lane >> 2)] = t;
     }
     __syncthreads();
     RES_MARK(3);
@@ -797,9 +807,15 @@ __global__ void __launch_bounds__(kResThreads) resident_epoch_kernel(ResArgs a) 
           A4[k] = (wp < G && li < M) ? hld4(rDZ, (((par * 16 + li) * G + wp) * 4) * 4) : zv;
         }
 #pragma unroll
-        for (int k = 0; k < KB; ++k)
+        for (int k = 0; k < KB; k += 2) {   // two chains: consecutive MFMAs independent
+          f32x4 acc1 = zv;
 #pragma unroll
-          for (int c = 0; c < 4; ++c) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A4[k][c], B4[k][c], acc, 0, 0, 0);
+          for (int c = 0; c < 4; ++c) {
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A4[k][c], B4[k][c], acc, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(A4[k + 1][c], B4[k + 1][c], acc1, 0, 0, 0);
+          }
+          acc += acc1;
+        }
         red[r * 64 + lane] = acc;
       }
       __syncthreads();
@@ -846,7 +862,6 @@ __global__ void __launch_bounds__(kResThreads) resident_epoch_kernel(ResArgs a) 
             if (n1 < N1) res_update4<ADAM>(o, ss, ib, p[ct][0], g0, s0[ct][0], s1[ct][0]);
             if (n1 + 8 < N1) res_update4<ADAM>(o, ss, ib, p[ct][1], g1, s0[ct][1], s1[ct][1]);
           }
-          __builtin_amdgcn_sched_barrier(0);   // one tile's update live at a time
         }
       }
       RES_MARK(12);
