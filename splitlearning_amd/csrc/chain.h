@@ -17,9 +17,10 @@ constexpr int kChMaxCB = 32;         // fc2 column blocks (<= 40 float4 each)
 constexpr int kChMaxWR = 128;        // tile rows
 constexpr int kChMaxWC4 = 40;        // tile columns / 4
 constexpr int kChMaxC = 128;         // classes
+constexpr int kChMaxSlabs = 24;      // fc1 look-ahead slabs (fc1 input width <= 6144)
 constexpr int kChSeams = 4;          // 0: fc2 partials, 1: logit partials, 2: dlogits, 3: dz2
 constexpr int kChStride = 32;        // counter words between counters (128 B)
-constexpr int kChCounters = kChSeams * 8 + kChMaxCB;   // seam shards, then one dz1 counter per column group
+constexpr int kChCounters = kChSeams * 8 + 2 * kChMaxCB;   // seam shards, then 2 sets of column-group counters
 
 struct ChainArgs {
   int M, N1, N2, C, C4;

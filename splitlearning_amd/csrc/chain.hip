@@ -18,10 +18,9 @@
 //   tile (rb, cb), 8 x NCB of them: W2[r0 .. r0 + WR)[c0 .. c0 + WC), at most 128 x 160,
 //        loaded once into LDS and used by both products.  The 8 row blocks of column block cb
 //        are workgroups cb, cb + NCB, ..., i.e. one XCD's L2 when NCB % 8 == 0.
-//        F1  the h1 slice: the look-ahead slabs summed in slab order, plus bias, ReLU and
-//            dropout (engine.cpp linear_epilogue's math), formed by each of the column block's
-//            8 workgroups from its XCD's L2 (measured cheaper than a hand-off); row block 0
-//            stores it to h1.
+//        F1  h1 rows {rb, rb + 8} of the slice: the look-ahead slabs summed in a fixed order,
+//            plus bias, ReLU and dropout (engine.cpp linear_epilogue's math).  Stored to h1;
+//            the column group exchanges them (group counter 0).
 //        F4  fc2 partial FP[cb][m][r0 + n] = h1[m, slice] . W2[r0 + n, slice]
 //            (exact-fp32 MFMA 16x16x4; one wave per 16 rows)                    -> seam 0
 //   head w < N2 / 4: fc2 rows 4w .. 4w + 3.
@@ -32,7 +31,7 @@
 //                                                                                -> seam 2
 //   head (again): dh2 = dlogits . W3[:, rows], then dz2 via the ReLU / dropout mask
 //                                                                                -> seam 3
-//   tile (again): dz1 partial over its rows, DP[rb][m][slice] (MFMA).  The column group's counter, then
+//   tile (again): dz1 partial over its rows, DP[rb][m][slice] (MFMA).  Group counter 1, then
 //        rows {rb, rb + 8} of the slice: the 8 partials in order, h1 > 0 mask, dropout scale
 //        -> dz1.
 // Summation orders are fixed, so a launch is deterministic.  They differ from the six-kernel
@@ -93,8 +92,8 @@ __device__ __forceinline__ bool ch_spin(const ChainArgs& a, const unsigned* p, u
 __device__ __forceinline__ unsigned* ch_seam(const ChainArgs& a, int seam, int shard) {
   return a.cnt + (seam * 8 + shard) * kChStride;
 }
-__device__ __forceinline__ unsigned* ch_group(const ChainArgs& a, int cb) {
-  return a.cnt + (kChSeams * 8 + cb) * kChStride;
+__device__ __forceinline__ unsigned* ch_group(const ChainArgs& a, int set, int cb) {
+  return a.cnt + (kChSeams * 8 + set * kChMaxCB + cb) * kChStride;
 }
 
 // every shard of `seam` holds this launch's arrivals (lanes 0..7 of wave 0 poll one shard
@@ -114,8 +113,8 @@ __device__ __forceinline__ bool ch_seam_wait(const ChainArgs& a, int seam, int* 
   return *s_ok != 0;
 }
 
-__device__ __forceinline__ bool ch_group_wait(const ChainArgs& a, int cb, int* s_ok) {
-  if (threadIdx.x == 0) *s_ok = ch_spin(a, ch_group(a, cb), a.gen * (unsigned)kChRB) ? 1 : 0;
+__device__ __forceinline__ bool ch_group_wait(const ChainArgs& a, int set, int cb, int* s_ok) {
+  if (threadIdx.x == 0) *s_ok = ch_spin(a, ch_group(a, set, cb), a.gen * (unsigned)kChRB) ? 1 : 0;
   __syncthreads();
   return *s_ok != 0;
 }
@@ -172,11 +171,27 @@ __global__ void __launch_bounds__(kChThreads) chain_step_kernel(ChainArgs a) {
   const int r0 = 4 * g0, WR = 4 * (g1 - g0);
   const int q0 = cb * Q4 / NCB, q1 = (cb + 1) * Q4 / NCB;
   const int c0 = 4 * q0, WC4 = q1 - q0, WC = 4 * WC4;
-  const __amdgpu_buffer_rsrc_t rFP = ch_rs(a.FP), rLP = ch_rs(a.LP), rDL = ch_rs(a.DL),
+  const __amdgpu_buffer_rsrc_t rH1 = ch_rs(a.h1), rFP = ch_rs(a.FP), rLP = ch_rs(a.LP), rDL = ch_rs(a.DL),
                                rDZ2 = ch_rs(a.dz2), rDP = ch_rs(a.DP);
 
-  // independent loads first: this tile's W2 block (registers, rows >= WR zero) and the head
-  // rows' W3 columns (LDS)
+  // Loads in the order they are consumed (a wave's loads complete in order, so consuming one
+  // waits for every load issued before it; W2's block issued first held the slab sums until
+  // it had arrived, 10.6 us measured): the look-ahead slabs of this workgroup's two h1 rows
+  // {rb, rb + 8} of the slice (6 slab groups x 2 rows x WC4 float4, <= 4 per thread), then the
+  // tile's W2 block (first needed after h1 is formed and exchanged), then the head rows' W3
+  // columns (one float per thread, into LDS at the head phase)
+  constexpr int EW = 2 * kChMaxWC4, SG = kChThreads / EW, SPT = kChMaxSlabs / SG;   // 80 x 6, 4
+  const int e1 = tid % EW, sg1 = tid / EW;
+  const int k1 = e1 / max(WC4, 1), qe1 = e1 - k1 * max(WC4, 1), m1 = rb + kChRB * k1;
+  const bool act1 = tile && tid < SG * EW && k1 < 2 && m1 < M && WC4 > 0;
+  f32x4 sl[SPT];
+#pragma unroll
+  for (int u = 0; u < SPT; ++u) {
+    const int sb = sg1 + SG * u;
+    sl[u] = (act1 && sb < a.S1)
+                ? *reinterpret_cast<const f32x4*>(a.pn + (int64_t)sb * a.slab + (int64_t)m1 * N1 + c0 + 4 * qe1)
+                : zv;
+  }
   constexpr int U2 = kChMaxWR * kChMaxWC4 / kChThreads;
   f32x4 wv[U2];
 #pragma unroll
@@ -187,42 +202,49 @@ __global__ void __launch_bounds__(kChThreads) chain_step_kernel(ChainArgs a) {
                 ? *reinterpret_cast<const f32x4*>(a.W2 + (int64_t)(r0 + row) * N1 + c0 + 4 * q)
                 : zv;
   }
-  if (head) {
-    for (int e = tid; e < 4 * MC; e += kChThreads) {
-      const int ii = e / MC, c = e - ii * MC;
-      sW3[ii * MC + c] = c < C ? a.W3[(int64_t)c * N2 + 4 * w + ii] : 0.f;
-    }
+  static_assert(4 * MC == kChThreads, "one W3 element per thread");
+  float w3r = 0.f;
+  {
+    const int ii = tid / MC, c = tid - ii * MC;
+    if (head && c < C) w3r = a.W3[(int64_t)c * N2 + 4 * w + ii];
   }
 
   // ================= F: h1 slice, fc2 partial products
   if (tile) {
-    // F1: the h1 slice, all rows, formed by each of the column block's 8 workgroups (the
-    // slabs come from their XCD's L2 after the first touch; measured cheaper than one
-    // hand-off): the slabs summed in order, bias, ReLU, dropout -> LDS (rows >= M zero); row
-    // block 0 also stores it to h1 (the wgrad launch's operand)
+    // F1: h1 rows {rb, rb + 8} of the slice: the slab groups' sums in group order, bias,
+    // ReLU, dropout (engine.cpp linear_epilogue's math) -> h1, exchanged within the column
+    // group (its 8 workgroups share one XCD's L2 when NCB % 8 == 0)
+    {
+      f32x4 v = sl[0];
+#pragma unroll
+      for (int u = 1; u < SPT; ++u) v += sl[u];
+      if (tid < SG * EW) red[sg1 * EW + e1] = v;
+    }
+    __syncthreads();
+    if (tid < 2 * WC4) {
+      const int kk = tid / WC4, qq = tid - kk * WC4;
+      const int mm = rb + kChRB * kk;
+      if (mm < M) {
+        f32x4 s = red[tid];
+#pragma unroll
+        for (int g = 1; g < SG; ++g) s += red[g * EW + tid];
+        f32x4 o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = apply_epi(a.e1, s[i], mm, c0 + 4 * qq + i);
+        ch_st4(rH1, ((mm * N1) + c0 + 4 * qq) * 4, o);
+      }
+    }
+    ch_arrive(ch_group(a, 0, cb));
+    CH_MARK(1);
+    if (!ch_group_wait(a, 0, cb, s_ok)) return;
+    CH_MARK(2);
+    // F2: the whole h1 slice (rows >= M zero) -> LDS
     for (int e = tid; e < 16 * WC4; e += kChThreads) {
       const int m = e / WC4, q = e - m * WC4;
-      f32x4 o = zv;
-      if (m < M) {
-        constexpr int SU = 11;                   // slabs in flight per batch
-        const float* src = a.pn + (int64_t)m * N1 + c0 + 4 * q;
-        f32x4 acc = zv;
-        for (int s0 = 0; s0 < a.S1; s0 += SU) {
-          f32x4 v[SU];
+      const f32x4 v = m < M ? ch_ld4(rH1, ((m * N1) + c0 + 4 * q) * 4) : zv;
 #pragma unroll
-          for (int u = 0; u < SU; ++u)
-            v[u] = s0 + u < a.S1 ? *reinterpret_cast<const f32x4*>(src + (int64_t)(s0 + u) * a.slab) : zv;
-#pragma unroll
-          for (int u = 0; u < SU; ++u) acc += v[u];
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) o[i] = apply_epi(a.e1, acc[i], m, c0 + 4 * q + i);
-        if (rb == 0) *reinterpret_cast<f32x4*>(a.h1 + (int64_t)m * N1 + c0 + 4 * q) = o;
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) sh1[m * kPW + 4 * q + i] = o[i];
+      for (int i = 0; i < 4; ++i) sh1[m * kPW + 4 * q + i] = v[i];
     }
-    CH_MARK(1);   // (mark 2 was the column group's h1 exchange, replaced by the formation above)
     // F3: the W2 block -> LDS
 #pragma unroll
     for (int u = 0; u < U2; ++u) {
@@ -260,6 +282,7 @@ __global__ void __launch_bounds__(kChThreads) chain_step_kernel(ChainArgs a) {
 
   // ================= H: P2 of the head rows, h2, logit partials
   if (head) {
+    sW3[tid] = w3r;                              // ordered before its readers by the wait's barrier
     if (!ch_seam_wait(a, 0, s_ok)) return;
     CH_MARK(5);
     {
@@ -500,9 +523,9 @@ __global__ void __launch_bounds__(kChThreads) chain_step_kernel(ChainArgs a) {
         }
       }
     }
-    ch_arrive(ch_group(a, cb));
+    ch_arrive(ch_group(a, 1, cb));
     CH_MARK(12);
-    if (!ch_group_wait(a, cb, s_ok)) return;
+    if (!ch_group_wait(a, 1, cb, s_ok)) return;
     CH_MARK(13);
     if (tid < 2 * WC4) {
       const int k = tid / WC4, q = tid - k * WC4;
@@ -534,7 +557,7 @@ std::string chain_check(const ChainArgs& a) {
   if ((a.N1 / 4 + a.NCB - 1) / a.NCB > kChMaxWC4) return "fc1 shard too wide for the tiles";
   if (a.C < 1 || a.C > kChMaxC || a.C4 % 4 || a.C4 < a.C) return "classes <= 128";
   if (a.G < a.M || a.G > 1024) return "workgroups";
-  if (a.S1 < 1 || a.slab < (int64_t)a.M * a.N1) return "look-ahead slabs";
+  if (a.S1 < 1 || a.S1 > kChMaxSlabs || a.slab < (int64_t)a.M * a.N1) return "look-ahead slabs";
   if (a.ipc.T > 0 && ((int64_t)a.HW * 64 * 2 > a.ipc.cap || a.ipc.T > kIpcMaxRanks))
     return "peer-mapped exchange region";
   return "";
