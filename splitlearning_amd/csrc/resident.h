@@ -44,7 +44,7 @@ struct ResArgs {
   int lookahead_last;     // 1: the last step also forms the next batch's fc1 product (unused: 0)
   // hand-off buffers (zeroed once by the host; double-buffered by step parity)
   float* LA;              // [2][ngrp][16][N1p] fc1 look-ahead partial pre-activations
-  float* H1;              // [2][16][N1p] h1 rows published by each row block's group-0 workgroup
+  float* H1;              // [2][16][N1p] h1 rows published by each row block's last-arriving column group
   float* LP;              // [2][G][16][C4] logit partials of each workgroup's fc2 rows
   float* DL;              // [2][16][C4] dlogits
   float* DZ2;             // [2][16][G][4] fc2 output gradient, dz2[m][w + G ii] at [m][w][ii]

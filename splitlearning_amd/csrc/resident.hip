@@ -21,8 +21,9 @@
 // Step t, four in-launch hand-offs ("seams", each: write-through (sc1) payload stores, every
 // wave drains, one agent-scope counter add per workgroup on a per-XCD shard; consumers poll
 // the shards, then read with sc1 loads — MI355X_MICROARCH.md, the valid-forms table row 1):
-//   [A]  fc1 workgroups published their look-ahead partials of x_t W1_t^T (per column group)
-//        and b1_t; every workgroup forms h1_t = drop(relu(sum + b1)) in LDS, then its fc2
+//   [A]  each fc1 row block's last-arriving column group summed the groups' look-ahead
+//        partials of x_t W1_t^T (+ b1_t) and published h1_t = drop(relu(.)); every workgroup
+//        reads h1_t into LDS, then its fc2
 //        rows' product P2[:, n] = h1 W2[n, :]^T (tensor-parallel: the peer-mapped exchange of
 //        those rows with the other ranks, summed in rank order), h2 = drop(relu(P2 + b2)) and
 //        its share of the logits, sum_n h2[:, n] W3[:, n]^T;
@@ -85,16 +86,10 @@ __device__ __forceinline__ void arrive(unsigned* cnt, int seam, int w) {
                            __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Row-block hand-off (fc1 look-ahead partials of one 16-row block's column groups to its
-// group-0 workgroup): one counter per row block after the seam shards.
+// Row-block hand-off (fc1 look-ahead partials of one 16-row block's column groups to the
+// block's last-arriving group): one counter per row block after the seam shards.
 __device__ __forceinline__ unsigned* rb_counter(unsigned* cnt, int rb) {
   return cnt + (kResSeams * 8 + rb) * kResShardStride;
-}
-__device__ __forceinline__ void arrive_rb(unsigned* cnt, int rb) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0)
-    __hip_atomic_fetch_add(rb_counter(cnt, rb), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Wait until every shard of `seam` holds `mult` arrivals per producer of that shard (lanes
@@ -126,32 +121,6 @@ __device__ __forceinline__ bool seam_wait(const ResArgs& a, int seam, unsigned m
     }
     ok = __all(ok);
     if (lane == 0) *s_ok = ok ? 1 : 0;
-  }
-  __syncthreads();
-  return *s_ok != 0;
-}
-
-// Wait until the row-block counter reaches `tgt` (thread 0 polls); false on give-up.
-__device__ __forceinline__ bool rb_wait(const ResArgs& a, int rb, unsigned tgt, int* s_ok) {
-  if (threadIdx.x == 0) {
-    bool ok = true;
-    const unsigned* p = rb_counter(a.cnt, rb);
-    if (poll(p) < tgt) {
-      const uint64_t t0 = wall_clock64();
-      while (poll(p) < tgt) {
-        if (failed(a.err)) {
-          ok = false;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-        if ((int64_t)(wall_clock64() - t0) > a.timeout) {
-          __hip_atomic_fetch_or(a.err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          ok = false;
-          break;
-        }
-      }
-    }
-    *s_ok = ok ? 1 : 0;
   }
   __syncthreads();
   return *s_ok != 0;
@@ -395,8 +364,9 @@ __global__ void __launch_bounds__(kResThreads) resident_epoch_kernel(ResArgs a) 
   // the look-ahead: pre[m][n0 + nn] = sum over this workgroup's columns of x[m] . W1[n0 + nn]
   // (exact-fp32 MFMA 16x16x4; the updated tile staged through LDS into B layout, rows padded
   // to 65 float4, as wgrad_group_kernel; wave r covers the tile's 16-column groups r and
-  // r + 8) -> LA[par][grp]; the row block's group-0 workgroup turns the groups' partials into
-  // h1 rows (H1[par]) for step `step` and publishes them (seam A).  False: a wait gave up.
+  // r + 8) -> LA[par][grp]; the row block's last-arriving column group turns the groups'
+  // partials into h1 rows (H1[par]) for step `step` and publishes them (seam A).  (Returns
+  // true: no wait in it can give up.)
   auto lookahead = [&](const f32x4 (&xv)[kResTiles][2], int par, int step, unsigned mult) -> bool {
     RES_IDX();
     f32x4 z = zv;
@@ -429,35 +399,42 @@ __global__ void __launch_bounds__(kResThreads) resident_epoch_kernel(ResArgs a) 
     }
     red[r * 64 + lane] = z;   // z[j] = partial(m = 4 lq + j, n = n0 + li)
     __syncthreads();
-    float own = 0.f;
+    // every column group publishes its partial (group 0's with b1 added: it holds the bias);
+    // the row block's LAST arriver (the returning counter add tells it) sums the ngrp partials
+    // in group order, applies ReLU and dropout (the consuming step's seed), publishes h1 rows
+    // [n0, n0 + 16) and arrives at seam A.  No workgroup waits: a fixed reducer (group 0)
+    // polled for the other groups, 0.5-1 us of the step.
     if (tid < 256) {
       const int m = tid >> 4, nn = tid & 15;
+      float own = 0.f;
 #pragma unroll
       for (int ww = 0; ww < NW; ++ww) own += red[ww * 64 + 16 * (m >> 2) + nn][m & 3];
-      if (grp != 0 && m < M && n0 + nn < N1) hst1(rLA, ((((par * a.ngrp + grp) * 16) + m) * N1p + n0 + nn) * 4, own);
+      if (grp == 0) own += sb1[nn];
+      if (m < M && n0 + nn < N1) hst1(rLA, ((((par * a.ngrp + grp) * 16) + m) * N1p + n0 + nn) * 4, own);
     }
-    if (grp != 0) {
-      arrive_rb(a.cnt, rb);          // this column group's partial is published to the row block
-      return true;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned old = __hip_atomic_fetch_add(rb_counter(a.cnt, rb), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *s_ok = (old == (unsigned)a.ngrp * mult - 1u) ? 1 : 0;
     }
-    // group 0: wait for the row block's other column groups, sum the partials in group order,
-    // bias, ReLU, dropout (the consuming step's seed) -> h1 rows [n0, n0 + 16) -> seam A
-    if (!rb_wait(a, rb, (unsigned)(a.ngrp - 1) * mult, s_ok)) return false;
+    __syncthreads();
+    if (*s_ok == 0) return true;
     if (tid < 256) {
       const int m = tid >> 4, nn = tid & 15, n = n0 + nn;
       if (m < M && n < N1) {
         float parts[kResGroups];
 #pragma unroll
-        for (int g = 1; g < kResGroups; ++g)
+        for (int g = 0; g < kResGroups; ++g)
           parts[g] = g < a.ngrp ? hld1(rLA, ((((par * a.ngrp + g) * 16) + m) * N1p + n) * 4) : 0.f;
-        float v = own;
+        float v = parts[0];
 #pragma unroll
         for (int g = 1; g < kResGroups; ++g) v += parts[g];
-        v = drop_relu(v + sb1[nn], a.seeds[4 * step], a.seeds[4 * step + 1], m, a.col_off1 + n, a.thr1, a.dsc1);
+        v = drop_relu(v, a.seeds[4 * step], a.seeds[4 * step + 1], m, a.col_off1 + n, a.thr1, a.dsc1);
         hst1(rH1, ((par * 16 + m) * N1p + n) * 4, v);
       }
     }
-    arrive(a.cnt, 0, w);
+    arrive(a.cnt, 0, rb);            // seam A's shards count row blocks (rb % 8)
     return true;
   };
   // W2 after a step, in the fc1 tiles' layout W2B[par][rb(j)][w][j % 16][ii] (this workgroup's
@@ -504,7 +481,7 @@ __global__ void __launch_bounds__(kResThreads) resident_epoch_kernel(ResArgs a) 
     RES_MARK(1);
     {
       RES_IDX();
-      // h1_t rows as published by each row block's group-0 workgroup (rows >= M are zero)
+      // h1_t rows as published by each row block's last-arriving column group (rows >= M are zero)
       const int q4 = N1p >> 2;
       constexpr int U = (16 * kSh1Max / 4 + kResThreads - 1) / kResThreads;   // float4 per thread
       f32x4 v[U];

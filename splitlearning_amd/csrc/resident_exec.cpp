@@ -113,7 +113,7 @@ class ResidentEpoch {
     // arrivals per counter shard (producer workgroup w lands on shard w % 8)
     std::vector<int> sn(sl::kResSeams * 8, 0);
     for (int w = 0; w < a.G; ++w) {
-      if (w < a.nfc1 && w % a.ngrp == 0) ++sn[0 * 8 + (w & 7)];   // row blocks' group-0 workgroups
+      if (w < a.nrb) ++sn[0 * 8 + (w & 7)];   // seam A: one arrival per row block (its last column group)
       ++sn[1 * 8 + (w & 7)];
       if (w < a.M) ++sn[2 * 8 + (w & 7)];
       ++sn[3 * 8 + (w & 7)];
