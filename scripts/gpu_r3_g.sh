@@ -1,13 +1,20 @@
 #!/bin/bash
-# Round 3, call G: vanilla fc2/fc3 update overlapped with the Alice's step (side stream) —
-# bitwise tests against the Python loop, and the vanilla ws = 2 bench with / without it.
+# Round 3, call G (final, after the resident changes): the GEMM routing bench, the whole GPU suite, the default bench, and its rocprofv3 kernel table.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export PYTHONUNBUFFERED=1
+export TMPDIR=/tmp
 T="timeout -k 10"
-$T 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_split_native_gpu.py tests/test_kernels_gpu.py -k "split or wgrad" > gpurun_out/r3g_tests.log 2>&1 || { tail -60 gpurun_out/r3g_tests.log; exit 1; }
-tail -4 gpurun_out/r3g_tests.log
-for ov in 1 0 1 0; do
-  SL_SPLIT_OVERLAP=$ov $T 300 python -u bench.py --mode vanilla --world_size 2 --steps 2 --warmup 1 --json_out gpurun_out/r3g_bench_vanilla_ov$ov.json > gpurun_out/r3g_bench_vanilla_ov$ov.log 2>&1 || { tail -20 gpurun_out/r3g_bench_vanilla_ov$ov.log; exit 1; }
-  python -c "import json;d=json.load(open('gpurun_out/r3g_bench_vanilla_ov$ov.json'));print('vanilla overlap=$ov', d['value'], d['config']['phase_seconds'])"
-done
+$T 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r3g_suite.log 2>&1
+rc=$?
+tail -3 gpurun_out/r3g_suite.log
+[ $rc -eq 0 ] || { grep -E "FAILED|Error|error" gpurun_out/r3g_suite.log | head -20; tail -40 gpurun_out/r3g_suite.log; exit 1; }
+$T 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/r3g_smoke.log 2>&1 || { tail -20 gpurun_out/r3g_smoke.log; exit 1; }
+tail -1 gpurun_out/r3g_smoke.log
+$T 300 python -u bench.py > gpurun_out/r3g_bench.json 2> gpurun_out/r3g_bench.err || { tail -20 gpurun_out/r3g_bench.err; exit 1; }
+cat gpurun_out/r3g_bench.json
+$T 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r3g_prof -o prof -- python3 bench.py --steps 1 --warmup 1 > gpurun_out/r3g_prof.log 2>&1 || { tail -20 gpurun_out/r3g_prof.log; exit 1; }
+f=$(find gpurun_out/r3g_prof -name '*kernel_stats.csv' | sort | tail -1)
+cp "$f" gpurun_out/r3g_bench_kernel_stats.csv
+find gpurun_out/r3g_prof -name '*.csv' -delete
+python scripts/kstats.py gpurun_out/r3g_bench_kernel_stats.csv | head -24
