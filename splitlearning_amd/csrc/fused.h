@@ -36,6 +36,7 @@ struct WgGroup {
   int grid2d;           // 2-D grid (set by wgrad_group: when few of its workgroups are empty)
   int wt;               // write-through (sc1) W/m/v stores (set by wgrad_group)
   int bf16;             // bf16 compute: dZ / A / look-ahead operands rounded to bf16 (set by wgrad_group)
+  int afirst;           // load the first chunk's A / dZ before W / m / v (set by wgrad_group)
 };
 
 int head3_slices(int N2);

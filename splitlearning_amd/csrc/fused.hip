@@ -346,6 +346,15 @@ wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
   const bool act = (n < L.N) && (k < L.K);
   const f32x4 zv = {0.f, 0.f, 0.f, 0.f};
   const int64_t off = (int64_t)n * L.ldw + k;
+  // A / dZ of the first 16-row chunk ahead of W / m / v (grp.afirst, TP shards): a wave's
+  // loads complete in order, so staged behind the state stream they held the LDS staging and
+  // the dW product until W / m / v had arrived
+  f32x4 av0 = zv;
+  float dzv0 = 0.f;
+  if (grp.afirst) {
+    if (r < M && k < L.K) av0 = *reinterpret_cast<const f32x4*>(L.A + (int64_t)r * L.lda + k);
+    if (tid < 256 && (tid >> 4) < M && n0 + (tid & 15) < L.N) dzv0 = L.dz[(int64_t)(tid >> 4) * L.ldz + n0 + (tid & 15)];
+  }
   f32x4 p = zv, q0 = zv, q1 = zv;
   if (act) {
     p = *reinterpret_cast<const f32x4*>(L.W + off);
@@ -369,12 +378,15 @@ wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
     if (mc) __syncthreads();
     {
       const int mm = mc + r;
-      const f32x4 av = (mm < M && k < L.K) ? *reinterpret_cast<const f32x4*>(L.A + (int64_t)mm * L.lda + k) : zv;
+      const bool pre = mc == 0 && grp.afirst;
+      const f32x4 av = pre ? av0
+                           : ((mm < M && k < L.K) ? *reinterpret_cast<const f32x4*>(L.A + (int64_t)mm * L.lda + k) : zv);
       sa[r][lane] = grp.bf16 ? bfr4(av) : av;
       if (tid < 256) {
         const int mr = mc + (tid >> 4), nn = n0 + (tid & 15);
         float v = 0.f;
-        if (mr < M && nn < L.N) v = L.dz[(int64_t)mr * L.ldz + nn];
+        if (pre) v = dzv0;
+        else if (mr < M && nn < L.N) v = L.dz[(int64_t)mr * L.ldz + nn];
         sdz[tid >> 4][tid & 15] = grp.bf16 ? bfr(v) : v;
       }
     }
@@ -552,6 +564,11 @@ hipError_t wgrad_group(const WgGroup& g, int M, SlOpt o, hipStream_t st) {
   const int64_t g2 = (int64_t)grid.x * grid.y;
   gg.grid2d = (g2 - wb) * 10 < g2 ? 1 : 0;
   const dim3 gr = gg.grid2d ? grid : grid1;
+  // the first chunk's A / dZ loads ahead of W / m / v on a TP shard (1-D grid), whose state
+  // streams from the Infinity Cache: native executor, us per server step, TP = 4 68.8 -> 66.2,
+  // TP = 8 52.5 -> 51.2; at TP = 1 (2-D grid, HBM-bound) 170.9 vs 171.2, so not there
+  // (profiles/r3w_wgrad_a_first_ab.txt)
+  gg.afirst = gg.grid2d ? 0 : 1;
   // bf16 compute: a separate instantiation (dW on bf16 MFMA), so the fp32 kernels' registers
   // and schedule are untouched
 #define SL_WG_LAUNCH(A, F)                                                          \
