@@ -1,19 +1,15 @@
 #!/bin/bash
-# Round 3, call H: concat native-vs-Python bitwise test; rocprofv3 kernel tables of the native
-# server step at TP = 1 and a TP = 8 shard (1-rank peer-mapped all-reduce stand-in).
+# Round 3, call H: server-head kernels with the consumed-first loads (variant 6 = 0, new)
+# against W3 first (6 = 1), per server step; the head / executor tests.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export PYTHONUNBUFFERED=1
-export TMPDIR=/tmp
 T="timeout -k 10"
-$T 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_split_native_gpu.py > gpurun_out/r3h_tests.log 2>&1 || { tail -60 gpurun_out/r3h_tests.log; exit 1; }
-tail -4 gpurun_out/r3h_tests.log
-for tp in 1 8; do
-  $T 300 python -u scripts/prof_step.py --path native --tp $tp --allreduce ipc --steps 640 --time > gpurun_out/r3h_step_tp$tp.txt 2>&1 || { tail -20 gpurun_out/r3h_step_tp$tp.txt; exit 1; }
-  grep us_per_step gpurun_out/r3h_step_tp$tp.txt
-  $T 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r3h_prof_tp$tp -o prof -- python3 scripts/prof_step.py --path native --tp $tp --allreduce ipc --steps 640 > gpurun_out/r3h_prof_tp$tp.log 2>&1 || { tail -20 gpurun_out/r3h_prof_tp$tp.log; exit 1; }
-  f=$(find gpurun_out/r3h_prof_tp$tp -name '*kernel_stats.csv' | sort | tail -1)
-  cp "$f" gpurun_out/r3h_tp${tp}_kernel_stats.csv
-  find gpurun_out/r3h_prof_tp$tp -name '*.csv' -delete
-  echo "== TP $tp"; python scripts/kstats.py gpurun_out/r3h_tp${tp}_kernel_stats.csv
-done
+$T 400 python -u scripts/native_ab.py --tp 1 8 --variants 6=1 6=0 --allreduce ipc --rounds 5 --epochs 3 > gpurun_out/r3h_head_order_ab.txt 2>&1
+rc=$?
+grep -v amdgpu.ids gpurun_out/r3h_head_order_ab.txt
+[ $rc -eq 0 ] || exit $rc
+$T 400 python -u -m pytest tests/test_graphs_gpu.py tests/test_golden_gpu.py tests/test_golden_modes_gpu.py tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/r3h_tests.txt 2>&1
+rc=$?
+tail -3 gpurun_out/r3h_tests.txt
+exit $rc
