@@ -77,15 +77,6 @@ def _phase_kind(mode: str, name: str):
     return None
 
 
-def _chain_label(sess):
-    """Bob's launch-per-stage executor on this rank: with the persistent chain launch
-    (csrc/chain.hip) when its last epoch's executor had it set up."""
-    nat = getattr(getattr(sess, "tail", None), "_native", None)
-    if nat is not None and nat[2].chain_enabled():
-        return "launch_per_stage+chain"
-    return "launch_per_stage"
-
-
 def _ipc_status():
     """The peer-mapped TP all-reduce's set-up outcome on this process (parallel/rccl.py)."""
     from splitlearning_amd.parallel.rccl import IPC_STATUS
@@ -116,9 +107,6 @@ def main(argv=None):
     ap.add_argument("--resident", choices=("auto", "off"), default="auto",
                     help="SISA server epochs of a narrow Bob shard (TP >= 7) on the register-resident "
                          "persistent executor (csrc/resident.hip) after its cross-rank self-test")
-    ap.add_argument("--server_chain", choices=("off", "on"), default="off",
-                    help="launch-per-stage server steps: forward / backward as one persistent launch "
-                         "(csrc/chain.hip, opt-in) or six kernels")
     ap.add_argument("--tp_allreduce", choices=("auto", "rccl"), default="auto",
                     help="Bob's TP all-reduce: peer-mapped one-kernel path when it passes set-up (auto) or RCCL")
     ap.add_argument("--act_dtype", choices=("fp32", "bf16"), default="fp32")
@@ -173,7 +161,7 @@ def main(argv=None):
         "--batch_size", str(a.batch_size), "--partition_alpha", str(a.partition_alpha),
         "--server_epochs", str(a.server_epochs), "--seed", str(a.seed), "--num_samples", str(a.num_samples),
         "--kernels", a.kernels, "--graphs", a.graphs, "--act_dtype", a.act_dtype, "--dtype", a.dtype, "--no_tqdm",
-        "--tp_allreduce", a.tp_allreduce, "--resident", a.resident, "--server_chain", a.server_chain,
+        "--tp_allreduce", a.tp_allreduce, "--resident", a.resident,
         "--log_dir", log_dir, "--watchdog", "off"]
     if a.mode == "concat" and a.concat_unlearn:
         argv_s.append("--concat_unlearn")
@@ -293,7 +281,9 @@ def main(argv=None):
                 # Bob's server-epoch executor: the register-resident persistent launch (a shard
                 # narrow enough to keep on-chip, its self-test passed) or the launch-per-stage one
                 "server_executor": ("resident" if getattr(sess, "_resident_ok", False) else
-                                    _chain_label(sess)) if sargs.mode in ("sisa", "control") else None,
+                                    "launch_per_stage") if sargs.mode in ("sisa", "control") else None,
+                # why: adopted, or the fit / self-test outcome that kept launch-per-stage
+                "server_executor_reason": (getattr(sess, "resident_status", None) or {}).get("reason"),
                 "calib": calib,
             },
         }

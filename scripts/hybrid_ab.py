@@ -1,0 +1,115 @@
+"""Server step time of the hybrid persistent epoch (`_C.HybridEpoch`, csrc/hybrid.hip) against
+the launch-per-stage native executor (`_C.ServerEpoch`, csrc/engine.cpp) on the same shard of
+model2_sisa, one MI355X.
+
+TP > 1 runs shard 0 of the full model with a 1-rank peer-mapped region standing in for the
+other ranks (the exchange's stores and tag polls run, there is no peer to wait for).
+Interleaved rounds, us per server step over one client epoch of `--steps` batches of 16 (a
+ws = 2 SISA client holds 3,500 batches).  `--trace` prints the hybrid launch's phase stamps.
+
+    python scripts/hybrid_ab.py --tp 1 2 4 --steps 500 --rounds 3
+"""
+import argparse
+import os
+import statistics
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from splitlearning_amd import ops  # noqa: E402
+from splitlearning_amd.engine import OptSlot, TailEngine, adam  # noqa: E402
+from splitlearning_amd.models import ServerTailSisa, sisa_server_spec  # noqa: E402
+from splitlearning_amd.ops import hip_ops as H  # noqa: E402
+
+PHASES = ["F wait", "F h1 load+mma", "H wait", "H+L", "S wait", "S", "H2 wait", "H2", "B wait", "B dgrad",
+          "W2 update", "U wait P", "U dz1+stream", "flush", "end"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tp", type=int, nargs="+", default=[1])
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--epochs", type=int, default=1)
+    ap.add_argument("--trace", action="store_true")
+    ap.add_argument("--only", choices=("both", "hybrid", "native"), default="both")
+    a = ap.parse_args()
+    C = H.C()
+    dev = torch.device("cuda", 0)
+    ops.set_backend("hip")
+    B = 16
+    for tp in a.tp:
+        torch.manual_seed(0)
+        n = B * a.steps
+        acts = torch.rand(n, 5408, device=dev) * 20
+        labels = torch.randint(0, 100, (n,), device=dev)
+        ar = None
+        if tp > 1:
+            from splitlearning_amd.parallel.rccl import ipc_allreduce
+            ipc = C.IpcAllReduce(1, 0, 64 * 1024)
+            ipc.open([ipc.handle()])
+            ar = ipc_allreduce(ipc)
+        kinds = ("native", "hybrid") if a.only == "both" else (a.only,)
+        mods = {}
+        for kind in kinds:
+            torch.manual_seed(1)
+            tail = TailEngine(ServerTailSisa(), sisa_server_spec(), dev, tp_rank=0, tp_size=tp, allreduce=ar,
+                              ws_tag="#" + kind)
+            slot = OptSlot(adam(1e-3, 1e-5))
+            mods[kind] = (tail, slot)
+        if "hybrid" in mods:
+            tail, slot = mods["hybrid"]
+            if not tail.hybrid_ok(slot, B):
+                print(f"tp={tp}: hybrid epoch does not fit: {tail._hybrid_executor(slot, B).why()}", flush=True)
+                continue
+
+        def run(kind, k):
+            tail, slot = mods[kind]
+            for _ in range(k):
+                if kind == "native":
+                    tail.lookahead_prologue(acts[:B])
+                    tail.run_native_epoch(acts, labels, slot, B, True)
+                else:
+                    tail.run_hybrid_epoch(acts, labels, slot, B)
+
+        res = {k: [] for k in mods}
+        for _ in range(a.rounds):
+            for kind in mods:
+                run(kind, 1)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                run(kind, a.epochs)
+                torch.cuda.synchronize()
+                res[kind].append((time.perf_counter() - t0) / (a.epochs * a.steps) * 1e6)
+        for kind, xs in res.items():
+            print(f"tp={tp} {kind:8s} median {statistics.median(xs):7.2f} us/step  min {min(xs):7.2f}  "
+                  f"({' '.join(f'{x:.1f}' for x in xs)})", flush=True)
+        if a.trace and "hybrid" in mods:
+            tail, slot = mods["hybrid"]
+            ex = tail._hybrid_executor(slot, B)
+            ts = 64
+            tr = torch.zeros(2, ts, 16, dtype=torch.int64, device=dev)
+            loss = torch.empty(n, device=dev)
+            ex.run(acts, labels, loss, tail.seed_base, tail.fwd_count, slot.t, tr)
+            torch.cuda.synchronize()
+            khz = 100000.0
+            t = tr.cpu().double()
+            for wgi, name in ((0, "wg 0"), (1, "wg G-1")):
+                d = (t[wgi, 8:ts - 1, 1:] - t[wgi, 8:ts - 1, :-1]) / khz * 1e3
+                valid = (t[wgi, 8:ts - 1, 1:] > 0) & (t[wgi, 8:ts - 1, :-1] > 0)
+                parts = []
+                for k in range(15):
+                    v = d[:, k][valid[:, k]]
+                    if v.numel():
+                        parts.append(f"{PHASES[k]} {v.mean().item():.2f}")
+                step = (t[wgi, 9:ts - 1, 0] - t[wgi, 8:ts - 2, 0]) / khz * 1e3
+                print(f"tp={tp} trace {name}: step {step.mean().item():.2f} us | " + ", ".join(parts), flush=True)
+        del mods, acts
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

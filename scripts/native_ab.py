@@ -84,14 +84,9 @@ def main():
             for v in a.variants:
                 for s in slots:
                     C.set_variant(s, 0)
-                ch = bool(parse(v).get("chain", 0))
-                if getattr(tail, "server_chain", False) != ch or getattr(tail, "_native", None) is None:
-                    tail.server_chain = ch
-                    tail._native = None           # rebuilt with / without the chain launch
+                if getattr(tail, "_native", None) is None:
                     pre = False
                 for s, val in parse(v).items():
-                    if s == "chain":
-                        continue
                     if s == "fences":
                         if ipc is not None:
                             ipc.set_fences(bool(val))

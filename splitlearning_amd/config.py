@@ -132,11 +132,6 @@ def build_parser() -> argparse.ArgumentParser:
                         "held on-chip (csrc/resident.hip); 'auto' uses it where it fits and, "
                         "tensor-parallel, after a cross-rank self-test passed; 'off' = the "
                         "launch-per-stage executor")
-    g.add_argument("--server_chain", choices=("off", "on"), default="off",
-                   help="'on': the launch-per-stage server step's forward / backward (fc1 epilogue, "
-                        "fc2, head, fc2 dgrad) as ONE persistent launch with in-launch hand-offs "
-                        "(csrc/chain.hip) where the shapes fit; measured 0.6-6.6 us per step slower "
-                        "than the six kernels except at TP = 2 (docs/PERF.md), so 'off' by default")
     g.add_argument("--tp_allreduce", choices=("auto", "rccl"), default="auto",
                    help="Bob's per-step TP all-reduce: 'auto' = one kernel over peer-mapped HBM "
                         "(csrc/ipc_ar.h) when every Bob rank sets it up and passes its self-test, "

@@ -141,6 +141,8 @@ void sl_register_comm(py::module& m) {
       .def("host_error", &sl::IpcAllReduce::host_error)
       .def("set_fences", &sl::IpcAllReduce::set_fences)
       .def("set_timeout_s", &sl::IpcAllReduce::set_timeout_s)
+      .def("rearm", &sl::IpcAllReduce::rearm, py::arg("gen"))
+      .def_property_readonly("generation", &sl::IpcAllReduce::generation)
       .def_property_readonly("timeout_s", &sl::IpcAllReduce::timeout_s)
       .def_property_readonly("cap", &sl::IpcAllReduce::cap)
       .def_property_readonly("rank", &sl::IpcAllReduce::rank)

@@ -25,7 +25,6 @@
 #include <algorithm>
 #include <string>
 
-#include "chain.h"
 #include "comm.h"
 #include "common.h"
 #include "fused.h"
@@ -132,14 +131,7 @@ class ServerEpoch {
     TORCH_CHECK(dlog_.numel() >= (int64_t)B_ * L_[2].N, "dlog");
     TORCH_CHECK(p2ws_.numel() >= (int64_t)16 * B_ * L_[1].N, "fc2 slab workspace");
     TORCH_CHECK(headws_.numel() >= (int64_t)sl::head3_slices(L_[1].N) * B_ * L_[2].N, "head workspace");
-    // chain: the step's forward / backward between two wgrad launches as one persistent
-    // launch (csrc/chain.hip) instead of six kernels, where the shapes allow it
-    if (cfg.contains("chain") && cfg["chain"].cast<bool>()) setup_chain(cfg);
   }
-
-  // whether the persistent chain launch is set up for this executor (and why not)
-  bool chain_enabled() const { return chain_; }
-  std::string chain_why() const { return chain_why_; }
 
   // One epoch over acts [n, K1] / labels [n] in batches of B.  `pre`: fc1's product for the
   // first batch is pending in pn (look-ahead prologue / previous step).  Returns the
@@ -157,12 +149,6 @@ class ServerEpoch {
     }
     const int64_t n = acts.size(0);
     const sl::IpcAllReduce* ipc = row2_ ? ipc_obj() : nullptr;
-    bool chained = false;
-    if (chain_) {
-      // the chain launches' counters count up from zero over this epoch
-      ck(hipMemsetAsync(ch_cnt_.data_ptr<int>(), 0, ch_cnt_.numel() * sizeof(int), stream()), "chain counters");
-      ch_gen_ = 0;
-    }
     for (int64_t s = 0, i = 0; s < n; s += B_, ++i) {
       // a peer-mapped wait that timed out (stalled / dead peer) raises the error word and
       // every later wait gives up at once; its host-pinned mirror is read here without a
@@ -171,23 +157,12 @@ class ServerEpoch {
         TORCH_CHECK(false, "peer-mapped TP all-reduce: a flag wait timed out on this rank (a peer stalled or "
                            "died); aborting the server epoch at step ", i);
       Step st = begin(acts, labels, s, seed_base, fwd_count, t, pre, lookahead);
-      if (chain_ok(st)) {
-        chain_step(st, loss_rows);
-        chained = true;
-        wgrad(st);
-      } else {
-        forward_product(st);
-        if (row2_ && !ipc_head(st.M)) allreduce(p2ws_.data_ptr<float>(), (size_t)st.M * L_[1].N);
-        finish(st, loss_rows);
-      }
+      forward_product(st);
+      if (row2_ && !ipc_head(st.M)) allreduce(p2ws_.data_ptr<float>(), (size_t)st.M * L_[1].N);
+      finish(st, loss_rows);
       fwd_count = st.fwd_count;
       t = st.t;
       pre = st.next_pre;
-    }
-    if (chained) {
-      const int e = ch_err_.item<int>();   // one sync per epoch
-      TORCH_CHECK(e == 0, "server epoch: a wait of the persistent chain launch gave up (error ", e,
-                  "; 2 = timeout, 4 = tensor-parallel exchange)");
     }
     return py::make_tuple(fwd_count, t, pre);
   }
@@ -358,106 +333,6 @@ class ServerEpoch {
     st.next_pre = next_full;
   }
 
-  // ---- the persistent chain launch
-  void setup_chain(const py::dict& cfg) {
-    const int N1 = L_[0].N, N2 = L_[1].N, C = L_[2].N;
-    const at::Device dev = L_[0].W.device();
-    const int dv = dev.index();
-    int khz = 0;
-    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dv) != hipSuccess || khz <= 0) khz = 100000;
-    const double tmo = cfg.contains("chain_timeout_s") ? cfg["chain_timeout_s"].cast<double>() : 10.0;
-    ch_timeout_ = (int64_t)(tmo * 1000.0 * khz);
-    const int resident = sl::chain_max_workgroups(dv);
-    const int want = cfg.contains("chain_workgroups") ? cfg["chain_workgroups"].cast<int>() : 0;
-    const int G = std::min(want > 0 ? want : 256, std::min(256, resident));
-    sl::ChainArgs& a = ch_;
-    a = sl::ChainArgs{};
-    a.M = std::min(B_, 16);
-    a.N1 = N1;
-    a.N2 = N2;
-    a.C = C;
-    a.C4 = (C + 3) & ~3;
-    a.G = G;
-    a.NCB = std::min(sl::kChMaxCB, G / sl::kChRB);
-    a.HW = N2 / 4;
-    a.S1 = (L_[0].K + 255) / 256;
-    a.slab = (int64_t)a.M * N1;
-    a.pn = pn_.data_ptr<float>();
-    const sl::IpcAllReduce* ipc = row2_ ? ipc_obj() : nullptr;
-    if (ipc != nullptr) {
-      a.ipc.T = ipc->size();
-      a.ipc.cap = ipc->cap();
-    }
-    chain_why_ = B_ > 16 ? "batch > 16" : (G_ > 1 ? "grouped cross-entropy" : "");
-    if (chain_why_.empty() && row2_ && ipc == nullptr) chain_why_ = "row-parallel fc2 without the peer-mapped region";
-    if (chain_why_.empty()) chain_why_ = sl::chain_check(a);
-    a.ipc = sl::IpcStep{};
-    if (!chain_why_.empty()) return;
-    auto opt = at::TensorOptions().dtype(at::kFloat).device(dev);
-    ch_fp_ = at::zeros({(int64_t)a.NCB * 16 * N2}, opt);
-    ch_lp_ = at::zeros({(int64_t)a.HW * 16 * a.C4}, opt);
-    ch_dl_ = at::zeros({16LL * a.C4}, opt);
-    ch_dp_ = at::zeros({(int64_t)sl::kChRB * 16 * N1}, opt);
-    ch_cnt_ = at::zeros({(int64_t)sl::kChCounters * sl::kChStride}, opt.dtype(at::kInt));
-    ch_err_ = at::zeros({1}, opt.dtype(at::kInt));
-    std::vector<int> sn(sl::kChSeams * 8, 0);
-    for (int w = 0; w < G; ++w) {
-      if (w < sl::kChRB * a.NCB) ++sn[0 * 8 + (w & 7)];
-      if (w < a.HW) ++sn[1 * 8 + (w & 7)];
-      if (w < a.M) ++sn[2 * 8 + (w & 7)];
-      if (w < a.HW) ++sn[3 * 8 + (w & 7)];
-    }
-    ch_shard_ = at::from_blob(sn.data(), {(int64_t)sn.size()}, at::TensorOptions().dtype(at::kInt)).to(dev);
-    a.FP = ch_fp_.data_ptr<float>();
-    a.LP = ch_lp_.data_ptr<float>();
-    a.DL = ch_dl_.data_ptr<float>();
-    a.DP = ch_dp_.data_ptr<float>();
-    a.cnt = reinterpret_cast<unsigned*>(ch_cnt_.data_ptr<int>());
-    a.shard_n = ch_shard_.data_ptr<int>();
-    a.err = ch_err_.data_ptr<int>();
-    a.timeout = ch_timeout_;
-    if (cfg.contains("chain_trace") && cfg["chain_trace"].cast<bool>()) {
-      ch_trace_ = at::zeros({32}, opt.dtype(at::kLong));
-      a.trace = ch_trace_.data_ptr<int64_t>();
-    }
-    chain_ = true;
-  }
-
-  // the last chain launch's phase stamps (wall clock) of workgroups 0 and G - 1, [2][16]
-  at::Tensor chain_trace() const { return ch_trace_.defined() ? ch_trace_.clone() : at::Tensor(); }
-
-  // a step the chain launch can run: the look-ahead product is pending, fp32 compute, a full
-  // batch of the configured rows, not under graph capture (the launch generation is an argument)
-  bool chain_ok(const Step& st) const {
-    if (!chain_ || !st.pre || st.M != ch_.M || sl::g_bf16 != 0) return false;
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(stream(), &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
-    return true;
-  }
-
-  void chain_step(Step& st, at::Tensor& loss_rows) {
-    sl::ChainArgs a = ch_;
-    const int M = st.M;
-    a.e1 = sl::make_epi_raw(L_[0].b.data_ptr<float>(), true, p1_, st.sd0, col_off1_, nullptr);
-    a.s1 = p1_ > 0 ? (float)(1.0 / (1.0 - p1_)) : 1.f;
-    a.W2 = L_[1].W.data_ptr<float>();
-    a.e2 = sl::make_epi_raw(L_[1].b.data_ptr<float>(), true, p2_, st.sd1, 0, nullptr);
-    a.W3 = L_[2].W.data_ptr<float>();
-    a.b3 = L_[2].b.data_ptr<float>();
-    a.Y = st.labels->data_ptr<int64_t>() + st.s;
-    a.ignore = -100;
-    a.ce_scale = (float)(1.0 / M);
-    a.h1 = h1_.data_ptr<float>();
-    a.h2 = h2_.data_ptr<float>();
-    a.dlog = dlog_.data_ptr<float>();
-    a.dz2 = dz2_.data_ptr<float>();
-    a.dz1 = dz1_.data_ptr<float>();
-    a.loss = loss_rows.data_ptr<float>() + st.s;
-    a.gen = ++ch_gen_;
-    if (row2_) a.ipc = ipc_obj()->begin_step();
-    ck(sl::chain_step_launch(a, stream()), "chain step");
-  }
-
   // the peer-mapped all-reduce in use for this executor (attached to the RCCL communicator
   // or given bare), or null
   sl::IpcAllReduce* ipc_obj() const { return comm_ != nullptr ? comm_->ipc() : ipc_; }
@@ -510,12 +385,6 @@ class ServerEpoch {
   int G_ = 1;
   const float* gscale_ = nullptr;
   at::Tensor pn_, p2ws_, fwdws_, dgws_, headws_, h1_, h2_, dz1_, dz2_, dlog_;
-  bool chain_ = false;
-  std::string chain_why_ = "off";
-  sl::ChainArgs ch_{};
-  unsigned ch_gen_ = 0;
-  int64_t ch_timeout_ = 0;
-  at::Tensor ch_fp_, ch_lp_, ch_dl_, ch_dp_, ch_cnt_, ch_err_, ch_shard_, ch_trace_;
   static hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
 };
 
@@ -567,8 +436,5 @@ void sl_register_engine(py::module& m) {
       .def(py::init<const py::dict&>())
       .def("run", &ServerEpoch::run, py::arg("acts"), py::arg("labels"), py::arg("loss_rows"), py::arg("seed_base"),
            py::arg("fwd_count"), py::arg("t"), py::arg("pre"), py::arg("lookahead"),
-           py::arg("gscale") = py::none())
-      .def("chain_enabled", &ServerEpoch::chain_enabled)
-      .def("chain_why", &ServerEpoch::chain_why)
-      .def("chain_trace", &ServerEpoch::chain_trace);
+           py::arg("gscale") = py::none());
 }

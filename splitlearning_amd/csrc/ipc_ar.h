@@ -174,6 +174,14 @@ class IpcAllReduce {
   void set_timeout_s(double s) { timeout_ = (int64_t)(s * 1000.0 * clock_khz_); }
   double timeout_s() const { return (double)timeout_ / (1000.0 * clock_khz_); }
   void set_fences(bool on) { fences_ = on; }
+  // Re-arm after a failed wait, as one collective step of every rank: the caller has
+  // synchronised its device (no kernel of this rank still reads or writes the region) and the
+  // ranks have agreed `gen` = the largest generation any of them reserved (generation()).
+  // Clears the error word and its host mirror and continues at gen + 1 on every rank: every
+  // flag and tagged granule already in the regions carries a generation <= gen, so none can
+  // satisfy a later wait, and the parities of the two buffers stay in step across ranks.
+  void rearm(uint32_t gen);
+  uint32_t generation() const { return gen_; }
 
  private:
   int nranks_, rank_;

@@ -187,6 +187,15 @@ IpcStep IpcAllReduce::begin_step() {
   return s;
 }
 
+void IpcAllReduce::rearm(uint32_t gen) {
+  if ((int32_t)(gen - gen_) < 0) throw std::runtime_error("IpcAllReduce.rearm: generation behind this rank's");
+  SL_HIP_THROW(hipDeviceSynchronize());
+  SL_HIP_THROW(hipMemset(err_, 0, sizeof(int)));
+  SL_HIP_THROW(hipDeviceSynchronize());
+  __atomic_store_n(herr_, 0, __ATOMIC_RELEASE);
+  gen_ = gen;
+}
+
 int IpcAllReduce::error() const {
   int e = 0;
   SL_HIP_THROW(hipMemcpy(&e, err_, sizeof(int), hipMemcpyDeviceToHost));

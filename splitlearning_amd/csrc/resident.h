@@ -60,6 +60,10 @@ struct ResArgs {
   // trace_steps steps: [2][trace_steps][16] (scripts/resident_trace.py)
   int64_t* trace;
   int trace_steps;
+  // 1: cooperative launch (the runtime refuses a grid the device cannot hold at once); 0: a
+  // plain launch, for ranks that deliberately share one GPU with a partial grid each (the
+  // one-GPU multi-process rehearsal), where the device-wide check does not describe the split
+  int coop;
 };
 
 hipError_t resident_epoch_launch(const ResArgs& a, hipStream_t st);

@@ -90,6 +90,7 @@ class ResidentEpoch {
     // launches share one GPU (the multi-process test, scripts/resident_tp_one_gpu.py)
     const int wg = cfg.contains("workgroups") ? cfg["workgroups"].cast<int>() : 0;
     a.G = wg > 0 ? std::min(wg, std::min(256, cus)) : std::min(256, cus);
+    a.coop = wg > 0 ? 0 : 1;
     a.nrb = (a.N1 + 15) / 16;
     a.ncb = (a.K1 + 255) / 256;
     a.ngrp = (a.ncb + sl::kResTiles - 1) / sl::kResTiles;
@@ -208,7 +209,11 @@ class ResidentEpoch {
       a.trace_steps = (int)(trace->numel() / 32);
     }
     const hipStream_t st = c10::hip::getCurrentHIPStream().stream();
-    TORCH_CHECK(sl::resident_epoch_launch(a, st) == hipSuccess, "resident epoch launch");
+    // the executor's own error word starts clear on every launch: a wait that gave up in an
+    // earlier run (whose exception the caller handled) must not make this launch give up
+    TORCH_CHECK(hipMemsetAsync(a.err, 0, sizeof(int), st) == hipSuccess, "resident error word");
+    const hipError_t le = sl::resident_epoch_launch(a, st);
+    TORCH_CHECK(le == hipSuccess, "resident epoch launch: ", hipGetErrorString(le));
     const int e = err_.item<int>();   // one sync per client epoch
     TORCH_CHECK(e == 0, "resident server epoch: an in-launch wait gave up (error word ", e,
                 "; 2 = a seam timed out, 4 = the peer-mapped fc2 exchange failed)");

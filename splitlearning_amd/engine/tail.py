@@ -400,13 +400,6 @@ class TailEngine:
              "ipc": getattr(self.allreduce, "ipc", None) if L2.style == "row" else None, "B": B,
              "groups": self.ce_groups,
              "emulate_tp": L2.style == "row" and self.allreduce is None,
-             # the step's forward / backward as one persistent launch (csrc/chain.hip) where it
-             # fits (opt-in: slower than the six kernels except at TP = 2, docs/PERF.md); off:
-             # the six-kernel chain, bitwise the Python path's launches
-             "chain": bool(getattr(self, "server_chain", False)),
-             "chain_timeout_s": float(getattr(self, "chain_timeout_s", 10.0)),
-             "chain_workgroups": int(getattr(self, "chain_workgroups", 0)),
-             "chain_trace": bool(getattr(self, "chain_trace", False)),
              "pn": self.lookahead_slabs(B),
              "p2ws": ops._workspace(dev, 16 * B * N2, "fc2p" + tg),
              "fwdws": ops._workspace(dev, 16 * B * nmax, "fwd" + tg),
@@ -472,6 +465,61 @@ class TailEngine:
              "workgroups": int(getattr(self, "resident_workgroups", 0))}
         ex = self.ops.C().ResidentEpoch(d)
         self._resident = (slot, B, ex, d)
+        return ex
+
+    # ------------------------------------------------------------------ hybrid epoch
+    def hybrid_ok(self, slot: OptSlot, B: int) -> bool:
+        """Whether `run_hybrid_epoch` can drive this shard (`_C.HybridEpoch`, csrc/hybrid.hip):
+        the fused 3-layer tail with one cross-entropy group, <= 16 rows per step, a WIDE shard
+        (fc1 shard <= 5120 rows in 8 x 32 fc2 tiles of <= 128 x 160, fc2 <= 1024 rows, <= 128
+        classes) and, tensor-parallel, the peer-mapped region for the in-launch exchange."""
+        if (self.device.type != "cuda" or not self.fused3_ok() or not hasattr(self.ops, "C")
+                or self.ce_groups != 1 or not 1 <= B <= 16):
+            return False
+        if self.layers[1].style == "row" and getattr(self.allreduce, "ipc", None) is None:
+            return False
+        return self._hybrid_executor(slot, B).ok()
+
+    def run_hybrid_epoch(self, acts: torch.Tensor, labels: torch.Tensor, slot: OptSlot, B: int) -> torch.Tensor:
+        """One epoch over `acts` / `labels` with every full batch in ONE persistent launch that
+        keeps fc2 / fc3 and the biases on-chip and streams fc1 (csrc/hybrid.hip); a trailing
+        partial batch runs on the launch-per-stage executor.  Same step / seed / Adam-count
+        bookkeeping as `run_native_epoch`; the sums run in another order, so results agree
+        with it to fp32 rounding, not bitwise.  Returns the per-row losses."""
+        ex = self._hybrid_executor(slot, B)
+        n = acts.shape[0]
+        loss = torch.empty(n, device=self.device)
+        fc, t, done = ex.run(acts, labels, loss, self.seed_base, self.fwd_count, slot.t)
+        self.fwd_count, slot.t = int(fc), int(t)
+        self._pre = None
+        if done < n:
+            rest_a, rest_y = acts[done:], labels[done:]
+            if self.native_epoch_ok(B):
+                loss[done:] = self.run_native_epoch(rest_a, rest_y, slot, B, False)
+            else:
+                loss[done:], _ = self.train_fwd_bwd3(rest_a, rest_y, need_dx=False)
+                self.fused_step(slot)
+        return loss
+
+    def _hybrid_executor(self, slot: OptSlot, B: int):
+        cached = getattr(self, "_hybrid", None)
+        if cached is not None and cached[0] is slot and cached[1] == B:
+            return cached[2]
+        L1, L2, _ = self.layers
+        layers = []
+        for L in self.layers:
+            sw, sb = slot.state(f"{L.spec.name}.weight", L.W), slot.state(f"{L.spec.name}.bias", L.b)
+            layers.append({"W": L.W, "b": L.b, "s0": sw.get("m", sw.get("buf")), "s1": sw.get("v"),
+                           "sb0": sb.get("m", sb.get("buf")), "sb1": sb.get("v")})
+        cfg = slot.cfg
+        d = {"layers": layers, "kind": {"sgd": 1, "adam": 2}[cfg.kind], "lr": cfg.lr, "beta1": cfg.beta1,
+             "beta2": cfg.beta2, "eps": cfg.eps, "wd": cfg.weight_decay, "momentum": cfg.momentum,
+             "p1": L1.spec.dropout, "p2": L2.spec.dropout, "col_off1": L1.col_off, "B": B,
+             "ipc": getattr(self.allreduce, "ipc", None) if L2.style == "row" else None,
+             "timeout_s": float(getattr(self, "resident_timeout_s", 10.0)),
+             "workgroups": int(getattr(self, "resident_workgroups", 0))}
+        ex = self.ops.C().HybridEpoch(d)
+        self._hybrid = (slot, B, ex, d)
         return ex
 
     # ------------------------------------------------------------------ TP emulation

@@ -215,7 +215,6 @@ class Session:
         tp_rank = self.pl.bob_ranks.index(self.rank)
         self.tail = TailEngine(module, spec, self.device, tp_rank, tp_size,
                                allreduce=self.tp_allreduce, seed_base=self.seed)
-        self.tail.server_chain = getattr(self.args, "server_chain", "off") == "on"
 
     def make_bob_module(self, cls, *a):
         # identical init on every TP rank: seed the default generator with the agreed seed

@@ -21,8 +21,6 @@ Phases and their MI355X mapping:
 """
 from __future__ import annotations
 
-import copy
-
 import torch
 
 from ..config import ADAM_WEIGHT_DECAY, CUT_FEATURES
@@ -279,67 +277,16 @@ class SisaSession(Session):
 
     def _decide_resident(self) -> bool:
         """Collective over every rank (Session.__init__): whether Bob's server epochs run on the
-        register-resident executor.  Single shard: it fits.  Tensor-parallel: every Bob rank
-        builds a scratch copy of its shard (same layout, same peer-mapped region, fixed random
-        weights), runs an 8-step resident epoch on synthetic inputs with a 5 s bound on every
-        in-launch wait, and fingerprints the replicated fc3 weight; all ranks adopt the
-        executor only if every Bob rank finished and the fingerprints agree (MIN / MAX
-        all-reduces), otherwise Bob keeps the launch-per-stage executor."""
-        if getattr(self.args, "resident", "auto") == "off" or getattr(self.args, "dtype", "fp32") != "fp32":
-            return False
-        ok, fp = True, None
-        if self.is_bob:
-            tail = self.tail
-            ok = tail.resident_ok(self.bob_slot, self.B)
-            if ok and tail.tp_size > 1:
-                try:
-                    fp = self._resident_probe()
-                except RuntimeError as e:        # a wait gave up or the launch was refused
-                    import warnings
-                    warnings.warn(f"resident server epoch self-test failed: {e}")
-                    ok = False
-        if not self.comm.distributed or self.pl.bob_tp <= 1:
-            if self.comm.distributed:
-                return self._all_true(ok)
-            return ok
-        import torch.distributed as dist
-        dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else "cpu"
-        big = (1 << 62)
-        lo = torch.tensor([fp if fp is not None else big, 1 if ok else 0], dtype=torch.int64, device=dev)
-        hi = torch.tensor([fp if fp is not None else -big], dtype=torch.int64, device=dev)
-        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
-        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
-        return int(lo[1].item()) == 1 and int(lo[0].item()) == int(hi[0].item())
-
-    def _all_true(self, ok: bool) -> bool:
-        import torch.distributed as dist
-        dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else "cpu"
-        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MIN)
-        return int(t.item()) == 1
-
-    def _resident_probe(self) -> int:
-        """One short resident epoch of a scratch shard (see _decide_resident); returns an
-        integer fingerprint of the replicated fc3 weight it produced."""
-        from ..engine import OptSlot, TailEngine
-        tail, dev = self.tail, self.device
-        g = torch.Generator().manual_seed(1234)
-        mod = copy.deepcopy(tail.module)
-        for prm in mod.parameters():
-            prm.data = (torch.rand(prm.shape, generator=g) - 0.5) * 0.05
-        probe = TailEngine(mod, tail.spec, dev, tail.tp_rank, tail.tp_size, allreduce=tail.allreduce,
-                           seed_base=77, ws_tag="#resident_probe")
-        probe.resident_timeout_s = 5.0
-        slot = OptSlot(self.bob_slot.cfg)
-        n = 8 * self.B
-        x = (torch.rand(n, probe.layers[0].W.shape[1], generator=g) * 4).to(dev)
-        y = torch.randint(0, probe.layers[2].W.shape[0], (n,), generator=g).to(dev)
-        loss = probe.run_resident_epoch(x, y, slot, self.B)
-        if not bool(torch.isfinite(loss).all().item()):
-            raise RuntimeError("non-finite losses")
-        bits = probe.layers[2].W.detach().reshape(-1).view(torch.int32).to(torch.int64)
-        mult = torch.arange(1, bits.numel() + 1, device=dev, dtype=torch.int64) % 1000003
-        return int(((bits * mult) % ((1 << 61) - 1)).sum().item())
+        register-resident executor (engine/resident.py decide: fits on one shard; tensor-
+        parallel, every Bob rank's self-test passed with the same replicated fc3, otherwise the
+        peer-mapped region is re-armed on every rank and Bob keeps the launch-per-stage
+        executor).  The outcome and its reason land in `resident_status` (bench JSON)."""
+        from ..engine import resident
+        want = getattr(self.args, "resident", "auto") != "off" and getattr(self.args, "dtype", "fp32") == "fp32"
+        ok, why = resident.decide(self.tail if self.is_bob else None, self.bob_slot if self.is_bob else None,
+                                  self.B, self.comm.distributed, want)
+        self.resident_status = {"adopted": ok, "reason": why}
+        return ok
 
     def server_epoch(self, acts, labels):
         """One pass of Bob's optimizer over one client's cached activations (batch order as

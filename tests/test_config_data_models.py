@@ -29,13 +29,13 @@ def test_reference_flags_and_defaults():
 
 def test_server_executor_flags():
     """Bob's server-epoch executors beyond the reference's flags: the register-resident epoch
-    (default where it fits) and the persistent chain launch (opt-in)."""
+    (default where it fits) or the launch-per-stage executor."""
     a = parse_args(["--sisa"])
-    assert a.resident == "auto" and a.server_chain == "off"
-    a = parse_args(["--sisa", "--resident", "off", "--server_chain", "on"])
-    assert a.resident == "off" and a.server_chain == "on"
+    assert a.resident == "auto"
+    a = parse_args(["--sisa", "--resident", "off"])
+    assert a.resident == "off"
     with pytest.raises(SystemExit):
-        parse_args(["--server_chain", "auto"])
+        parse_args(["--resident", "on"])
 
 
 @pytest.mark.parametrize("argv,msg", [

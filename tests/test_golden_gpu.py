@@ -76,7 +76,6 @@ def test_sisa_server_epoch_matches_torch_adam_every_step(cuda, scale, B):
     base = ServerTailSisa()
     # the native executor, free-running
     nat = TailEngine(copy.deepcopy(base), sisa_server_spec(), cuda, seed_base=seed_base, ws_tag="#nat")
-    nat.server_chain = False     # bitwise the per-step launches below (the chain launch: test_chain_gpu.py)
     nslot = OptSlot(adam(lr, 1e-5))
     nat.lookahead_prologue(acts[:B])
     loss_nat = nat.run_native_epoch(acts, labels, nslot, B, True)

@@ -284,7 +284,6 @@ def test_native_server_epoch_matches_python(cuda, tp, kind, B):
                           seed_base=1234567)
     ta, sa = mk(), mk_slot()
     tb, sb = mk(), mk_slot()
-    tb.server_chain = False      # the six-kernel chain: the Python path's launches (chain: test_chain_gpu.py)
     assert tb.native_epoch_ok(B)
     losses = []
     ta.lookahead_prologue(acts[:B])

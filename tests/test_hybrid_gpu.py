@@ -1,0 +1,187 @@
+"""The hybrid persistent server epoch (`_C.HybridEpoch`, csrc/hybrid.hip) against fp32 PyTorch.
+
+One launch runs a whole client epoch of Bob's SISA server training for a WIDE shard (TP = 1 /
+2 / 4 of model2_sisa): fc2 / fc3 / biases and their Adam state stay on-chip, fc1 streams.
+As for the register-resident epoch (tests/test_resident_gpu.py), torch cannot be
+re-synchronised inside one launch, so:
+* one launch per step (S = 1), torch re-synchronised before every step (weights, moments, step
+  count), post-step weights / moments and losses compared (`torch.optim.Adam(lr,
+  weight_decay=1e-5)`, data_entities_vanilla_sisa.py:266,305-313) on the full model2_sisa
+  (fc1 5408 -> 5000, fc2 5000 -> 1000, fc3 1000 -> 100, dropout 0.5 on fc1 / fc2);
+* one launch of S steps is bitwise the S one-step launches (the in-launch hand-offs and the
+  prologue's look-ahead compute exactly what the launch boundaries do);
+* other shard shapes (TP = 2 / 4 widths, fewer rows per step, a partial last batch through
+  the launch-per-stage executor, small odd shapes) stay close to torch over free-running steps.
+"""
+import copy
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from splitlearning_amd.engine import OptSlot, TailEngine, adam
+from splitlearning_amd.models.zoo import LinearSpec, TailSpec, _MLP
+from splitlearning_amd.ops import rng
+
+pytestmark = pytest.mark.gpu
+
+
+def _spec(n1=5000, k1=5408, n2=1000, c=100, p=0.5):
+    return TailSpec([LinearSpec("fc1", k1, n1, True, p), LinearSpec("fc2", n1, n2, True, p),
+                     LinearSpec("fc3", n2, c, False, 0.0)])
+
+
+def _ref_forward(mod, x, seed_base, step):
+    h = x
+    for i, lin in enumerate(mod.linears()):
+        ls = mod.spec.layers[i]
+        h = F.relu(F.linear(h, lin.weight, lin.bias)) if ls.relu else F.linear(h, lin.weight, lin.bias)
+        if ls.dropout:
+            keep = rng.keep_mask(rng.step_seed(seed_base, i, step), h.shape[0], h.shape[1], ls.dropout,
+                                 device=h.device)
+            h = h * keep / (1 - ls.dropout)
+    return h
+
+
+def _sync_torch(ref, opt, te, slot, t):
+    with torch.no_grad():
+        for name, p in ref.named_parameters():
+            L = te.layers[int(name[2]) - 1]
+            p.copy_(L.W if name.endswith("weight") else L.b)
+            st = slot.states[name]
+            opt.state[p] = {"step": torch.tensor(float(t)), "exp_avg": st["m"].clone(),
+                            "exp_avg_sq": st["v"].clone()}
+
+
+def _engine(base, spec, cuda, seed_base, tag):
+    te = TailEngine(copy.deepcopy(base), spec, cuda, seed_base=seed_base, ws_tag=tag)
+    slot = OptSlot(adam(1e-3, 1e-5))
+    for L in te.layers:
+        slot.state(f"{L.spec.name}.weight", L.W)
+        slot.state(f"{L.spec.name}.bias", L.b)
+    return te, slot
+
+
+def test_hybrid_step_matches_torch_adam_every_step(cuda):
+    B, steps, lr, seed_base = 16, 12, 1e-3, 7
+    spec = _spec()
+    g = torch.Generator().manual_seed(3)
+    acts = (torch.rand(B * steps, 5408, generator=g) * 20).to(cuda)
+    labels = torch.randint(0, 100, (B * steps,), generator=g).to(cuda)
+    torch.manual_seed(11)
+    base = _MLP(spec)
+    te, slot = _engine(base, spec, cuda, seed_base, "#hy1")
+    assert te.hybrid_ok(slot, B), te._hybrid_executor(slot, B).why()
+    ex = te._hybrid_executor(slot, B)
+    ref = copy.deepcopy(base).to(cuda)
+    opt = torch.optim.Adam(ref.parameters(), lr=lr, weight_decay=1e-5)
+    for i in range(steps):
+        x, y = acts[i * B:(i + 1) * B], labels[i * B:(i + 1) * B]
+        _sync_torch(ref, opt, te, slot, i)
+        opt.zero_grad()
+        loss_r = F.cross_entropy(_ref_forward(ref, x, seed_base, i + 1), y, reduction="none")
+        loss_r.mean().backward()
+        opt.step()
+        loss_e = torch.empty(B, device=cuda)
+        fc, t, done = ex.run(x.contiguous(), y.contiguous(), loss_e, seed_base, te.fwd_count, slot.t)
+        te.fwd_count, slot.t = int(fc), int(t)
+        assert done == B
+        torch.testing.assert_close(loss_e, loss_r.detach(), rtol=2e-4, atol=1e-4, msg=f"step {i} loss")
+        for name, p in ref.named_parameters():
+            L = te.layers[int(name[2]) - 1]
+            e = L.W if name.endswith("weight") else L.b
+            d = (e - p.detach()).abs()
+            assert d.max().item() <= 2 * lr + 1e-6, (i, name, d.max().item())
+            assert (d > 1e-6).float().mean().item() < 1e-4, (i, name, (d > 1e-6).float().mean().item())
+            st, mine = opt.state[p], slot.states[name]
+            for k, tk in (("m", "exp_avg"), ("v", "exp_avg_sq")):
+                ref_k = st[tk]
+                torch.testing.assert_close(mine[k], ref_k, rtol=1e-3, atol=1e-5 * ref_k.abs().max().item() + 1e-30,
+                                           msg=f"step {i} {name} {k}")
+    assert (te.fwd_count, slot.t) == (steps, steps)
+
+
+def test_hybrid_one_launch_is_bitwise_per_step_launches(cuda):
+    B, steps, seed_base = 16, 24, 5
+    spec = _spec()
+    g = torch.Generator().manual_seed(8)
+    acts = (torch.rand(B * steps, 5408, generator=g) * 20).to(cuda)
+    labels = torch.randint(0, 100, (B * steps,), generator=g).to(cuda)
+    torch.manual_seed(12)
+    base = _MLP(spec)
+    one, s1 = _engine(base, spec, cuda, seed_base, "#hy2a")
+    many, s2 = _engine(base, spec, cuda, seed_base, "#hy2b")
+    loss_one = one.run_hybrid_epoch(acts, labels, s1, B)
+    ex = many._hybrid_executor(s2, B)
+    losses = []
+    for i in range(steps):
+        le = torch.empty(B, device=cuda)
+        fc, t, _ = ex.run(acts[i * B:(i + 1) * B], labels[i * B:(i + 1) * B], le, seed_base, many.fwd_count, s2.t)
+        many.fwd_count, s2.t = int(fc), int(t)
+        losses.append(le)
+    torch.cuda.synchronize()
+    assert torch.equal(loss_one, torch.cat(losses))
+    for La, Lb in zip(one.layers, many.layers):
+        assert torch.equal(La.W, Lb.W) and torch.equal(La.b, Lb.b)
+    for k in s1.states:
+        for kk in ("m", "v"):
+            assert torch.equal(s1.states[k][kk], s2.states[k][kk]), (k, kk)
+    assert (one.fwd_count, s1.t) == (many.fwd_count, s2.t) == (steps, steps)
+
+
+@pytest.mark.parametrize("n1,n2,c,k1,B,rows", [(2500, 1000, 100, 5408, 16, 16 * 5 + 7),
+                                                (1252, 1000, 100, 5408, 8, 8 * 6),
+                                                (300, 256, 10, 1024, 16, 16 * 6 + 5),
+                                                (160, 64, 12, 1024, 4, 4 * 9 + 3)])
+def test_hybrid_shapes_free_running_close_to_torch(cuda, n1, n2, c, k1, B, rows):
+    lr, seed_base = 1e-3, 2
+    spec = _spec(n1=n1, n2=n2, c=c, k1=k1, p=0.25)
+    g = torch.Generator().manual_seed(n1)
+    acts = (torch.rand(rows, k1, generator=g) * 4).to(cuda)
+    labels = torch.randint(0, c, (rows,), generator=g).to(cuda)
+    torch.manual_seed(13)
+    base = _MLP(spec)
+    te, slot = _engine(base, spec, cuda, seed_base, f"#hy3{n1}")
+    assert te.hybrid_ok(slot, B), te._hybrid_executor(slot, B).why()
+    loss_e = te.run_hybrid_epoch(acts, labels, slot, B)
+    ref = copy.deepcopy(base).to(cuda)
+    opt = torch.optim.Adam(ref.parameters(), lr=lr, weight_decay=1e-5)
+    losses = []
+    for i, s in enumerate(range(0, rows, B)):
+        x, y = acts[s:s + B], labels[s:s + B]
+        opt.zero_grad()
+        loss_r = F.cross_entropy(_ref_forward(ref, x, seed_base, i + 1), y, reduction="none")
+        loss_r.mean().backward()
+        opt.step()
+        losses.append(loss_r.detach())
+    torch.testing.assert_close(loss_e, torch.cat(losses), rtol=1e-3, atol=1e-3)
+    for name, p in ref.named_parameters():
+        L = te.layers[int(name[2]) - 1]
+        e = L.W if name.endswith("weight") else L.b
+        d = (e - p.detach()).abs()
+        steps = -(-rows // B)
+        assert d.max().item() <= 2 * lr * steps + 1e-6, (name, d.max().item())
+        assert (d > 1e-4).float().mean().item() < 1e-3, (name, (d > 1e-4).float().mean().item())
+    assert slot.t == -(-rows // B)
+
+
+def test_hybrid_table_covers_every_tile_once(cuda):
+    """The workgroups' fc1 tile runs partition the tiles in order, every row block's first
+    workgroup and workgroup count match the runs, and every fc2 column block counts the fc1
+    row blocks that overlap it (csrc/hybrid_exec.cpp tables)."""
+    spec = _spec()
+    te, slot = _engine(_MLP(spec), spec, cuda, 1, "#hy4")
+    ex = te._hybrid_executor(slot, 16)
+    assert ex.ok(), ex.why()
+    G = ex.workgroups()
+    tab = ex.table().cpu().tolist()
+    nrb, ncb = (5000 + 15) // 16, (5408 + 255) // 256
+    tile0 = tab[:G + 1]
+    assert tile0[0] == 0 and tile0[-1] == nrb * ncb and all(b >= a for a, b in zip(tile0, tile0[1:]))
+    rbw0, rbn = tab[G + 1:G + 1 + nrb], tab[G + 1 + nrb:G + 1 + 2 * nrb]
+    for rb in range(nrb):
+        owners = [w for w in range(G) if tile0[w] < (rb + 1) * ncb and tile0[w + 1] > rb * ncb]
+        assert rbw0[rb] == owners[0] and rbn[rb] == len(owners), rb
+    NC = G // 8
+    hn = tab[G + 1 + 2 * nrb:]
+    assert len(hn) == NC and sum(hn) >= nrb and min(hn) >= 1

@@ -107,7 +107,6 @@ def test_tp_emulation_shard_equals_tp1_when_T_is_1(cuda):
     torch.manual_seed(0)
     base = ServerTailSisa()
     a = TailEngine(copy.deepcopy(base), sisa_server_spec(), cuda, seed_base=5)
-    a.server_chain = False       # the emulation steps the six-kernel chain
     sa = OptSlot(adam(1e-3, 1e-5))
     a.lookahead_prologue(acts[:B])
     la = a.run_native_epoch(acts, labels, sa, B, True)
