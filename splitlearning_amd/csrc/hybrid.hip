@@ -167,7 +167,7 @@ constexpr int OFF_DZ1 = OFF_B1 + kHyRuns * 3 * 16 * 4; // dz1 [kHyRuns][16 m][16
 constexpr int OFF_OK = OFF_DZ1 + kHyRuns * 256 * 4;    // ints
 constexpr int kHyLds = OFF_OK + 64;
 static_assert(kHyLds <= 160 * 1024, "LDS");
-static_assert(kHyThreads * 10 >= kHyMaxWR * kHyMaxWC4, "10 W2 float4 per thread");
+static_assert(kHyThreads / 64 * 10 * 256 >= kHyMaxWR * 4 * kHyMaxWC4, "10 W2 16 x 16 blocks per wave");
 
 }  // namespace
 
@@ -235,18 +235,26 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
     HY_IDX();
     for (int e = tid; e < kHyMaxWR * PW2; e += kHyThreads) sw2[e] = 0.f;
     __syncthreads();
+    for (int e = tid; e < WR * WC4; e += kHyThreads) {
+      const int n = e / WC4, q = e - n * WC4;
+      const f32x4 wv = *reinterpret_cast<const f32x4*>(a.L2.W + (int64_t)(r0 + n) * N1 + c0 + 4 * q);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) sw2[n * PW2 + 4 * q + k] = wv[k];
+    }
+    // m / v of the tile in the 16 x 16 MFMA accumulator layout of W2's update: block b = r + 8 u
+    // (rows 16 (b / 10) .., columns 16 (b % 10) ..), lane (li, lq) holds rows 4 lq + j, column li
 #pragma unroll
     for (int u = 0; u < 10; ++u) {
-      const int e = tid + u * kHyThreads;
-      const int n = e / WC4, q = e - n * WC4;
+      const int b = r + 8 * u, bn = b / 10, bk = b - (b / 10) * 10;
       m2[u] = v2[u] = zv;
-      if (n < WR) {
-        const int64_t off = (int64_t)(r0 + n) * N1 + c0 + 4 * q;
-        const f32x4 wv = *reinterpret_cast<const f32x4*>(a.L2.W + off);
-        m2[u] = *reinterpret_cast<const f32x4*>(a.L2.m + off);
-        if (ADAM) v2[u] = *reinterpret_cast<const f32x4*>(a.L2.v + off);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) sw2[n * PW2 + 4 * q + k] = wv[k];
+      for (int j = 0; j < 4; ++j) {
+        const int n = 16 * bn + 4 * lq + j, k = 16 * bk + li;
+        if (n < WR && k < WC) {
+          const int64_t off = (int64_t)(r0 + n) * N1 + c0 + k;
+          m2[u][j] = a.L2.m[off];
+          if (ADAM) v2[u][j] = a.L2.v[off];
+        }
       }
     }
     if (head && tid < 4 * MC) {
@@ -330,6 +338,7 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
   // MFMA accumulator per row block, stored to ZP when the run leaves the row block.  sp / sm /
   // sv [0] hold tile t_begin's state, already issued.
   f32x4 sp[2][2], sm[2][2], sv[2][2];
+  f32x4 zlast = zv;
   auto zp_store = [&](int k, f32x4 z) {
     HY_IDX();
     hst4(rHB, bZP + (((w * kHyRuns + k) * 8 + r) * 64 + lane) * 16, z);
@@ -417,7 +426,7 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
       tile(std::integral_constant<int, 1>{}, j + 1);
     }
     if (j < nt) tile(std::integral_constant<int, 0>{}, j);
-    if (LOOK) zp_store(kz, z);
+    zlast = z;   // the last row block's accumulators go to flush through LDS
   };
 
   // Publish the run's look-ahead partials for step `so` (parity so & 1, generation gen of the
@@ -427,6 +436,13 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
   // counts them into H[] of the fc2 column blocks they cover.
   auto flush = [&](int so, unsigned gen) {
     const int par = so & 1;
+    {
+      // the last row block's per-wave accumulators through LDS (the stream's buffers are free
+      // once every wave passed this barrier); earlier row blocks' from ZP
+      HY_IDX();
+      __syncthreads();
+      sa[r * 64 + lane] = zlast;
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     {
@@ -435,9 +451,14 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
         const int k = e >> 8, m = (e >> 4) & 15, nn = e & 15;
         const int rb = rbA + k, slot = w - a.tab[a.G + 1 + rb], n = 16 * rb + nn;
         float parts[8];
+        if (k == nruns - 1) {
 #pragma unroll
-        for (int ww = 0; ww < 8; ++ww)
-          parts[ww] = hld1(rHB, bZP + ((((w * kHyRuns + k) * 8 + ww) * 64 + 16 * (m >> 2) + nn) * 4 + (m & 3)) * 4);
+          for (int ww = 0; ww < 8; ++ww) parts[ww] = sa[ww * 64 + 16 * (m >> 2) + nn][m & 3];
+        } else {
+#pragma unroll
+          for (int ww = 0; ww < 8; ++ww)
+            parts[ww] = hld1(rHB, bZP + ((((w * kHyRuns + k) * 8 + ww) * 64 + 16 * (m >> 2) + nn) * 4 + (m & 3)) * 4);
+        }
         float v = parts[0];
 #pragma unroll
         for (int ww = 1; ww < 8; ++ww) v += parts[ww];
@@ -818,22 +839,26 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
     // the first fc1 tile's state in flight under W2's update and the dz1 wait
     if (nt > 0) load_state(t_begin, sp[0], sm[0], sv[0], true);
     {
+      // dW2 of the tile = dz2[:, rows]^T h1[:, slice] on exact-fp32 MFMA (K = the 16 batch rows),
+      // each wave 10 blocks of 16 x 16, the moments already in the accumulator layout; W2 in LDS
+      // updated in place (a VALU form with the dz2 / h1 operands re-read from LDS per element
+      // took 9.8 us of the critical path)
       HY_IDX();
 #pragma unroll
       for (int u = 0; u < 10; ++u) {
-        const int e = tid + u * kHyThreads;
-        const int n = e / WC4, q = e - n * WC4;
-        if (n < WR) {
+        const int b = r + 8 * u, bn = b / 10, bk = b - (b / 10) * 10;
+        if (16 * bn < WR && 16 * bk < WC) {
           f32x4 g = zv;
-#pragma unroll 4
-          for (int m = 0; m < 16; ++m)
-            g += sdz2[m * PD + n] * *reinterpret_cast<const f32x4*>(sh1 + m * PH + 4 * q);
+#pragma unroll
+          for (int st = 0; st < 4; ++st)
+            g = __builtin_amdgcn_mfma_f32_16x16x4f32(sdz2[(4 * st + lq) * PD + 16 * bn + li],
+                                                     sh1[(4 * st + lq) * PH + 16 * bk + li], g, 0, 0, 0);
           f32x4 p;
 #pragma unroll
-          for (int k = 0; k < 4; ++k) p[k] = sw2[n * PW2 + 4 * q + k];
+          for (int j = 0; j < 4; ++j) p[j] = sw2[(16 * bn + 4 * lq + j) * PW2 + 16 * bk + li];
           res_update4<ADAM>(o, ss, ib, p, g, m2[u], v2[u]);
 #pragma unroll
-          for (int k = 0; k < 4; ++k) sw2[n * PW2 + 4 * q + k] = p[k];
+          for (int j = 0; j < 4; ++j) sw2[(16 * bn + 4 * lq + j) * PW2 + 16 * bk + li] = p[j];
         }
       }
     }
@@ -904,18 +929,24 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
   __syncthreads();
   {
     HY_IDX();
+    for (int e = tid; e < WR * WC4; e += kHyThreads) {
+      const int n = e / WC4, q = e - n * WC4;
+      f32x4 wv;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) wv[k] = sw2[n * PW2 + 4 * q + k];
+      *reinterpret_cast<f32x4*>(a.L2.W + (int64_t)(r0 + n) * N1 + c0 + 4 * q) = wv;
+    }
 #pragma unroll
     for (int u = 0; u < 10; ++u) {
-      const int e = tid + u * kHyThreads;
-      const int n = e / WC4, q = e - n * WC4;
-      if (n < WR) {
-        const int64_t off = (int64_t)(r0 + n) * N1 + c0 + 4 * q;
-        f32x4 wv;
+      const int b = r + 8 * u, bn = b / 10, bk = b - (b / 10) * 10;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) wv[k] = sw2[n * PW2 + 4 * q + k];
-        *reinterpret_cast<f32x4*>(a.L2.W + off) = wv;
-        *reinterpret_cast<f32x4*>(a.L2.m + off) = m2[u];
-        if (ADAM) *reinterpret_cast<f32x4*>(a.L2.v + off) = v2[u];
+      for (int j = 0; j < 4; ++j) {
+        const int n = 16 * bn + 4 * lq + j, k = 16 * bk + li;
+        if (n < WR && k < WC) {
+          const int64_t off = (int64_t)(r0 + n) * N1 + c0 + k;
+          a.L2.m[off] = m2[u][j];
+          if (ADAM) a.L2.v[off] = v2[u][j];
+        }
       }
     }
     if (head && tid < 4 * MC) {

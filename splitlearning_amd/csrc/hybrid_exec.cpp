@@ -239,12 +239,17 @@ class HybridEpoch {
     if (a.N1 % 4 || a.N1 < 4) return "fc1 shard width % 4";
     const int Q4 = a.N1 / 4;
     std::vector<int> tab(G + 1 + 2 * nrb + NC, 0);
-    for (int w = 0; w <= G; ++w) tab[w] = (int)((int64_t)w * T / G);
-    auto wg_of = [&](int t) {
-      int w = (int)(((int64_t)(t + 1) * G + T - 1) / T) - 1;
-      while (w > 0 && tab[w] > t) --w;
-      while (w + 1 < G && tab[w + 1] <= t) ++w;
-      return w;
+    // balanced contiguous runs; with fewer tiles than workgroups the first T workgroups take
+    // one tile each (no empty run between two workgroups that share a row block)
+    for (int w = 0; w <= G; ++w) tab[w] = T >= G ? (int)((int64_t)w * T / G) : std::min(w, T);
+    auto wg_of = [&](int t) {   // the workgroup whose run holds tile t
+      int lo = 0, hi = G - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) / 2;
+        if (tab[mid] <= t) lo = mid;
+        else hi = mid - 1;
+      }
+      return lo;
     };
     auto colblk = [&](int n4) { return (int)(((int64_t)(n4 + 1) * NC + Q4 - 1) / Q4) - 1; };
     for (int rb = 0; rb < nrb; ++rb) {
