@@ -104,6 +104,9 @@ def main(argv=None):
     ap.add_argument("--bob_tp", type=int, default=0,
                     help="0 = the policy (parallel/dist.py choose_bob_tp: all GPUs for the SISA modes)")
     ap.add_argument("--graphs", choices=("auto", "on", "off"), default="auto")
+    ap.add_argument("--hybrid", choices=("auto", "off"), default="auto",
+                    help="SISA server epochs of a wide Bob shard (TP <= 4) on the hybrid persistent "
+                         "executor (csrc/hybrid.hip: fc2 / fc3 on-chip, fc1 streamed in one launch)")
     ap.add_argument("--resident", choices=("auto", "off"), default="auto",
                     help="SISA server epochs of a narrow Bob shard (TP >= 7) on the register-resident "
                          "persistent executor (csrc/resident.hip) after its cross-rank self-test")
@@ -161,7 +164,7 @@ def main(argv=None):
         "--batch_size", str(a.batch_size), "--partition_alpha", str(a.partition_alpha),
         "--server_epochs", str(a.server_epochs), "--seed", str(a.seed), "--num_samples", str(a.num_samples),
         "--kernels", a.kernels, "--graphs", a.graphs, "--act_dtype", a.act_dtype, "--dtype", a.dtype, "--no_tqdm",
-        "--tp_allreduce", a.tp_allreduce, "--resident", a.resident,
+        "--tp_allreduce", a.tp_allreduce, "--resident", a.resident, "--hybrid", a.hybrid,
         "--log_dir", log_dir, "--watchdog", "off"]
     if a.mode == "concat" and a.concat_unlearn:
         argv_s.append("--concat_unlearn")
@@ -280,8 +283,8 @@ def main(argv=None):
                 "tp_ipc_setup": _ipc_status(),
                 # Bob's server-epoch executor: the register-resident persistent launch (a shard
                 # narrow enough to keep on-chip, its self-test passed) or the launch-per-stage one
-                "server_executor": ("resident" if getattr(sess, "_resident_ok", False) else
-                                    "launch_per_stage") if sargs.mode in ("sisa", "control") else None,
+                "server_executor": getattr(sess, "server_executor", "launch_per_stage")
+                if sargs.mode in ("sisa", "control") else None,
                 # why: adopted, or the fit / self-test outcome that kept launch-per-stage
                 "server_executor_reason": (getattr(sess, "resident_status", None) or {}).get("reason"),
                 "calib": calib,

@@ -7,11 +7,11 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" && mkdir -p gpurun_out/r4
 if [ -n "$TESTS" ]; then
   timeout -k 10 ${TEST_TMO:-900} python -u -m pytest $TESTS -x -v --timeout 120 --timeout-method thread \
-    > gpurun_out/r4/tests.log 2>&1 || { echo TEST_FAIL; tail -60 gpurun_out/r4/tests.log; exit 1; }
-  tail -3 gpurun_out/r4/tests.log
+    > gpurun_out/r4/tests.log 2>&1 || { echo TEST_FAIL; grep -E "PASS|FAIL|Error|assert" gpurun_out/r4/tests.log | tail -40; tail -30 gpurun_out/r4/tests.log; exit 1; }
+  grep -cE "PASSED" gpurun_out/r4/tests.log; tail -2 gpurun_out/r4/tests.log
 fi
 if [ -n "$BENCH" ]; then
-  timeout -k 10 400 python bench.py ${BENCH_ARGS:---steps 3 --warmup 1} > gpurun_out/r4/bench.log 2>&1 \
+  timeout -k 10 600 python bench.py ${BENCH_ARGS:---steps 3 --warmup 1} > gpurun_out/r4/bench.log 2>&1 \
     || { echo BENCH_FAIL; tail -30 gpurun_out/r4/bench.log; exit 1; }
   tail -1 gpurun_out/r4/bench.log
 fi

@@ -93,8 +93,25 @@ def main():
             ts = 64
             tr = torch.zeros(2, ts, 16, dtype=torch.int64, device=dev)
             loss = torch.empty(n, device=dev)
-            ex.run(acts, labels, loss, tail.seed_base, tail.fwd_count, slot.t, tr)
+            G = ex.workgroups()
+            tall = torch.zeros(G, 4, dtype=torch.int64, device=dev)
+            ex.run(acts, labels, loss, tail.seed_base, tail.fwd_count, slot.t, tr, tall, 40)
             torch.cuda.synchronize()
+            ta = tall.cpu().double() / 100.0   # us (100 MHz wall clock)
+            s0 = ta[:, 0].min()
+            st, en, fl, nx = ta[:, 0] - s0, ta[:, 1] - s0, ta[:, 2] - s0, ta[:, 3] - s0
+            dur = en - st
+            print(f"tp={tp} per-workgroup (step 40, us from the first stream start): stream start "
+                  f"min/med/max {st.min():.1f}/{st.median():.1f}/{st.max():.1f}; stream length "
+                  f"{dur.min():.1f}/{dur.median():.1f}/{dur.max():.1f}; stream end {en.min():.1f}/{en.median():.1f}/"
+                  f"{en.max():.1f}; flush end {fl.min():.1f}/{fl.median():.1f}/{fl.max():.1f}; next F released "
+                  f"{nx.min():.1f}/{nx.median():.1f}/{nx.max():.1f}", flush=True)
+            xcd = [dur[x::8].mean().item() for x in range(8)]
+            print(f"tp={tp} stream length by w % 8: " + " ".join(f"{v:.1f}" for v in xcd), flush=True)
+            order = torch.argsort(dur, descending=True)[:8].tolist()
+            print(f"tp={tp} slowest workgroups: " + " ".join(f"{w}:{dur[w]:.1f}" for w in order), flush=True)
+            blk = [dur[i:i + 32].mean().item() for i in range(0, G, 32)]
+            print(f"tp={tp} stream length by w // 32: " + " ".join(f"{v:.1f}" for v in blk), flush=True)
             khz = 100000.0
             t = tr.cpu().double()
             for wgi, name in ((0, "wg 0"), (1, "wg G-1")):

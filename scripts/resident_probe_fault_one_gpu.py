@@ -53,8 +53,9 @@ def worker(rank, world, port, fault):
         tail = TailEngine(_MLP(spec), spec, dev, tp_rank=rank, tp_size=world, allreduce=ipc_allreduce(ipc), seed_base=5)
         tail.resident_workgroups = 256 // world
         slot = OptSlot(adam(1e-3, 1e-5))
-        adopted, why = resident.decide(tail, slot, B, distributed=True)
-        print(f"rank {rank}: adopted {adopted} ({why})", flush=True)
+        kind, why = resident.decide(tail, slot, B, distributed=True)
+        adopted = kind == "resident"
+        print(f"rank {rank}: adopted {adopted} ({kind}: {why})", flush=True)
         ok = adopted == (fault < 0)
         if fault >= 0:
             ok = ok and ipc.error() == 0 and ipc.host_error() == 0

@@ -6,7 +6,10 @@ multi-GPU code path minus the xGMI links.  Checks on every rank: no wait gave up
 replicated parameters (fc2 bias, fc3) and the per-row losses are bitwise identical across
 ranks, and the losses match an fp32 torch run of the whole (unsharded) tail.
 
-    python scripts/resident_tp_one_gpu.py [T]      (spawns its own T ranks)
+    python scripts/resident_tp_one_gpu.py [T] [resident|hybrid]     (spawns its own T ranks)
+
+`hybrid` runs the same check on the hybrid persistent executor (csrc/hybrid.hip: fc2 tiles
+on-chip, fc1 streamed, the fc2 product exchanged by the same granule protocol).
 """
 import copy
 import os
@@ -20,7 +23,7 @@ import torch.nn.functional as F
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def worker(rank, world, port):
+def worker(rank, world, port, kind):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -49,14 +52,15 @@ def worker(rank, world, port):
         mine.resident_workgroups = 256 // world
         mine.resident_timeout_s = 5.0
         slot = OptSlot(adam(1e-3, 1e-5))
-        ok = mine.resident_ok(slot, B)
-        print(f"rank {rank}: resident fits {ok}", flush=True)
+        ok = mine.hybrid_ok(slot, B) if kind == "hybrid" else mine.resident_ok(slot, B)
+        print(f"rank {rank}: {kind} fits {ok}", flush=True)
         if ok:
             try:
-                loss = mine.run_resident_epoch(acts, labels, slot, B)
+                run = mine.run_hybrid_epoch if kind == "hybrid" else mine.run_resident_epoch
+                loss = run(acts, labels, slot, B)
                 torch.cuda.synchronize()
             except RuntimeError as e:
-                print(f"rank {rank}: resident epoch failed: {e}", flush=True)
+                print(f"rank {rank}: {kind} epoch failed: {e}", flush=True)
                 ok = False
         if ok:
             rep = torch.cat([loss, mine.layers[1].b, mine.layers[2].W.reshape(-1), mine.layers[2].b]).cpu()
@@ -98,8 +102,9 @@ def worker(rank, world, port):
 
 def main():
     T = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+    kind = sys.argv[2] if len(sys.argv) > 2 else "resident"
     port = 29500 + (os.getpid() % 1000)
-    mp.spawn(worker, args=(T, port), nprocs=T, join=True)
+    mp.spawn(worker, args=(T, port, kind), nprocs=T, join=True)
 
 
 if __name__ == "__main__":

@@ -132,6 +132,12 @@ def build_parser() -> argparse.ArgumentParser:
                         "held on-chip (csrc/resident.hip); 'auto' uses it where it fits and, "
                         "tensor-parallel, after a cross-rank self-test passed; 'off' = the "
                         "launch-per-stage executor")
+    g.add_argument("--hybrid", choices=("auto", "off"), default="auto",
+                   help="SISA server epochs of a WIDE Bob shard (TP 1..4: fc1 up to 5120 rows) as ONE "
+                        "persistent launch per client epoch with fc2 / fc3 and the biases on-chip and "
+                        "fc1's weights / Adam state streamed through the launch (csrc/hybrid.hip); "
+                        "'auto' uses it where it fits and, tensor-parallel, after a cross-rank "
+                        "self-test passed; 'off' = the launch-per-stage executor")
     g.add_argument("--tp_allreduce", choices=("auto", "rccl"), default="auto",
                    help="Bob's per-step TP all-reduce: 'auto' = one kernel over peer-mapped HBM "
                         "(csrc/ipc_ar.h) when every Bob rank sets it up and passes its self-test, "

@@ -180,6 +180,12 @@ static_assert(kHyThreads / 64 * 10 * 256 >= kHyMaxWR * 4 * kHyMaxWC4, "10 W2 16 
   const int tid = tid_l_, r = tid >> 6, lane = tid & 63, li = lane & 15, lq = lane >> 4; \
   (void)r; (void)lane; (void)li; (void)lq
 
+#define HY_ALL(i_, k)                                                                           \
+  do {                                                                                           \
+    if (a.tall != nullptr && (i_) == a.tall_step && threadIdx.x == 0)                           \
+      a.tall[w * 4 + (k)] = (int64_t)wall_clock64();                                            \
+  } while (0)
+
 #define HY_MARK(k)                                                                               \
   do {                                                                                           \
     if (a.trace != nullptr && i < a.trace_steps && threadIdx.x == 0 && (w == 0 || w == G - 1))  \
@@ -535,6 +541,7 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
       if (!hy_wait(a, 1, idx, tgt, s_ok)) break;
     }
     HY_MARK(1);
+    HY_ALL(i - 1, 3);
     {
       HY_IDX();
 #pragma unroll
@@ -881,6 +888,7 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
       if (nruns > 0 && *s_ok == 0) break;
     }
     HY_MARK(12);
+    HY_ALL(i, 0);
     {
       HY_IDX();
       for (int e = tid; e < kHyRuns * 256; e += kHyThreads) {
@@ -918,7 +926,9 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
     if (more) {
       stream(std::true_type{}, std::true_type{}, xt, xn, ss, ib);
       HY_MARK(13);
+      HY_ALL(i, 1);
       flush(i + 1, (unsigned)(i + 2));
+      HY_ALL(i, 2);
     } else {
       stream(std::true_type{}, std::false_type{}, xt, xn, ss, ib);
     }
@@ -982,6 +992,7 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
 }
 #undef HY_IDX
 #undef HY_MARK
+#undef HY_ALL
 
 int hybrid_lds_bytes() { return kHyLds; }
 

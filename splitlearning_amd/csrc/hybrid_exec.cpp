@@ -170,7 +170,8 @@ class HybridEpoch {
   // Every full batch of acts [n, K1] / labels [n] (the first n - n % B rows) in ONE launch;
   // losses into loss_rows [n].  Returns (fwd_count, t, rows done).
   py::tuple run(const at::Tensor& acts, const at::Tensor& labels, at::Tensor& loss_rows, int64_t seed_base,
-                int64_t fwd_count, int64_t t, const c10::optional<at::Tensor>& trace) {
+                int64_t fwd_count, int64_t t, const c10::optional<at::Tensor>& trace,
+                const c10::optional<at::Tensor>& trace_all, int64_t trace_all_step) {
     TORCH_CHECK(ok_, "HybridEpoch: this shard does not fit: ", why_);
     TORCH_CHECK(acts.is_cuda() && acts.scalar_type() == at::kFloat && acts.dim() == 2 && acts.is_contiguous() &&
                     acts.size(1) == a_.K1,
@@ -215,6 +216,14 @@ class HybridEpoch {
                   "trace int64 [2, steps, 16]");
       a.trace = trace->data_ptr<int64_t>();
       a.trace_steps = (int)(trace->numel() / 32);
+    }
+    a.tall = nullptr;
+    a.tall_step = (int)trace_all_step;
+    if (trace_all.has_value()) {
+      TORCH_CHECK(trace_all->is_cuda() && trace_all->scalar_type() == at::kLong && trace_all->is_contiguous() &&
+                      trace_all->numel() >= 4LL * a.G,
+                  "trace_all int64 [G, 4]");
+      a.tall = trace_all->data_ptr<int64_t>();
     }
     const std::string why = sl::hybrid_check(a);
     TORCH_CHECK(why.empty(), "HybridEpoch: ", why);
@@ -291,5 +300,6 @@ void sl_register_hybrid(py::module& m) {
       .def("workgroups", &HybridEpoch::workgroups)
       .def("table", &HybridEpoch::table)
       .def("run", &HybridEpoch::run, py::arg("acts"), py::arg("labels"), py::arg("loss_rows"),
-           py::arg("seed_base"), py::arg("fwd_count"), py::arg("t"), py::arg("trace") = py::none());
+           py::arg("seed_base"), py::arg("fwd_count"), py::arg("t"), py::arg("trace") = py::none(),
+           py::arg("trace_all") = py::none(), py::arg("trace_all_step") = 0);
 }

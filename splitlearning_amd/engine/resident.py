@@ -29,11 +29,12 @@ PROBE_TIMEOUT_S = 5.0
 FAULT_ENV = "SL_FAULT_RESIDENT_PROBE"
 
 
-def probe(tail, slot, B: int) -> int:
-    """One short resident epoch of a scratch shard with this rank's layout and peer-mapped
+def probe(tail, slot, B: int, kind: str = "resident") -> int:
+    """One short epoch of a scratch shard on the persistent executor `kind` ("resident":
+    csrc/resident.hip, "hybrid": csrc/hybrid.hip) with this rank's layout and peer-mapped
     region (fixed random weights, synthetic inputs, every in-launch wait bounded by
-    PROBE_TIMEOUT_S: the seams and the peer exchange).  Returns an integer fingerprint of the
-    replicated fc3 weight it produced; raises RuntimeError when a wait gave up."""
+    PROBE_TIMEOUT_S: the hand-offs and the peer exchange).  Returns an integer fingerprint of
+    the replicated fc3 weight it produced; raises RuntimeError when a wait gave up."""
     from . import OptSlot, TailEngine
     dev = tail.device
     if os.environ.get(FAULT_ENV, "") == str(tail.tp_rank):
@@ -55,7 +56,8 @@ def probe(tail, slot, B: int) -> int:
     if ipc is not None:
         ipc.set_timeout_s(PROBE_TIMEOUT_S)
     try:
-        loss = pt.run_resident_epoch(x, y, pslot, B)
+        run = pt.run_hybrid_epoch if kind == "hybrid" else pt.run_resident_epoch
+        loss = run(x, y, pslot, B)
         torch.cuda.synchronize(dev)
     finally:
         if ipc is not None:
@@ -72,47 +74,60 @@ def _coll_device():
     return torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else "cpu"
 
 
-def decide(tail, slot, B: int, distributed: bool, want: bool = True) -> tuple[bool, str]:
-    """Collective over every process of the default group when `distributed` (ranks that are
-    not Bob pass tail=None): whether Bob's server epochs run on the resident executor, and why
-    (the reason string the bench JSON reports next to `server_executor`).
+KINDS = ("resident", "hybrid")
 
-    Single shard: it fits or not.  Tensor-parallel: every Bob rank probes; adopted only if every
-    rank passed with the same fc3 fingerprint.  When not adopted after any probe ran, every rank
-    re-arms the peer-mapped region at the largest generation any rank reserved."""
-    ok, fp, why = bool(want), None, "" if want else "off"
+
+def decide(tail, slot, B: int, distributed: bool, want: bool = True, want_hybrid: bool = True) -> tuple[str, str]:
+    """Collective over every process of the default group when `distributed` (ranks that are
+    not Bob pass tail=None): which persistent executor Bob's server epochs run on, and why (the
+    reason string the bench JSON reports next to `server_executor`).  Returns (kind, why) with
+    kind "resident" (the whole shard on-chip: TP >= 7), "hybrid" (a wide shard: fc2 / fc3 on-
+    chip, fc1 streamed) or "launch_per_stage".
+
+    Single shard: the first that fits.  Tensor-parallel: every Bob rank probes that executor;
+    adopted only if every rank chose the same one and passed with the same fc3 fingerprint.
+    When not adopted after any probe ran, every rank re-arms the peer-mapped region at the
+    largest generation any rank reserved."""
+    kind, fp, why = None, None, "" if want else "off"
     ran_probe = False
-    if tail is not None and ok:
-        ok = tail.resident_ok(slot, B)
-        if not ok:
-            why = "shard does not fit on-chip"
-        elif tail.tp_size > 1:
+    if tail is not None and want:
+        if tail.resident_ok(slot, B):
+            kind = "resident"
+        elif want_hybrid and tail.hybrid_ok(slot, B):
+            kind = "hybrid"
+        else:
+            why = "no persistent executor fits this shard"
+        if kind is not None and tail.tp_size > 1:
             ran_probe = True
             try:
-                fp = probe(tail, slot, B)
+                fp = probe(tail, slot, B, kind)
             except RuntimeError as e:            # a wait gave up, or the launch was refused
-                warnings.warn(f"resident server epoch self-test failed: {e}")
-                ok, why = False, f"self-test failed on this rank: {str(e).splitlines()[0][:160]}"
+                warnings.warn(f"{kind} server epoch self-test failed: {e}")
+                why = f"{kind} self-test failed on this rank: {str(e).splitlines()[0][:160]}"
+                kind = None
+    code = KINDS.index(kind) + 1 if kind is not None else 0
     if not distributed:
-        return ok, ("adopted" if ok else why)
+        return (kind, "adopted") if kind is not None else ("launch_per_stage", why)
     import torch.distributed as dist
     dev = _coll_device()
     big = 1 << 62
-    lo = torch.tensor([fp if fp is not None else big, 1 if ok else 0, 0 if ran_probe else 1], dtype=torch.int64,
-                      device=dev)
-    hi = torch.tensor([fp if fp is not None else -big], dtype=torch.int64, device=dev)
+    is_bob = tail is not None
+    # MIN / MAX over the Bob ranks of (fingerprint, executor code); the other ranks are neutral
+    lo = torch.tensor([fp if fp is not None else big, code if is_bob else 99, 0 if ran_probe else 1],
+                      dtype=torch.int64, device=dev)
+    hi = torch.tensor([fp if fp is not None else -big, code if is_bob else -1], dtype=torch.int64, device=dev)
     dist.all_reduce(lo, op=dist.ReduceOp.MIN)
     dist.all_reduce(hi, op=dist.ReduceOp.MAX)
-    all_ok = int(lo[1].item()) == 1
-    agree = all_ok and (int(lo[0].item()) == int(hi[0].item()) or int(lo[0].item()) == big)
+    same_kind = int(lo[1].item()) == int(hi[1].item()) and int(lo[1].item()) > 0
+    fp_ok = int(lo[0].item()) == int(hi[0].item()) or int(lo[0].item()) == big
     any_probe = int(lo[2].item()) == 0
-    if agree:
-        return True, "adopted"
+    if same_kind and fp_ok:
+        return KINDS[int(lo[1].item()) - 1], "adopted"
     if not why:
-        why = ("self-test failed on another rank" if not all_ok else "replicated fc3 differs across ranks")
+        why = ("self-test failed on another rank" if not same_kind else "replicated fc3 differs across ranks")
     if any_probe:
         rearm(tail)
-    return False, why
+    return "launch_per_stage", why
 
 
 def rearm(tail):

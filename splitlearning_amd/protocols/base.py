@@ -215,6 +215,10 @@ class Session:
         tp_rank = self.pl.bob_ranks.index(self.rank)
         self.tail = TailEngine(module, spec, self.device, tp_rank, tp_size,
                                allreduce=self.tp_allreduce, seed_base=self.seed)
+        if getattr(self.comm, "host_staging", False) and tp_size > 1:
+            # Bob's TP ranks share ONE GPU (the --ranks_share_gpu rehearsal): each persistent
+            # launch takes its share of the CUs so all of them are resident together
+            self.tail.resident_workgroups = max(8, (256 // tp_size) // 8 * 8)
 
     def make_bob_module(self, cls, *a):
         # identical init on every TP rank: seed the default generator with the agreed seed

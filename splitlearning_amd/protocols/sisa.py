@@ -270,23 +270,29 @@ class SisaSession(Session):
         return _ops.get_backend() != "torch"
 
     def _use_resident(self) -> bool:
-        """`--resident auto`: the register-resident epoch where this rank's Bob shard fits it
-        (engine/tail.py resident_ok) and every Bob rank passed the set-up check
-        (`_decide_resident`, run once by every rank at construction)."""
-        return bool(getattr(self, "_resident_ok", False))
+        """Bob's server epochs on the register-resident executor (the whole shard on-chip)."""
+        return getattr(self, "server_executor", "launch_per_stage") == "resident"
+
+    def _use_hybrid(self) -> bool:
+        """Bob's server epochs on the hybrid persistent executor (wide shard, fc1 streamed)."""
+        return getattr(self, "server_executor", "launch_per_stage") == "hybrid"
 
     def _decide_resident(self) -> bool:
-        """Collective over every rank (Session.__init__): whether Bob's server epochs run on the
-        register-resident executor (engine/resident.py decide: fits on one shard; tensor-
-        parallel, every Bob rank's self-test passed with the same replicated fc3, otherwise the
-        peer-mapped region is re-armed on every rank and Bob keeps the launch-per-stage
-        executor).  The outcome and its reason land in `resident_status` (bench JSON)."""
+        """Collective over every rank (Session.__init__): which persistent executor, if any,
+        runs Bob's server epochs (engine/resident.py decide: the register-resident epoch where
+        the shard fits on-chip, else the hybrid epoch; tensor-parallel, only after every Bob
+        rank's self-test passed with the same replicated fc3, otherwise the peer-mapped region
+        is re-armed on every rank and Bob keeps the launch-per-stage executor).  The outcome
+        and its reason land in `server_executor` / `resident_status` (bench JSON).  Returns
+        whether the register-resident executor was adopted."""
         from ..engine import resident
         want = getattr(self.args, "resident", "auto") != "off" and getattr(self.args, "dtype", "fp32") == "fp32"
-        ok, why = resident.decide(self.tail if self.is_bob else None, self.bob_slot if self.is_bob else None,
-                                  self.B, self.comm.distributed, want)
-        self.resident_status = {"adopted": ok, "reason": why}
-        return ok
+        want_h = getattr(self.args, "hybrid", "auto") != "off"
+        kind, why = resident.decide(self.tail if self.is_bob else None, self.bob_slot if self.is_bob else None,
+                                    self.B, self.comm.distributed, want, want_h)
+        self.server_executor = kind
+        self.resident_status = {"executor": kind, "reason": why, "adopted": kind == "resident"}
+        return kind == "resident"
 
     def server_epoch(self, acts, labels):
         """One pass of Bob's optimizer over one client's cached activations (batch order as
@@ -302,6 +308,12 @@ class SisaSession(Session):
             # a narrow (tensor-parallel) shard: every full batch in one persistent launch with
             # the shard's weights and Adam state on-chip (csrc/resident.hip)
             self.tail.run_resident_epoch(acts.contiguous(), labels.contiguous(), self.bob_slot, B)
+            self.comm.progress()
+            return
+        if n >= B and self._use_hybrid():
+            # a wide shard: every full batch in one persistent launch with fc2 / fc3 on-chip and
+            # fc1 streamed (csrc/hybrid.hip)
+            self.tail.run_hybrid_epoch(acts.contiguous(), labels.contiguous(), self.bob_slot, B)
             self.comm.progress()
             return
         if self._use_graphs() and n // B >= G:

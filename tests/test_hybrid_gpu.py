@@ -14,6 +14,9 @@ re-synchronised inside one launch, so:
   the launch-per-stage executor, small odd shapes) stay close to torch over free-running steps.
 """
 import copy
+import os
+import subprocess
+import sys
 
 import pytest
 import torch
@@ -185,3 +188,17 @@ def test_hybrid_table_covers_every_tile_once(cuda):
     NC = G // 8
     hn = tab[G + 1 + 2 * nrb:]
     assert len(hn) == NC and sum(hn) >= nrb and min(hn) >= 1
+
+
+@pytest.mark.parametrize("T", [2, 4])
+def test_hybrid_tensor_parallel_across_processes_on_one_gpu(T):
+    """T = 2 / 4 real processes, each a hybrid persistent launch of 256 / T workgroups on the one
+    GPU, the fc2 product exchanged through the peer-mapped region in-launch (8-byte tagged
+    granules summed in rank order): replicated state and losses bitwise equal across ranks and
+    close to torch (scripts/resident_tp_one_gpu.py hybrid)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, os.path.join(root, "scripts", "resident_tp_one_gpu.py"), str(T), "hybrid"],
+                         capture_output=True, text=True, timeout=110, cwd=root)
+    text = out.stdout + out.stderr
+    assert out.returncode == 0, text[-3000:]
+    assert out.stdout.count("PASS") == T, text[-3000:]
