@@ -39,8 +39,10 @@ def worker(rank, world, port, kind):
     print(f"rank {rank}: ipc {'up' if ipc is not None else 'unavailable'}", flush=True)
     ok = ipc is not None
     if ok:
-        spec = TailSpec([LinearSpec("fc1", 1024, 96 * world, True, 0.25), LinearSpec("fc2", 96 * world, 256, True, 0.25),
-                         LinearSpec("fc3", 256, 10, False, 0.0)])
+        # fc2 width: the resident executor holds <= 4 fc2 rows per workgroup (256 / T workgroups)
+        n2 = min(256, 4 * (256 // world))
+        spec = TailSpec([LinearSpec("fc1", 1024, 96 * world, True, 0.25), LinearSpec("fc2", 96 * world, n2, True, 0.25),
+                         LinearSpec("fc3", n2, 10, False, 0.0)])
         B, n, seed_base = 16, 16 * 6, 5
         g = torch.Generator().manual_seed(3)
         acts = (torch.rand(n, 1024, generator=g) * 4).to(dev)

@@ -190,7 +190,7 @@ def test_hybrid_table_covers_every_tile_once(cuda):
     assert len(hn) == NC and sum(hn) >= nrb and min(hn) >= 1
 
 
-@pytest.mark.parametrize("T", [2, 4])
+@pytest.mark.parametrize("T", [2, 4, 8])
 def test_hybrid_tensor_parallel_across_processes_on_one_gpu(T):
     """T = 2 / 4 real processes, each a hybrid persistent launch of 256 / T workgroups on the one
     GPU, the fc2 product exchanged through the peer-mapped region in-launch (8-byte tagged

@@ -176,9 +176,10 @@ def test_resident_rejects_a_wide_shard(cuda):
     assert not te.resident_ok(slot, 16)          # fc1 5000 rows: the launch-per-stage executor
 
 
-@pytest.mark.parametrize("T", [2, 4])
+@pytest.mark.parametrize("T", [2, 4, 8])
 def test_resident_tensor_parallel_across_processes_on_one_gpu(T):
-    """T = 2 / 4 real processes, each a persistent launch of 256 / T workgroups on the one GPU,
+    """T = 2 / 4 / 8 real processes, each a persistent launch of 256 / T workgroups on the one GPU
+    (T = 8: the multi-GPU granule protocol at its production width, on a scaled-down tail),
     the fc2 exchange through the peer-mapped region in-launch (T-source granule sums): replicated
     state and losses bitwise equal across ranks and close to torch
     (scripts/resident_tp_one_gpu.py)."""
