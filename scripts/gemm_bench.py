@@ -4,7 +4,10 @@ fp32 tile forms (slot 10: 0 = the default routing (32x32x2 MFMA, 256 x 128 tiles
 tiles split over K for small grids); 1..4 = 32x32x2 with (WM, BK) = (2, 16) (4, 16) (2, 32)
 (4, 32), no split; 5 = 16x16x4, 256 x 128), checked against torch, plus the bf16 form.
 
-    python scripts/gemm_bench.py [--forms 0 1 2 3 4] [--reps 8]
+    python scripts/gemm_bench.py [--forms 0 1 2 3 4] [--reps 8] [--dgrad]
+
+`--dgrad`: the data-gradient product dX = dZ . W (NN layout, csrc/gemm.hip gemm_nn_dgrad, the
+previous layer's ReLU mask fused) against torch.mm(dZ, W) on the same shapes.
 """
 import argparse
 import os
@@ -32,6 +35,7 @@ def main():
     ap.add_argument("--forms", type=int, nargs="+", default=[0, 2, 5])
     ap.add_argument("--reps", type=int, default=8)
     ap.add_argument("--shapes", default="all", choices=("all", "eval", "big"))
+    ap.add_argument("--dgrad", action="store_true")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     C = H.C()
@@ -41,6 +45,22 @@ def main():
             shapes += [(M, 5000, 5408), (M, 1000, 5000), (M, 100, 1000)]
     if a.shapes in ("all", "big"):
         shapes.append((4096, 4096, 4096))
+    if a.dgrad:
+        for M, N, K in shapes:
+            # forward Y[M, N] = X[M, K] W[N, K]^T  ->  its data gradient dX[M, K] = dY[M, N] W[N, K]
+            torch.manual_seed(0)
+            dz = torch.randn(M, N, device=dev)
+            w = torch.randn(N, K, device=dev) / N ** 0.5
+            h = torch.relu(torch.randn(M, K, device=dev))
+            fl = 2.0 * M * N * K
+            ref = torch.where(h > 0, (dz @ w) * 2.0, torch.zeros(1, device=dev))
+            t_mm = bench(lambda: torch.mm(dz, w), a.reps)
+            y = H.linear_dgrad(dz, w, h, 2.0)
+            err = ((y - ref).abs().max() / ref.abs().max()).item()
+            t = bench(lambda: H.linear_dgrad(dz, w, h, 2.0), a.reps)
+            print(f"dgrad M={M} N={N} K={K}: torch.mm fp32 {fl / t_mm / 1e12:.1f} TF | in-tree NN (mask fused) "
+                  f"{fl / t / 1e12:.1f} TF ({100 * t_mm / t:.0f} %, rel err {err:.1e})", flush=True)
+        return
     for M, N, K in shapes:
         torch.manual_seed(0)
         x = torch.randn(M, K, device=dev)

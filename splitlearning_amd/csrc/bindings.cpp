@@ -47,6 +47,8 @@ hipError_t linear_dgrad(const float* dZ, int ldz, const float* W, int ldw, const
                         hipStream_t st);
 hipError_t linear_epilogue(const float* P, int ldp, float* Y, int ldy, int M, int N, Epi e, int S, int64_t slab,
                            hipStream_t st);
+hipError_t gemm_nn_dgrad(const float* dZ, int ldz, const float* W, int ldw, const float* hprev, int ldh, float scale,
+                         float* dX, int ldx, int M, int R, int K, float* ws, int64_t ws_elems, hipStream_t st);
 hipError_t linear_fwd_partial(const float* X, int ldx, const float* W, int ldw, int M, int N, int K, float* ws,
                               int64_t ws_elems, int max_split, int* S_out, hipStream_t st);
 hipError_t linear_wgrad_opt(const float* dZ, int ldz, const float* A, int lda, float* W, int ldw, float* s0,
@@ -485,6 +487,38 @@ void linear_dgrad(const at::Tensor& dZ, const at::Tensor& W, const OptT& hprev, 
         "linear_dgrad");
 }
 
+// the data gradient of many rows on the in-tree NN-layout MFMA GEMM (csrc/gemm.hip)
+void gemm_nn_dgrad(const at::Tensor& dZ, const at::Tensor& W, const OptT& hprev, double scale, at::Tensor& dX,
+                   const OptT& ws) {
+  need_2d(dZ, "dZ");
+  need_rows(W, "W");
+  need_2d(dX, "dX");
+  const int64_t M = dZ.size(0), N = dZ.size(1), K = W.size(1);
+  TORCH_CHECK(W.size(0) == N && K % 4 == 0 && N % 4 == 0, "W must be [N,K], N and K % 4 == 0");
+  TORCH_CHECK(dX.size(0) == M && dX.size(1) == K, "dX must be [M,K]");
+  TORCH_CHECK(dZ.stride(0) % 4 == 0 && W.stride(0) % 4 == 0, "rows 16-B aligned");
+  const float* hp = nullptr;
+  int ldh = 0;
+  if (hprev.has_value() && hprev->defined()) {
+    need_2d(*hprev, "hprev");
+    TORCH_CHECK(hprev->size(0) == M && hprev->size(1) == K, "hprev shape");
+    hp = hprev->data_ptr<float>();
+    ldh = (int)hprev->stride(0);
+  }
+  float* wp = nullptr;
+  int64_t wn = 0;
+  if (ws.has_value() && ws->defined()) {
+    need_f32(*ws, "ws");
+    TORCH_CHECK(ws->is_contiguous(), "ws contiguous");
+    wp = ws->data_ptr<float>();
+    wn = ws->numel();
+  }
+  check(sl::gemm_nn_dgrad(dZ.data_ptr<float>(), (int)dZ.stride(0), W.data_ptr<float>(), (int)W.stride(0), hp, ldh,
+                          (float)scale, dX.data_ptr<float>(), (int)dX.stride(0), (int)M, (int)N, (int)K, wp, wn,
+                          cur_stream()),
+        "gemm_nn_dgrad");
+}
+
 void linear_wgrad_opt(const at::Tensor& dZ, const at::Tensor& A, at::Tensor& W, at::Tensor& s0, const OptT& s1,
                       const OptT& bias, const OptT& sb0, const OptT& sb1, OPT_ARGS) {
   need_2d(dZ, "dZ");
@@ -698,6 +732,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("linear_fwd", &linear_fwd);
   m.def("linear_epilogue", &linear_epilogue);
   m.def("linear_dgrad", &linear_dgrad);
+  m.def("gemm_nn_dgrad", &gemm_nn_dgrad);
   m.def("linear_wgrad_opt", &linear_wgrad_opt);
   m.def("opt_flat", &opt_flat);
   m.def("softmax_ce", &softmax_ce);

@@ -281,6 +281,150 @@ gemm_nt_f32x32_kernel(const float* __restrict__ X, int ldx, const float* __restr
     }
 }
 
+// NN layout for the data gradient of many rows: dX[M, K] = mask(dZ[M, R] . W[R, K]) (W as
+// stored, [out features][in features]; reference: the backward of nn.Linear through
+// split_nn.py:156's --batch_size rows, data_entities_vanilla.py:231).  Same 32 x 32 x 2 fp32
+// MFMA tiling as gemm_nt_f32x32_kernel (BM x 128 output tile, 16-deep reduction stages,
+// double-buffered LDS, next stage's loads before this stage's MFMAs).  A (= dZ) is staged as
+// in the NT form; B (= W) is read along its rows (coalesced float4 along the output columns)
+// and kept in LDS as [reduction][column] (pitch 132: the two lane halves' rows land 32 banks
+// apart), each MFMA's B operand one conflict-free scalar read per lane (the float4-per-k
+// reads of the NT form would need a transposed, 8-way bank-conflicted staging store).
+// Epilogue: the previous layer's ReLU / dropout mask (hprev > 0 ? v scale : 0) fused into the
+// store; split over the reduction (gridDim.y = S > 1) stores raw slabs to P, reduced and
+// masked by dgrad_reduce.
+template <int WM>
+__global__ void __launch_bounds__(128 * WM)
+gemm_nn_f32x32_kernel(const float* __restrict__ A, int lda, const float* __restrict__ B, int ldb,
+                      float* __restrict__ Y, int ldy, int M, int N, int R, const float* __restrict__ hprev, int ldh,
+                      float scale, int kc, float* __restrict__ P) {
+  constexpr int BM = 64 * WM, BN = 128, NT = 128 * WM, BK = 16;
+  constexpr int LDA = BK + 4, LDB = BN + 4;
+  constexpr int F4A = BK / 4, F4B = BN / 4;
+  constexpr int APER = BM * F4A / NT, BPER = BK * F4B / NT;
+  static_assert(APER * NT == BM * F4A && BPER * NT == BK * F4B, "tile / thread split");
+  typedef float f32x16 __attribute__((ext_vector_type(16)));
+  __shared__ __attribute__((aligned(16))) float As[2][BM][LDA];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BK][LDB];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int tilesM = (M + BM - 1) / BM;
+  const int tm = blockIdx.x % tilesM, tn = blockIdx.x / tilesM;
+  const int m0 = tm * BM, n0 = tn * BN;
+  float4 ra[APER], rb[BPER];
+  const __amdgpu_buffer_rsrc_t rA = gemm_rsrc(A, (int64_t)M * lda * 4), rB = gemm_rsrc(B, (int64_t)R * ldb * 4);
+  const int kb = (int)blockIdx.y * kc, ke = min(R, kb + kc);
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int p = 0; p < APER; ++p) {
+      const int i = tid + p * NT, r = i / F4A, k = k0 + (i % F4A) * 4, gm = m0 + r;
+      ra[p] = gemm_ld(rA, gm < M && k < ke, (int64_t)gm * lda + k);
+    }
+#pragma unroll
+    for (int p = 0; p < BPER; ++p) {
+      const int i = tid + p * NT, r = k0 + i / F4B, c = n0 + (i % F4B) * 4;
+      rb[p] = gemm_ld(rB, r < ke && c < N, (int64_t)r * ldb + c);
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int p = 0; p < APER; ++p) {
+      const int i = tid + p * NT, r = i / F4A, k = (i % F4A) * 4;
+      *reinterpret_cast<float4*>(&As[buf][r][k]) = ra[p];
+    }
+#pragma unroll
+    for (int p = 0; p < BPER; ++p) {
+      const int i = tid + p * NT, r = i / F4B, c = (i % F4B) * 4;
+      *reinterpret_cast<float4*>(&Bs[buf][r][c]) = rb[p];
+    }
+  };
+  const int wm = (wv % WM) * 64, wn = (wv / WM) * 64;
+  const int lr = lane & 31, h = lane >> 5;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const int nk = (ke - kb + BK - 1) / BK;
+  gload(kb);
+  sstore(0);
+  __syncthreads();
+  for (int s = 0; s < nk; ++s) {
+    const int buf = s & 1;
+    gload(kb + (s + 1 < nk ? s + 1 : s) * BK);
+    __builtin_amdgcn_sched_barrier(0);          // the loads go out before the MFMAs
+    // step (q, c) of lane half h reduces logical k = 8 h + 4 q + c (the NT form's order)
+    f32x4 a[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) a[i][q] = *reinterpret_cast<const f32x4*>(&As[buf][wm + 32 * i + lr][8 * h + 4 * q]);
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int k = 8 * h + 4 * q + c;
+        const float b0 = Bs[buf][k][wn + lr], b1 = Bs[buf][k][wn + 32 + lr];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][q][c], b0, acc[i][0], 0, 0, 0);
+          acc[i][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][q][c], b1, acc[i][1], 0, 0, 0);
+        }
+      }
+    __builtin_amdgcn_sched_barrier(0);
+    sstore(buf ^ 1);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + wn + 32 * j + lr;
+      if (n >= N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (m >= M) continue;
+        const float v = acc[i][j][r];
+        if (P) {
+          P[((int64_t)blockIdx.y * M + m) * N + n] = v;
+        } else {
+          Y[(int64_t)m * ldy + n] = hprev ? (hprev[(int64_t)m * ldh + n] > 0.f ? v * scale : 0.f) : v;
+        }
+      }
+    }
+}
+
+hipError_t dgrad_reduce(const float* P, int S, int64_t slab, const float* hprev, int ldh, float scale, float* out,
+                        int ldo, int M, int K, hipStream_t st);
+
+// dX[M, K] = mask(dZ[M, R] . W[R, K]): 256 x 128 tiles when they fill the chip, else 128 x 128
+// tiles split over the reduction until ~2 workgroups per CU (slices >= 256 deep, <= 8).
+hipError_t gemm_nn_dgrad(const float* dZ, int ldz, const float* W, int ldw, const float* hprev, int ldh, float scale,
+                         float* dX, int ldx, int M, int R, int K, float* ws, int64_t ws_elems, hipStream_t st) {
+  if (M <= 0 || K <= 0) return hipSuccess;
+  if ((R & 3) || (K & 3) || (ldz & 3) || (ldw & 3)) return hipErrorInvalidValue;
+  constexpr int64_t kMax = 0x7fff0000;
+  if ((int64_t)M * ldz * 4 > kMax || (int64_t)R * ldw * 4 > kMax) return hipErrorInvalidValue;
+  const int64_t t4 = (int64_t)((M + 255) / 256) * ((K + 127) / 128);
+  if (t4 >= 384) {
+    gemm_nn_f32x32_kernel<4><<<(unsigned)t4, 512, 0, st>>>(dZ, ldz, W, ldw, dX, ldx, M, K, R, hprev, ldh, scale, R,
+                                                          nullptr);
+    return hipGetLastError();
+  }
+  const int64_t t2 = (int64_t)((M + 127) / 128) * ((K + 127) / 128);
+  if (t2 > 0x7fffffff) return hipErrorInvalidValue;
+  int S = 1;
+  if (ws == nullptr) ws_elems = 0;
+  while (S < 8 && t2 * S * 2 <= 640 && R / (S * 2) >= 256 && (int64_t)S * 2 * M * K <= ws_elems) S *= 2;
+  const int kc = S > 1 ? ((R + S - 1) / S + 15) / 16 * 16 : R;
+  gemm_nn_f32x32_kernel<2><<<dim3((unsigned)t2, S), 256, 0, st>>>(dZ, ldz, W, ldw, dX, ldx, M, K, R, hprev, ldh,
+                                                                 scale, kc, S > 1 ? ws : nullptr);
+  if (S > 1) return dgrad_reduce(ws, S, (int64_t)M * K, hprev, ldh, scale, dX, ldx, M, K, st);
+  return hipGetLastError();
+}
+
 hipError_t linear_epilogue(const float* P, int ldp, float* Y, int ldy, int M, int N, Epi e, int S, int64_t slab,
                            hipStream_t st);
 

@@ -474,6 +474,14 @@ static void launch_dgrad_reduce(const float* P, int S, int64_t slab, const float
   dgrad_reduce_kernel<<<(unsigned)((tot + 255) / 256), 256, 0, st>>>(P, S, slab, hprev, ldh, scale, out, ldo, M, K);
 }
 
+// the split-K reduction + ReLU / dropout mask of a data gradient computed elsewhere (gemm.hip)
+hipError_t dgrad_reduce(const float* P, int S, int64_t slab, const float* hprev, int ldh, float scale, float* out,
+                        int ldo, int M, int K, hipStream_t st) {
+  if (M <= 0 || K <= 0) return hipSuccess;
+  launch_dgrad_reduce(P, S, slab, hprev, ldh, scale, out, ldo, M, K, st);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------- wgrad + optimizer
 // v3: memory-level parallelism first.  A 1024-thread workgroup owns a 16-row x 256-column
 // tile; every wave covers one row's 256 contiguous weights (1 KB per instruction), so each

@@ -206,15 +206,13 @@ def set_compute_dtype(dtype: str):
 
 
 def _library_gemm(M: int, dgrad: bool = False) -> bool:
-    """Whether a product of M > 128 rows goes to hipBLASLt: the forward only under variant
-    11 = 2, the fp32 data gradient unless variant 11 = 1; never inside a HIP graph capture
-    (the library may not allocate or initialise there)."""
+    """Whether a product of M > 128 rows goes to hipBLASLt: only under variant 11 = 2 (the A/B
+    slot of scripts/gemm_bench.py); never inside a HIP graph capture (the library may not
+    allocate or initialise there).  Default: the in-tree tiled MFMA GEMMs (csrc/gemm.hip: the NT
+    form for forwards, the NN form for data gradients)."""
     if M <= LARGE_M or torch.cuda.is_current_stream_capturing():
         return False
-    v = C().get_variant(11)
-    if dgrad:
-        return C().get_compute_dtype() == "fp32" and v != 1
-    return v == 2
+    return C().get_variant(11) == 2
 
 
 def linear_fwd(x, w, b, relu: bool, drop_p: float, seed: int, col_offset: int = 0, out=None, dseed=None):
@@ -277,15 +275,20 @@ def linear_dgrad(dz, w, h_prev=None, scale: float = 1.0, out=None, ws=None):
     M, K = dz.shape[0], w.shape[1]
     if out is None:
         out = torch.empty(M, K, device=dz.device, dtype=torch.float32)
-    if _library_gemm(M, dgrad=True):
-        # many rows (large --batch_size): the skinny kernel would re-read W once per 16 rows;
-        # the product goes to hipBLASLt (as the forward does) and the previous layer's
-        # ReLU/dropout mask + scale is one in-tree elementwise launch
-        P = torch.mm(dz, w.detach())
-        if h_prev is not None:                   # scale belongs to the mask (dropout 1/(1-p))
-            C().relu_mask(P, h_prev.contiguous(), float(scale), out)
-        else:
-            out.copy_(P)
+    if M > LARGE_M and dz.shape[1] % 4 == 0 and K % 4 == 0 and C().get_compute_dtype() == "fp32":
+        if _library_gemm(M, dgrad=True):
+            # A/B only (variant 11 = 2): hipBLASLt product + the in-tree mask launch
+            P = torch.mm(dz, w.detach())
+            if h_prev is not None:               # scale belongs to the mask (dropout 1/(1-p))
+                C().relu_mask(P, h_prev.contiguous(), float(scale), out)
+            else:
+                out.copy_(P)
+            return out
+        # many rows (large --batch_size, evaluation): the in-tree NN-layout MFMA GEMM
+        # (csrc/gemm.hip gemm_nn_dgrad) with the previous layer's ReLU / dropout mask fused
+        if ws is None and ((M + 127) // 128) * ((K + 127) // 128) < 384:
+            ws = _workspace(dz.device, 8 * M * K, "gemm")
+        C().gemm_nn_dgrad(dz, w.detach(), h_prev.contiguous() if h_prev is not None else None, float(scale), out, ws)
         return out
     if ws is None:
         ws = _workspace(dz.device, 16 * M * K)

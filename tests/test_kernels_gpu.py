@@ -539,3 +539,24 @@ def test_xcd_grouped_fc2_products(cuda, M):
     _close(hip_ops.linear_dgrad(dz, w, h, 2.0), torch_ops.linear_dgrad(dz, w, h, 2.0), rtol=1e-4, atol=1e-4)
     w8, h8 = w[:, :628].contiguous(), h[:, :628].contiguous()
     _close(hip_ops.linear_dgrad(dz, w8, h8, 2.0), torch_ops.linear_dgrad(dz, w8, h8, 2.0), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("M,R,K,mask", [(200, 1000, 5000, True), (1000, 5000, 5408, False), (14000, 1000, 5000, True),
+                                        (130, 100, 1000, True)])
+def test_nn_dgrad_gemm_matches_torch(M, R, K, mask):
+    """The in-tree NN-layout MFMA GEMM for data gradients of many rows (csrc/gemm.hip
+    gemm_nn_dgrad; reference: nn.Linear's backward at --batch_size rows, split_nn.py:156):
+    dX = (dZ . W) masked by the previous layer's ReLU / dropout (h > 0 ? . scale : 0), against
+    fp32 torch, through ops.hip_ops.linear_dgrad's large-M route (no hipBLASLt)."""
+    import torch
+    from splitlearning_amd.ops import hip_ops as H
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device="cpu").manual_seed(M + K)
+    dz = torch.randn(M, R, generator=g).to(dev)
+    w = (torch.randn(R, K, generator=g) / R ** 0.5).to(dev)
+    h = torch.relu(torch.randn(M, K, generator=g)).to(dev) if mask else None
+    out = H.linear_dgrad(dz, w, h, 2.0 if mask else 1.0)
+    ref = (dz.double() @ w.double())
+    if mask:
+        ref = torch.where(h > 0, ref * 2.0, torch.zeros_like(ref))
+    torch.testing.assert_close(out.double(), ref, rtol=1e-4, atol=1e-4 * ref.abs().max().item())
