@@ -83,6 +83,22 @@ def _ipc_status():
     return dict(IPC_STATUS) if IPC_STATUS else None
 
 
+def _channel_kind(sess):
+    ch = getattr(sess, "split_channel", None)
+    if ch is None:
+        return None
+    return "ipc" if hasattr(ch, "host_error") else "rccl"
+
+
+def _gathered_split(sess):
+    """Native split epochs by kind, summed over the ranks (gathered before rank 0 reports)."""
+    tot = {}
+    for d in getattr(sess, "_split_counts_all", None) or []:
+        for k, v in (d or {}).items():
+            tot[k] = tot.get(k, 0) + v
+    return tot
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -251,6 +267,7 @@ def main(argv=None):
                     if _phase_kind(sargs.mode, r["phase"]) is not None)
         base = samples / ref_t
     sent = comm.gather_obj((comm.bytes_sent - b0) // max(1, a.steps), 0)
+    sess._split_counts_all = comm.gather_obj(dict(getattr(sess, "native_split_epochs", {})), 0)
     if rank == 0:
         kern = "torch" if (not use_gpu or ops.get_backend() == "torch") else "hip"
         tpc = getattr(sess, "tp_native_comm", None)
@@ -288,6 +305,10 @@ def main(argv=None):
                 # why: adopted, or the fit / self-test outcome that kept launch-per-stage
                 "server_executor_reason": (getattr(sess, "resident_status", None) or {}).get("reason"),
                 "calib": calib,
+                # vanilla / U-shape: the native split epochs this rank ran (co-located, or its
+                # side of a remote Alice's) and the per-batch link of the remote ones
+                "split_epochs": _gathered_split(sess) if sargs.mode in ("vanilla", "ushape") else None,
+                "split_channel": _channel_kind(sess) if sargs.mode in ("vanilla", "ushape") else None,
             },
         }
         line = json.dumps(out)

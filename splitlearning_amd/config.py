@@ -138,6 +138,11 @@ def build_parser() -> argparse.ArgumentParser:
                         "fc1's weights / Adam state streamed through the launch (csrc/hybrid.hip); "
                         "'auto' uses it where it fits and, tensor-parallel, after a cross-rank "
                         "self-test passed; 'off' = the launch-per-stage executor")
+    g.add_argument("--split_channel", choices=("auto", "ipc", "rccl"), default="auto",
+                   help="vanilla / U-shape with the Alice remote from a one-shard Bob: the native "
+                        "split epoch's per-batch link.  'auto' / 'ipc' = one-kernel messages over "
+                        "peer-mapped HBM (csrc/ipc_p2p.h) when every rank sets it up and passes its "
+                        "self-test ('auto' falls back to RCCL), 'rccl' = ncclSend / ncclRecv")
     g.add_argument("--tp_allreduce", choices=("auto", "rccl"), default="auto",
                    help="Bob's per-step TP all-reduce: 'auto' = one kernel over peer-mapped HBM "
                         "(csrc/ipc_ar.h) when every Bob rank sets it up and passes its self-test, "

@@ -15,6 +15,7 @@
 #include <string>
 
 #include "comm.h"
+#include "ipc_p2p.h"
 
 namespace py = pybind11;
 
@@ -147,6 +148,34 @@ void sl_register_comm(py::module& m) {
       .def_property_readonly("cap", &sl::IpcAllReduce::cap)
       .def_property_readonly("rank", &sl::IpcAllReduce::rank)
       .def_property_readonly("size", &sl::IpcAllReduce::size);
+  py::class_<sl::IpcChannel>(m, "IpcChannel")
+      .def(py::init<int, int, int64_t>(), py::arg("nranks"), py::arg("rank"), py::arg("cap"))
+      .def("handle", [](const sl::IpcChannel& a) { return py::bytes(a.handle()); })
+      .def("open", [](sl::IpcChannel& a, const std::vector<py::bytes>& hs) {
+        std::vector<std::string> v;
+        for (const auto& h : hs) v.emplace_back(std::string(h));
+        a.open(v);
+      })
+      // tensor-level send / recv (any dtype, viewed as 4-byte words) on the current stream
+      .def("send", [](sl::IpcChannel& a, const at::Tensor& t, int peer) {
+        need(t);
+        TORCH_CHECK(t.nbytes() % 16 == 0, "IpcChannel: messages are whole 16-byte units");
+        a.send(static_cast<const float*>(t.data_ptr()), (int64_t)(t.nbytes() / 4), peer, stream());
+      })
+      .def("recv", [](sl::IpcChannel& a, at::Tensor& t, int peer) {
+        need(t);
+        TORCH_CHECK(t.nbytes() % 16 == 0, "IpcChannel: messages are whole 16-byte units");
+        a.recv(static_cast<float*>(t.data_ptr()), (int64_t)(t.nbytes() / 4), peer, stream());
+      })
+      .def("error", &sl::IpcChannel::error)
+      .def("host_error", &sl::IpcChannel::host_error)
+      .def("set_timeout_s", &sl::IpcChannel::set_timeout_s)
+      .def("sent", &sl::IpcChannel::sent)
+      .def("received", &sl::IpcChannel::received)
+      .def_property_readonly("timeout_s", &sl::IpcChannel::timeout_s)
+      .def_property_readonly("cap", &sl::IpcChannel::cap)
+      .def_property_readonly("rank", &sl::IpcChannel::rank)
+      .def_property_readonly("size", &sl::IpcChannel::size);
   m.def("nccl_unique_id", &unique_id);
   int v = 0;
   ncclGetVersion(&v);

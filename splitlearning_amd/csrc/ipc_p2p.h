@@ -1,0 +1,101 @@
+// Point-to-point messages over peer-mapped HBM (`_C.IpcChannel`): the split-mode data plane
+// (activation + labels to Bob, cut gradient back; U-shape also the middle output and its
+// gradient) between two processes, issued from C++ on the compute stream.
+//
+// Why: the split modes move 2 - 4 latency-bound messages per batch.  RCCL cannot pair two
+// ranks on one GPU at all (the --ranks_share_gpu rehearsal), and across GPUs an ncclSend /
+// ncclRecv pair is a proxy-driven protocol with its own launch per call.  Here every rank
+// exports one receive region (uncached device memory) and maps every peer's once; a send is
+// ONE kernel on the sender that writes the message straight into the receiver's region over
+// the xGMI link (one hop) and raises a per-chunk flag, a receive is ONE kernel that waits on
+// its own flags and copies the message out.
+//
+// Protocol (per ordered pair s -> d, generation g = the pair's message count, kept by both
+// sides in program order):
+//   sender s, workgroup c (chunk c of kIpcChunk floats):
+//     wait ack[d][par][c] >= g - 2 in ITS OWN region (d has read what the slot held two
+//     messages ago; parity par = g & 1 double-buffers the slot) ->
+//     16-B write-through stores of the chunk into d's data[s][par] -> drain -> release ->
+//     flag[s][par][c] = g in d's region;
+//   receiver d, workgroup c:
+//     wait flag[s][par][c] >= g in its own region -> acquire -> copy the chunk out -> drain ->
+//     ack[d][par][c] = g in s's region.
+// Memory ordering as ipc_ar.h (system scope, release before the flag, acquire after it).
+// Every wait is bounded by wall clock; a timeout raises the error word (and its host-pinned
+// mirror) and every later wait on this rank gives up at once, so a dead peer costs one
+// timeout and the job reads the word at the end of the epoch.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "ipc_ar.h"
+
+namespace sl {
+
+// One message's view of the regions, handed to the send / receive kernel
+struct P2PMsg {
+  float* data;          // send: the receiver's slot data[me][par]; recv: own slot data[src][par]
+  uint32_t* flag;       // send: the receiver's flag[me][par][0..]; recv: own flag[src][par][0..]
+  uint32_t* ack;        // send: own ack[dst][par][0..];           recv: the sender's ack[me][par][0..]
+  uint32_t gen;
+  int* err;
+  int* herr;
+  int64_t timeout;      // wall-clock ticks
+};
+
+class IpcChannel {
+ public:
+  // cap: the largest message (floats) this channel carries
+  IpcChannel(int nranks, int rank, int64_t cap);
+  ~IpcChannel();
+  IpcChannel(const IpcChannel&) = delete;
+  IpcChannel& operator=(const IpcChannel&) = delete;
+  std::string handle() const;
+  void open(const std::vector<std::string>& handles);
+  // n floats from x (16-B aligned, n % 4 == 0, n <= cap) to / from rank `peer`, on stream st.
+  // Stream-ordered; every call of a pair advances that pair's generation on both sides.
+  void send(const float* x, int64_t n, int peer, hipStream_t st);
+  void recv(float* x, int64_t n, int peer, hipStream_t st);
+  bool serves(const void* p, int64_t n) const {
+    return n <= cap_ && n % 4 == 0 && (reinterpret_cast<uintptr_t>(p) & 15) == 0;
+  }
+  int error() const;
+  int host_error() const { return __atomic_load_n(herr_, __ATOMIC_ACQUIRE); }
+  void set_timeout_s(double s) { timeout_ = (int64_t)(s * 1000.0 * clock_khz_); }
+  double timeout_s() const { return (double)timeout_ / (1000.0 * clock_khz_); }
+  int64_t cap() const { return cap_; }
+  int rank() const { return rank_; }
+  int size() const { return nranks_; }
+  bool opened() const { return opened_; }
+  uint32_t sent(int peer) const { return send_gen_.at(peer); }
+  uint32_t received(int peer) const { return recv_gen_.at(peer); }
+
+ private:
+  // region layout (floats / words): data [T src][2][cap]; sync words [2 kinds][T][2][nch]
+  // (kind 0 flags indexed by the source, kind 1 acks indexed by the destination)
+  void check(const void* x, int64_t n, int peer) const;
+  int64_t flag_off(int src, int par) const { return ((int64_t)src * 2 + par) * nch_; }
+  int64_t ack_off(int dst, int par) const { return ((int64_t)(nranks_ + dst) * 2 + par) * nch_; }
+  int nranks_, rank_;
+  int64_t cap_;
+  int nch_;
+  float* data_ = nullptr;
+  uint32_t* syncw_ = nullptr;
+  int* err_ = nullptr;
+  int* herr_ = nullptr;
+  int* herr_dev_ = nullptr;
+  float* peer_data_[kIpcMaxRanks] = {};
+  uint32_t* sync_[kIpcMaxRanks] = {};
+  std::vector<void*> mapped_;
+  std::vector<uint32_t> send_gen_, recv_gen_;
+  std::vector<int> hist_;      // [peer][parity]: chunk count of the last message sent on it
+  bool opened_ = false;
+  int64_t timeout_ = 0;
+  int clock_khz_ = 100000;
+};
+
+}  // namespace sl

@@ -35,7 +35,7 @@ def measure(comm, device, B: int = 16, iters: int = 20, warmup: int = 3, allredu
     the Bob ranks `tp_ranks` are given; every Bob rank must pass the same hook)."""
     if not comm.distributed:
         return {}
-    n_pkt, n_grad = B * CUT_FEATURES + B, B * CUT_FEATURES
+    n_pkt, n_grad = B * CUT_FEATURES + 2 * B, B * CUT_FEATURES   # labels as int64 words (Session.pack)
     pkt = torch.ones(n_pkt, device=device)
     grad = torch.ones(n_grad, device=device)
     per_peer = {}

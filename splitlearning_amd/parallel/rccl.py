@@ -169,3 +169,70 @@ def make_ipc_allreduce(ranks: list[int], my_rank: int, cap: int = IPC_AR_CAP, gr
         IPC_STATUS["fallback"] = "rccl"
         return None
     return ipc if member else None
+
+
+def _channel_self_test(ch, iters: int = 12) -> bool:
+    """Ring messages over the channel (rank r -> r + 1), every size class it serves and both
+    parity slots several times over, checked element-wise (exact: the values are copied)."""
+    T, me = ch.size, ch.rank
+    if T < 2:
+        return True
+    dev = torch.device("cuda", torch.cuda.current_device())
+    old = ch.timeout_s
+    ch.set_timeout_s(5.0)
+    try:
+        for it in range(iters):
+            n = (4, 1028, 16 * 5408 + 32, ch.cap)[it % 4]
+            src = (me - 1) % T
+            out = (torch.arange(n, dtype=torch.float32) * 0.25 + 1000 * me + it).to(dev)
+            got = torch.empty(n, device=dev)
+            ch.send(out, (me + 1) % T)
+            ch.recv(got, src)
+            want = torch.arange(n, dtype=torch.float32) * 0.25 + 1000 * src + it
+            torch.cuda.synchronize(dev)
+            if ch.error() != 0 or not torch.equal(got.cpu(), want):
+                return False
+        return True
+    finally:
+        ch.set_timeout_s(old)
+
+
+# Outcome of the last split-channel set-up on this process (bench.py reports it)
+CHANNEL_STATUS: dict = {}
+
+
+def make_ipc_channel(cap: int, group=None):
+    """Collective over every process: a peer-mapped point-to-point channel (`_C.IpcChannel`,
+    csrc/ipc_p2p.h) over all ranks, carrying messages of up to `cap` floats — returned after
+    set-up AND a ring self-test passed on every rank; None everywhere otherwise."""
+    from .. import _native
+    C = _native.load()
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    ch, h, err = None, None, None
+    try:
+        ch = C.IpcChannel(world, rank, cap)
+        h = ch.handle()
+    except RuntimeError as e:
+        ch, err = None, e
+    hs = [None] * world
+    dist.all_gather_object(hs, h, group=group)
+    if ch is not None:
+        if any(x is None for x in hs):
+            err = "a peer could not export its region"
+        else:
+            try:
+                ch.open(hs)
+            except RuntimeError as e:
+                err = e
+    CHANNEL_STATUS.clear()
+    CHANNEL_STATUS.update({"kind": "ipc", "setup": "ok" if err is None else str(err)[:200], "self_test": None})
+    if not _agree(err is None, group):
+        CHANNEL_STATUS["setup"] = CHANNEL_STATUS["setup"] if err is not None else "failed on another rank"
+        return None
+    try:
+        ok = _channel_self_test(ch)
+    except RuntimeError:
+        ok = False
+    agreed = _agree(ok, group)
+    CHANNEL_STATUS["self_test"] = bool(ok and agreed)
+    return ch if agreed else None

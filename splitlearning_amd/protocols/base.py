@@ -79,6 +79,7 @@ class Session:
         self._exchange_meta()
         self.is_bob = self.pl.is_bob(self.rank)
         self._native_data_plane()                          # collective over all ranks
+        self.split_channel = self._split_channel()        # collective over all ranks
         self.tp_allreduce = self._tp_allreduce()          # collective over all ranks
         self.timer.check = self._check_transport
         self.tail: TailEngine | None = None
@@ -169,6 +170,24 @@ class Session:
             from ..parallel.rccl import make_native_comm
             self.comm.native = make_native_comm(list(range(self.comm.world)), self.rank)
 
+    def _split_channel(self):
+        """The native split epoch's per-batch link for Alices remote from a one-shard Bob
+        (vanilla / U-shape; protocols/split_native.py): the peer-mapped channel
+        (`--split_channel auto|ipc`, csrc/ipc_p2p.h) or the RCCL communicator over all ranks.
+        None when no such placement exists or no link could be set up (the Python loop then
+        moves the messages)."""
+        if self.mode not in ("vanilla", "ushape") or self.device.type != "cuda" or not self.comm.distributed:
+            return None
+        if self.pl.bob_tp != 1 or all(r == self.pl.bob_root for r in self.pl.alice_ranks.values()):
+            return None
+        kind = getattr(self.args, "split_channel", "auto")
+        if kind in ("auto", "ipc"):
+            from ..parallel.rccl import make_ipc_channel
+            ch = make_ipc_channel(self.packed_len(self.B, torch.float32))
+            if ch is not None or kind == "ipc":
+                return ch
+        return self.comm.native
+
     def _tp_allreduce(self):
         """Bob's TP all-reduce: a native RCCL communicator on GPUs (capturable in the
         server-step graph), the torch.distributed group otherwise (gloo on CPU)."""
@@ -204,6 +223,10 @@ class Session:
     def _check_transport(self):
         """Phase-end check (after the device sync): the peer-mapped all-reduce's bounded waits
         raise an error word instead of hanging; a phase that hit one fails loudly here."""
+        ch = getattr(self, "split_channel", None)
+        if ch is not None and hasattr(ch, "host_error") and ch.error() != 0:
+            raise RuntimeError("peer-mapped split channel: a message wait timed out on this rank (the peer "
+                               "stalled or the mapping is broken); rerun with --split_channel rccl")
         ipc = getattr(self, "tp_ipc", None)
         if ipc is not None and ipc.error() != 0:
             raise RuntimeError("peer-mapped TP all-reduce: a flag wait timed out on this rank (a peer "
@@ -289,19 +312,31 @@ class Session:
         return self.to_bob(cid, t, (rows,) + tuple(inner_shape), dtype)
 
     @staticmethod
-    def pack(act: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
-        """One message per batch: [B*5408 activation | B labels] in the activation's dtype
-        (labels are small integers, exact in fp32 below 2^24 and in bf16 below 256)."""
+    def packed_len(B: int, dtype) -> int:
+        """Elements of one packed [activation | labels] message in the wire dtype: the labels
+        ride as int64 words behind the rows, the whole padded to 16-byte units (the layout the
+        native split executor sends too, csrc/split.cpp act_msg_words)."""
+        es = torch.empty((), dtype=dtype).element_size()
+        n = B * CUT_FEATURES + B * (8 // es)
+        unit = 16 // es
+        return -(-n // unit) * unit
+
+    @classmethod
+    def pack(cls, act: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+        """One message per batch: [B*5408 activation | B int64 labels] in the activation's
+        dtype (labels bit-exact whatever the wire dtype)."""
         B = act.shape[0]
-        buf = torch.empty(B * CUT_FEATURES + B, device=act.device, dtype=act.dtype)
+        buf = torch.zeros(cls.packed_len(B, act.dtype), device=act.device, dtype=act.dtype)
         buf[:B * CUT_FEATURES].view(B, CUT_FEATURES).copy_(act)
-        buf[B * CUT_FEATURES:].copy_(labels)
+        per = 8 // act.element_size()
+        buf[B * CUT_FEATURES:B * CUT_FEATURES + B * per].view(torch.int64).copy_(labels)
         return buf
 
     @staticmethod
     def unpack(buf: torch.Tensor, B: int):
         act = buf[:B * CUT_FEATURES].view(B, CUT_FEATURES)
-        labels = buf[B * CUT_FEATURES:].to(torch.int64)
+        per = 8 // buf.element_size()
+        labels = buf[B * CUT_FEATURES:B * CUT_FEATURES + B * per].view(torch.int64)
         return act, labels
 
     def send_act_labels(self, cid, act, labels, B):
@@ -314,7 +349,7 @@ class Session:
         if not remote:
             return (act, labels) if self.is_bob else (None, None)
         pkt = self.pack(act.to(wire), labels) if self.rank == host else None
-        got = self.comm.multicast(pkt, host, self.bob_ranks, (B * CUT_FEATURES + B,), wire)
+        got = self.comm.multicast(pkt, host, self.bob_ranks, (self.packed_len(B, wire),), wire)
         if not self.is_bob:
             return None, None
         if self.rank == host:

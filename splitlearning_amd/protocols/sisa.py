@@ -217,7 +217,7 @@ class SisaSession(Session):
                 sends += [(local[cid], b) for b in self.bob_ranks if b != h]
                 got[cid] = local[cid]
             elif self.is_bob:
-                got[cid] = torch.empty(n * CUT_FEATURES + n, device=self.device, dtype=self.act_dtype)
+                got[cid] = torch.empty(self.packed_len(n, self.act_dtype), device=self.device, dtype=self.act_dtype)
                 recvs.append((got[cid], h))
         self.comm.exchange(sends, recvs)
         for key in keys:

@@ -1,6 +1,9 @@
 """Native split-mode epochs: a vanilla / U-shape `split_epoch` issued from C++
 (`_C.SplitEpoch`, csrc/split.cpp) when the Alice and the whole Bob (TP = 1) live in this
-process — the one-GPU BASELINE point (ws = 2) and every co-located placement.
+process — the one-GPU BASELINE point (ws = 2) and every co-located placement — and, for an
+Alice remote from a one-shard Bob (BASELINE config 2, U-shape ws = 2 on 2 GPUs; vanilla
+with `--bob_tp 1`), each side's half of the same loop with the per-batch messages on the
+split channel (csrc/ipc_p2p.h peer-mapped messages, or RCCL).
 
 The executor issues the same launches, with the same arguments, dropout seeds, workspaces
 and optimizer step counts, as `VanillaSession.split_epoch` / `UShapeSession.split_epoch` in
@@ -46,15 +49,23 @@ def native_split_ok(sess, cid: int, mode: str) -> bool:
             and a.head.head_step_ok(B))
 
 
-def run_native_split_epoch(sess, cid: int, order: torch.Tensor, mode: str):
-    """One split epoch of Alice_cid over `order` through `_C.SplitEpoch`."""
+def _alice_cfg(sess, cid: int, mode: str) -> dict:
     a = sess.alices[cid]
-    tail = sess.tail
-    ops, dev = sess.ops, sess.device
-    B = sess.B
     a.front.flush()
     w, b = a.front.params
     pre = "front." if mode == "ushape" else ""
+    cfg = {"x": a.train.x, "y": a.train.y,
+           "front": {"w": _param(a.slot, pre + "conv.weight", w), "b": _param(a.slot, pre + "conv.bias", b)},
+           "front_opt": _opt(a.slot.cfg)}
+    if mode == "ushape":
+        H = a.head.layers[0]
+        cfg["head"] = {"w": _param(a.slot, f"head.{H.spec.name}.weight", H.W),
+                       "b": _param(a.slot, f"head.{H.spec.name}.bias", H.b)}
+    return cfg
+
+
+def _bob_cfg(sess, cid: int, mode: str) -> dict:
+    tail, ops, dev, B = sess.tail, sess.ops, sess.device, sess.B
     bslot = sess.bob_slot(cid)
     layers = []
     for L in tail.layers:
@@ -63,9 +74,7 @@ def run_native_split_epoch(sess, cid: int, order: torch.Tensor, mode: str):
     N2 = tail.layers[1].W.shape[0]
     nmax = max(L.W.shape[0] for L in tail.layers)
     kmax = max(L.W.shape[1] for L in tail.layers)
-    cfg = {"mode": 1 if mode == "vanilla" else 2, "B": B, "x": a.train.x, "y": a.train.y,
-           "front": {"w": _param(a.slot, pre + "conv.weight", w), "b": _param(a.slot, pre + "conv.bias", b)},
-           "front_opt": _opt(a.slot.cfg), "bob_opt": _opt(bslot.cfg), "tail": layers,
+    cfg = {"bob_opt": _opt(bslot.cfg), "tail": layers,
            "p1": tail.layers[0].spec.dropout, "p2": tail.layers[1].spec.dropout,
            # the Python path's own workspaces (ops/hip_ops.py), so every split factor matches
            "fwdws": ops._workspace(dev, 16 * B * nmax, "fwd"),
@@ -74,17 +83,120 @@ def run_native_split_epoch(sess, cid: int, order: torch.Tensor, mode: str):
         C3 = tail.layers[2].W.shape[0]
         cfg["p2ws"] = ops._workspace(dev, 16 * B * N2, "fc2p")
         cfg["headws"] = ops._workspace(dev, ops.C().head3_slices(N2) * B * C3, "head")
-    else:
-        H = a.head.layers[0]
-        cfg["head"] = {"w": _param(a.slot, f"head.{H.spec.name}.weight", H.W),
-                       "b": _param(a.slot, f"head.{H.spec.name}.bias", H.b)}
-    ex = ops.C().SplitEpoch(cfg)
-    order = order.to(dev, torch.int64).contiguous()
+    return cfg
+
+
+def _bob_done(sess, cid: int, t_b: int, fc: int):
+    tail = sess.tail
+    sess.bob_slot(cid).t, tail.fwd_count = int(t_b), int(fc)
     tail._pre = None
-    t_a, t_b, fc = ex.run(order, a.slot.t, bslot.t, tail.fwd_count, tail.seed_base)
+    tail.acts, tail.dz, tail._wg = [], [], []
+
+
+def _count(sess, kind: str):
+    """Per-session tally of native split epochs by kind (bench.py reports it)."""
+    c = sess.__dict__.setdefault("native_split_epochs", {})
+    c[kind] = c.get(kind, 0) + 1
+
+
+def run_native_split_epoch(sess, cid: int, order: torch.Tensor, mode: str):
+    """One split epoch of Alice_cid over `order` through `_C.SplitEpoch`."""
+    _count(sess, "colocated")
+    a = sess.alices[cid]
+    B = sess.B
+    cfg = {"mode": 1 if mode == "vanilla" else 2, "B": B}
+    cfg.update(_alice_cfg(sess, cid, mode))
+    cfg.update(_bob_cfg(sess, cid, mode))
+    ex = sess.ops.C().SplitEpoch(cfg)
+    order = order.to(sess.device, torch.int64).contiguous()
+    sess.tail._pre = None
+    t_a, t_b, fc = ex.run(order, a.slot.t, sess.bob_slot(cid).t, sess.tail.fwd_count, sess.tail.seed_base)
     nb = -(-int(order.numel()) // B)
-    a.slot.t, bslot.t, tail.fwd_count = int(t_a), int(t_b), int(fc)
+    a.slot.t = int(t_a)
+    _bob_done(sess, cid, t_b, fc)
     if a.head is not None:
         a.head.fwd_count += nb
-    tail.acts, tail.dz, tail._wg = [], [], []
+    return ex
+
+
+# ---------------------------------------------------------------------- remote placements
+def _remote_placement_ok(sess, cid: int) -> bool:
+    """Conditions every rank evaluates identically (placement, flags, the link): the Alice
+    remote from a one-shard Bob, an fp32 wire, the native kernels, a split channel."""
+    return (getattr(sess.args, "native_epoch", True) and sess.device.type == "cuda"
+            and getattr(sess, "split_channel", None) is not None and sess.pl.bob_tp == 1
+            and sess.host(cid) != sess.pl.bob_root and sess.act_dtype == torch.float32
+            and hasattr(sess.ops, "C"))
+
+
+def _remote_side_ok(sess, cid: int, mode: str) -> bool:
+    """This rank's side of the pair can run natively (the same per-side rules as
+    `native_split_ok`)."""
+    B = sess.B
+    if sess.hosts(cid):
+        a = sess.alices[cid]
+        if a.front.frozen or a.train.x.dtype != torch.uint8:
+            return False
+        return mode == "vanilla" or (sess.head_fused(B) and a.head.head_step_ok(B))
+    t = sess.tail
+    if mode == "vanilla":
+        return t.fused3_ok()
+    return t.grouped_ok(B) and len(t.layers) == 2 and sess.head_fused(B)
+
+
+def native_remote_role(sess, cid: int, mode: str):
+    """Collective over the pair (the Alice's rank, Bob's): whether this epoch of a remote
+    Alice runs on the native split executor.  Returns "alice" / "bob" on the pair's ranks
+    when both sides agree, "skip" on every other rank (it moves nothing in this epoch either
+    way), None when the Python loop runs it."""
+    if not _remote_placement_ok(sess, cid):
+        return None
+    host, bob = sess.host(cid), sess.pl.bob_root
+    if sess.rank not in (host, bob):
+        return "skip"
+    peer = bob if sess.rank == host else host
+    mine = torch.tensor([1 if _remote_side_ok(sess, cid, mode) else 0], dtype=torch.int32, device=sess.device)
+    theirs = torch.empty_like(mine)
+    sess.comm.exchange([(mine, peer)], [(theirs, peer)])
+    if int(mine.item()) and int(theirs.item()):
+        return "alice" if sess.rank == host else "bob"
+    return None
+
+
+def run_native_remote_epoch(sess, cid: int, order, n: int, mode: str, role: str):
+    """This rank's half of one split epoch of a remote Alice_cid (`_C.SplitEpoch` roles 1 / 2,
+    csrc/split.cpp run_alice / run_bob): the per-batch messages go over `sess.split_channel`
+    on the compute stream.  Same launches and step counts as the Python loop of this
+    placement (the §3.2 overlap order: no look-ahead)."""
+    if role == "skip":
+        return None
+    _count(sess, "remote_" + role)
+    C = sess.ops.C()
+    host, bob = sess.host(cid), sess.pl.bob_root
+    cfg = {"mode": 1 if mode == "vanilla" else 2, "B": sess.B, "channel": sess.split_channel}
+    comm = sess.comm
+    comm.progress()
+    if role == "alice":
+        a = sess.alices[cid]
+        cfg.update(_alice_cfg(sess, cid, mode))
+        cfg.update({"role": 1, "peer": bob})
+        ex = C.SplitEpoch(cfg)
+        order = order.to(sess.device, torch.int64).contiguous()
+        a.slot.t = int(ex.run_alice(order, a.slot.t))
+        if a.head is not None:
+            a.head.fwd_count += -(-int(order.numel()) // sess.B)
+    else:
+        cfg.update(_bob_cfg(sess, cid, mode))
+        cfg.update({"role": 2, "peer": host})
+        ex = C.SplitEpoch(cfg)
+        sess.tail._pre = None
+        t_b, fc = ex.run_bob(int(n), sess.bob_slot(cid).t, sess.tail.fwd_count, sess.tail.seed_base)
+        _bob_done(sess, cid, t_b, fc)
+    for op, peer, nb in ex.messages():
+        if op == "send":
+            comm.bytes_sent += nb
+            comm.msgs_sent += 1
+            if comm.msg_log is not None:
+                comm.msg_log.append(("native_send", comm.rank, peer, nb))
+    comm.progress()
     return ex

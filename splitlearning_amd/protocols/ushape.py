@@ -22,7 +22,7 @@ from ..engine.slots import OptSlot, adam
 from ..engine.tail import TailEngine
 from ..models import ClientFront, Head, ServerTailUShape, head_spec, ushape_server_spec
 from .base import AliceState, Session, _progress
-from .split_native import native_split_ok, run_native_split_epoch
+from .split_native import native_remote_role, native_split_ok, run_native_remote_epoch, run_native_split_epoch
 
 
 class UShapeSession(Session):
@@ -142,6 +142,10 @@ class UShapeSession(Session):
             return
         if order is not None and native_split_ok(self, cid, "ushape"):
             run_native_split_epoch(self, cid, order, "ushape")   # the same launches, issued from C++
+            return
+        role = native_remote_role(self, cid, "ushape")   # collective over the Alice's and Bob's ranks
+        if role is not None:                      # remote Alice: each side's half from C++
+            run_native_remote_epoch(self, cid, order, n, "ushape", role)
             return
         grouped = self.is_bob and self.tail.grouped_ok()
         la = self.split_lookahead(cid)

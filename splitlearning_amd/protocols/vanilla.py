@@ -19,7 +19,7 @@ from ..config import CUT_FEATURES
 from ..engine.slots import OptSlot, sgd_momentum
 from ..models import ServerTailSisa, sisa_server_spec
 from .base import Session, _progress
-from .split_native import native_split_ok, run_native_split_epoch
+from .split_native import native_remote_role, native_split_ok, run_native_remote_epoch, run_native_split_epoch
 
 
 class VanillaSession(Session):
@@ -92,6 +92,10 @@ class VanillaSession(Session):
             return
         if order is not None and native_split_ok(self, cid, "vanilla"):
             run_native_split_epoch(self, cid, order, "vanilla")   # the same launches, issued from C++
+            return
+        role = native_remote_role(self, cid, "vanilla")   # collective over the Alice's and Bob's ranks
+        if role is not None:                      # remote Alice: each side's half from C++
+            run_native_remote_epoch(self, cid, order, n, "vanilla", role)
             return
         ahead = self.split_lookahead(cid)        # False: Alice remote from every Bob shard
         la = self.is_bob and self.tail.fused3_ok() and self.tail.lookahead_ok(B) and ahead

@@ -259,9 +259,12 @@ def test_vanilla_per_batch_message_sequence(tmp_path, tp):
     n_unl = int((y1 != 9).sum())
     bob_ranks = list(range(tp))
 
+    from splitlearning_amd.protocols.base import Session
+    # [M x 5408 activation | M int64 labels], padded to 16-byte units (Session.pack)
+    pack_bytes = {4 * Session.packed_len(M, torch.float32) for M in range(1, B + 1)}
+
     def packs(src, dst):
-        return [x for x in msgs if x[0] == "multicast" and x[1] == src and x[2] == dst
-                and x[3] % (4 * (5408 + 1)) == 0 and x[3] <= 4 * B * (5408 + 1)]
+        return [x for x in msgs if x[0] == "multicast" and x[1] == src and x[2] == dst and x[3] in pack_bytes]
 
     def grads(src, dst):
         return [x for x in msgs if x[0] == "reduce_to" and x[1] == src and x[2] == dst]
