@@ -538,8 +538,7 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
   auto pool_run = [&](auto upd_c, auto look_c, int phase, int so, unsigned gen, int xt, int xn, float ss, float ib) {
     constexpr bool UPD = decltype(upd_c)::value, LOOK = decltype(look_c)::value;
     if (a.np <= 0) return;
-    const int par = so & 1;                  // look-ahead partials / h1 of step so
-    const int cpar = (phase + 1) & 1;        // this step's dz1 partials and h1 (step phase - 1)
+    const int par = so & 1;
     const unsigned base = (unsigned)phase * (unsigned)(a.np + G);
     __syncthreads();
     if (threadIdx.x == 0)
@@ -557,9 +556,8 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
       if (UPD) load_xa(xt, t, xa);
       if (LOOK) load_xv(xn, t, xv);
       load_state(t, sp[0], sm[0], sv[0], UPD);
-      unsigned nxt = 0;
       if (threadIdx.x == 0)   // the next grab in flight under this tile (after its loads)
-        nxt = __hip_atomic_fetch_add(hy_cnt(a, hy_Q()), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_ok[8] = (int)(__hip_atomic_fetch_add(hy_cnt(a, hy_Q()), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - base);
       if (UPD && !own) {
         // dz1 of a row block outside this workgroup's runs: its fc2 column blocks' partials
         if (threadIdx.x < 64) {
@@ -580,8 +578,8 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
           if (m < M && n < N1) {
             float parts[kHyNR];
 #pragma unroll
-            for (int b = 0; b < kHyNR; ++b) parts[b] = hld1(rHB, bDP + (((cpar * kHyNR + b) * 16 + m) * N1 + n) * 4);
-            const float h = hld1(rHB, bH1 + ((cpar * 16 + m) * N1 + n) * 4);
+            for (int b = 0; b < kHyNR; ++b) parts[b] = hld1(rHB, bDP + (((par * kHyNR + b) * 16 + m) * N1 + n) * 4);
+            const float h = hld1(rHB, bH1 + ((par * 16 + m) * N1 + n) * 4);
             v = parts[0];
 #pragma unroll
             for (int b = 1; b < kHyNR; ++b) v += parts[b];
@@ -659,7 +657,6 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
         __syncthreads();
         if (s_ok[9]) publish_rb(rb, so);
       }
-      if (threadIdx.x == 0) s_ok[8] = (int)(nxt - base);
       __syncthreads();
       p = s_ok[8];
     }
