@@ -18,14 +18,12 @@ constexpr int kHyMaxWC4 = 40;       // fc2 tile columns / 4 (160)
 constexpr int kHyMaxC = 128;        // classes
 constexpr int kHyRuns = 3;          // fc1 row blocks one workgroup's tile run may touch
 constexpr int kHySlots = 8;         // workgroups whose runs may touch one fc1 row block
-constexpr int kHyPoolSlots = 8;     // pool tiles one fc1 row block may hold
 constexpr int kHyMaxRB = 320;       // fc1 row blocks of 16 rows (N1 <= 5120)
 constexpr int kHyStride = 32;       // counter words 128 B apart
 constexpr int kHySeams = 4;         // F: fc2 partials, L: logit partials, D: dlogits, Z: dz2
 // counter words: the seams' 8 shards each, then H[NC] (h1 column blocks published), P[NC]
-// (dz1 partials per fc2 column block), R[nrb] (look-ahead partials per fc1 row block), Q (the
-// tile pool's grab counter)
-constexpr int kHyCounters = kHySeams * 8 + 2 * kHyMaxNC + kHyMaxRB + 1;
+// (dz1 partials per fc2 column block), R[nrb] (look-ahead partials per fc1 row block)
+constexpr int kHyCounters = kHySeams * 8 + 2 * kHyMaxNC + kHyMaxRB;
 
 struct HyArgs {
   ResLayer L1, L2, L3;
@@ -34,15 +32,10 @@ struct HyArgs {
   int M, S, G;            // rows per step (<= 16), steps, workgroups
   int NC, HW;             // fc2 column blocks (G = 8 NC), head workgroups (N2 / 4)
   int nrb, ncb, ntile;    // fc1 row blocks (16 rows), column blocks (256), tiles nrb * ncb
-  // device table (int): tile0[G + 1] (workgroup w's static run: fc1 tiles [tile0[w],
-  // tile0[w + 1]) in row-major order), then rbw0[nrb] (first workgroup whose static run
-  // touches each row block), rbn[nrb] (workgroups touching it), hn[NC] (row blocks
-  // overlapping each fc2 column block); at oPT: the tile pool pt[np] (tiles left out of the
-  // static runs, in tile order, taken by whichever workgroup finishes its run first), at oPR /
-  // oPN: pr0[nrb] / pn[nrb] (each row block's pool tiles [pr0, pr0 + pn)), at oSE: se[G]
-  // (the end of each static run; its pool tiles are [se[w], tile0[w + 1]))
+  // device table (int): tile0[G + 1] (workgroup w streams fc1 tiles [tile0[w], tile0[w + 1])
+  // in row-major order), then rbw0[nrb] (first workgroup whose run touches each row block),
+  // rbn[nrb] (workgroups touching it), hn[NC] (row blocks overlapping each fc2 column block)
   const int* tab;
-  int np, oPT, oPR, oPN, oSE;
   const float* X;         // [S * M, K1] inputs (cut activations)
   const int64_t* Y;       // [S * M] labels
   float* loss;            // [S * M] per-row losses
@@ -64,9 +57,8 @@ struct HyArgs {
   //   DZ [2][16][N2] dz2
   //   DP [2][8][16][N1] dz1 partials per fc2 row block
   //   ZP [G][kHyRuns][8 waves][64] f32x4 per-wave look-ahead accumulators
-  //   LQ [2][np][16][16] look-ahead partials of the pool tiles
   float* HB;
-  int oLA, oH1, oFP, oLP, oDL, oDZ, oDP, oZP, oLQ;
+  int oLA, oH1, oFP, oLP, oDL, oDZ, oDP, oZP;
   unsigned* cnt;          // [kHyCounters][kHyStride] (zeroed per launch)
   const int* shard_n;     // [kHySeams][8] arrivals per seam shard and step
   int* err;               // nonzero after a wait gave up (2 timeout, 4 peer exchange)

@@ -68,7 +68,6 @@ __device__ __forceinline__ int hy_seam(int seam, int shard) { return seam * 8 + 
 __device__ __forceinline__ int hy_H(int b) { return kHySeams * 8 + b; }
 __device__ __forceinline__ int hy_P(int b) { return kHySeams * 8 + kHyMaxNC + b; }
 __device__ __forceinline__ int hy_R(int rb) { return kHySeams * 8 + 2 * kHyMaxNC + rb; }
-__device__ __forceinline__ int hy_Q() { return kHySeams * 8 + 2 * kHyMaxNC + kHyMaxRB; }
 
 // bounded wait until *p >= tgt (one lane); false when it gave up
 __device__ __forceinline__ bool hy_spin(const HyArgs& a, const unsigned* p, unsigned tgt) {
@@ -226,14 +225,14 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
   const int c0 = 4 * q0, WC = 4 * WC4;
   const bool head = w < a.HW;
   // fc1 tile run [t_begin, t_end), row blocks rbA .. rbA + nruns - 1
-  const int t_begin = a.tab[w], t_end = a.tab[a.oSE + w];
+  const int t_begin = a.tab[w], t_end = a.tab[w + 1];
   const int nt = t_end - t_begin;
   const int rbA = nt > 0 ? t_begin / ncb : 0;
   const int nruns = nt > 0 ? (t_end - 1) / ncb - rbA + 1 : 0;
   // every hand-off buffer through one resource (offsets in bytes: base + element * 4)
   const __amdgpu_buffer_rsrc_t rHB = rs_of(a.HB);
   const int bLA = 4 * a.oLA, bH1 = 4 * a.oH1, bFP = 4 * a.oFP, bLP = 4 * a.oLP, bDL = 4 * a.oDL, bDZ = 4 * a.oDZ,
-            bDP = 4 * a.oDP, bZP = 4 * a.oZP, bLQ = 4 * a.oLQ;
+            bDP = 4 * a.oDP, bZP = 4 * a.oZP;
   const __amdgpu_buffer_rsrc_t rW1 = rs_of(a.L1.W), rM1 = rs_of(a.L1.m), rV1 = rs_of(a.L1.v ? a.L1.v : a.L1.m);
 
   // ---- load the resident state: the W2 tile (LDS), its m / v (VGPRs), head columns, biases
@@ -441,49 +440,6 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
   // wave order, + b1 by its first workgroup) -> LA; the row block's last arriver sums all
   // partials in workgroup order, applies ReLU and step so's dropout, publishes h1 rows and
   // counts them into H[] of the fc2 column blocks they cover.
-  // arrivals per step on row block rb's counter: its static runs, then its pool tiles
-  auto r_count = [&](int rb) -> unsigned {
-    return (unsigned)(a.tab[a.G + 1 + a.nrb + rb] + a.tab[a.oPN + rb]);
-  };
-  // The row block's last arriver: the static runs' partials in workgroup order, then its pool
-  // tiles' in pool order (+ b1 came with slot 0), ReLU and step so's dropout -> h1 rows; then
-  // the fc2 column blocks they cover are counted
-  auto publish_rb = [&](int rb, int so) {
-    const int par = so & 1;
-    {
-      HY_IDX();
-      const int ns = a.tab[a.G + 1 + a.nrb + rb], q0 = a.tab[a.oPR + rb], nq = a.tab[a.oPN + rb];
-      if (tid < 256) {
-        const int m = tid >> 4, nn = tid & 15, n = 16 * rb + nn;
-        if (m < M && n < N1) {
-          float parts[kHySlots], pq[kHyPoolSlots];
-#pragma unroll
-          for (int s2 = 0; s2 < kHySlots; ++s2)
-            parts[s2] = s2 < ns ? hld1(rHB, bLA + (((par * a.nrb + rb) * kHySlots + s2) * 256 + m * 16 + nn) * 4) : 0.f;
-#pragma unroll
-          for (int q = 0; q < kHyPoolSlots; ++q)
-            pq[q] = q < nq ? hld1(rHB, bLQ + ((par * a.np + q0 + q) * 256 + m * 16 + nn) * 4) : 0.f;
-          float v = parts[0];
-#pragma unroll
-          for (int s2 = 1; s2 < kHySlots; ++s2) v += parts[s2];
-#pragma unroll
-          for (int q = 0; q < kHyPoolSlots; ++q) v += pq[q];
-          v = drop_relu(v, a.seeds[4 * so], a.seeds[4 * so + 1], m, a.col_off1 + n, a.thr1, a.dsc1);
-          hst1(rHB, bH1 + ((par * 16 + m) * N1 + n) * 4, v);
-        }
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const int blo = hy_colblk((16 * rb) >> 2, NC, Q4);
-      const int bhi = hy_colblk((min(16 * rb + 16, N1) - 1) >> 2, NC, Q4);
-      for (int b = blo; b <= bhi; ++b)
-        __hip_atomic_fetch_add(hy_cnt(a, hy_H(b)), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-  };
-
   auto flush = [&](int so, unsigned gen) {
     const int par = so & 1;
     {
@@ -522,151 +478,52 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
       for (int k = 0; k < nruns; ++k) {
         const int rb = rbA + k;
         const unsigned old = __hip_atomic_fetch_add(hy_cnt(a, hy_R(rb)), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_ok[1 + k] = (old == gen * r_count(rb) - 1u) ? 1 : 0;
+        s_ok[1 + k] = (old == gen * (unsigned)a.tab[a.G + 1 + a.nrb + rb] - 1u) ? 1 : 0;
       }
     }
     __syncthreads();
-    for (int k = 0; k < nruns; ++k)
-      if (s_ok[1 + k]) publish_rb(rbA + k, so);
-  };
-
-  // One pool tile per iteration, taken from the shared counter Q by whichever workgroup is free
-  // (phase: 0 the prologue, i + 1 step i; each phase takes np + G grabs, every workgroup's last
-  // one past the end).  The tile's update is the stream's; its look-ahead partial (the 8 waves'
-  // accumulators summed in wave order) goes to its own slot LQ[p], so the row block's sum does
-  // not depend on which workgroup took it.
-  auto pool_run = [&](auto upd_c, auto look_c, int phase, int so, unsigned gen, int xt, int xn, float ss, float ib) {
-    constexpr bool UPD = decltype(upd_c)::value, LOOK = decltype(look_c)::value;
-    if (a.np <= 0) return;
-    const int par = so & 1;
-    const unsigned base = (unsigned)phase * (unsigned)(a.np + G);
-    __syncthreads();
-    if (threadIdx.x == 0)
-      s_ok[8] = (int)(__hip_atomic_fetch_add(hy_cnt(a, hy_Q()), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - base);
-    __syncthreads();
-    int p = s_ok[8];
-    while (p < a.np) {
-      __syncthreads();   // every wave read p
-      const int t = a.tab[a.oPT + p];
-      const int rb = t / ncb, cb = t - (t / ncb) * ncb;
-      const int kr = rb - rbA;
-      const bool own = kr >= 0 && kr < nruns;
-      float* dz = own ? sdz1 + kr * 256 : reinterpret_cast<float*>(sa + 1024);
-      f32x4 xa[2], xv[2];
-      if (UPD) load_xa(xt, t, xa);
-      if (LOOK) load_xv(xn, t, xv);
-      load_state(t, sp[0], sm[0], sv[0], UPD);
-      if (threadIdx.x == 0)   // the next grab in flight under this tile (after its loads)
-        s_ok[8] = (int)(__hip_atomic_fetch_add(hy_cnt(a, hy_Q()), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - base);
-      if (UPD && !own) {
-        // dz1 of a row block outside this workgroup's runs: its fc2 column blocks' partials
-        if (threadIdx.x < 64) {
-          const int lane = threadIdx.x;
+    bool any = false;
+    for (int k = 0; k < nruns; ++k) {
+      if (!s_ok[1 + k]) continue;
+      any = true;
+      HY_IDX();
+      const int rb = rbA + k, ns = a.tab[a.G + 1 + a.nrb + rb];
+      if (tid < 256) {
+        const int m = tid >> 4, nn = tid & 15, n = 16 * rb + nn;
+        if (m < M && n < N1) {
+          float parts[kHySlots];
+#pragma unroll
+          for (int s = 0; s < kHySlots; ++s)
+            parts[s] = s < ns ? hld1(rHB, bLA + (((par * a.nrb + rb) * kHySlots + s) * 256 + m * 16 + nn) * 4) : 0.f;
+          float v = parts[0];
+#pragma unroll
+          for (int s = 1; s < kHySlots; ++s) v += parts[s];
+          v = drop_relu(v, a.seeds[4 * so], a.seeds[4 * so + 1], m, a.col_off1 + n, a.thr1, a.dsc1);
+          hst1(rHB, bH1 + ((par * 16 + m) * N1 + n) * 4, v);
+        }
+      }
+    }
+    if (any) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        for (int k = 0; k < nruns; ++k) {
+          if (!s_ok[1 + k]) continue;
+          const int rb = rbA + k;
           const int blo = hy_colblk((16 * rb) >> 2, NC, Q4);
           const int bhi = hy_colblk((min(16 * rb + 16, N1) - 1) >> 2, NC, Q4);
-          bool ok = true;
-          if (blo + lane <= bhi) ok = hy_spin(a, hy_cnt(a, hy_P(blo + lane)), (unsigned)phase * kHyNR);
-          ok = __all(ok);
-          if (lane == 0) s_ok[10] = ok ? 1 : 0;
-        }
-        __syncthreads();
-        if (!s_ok[10]) return;
-        HY_IDX();
-        if (tid < 256) {
-          const int m = tid >> 4, nn = tid & 15, n = 16 * rb + nn;
-          float v = 0.f;
-          if (m < M && n < N1) {
-            float parts[kHyNR];
-#pragma unroll
-            for (int b = 0; b < kHyNR; ++b) parts[b] = hld1(rHB, bDP + (((par * kHyNR + b) * 16 + m) * N1 + n) * 4);
-            const float h = hld1(rHB, bH1 + ((par * 16 + m) * N1 + n) * 4);
-            v = parts[0];
-#pragma unroll
-            for (int b = 1; b < kHyNR; ++b) v += parts[b];
-            v = h > 0.f ? v * a.dsc1 : 0.f;
-          }
-          dz[tid] = v;
+          for (int b = blo; b <= bhi; ++b)
+            __hip_atomic_fetch_add(hy_cnt(a, hy_H(b)), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
-      {
-        HY_IDX();
-        if (UPD) {
-          sa[r * 64 + lane] = xa[0];
-          sa[(r + 8) * 64 + lane] = xa[1];
-        }
-      }
-      __syncthreads();
-      {
-        HY_IDX();
-        const int n1 = 16 * rb + r;
-        const int k = cb * 256 + 4 * lane;
-        const bool kin = k < K1;
-        if (UPD) {
-          f32x4 g0 = zv, g1 = zv;
-#pragma unroll 4
-          for (int m = 0; m < 16; ++m) {
-            const f32x4 xm = sa[m * 64 + lane];
-            g0 += dz[m * 16 + r] * xm;
-            g1 += dz[m * 16 + r + 8] * xm;
-          }
-          if (kin && n1 < N1) {
-            res_update4<ADAM>(a.o, ss, ib, sp[0][0], g0, sm[0][0], sv[0][0]);
-            const int boff = (n1 * K1 + k) * 4;
-            hst4(rW1, boff, sp[0][0]);
-            hst4(rM1, boff, sm[0][0]);
-            if (ADAM) hst4(rV1, boff, sv[0][0]);
-          }
-          if (kin && n1 + 8 < N1) {
-            res_update4<ADAM>(a.o, ss, ib, sp[0][1], g1, sm[0][1], sv[0][1]);
-            const int boff = ((n1 + 8) * K1 + k) * 4;
-            hst4(rW1, boff, sp[0][1]);
-            hst4(rM1, boff, sm[0][1]);
-            if (ADAM) hst4(rV1, boff, sv[0][1]);
-          }
-        }
-        if (LOOK) {
-          sw[r * 65 + lane] = (kin && n1 < N1) ? sp[0][0] : zv;
-          sw[(r + 8) * 65 + lane] = (kin && n1 + 8 < N1) ? sp[0][1] : zv;
-        }
-      }
-      if (LOOK) {
-        __syncthreads();
-        HY_IDX();
-        f32x4 z = zv;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const f32x4 wv4 = sw[li * 65 + 4 * (r + 8 * h) + lq];
-#pragma unroll
-          for (int c = 0; c < 4; ++c) z = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[h][c], wv4[c], z, 0, 0, 0);
-        }
-        sw[1040 + r * 64 + lane] = z;
-        __syncthreads();
-        if (tid < 256) {
-          const int m = tid >> 4, nn = tid & 15, n = 16 * rb + nn;
-          float v = sw[1040 + 16 * (m >> 2) + nn][m & 3];
-#pragma unroll
-          for (int ww = 1; ww < 8; ++ww) v += sw[1040 + ww * 64 + 16 * (m >> 2) + nn][m & 3];
-          if (m < M && n < N1) hst1(rHB, bLQ + ((par * a.np + p) * 256 + m * 16 + nn) * 4, v);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0) {
-          const unsigned old = __hip_atomic_fetch_add(hy_cnt(a, hy_R(rb)), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          s_ok[9] = (old == gen * r_count(rb) - 1u) ? 1 : 0;
-        }
-        __syncthreads();
-        if (s_ok[9]) publish_rb(rb, so);
-      }
-      __syncthreads();
-      p = s_ok[8];
     }
+    __syncthreads();
   };
 
   // ---- prologue: h1_0 = drop(relu(x_0 W1_0^T + b1)) by a read-only pass over the run
   if (nt > 0) load_state(t_begin, sp[0], sm[0], sv[0], false);
   stream(std::false_type{}, std::true_type{}, 0, 0, 0.f, 0.f);
   flush(0, 1u);
-  pool_run(std::false_type{}, std::true_type{}, 0, 0, 1u, 0, 0, 0.f, 0.f);
 
   for (int i = 0; i < a.S; ++i) {
     const int par = i & 1;
@@ -1071,11 +928,9 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
       HY_MARK(13);
       HY_ALL(i, 1);
       flush(i + 1, (unsigned)(i + 2));
-      pool_run(std::true_type{}, std::true_type{}, i + 1, i + 1, (unsigned)(i + 2), xt, xn, ss, ib);
       HY_ALL(i, 2);
     } else {
       stream(std::true_type{}, std::false_type{}, xt, xn, ss, ib);
-      pool_run(std::true_type{}, std::false_type{}, i + 1, i + 1, 0u, xt, xn, ss, ib);
     }
     HY_MARK(14);
   }

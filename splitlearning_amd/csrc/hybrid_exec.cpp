@@ -68,9 +68,6 @@ class HybridEpoch {
     B_ = cfg["B"].cast<int>();
     if (cfg.contains("ipc") && !cfg["ipc"].is_none()) ipc_ = cfg["ipc"].cast<sl::IpcAllReduce*>();
     timeout_s_ = cfg.contains("timeout_s") ? cfg["timeout_s"].cast<double>() : 30.0;
-    // tiles per workgroup run left to the shared pool (0: static runs only)
-    if (cfg.contains("pool") && !cfg["pool"].is_none()) pool_ = cfg["pool"].cast<int>();
-    TORCH_CHECK(pool_ >= 0 && pool_ <= 8, "HybridEpoch: pool 0..8 tiles per run");
 
     const at::Device dev = L_[0].W.device();
     dev_ = dev.index();
@@ -124,7 +121,6 @@ class HybridEpoch {
       a.oDZ = take(2LL * 16 * a.N2);
       a.oDP = take(2LL * sl::kHyNR * 16 * a.N1);
       a.oZP = take((int64_t)G * sl::kHyRuns * 8 * 64 * 4);
-      a.oLQ = take(2LL * std::max(a.np, 1) * 256);
       HB_ = at::zeros({off}, opt);
       a.HB = HB_.data_ptr<float>();
       cnt_ = at::zeros({(int64_t)sl::kHyCounters * sl::kHyStride}, opt.dtype(at::kInt));
@@ -243,16 +239,6 @@ class HybridEpoch {
 
   // the device table (tile runs, row-block owners / counts, column-block counts) for checks
   at::Tensor table() const { return tab_.clone(); }
-  // where the pool's sections sit in table(): {np, pt, pr0, pn, se} (offsets)
-  py::dict layout() const {
-    py::dict d;
-    d["np"] = a_.np;
-    d["pt"] = a_.oPT;
-    d["pr0"] = a_.oPR;
-    d["pn"] = a_.oPN;
-    d["se"] = a_.oSE;
-    return d;
-  }
 
  private:
   // tile runs and arrival counts (hybrid.h HyArgs.tab); "" or the reason the shape is refused
@@ -261,66 +247,41 @@ class HybridEpoch {
     const int G = a.G, nrb = a.nrb, ncb = a.ncb, NC = a.NC, T = a.ntile;
     if (a.N1 % 4 || a.N1 < 4) return "fc1 shard width % 4";
     const int Q4 = a.N1 / 4;
+    std::vector<int> tab(G + 1 + 2 * nrb + NC, 0);
     // balanced contiguous runs; with fewer tiles than workgroups the first T workgroups take
     // one tile each (no empty run between two workgroups that share a row block)
-    std::vector<int> full(G + 1);
-    for (int w = 0; w <= G; ++w) full[w] = T >= G ? (int)((int64_t)w * T / G) : std::min(w, T);
-    // the pool: the last `pool_` tiles of every run of more than pool_ tiles (the static part
-    // keeps at least one); whichever workgroup finishes its static run first takes them
-    std::vector<int> pt, se(G);
-    for (int w = 0; w < G; ++w) {
-      const int len = full[w + 1] - full[w];
-      const int d = len > pool_ ? pool_ : 0;
-      se[w] = full[w + 1] - d;
-      for (int t = se[w]; t < full[w + 1]; ++t) pt.push_back(t);
-    }
-    const int np = (int)pt.size();
-    std::vector<int> tab(G + 1 + 2 * nrb + NC, 0);
-    for (int w = 0; w <= G; ++w) tab[w] = full[w];   // run starts (static ends: se)
+    for (int w = 0; w <= G; ++w) tab[w] = T >= G ? (int)((int64_t)w * T / G) : std::min(w, T);
+    auto wg_of = [&](int t) {   // the workgroup whose run holds tile t
+      int lo = 0, hi = G - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) / 2;
+        if (tab[mid] <= t) lo = mid;
+        else hi = mid - 1;
+      }
+      return lo;
+    };
     auto colblk = [&](int n4) { return (int)(((int64_t)(n4 + 1) * NC + Q4 - 1) / Q4) - 1; };
-    std::vector<int> pr0(nrb, 0), pn(nrb, 0);
-    for (int p = 0; p < np; ++p) {
-      const int rb = pt[p] / ncb;
-      if (pn[rb] == 0) pr0[rb] = p;
-      if (++pn[rb] > sl::kHyPoolSlots) return "an fc1 row block holds more pool tiles than its slots";
-    }
     for (int rb = 0; rb < nrb; ++rb) {
-      const int lo = rb * ncb, hi = std::min((rb + 1) * ncb, T);   // tiles [lo, hi)
-      int w0 = -1, n = 0;
-      for (int w = 0; w < G; ++w)
-        if (full[w] < hi && se[w] > lo && se[w] > full[w]) {
-          if (w0 < 0) w0 = w;
-          ++n;
-        }
-      if (w0 < 0) return "an fc1 row block without a static run";
+      const int w0 = wg_of(rb * ncb), w1 = wg_of(std::min((rb + 1) * ncb, T) - 1);
       tab[G + 1 + rb] = w0;
-      tab[G + 1 + nrb + rb] = n;
-      if (n > sl::kHySlots) return "an fc1 row block spans more workgroups than the partial slots";
+      tab[G + 1 + nrb + rb] = w1 - w0 + 1;
+      if (w1 - w0 + 1 > sl::kHySlots) return "an fc1 row block spans more workgroups than the partial slots";
       const int blo = colblk((16 * rb) / 4), bhi = colblk((std::min(16 * rb + 16, a.N1) - 1) / 4);
       for (int b = blo; b <= bhi; ++b) ++tab[G + 1 + 2 * nrb + b];
     }
     for (int w = 0; w < G; ++w) {
-      if (se[w] <= full[w]) continue;
-      const int runs = (se[w] - 1) / ncb - full[w] / ncb + 1;
+      if (tab[w + 1] <= tab[w]) continue;
+      const int runs = (tab[w + 1] - 1) / ncb - tab[w] / ncb + 1;
       if (runs > sl::kHyRuns) return "a tile run touches more than 3 fc1 row blocks";
     }
     for (int b = 0; b < NC; ++b)
       if (tab[G + 1 + 2 * nrb + b] < 1) return "an fc2 column block without fc1 rows";
-    a.np = np;
-    a.oPT = (int)tab.size();
-    tab.insert(tab.end(), pt.begin(), pt.end());
-    a.oPR = (int)tab.size();
-    tab.insert(tab.end(), pr0.begin(), pr0.end());
-    a.oPN = (int)tab.size();
-    tab.insert(tab.end(), pn.begin(), pn.end());
-    a.oSE = (int)tab.size();
-    tab.insert(tab.end(), se.begin(), se.end());
     tab_ = at::tensor(tab, at::TensorOptions().dtype(at::kInt)).to(L_[0].W.device());
     return "";
   }
 
   HyLayer L_[3];
-  int kind_ = 2, col_off1_ = 0, B_ = 16, dev_ = 0, clock_khz_ = 100000, pool_ = 2;
+  int kind_ = 2, col_off1_ = 0, B_ = 16, dev_ = 0, clock_khz_ = 100000;
   double lr_ = 0, beta1_ = 0, beta2_ = 0, eps_ = 0, wd_ = 0, mom_ = 0, p1_ = 0, p2_ = 0, timeout_s_ = 30.0;
   sl::IpcAllReduce* ipc_ = nullptr;
   sl::HyArgs a_{};
@@ -338,7 +299,6 @@ void sl_register_hybrid(py::module& m) {
       .def("why", &HybridEpoch::why)
       .def("workgroups", &HybridEpoch::workgroups)
       .def("table", &HybridEpoch::table)
-      .def("layout", &HybridEpoch::layout)
       .def("run", &HybridEpoch::run, py::arg("acts"), py::arg("labels"), py::arg("loss_rows"),
            py::arg("seed_base"), py::arg("fwd_count"), py::arg("t"), py::arg("trace") = py::none(),
            py::arg("trace_all") = py::none(), py::arg("trace_all_step") = 0);

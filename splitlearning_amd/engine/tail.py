@@ -27,20 +27,12 @@ from __future__ import annotations
 
 from dataclasses import dataclass
 
-import os
-
 import torch
 
 from .. import ops
 from ..models.zoo import LinearSpec, TailSpec
 from ..ops.rng import step_seed
 from .slots import OptSlot
-
-
-# Tiles of every hybrid-epoch workgroup run taken from a shared pool instead of a fixed owner
-# (balances the per-workgroup stream times, profiles/r4a_hybrid_per_wg_timing.txt); SL_HYBRID_POOL
-# overrides it for A/B runs (scripts/hybrid_ab.py --pool)
-HYBRID_POOL = int(os.environ.get("SL_HYBRID_POOL", "2"))
 
 
 @dataclass
@@ -525,9 +517,7 @@ class TailEngine:
              "p1": L1.spec.dropout, "p2": L2.spec.dropout, "col_off1": L1.col_off, "B": B,
              "ipc": getattr(self.allreduce, "ipc", None) if L2.style == "row" else None,
              "timeout_s": float(getattr(self, "resident_timeout_s", 10.0)),
-             "workgroups": int(getattr(self, "resident_workgroups", 0)),
-             # tiles per workgroup run left to the shared pool (csrc/hybrid.hip pool_run)
-             "pool": int(getattr(self, "hybrid_pool", HYBRID_POOL))}
+             "workgroups": int(getattr(self, "resident_workgroups", 0))}
         ex = self.ops.C().HybridEpoch(d)
         self._hybrid = (slot, B, ex, d)
         return ex

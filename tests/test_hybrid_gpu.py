@@ -169,36 +169,25 @@ def test_hybrid_shapes_free_running_close_to_torch(cuda, n1, n2, c, k1, B, rows)
 
 
 def test_hybrid_table_covers_every_tile_once(cuda):
-    """The workgroups' static fc1 tile runs plus the shared pool partition the tiles in order,
-    every row block's first static workgroup and static count match the runs, its pool range
-    holds exactly its pool tiles, and every fc2 column block counts the fc1 row blocks that
-    overlap it (csrc/hybrid_exec.cpp tables)."""
+    """The workgroups' fc1 tile runs partition the tiles in order, every row block's first
+    workgroup and workgroup count match the runs, and every fc2 column block counts the fc1
+    row blocks that overlap it (csrc/hybrid_exec.cpp tables)."""
     spec = _spec()
     te, slot = _engine(_MLP(spec), spec, cuda, 1, "#hy4")
     ex = te._hybrid_executor(slot, 16)
     assert ex.ok(), ex.why()
     G = ex.workgroups()
     tab = ex.table().cpu().tolist()
-    lay = ex.layout()
     nrb, ncb = (5000 + 15) // 16, (5408 + 255) // 256
-    T = nrb * ncb
     tile0 = tab[:G + 1]
-    se = tab[lay["se"]:lay["se"] + G]
-    pt = tab[lay["pt"]:lay["pt"] + lay["np"]]
-    assert tile0[0] == 0 and tile0[-1] == T and all(b >= a for a, b in zip(tile0, tile0[1:]))
-    assert all(tile0[w] < se[w] <= tile0[w + 1] for w in range(G) if tile0[w + 1] > tile0[w])
-    static = [t for w in range(G) for t in range(tile0[w], se[w])]
-    assert sorted(static + pt) == list(range(T)) and pt == sorted(pt) and len(pt) > 0
+    assert tile0[0] == 0 and tile0[-1] == nrb * ncb and all(b >= a for a, b in zip(tile0, tile0[1:]))
     rbw0, rbn = tab[G + 1:G + 1 + nrb], tab[G + 1 + nrb:G + 1 + 2 * nrb]
-    pr0, pn = tab[lay["pr0"]:lay["pr0"] + nrb], tab[lay["pn"]:lay["pn"] + nrb]
     for rb in range(nrb):
-        owners = [w for w in range(G) if tile0[w] < (rb + 1) * ncb and se[w] > rb * ncb and se[w] > tile0[w]]
+        owners = [w for w in range(G) if tile0[w] < (rb + 1) * ncb and tile0[w + 1] > rb * ncb]
         assert rbw0[rb] == owners[0] and rbn[rb] == len(owners), rb
-        mine = [p for p, t in enumerate(pt) if t // ncb == rb]
-        assert pn[rb] == len(mine) and (not mine or pr0[rb] == mine[0]), rb
     NC = G // 8
-    hn = tab[G + 1 + 2 * nrb:G + 1 + 2 * nrb + NC]
-    assert sum(hn) >= nrb and min(hn) >= 1
+    hn = tab[G + 1 + 2 * nrb:]
+    assert len(hn) == NC and sum(hn) >= nrb and min(hn) >= 1
 
 
 @pytest.mark.parametrize("T", [2, 4, 8])
