@@ -474,22 +474,22 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) {
-      for (int k = 0; k < nruns; ++k) {
-        const int rb = rbA + k;
-        const unsigned old = __hip_atomic_fetch_add(hy_cnt(a, hy_R(rb)), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_ok[1 + k] = (old == gen * (unsigned)a.tab[a.G + 1 + a.nrb + rb] - 1u) ? 1 : 0;
-      }
+    // one lane per run: the row blocks' arrivals in flight together (one round trip)
+    if (threadIdx.x < (unsigned)nruns) {
+      const int k = threadIdx.x, rb = rbA + k;
+      const unsigned old = __hip_atomic_fetch_add(hy_cnt(a, hy_R(rb)), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_ok[1 + k] = (old == gen * (unsigned)a.tab[a.G + 1 + a.nrb + rb] - 1u) ? 1 : 0;
     }
     __syncthreads();
     bool any = false;
-    for (int k = 0; k < nruns; ++k) {
-      if (!s_ok[1 + k]) continue;
-      any = true;
+    for (int k = 0; k < nruns; ++k) any = any || s_ok[1 + k] != 0;
+    // the row blocks this workgroup arrived last on, two at a time (256 lanes each)
+    for (int e0 = 0; e0 < nruns * 256; e0 += kHyThreads) {
       HY_IDX();
-      const int rb = rbA + k, ns = a.tab[a.G + 1 + a.nrb + rb];
-      if (tid < 256) {
-        const int m = tid >> 4, nn = tid & 15, n = 16 * rb + nn;
+      const int e = e0 + tid, k = e >> 8;
+      if (k < nruns && s_ok[1 + k]) {
+        const int rb = rbA + k, ns = a.tab[a.G + 1 + a.nrb + rb];
+        const int m = (e >> 4) & 15, nn = e & 15, n = 16 * rb + nn;
         if (m < M && n < N1) {
           float parts[kHySlots];
 #pragma unroll

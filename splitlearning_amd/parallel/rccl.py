@@ -182,7 +182,7 @@ def _channel_self_test(ch, iters: int = 12) -> bool:
     ch.set_timeout_s(5.0)
     try:
         for it in range(iters):
-            n = (4, 1028, 16 * 5408 + 32, ch.cap)[it % 4]
+            n = min((4, 1028, 16 * 5408 + 32, ch.cap)[it % 4], ch.cap)
             src = (me - 1) % T
             out = (torch.arange(n, dtype=torch.float32) * 0.25 + 1000 * me + it).to(dev)
             got = torch.empty(n, device=dev)
