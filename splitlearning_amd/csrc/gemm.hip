@@ -179,10 +179,28 @@ gemm_nt_kernel(const float* __restrict__ X, int ldx, const float* __restrict__ W
 // Split-K (gridDim.y = S > 1, for grids of few tiles): slice z = blockIdx.y covers k in
 // [z kc, z kc + kc) and stores its raw partial sums into slab z of P ([S][M][N]); the slabs are
 // then reduced with the epilogue applied (linear_epilogue).
+// Logical tile index -> (tm, tn).  grouped == 0: tm fastest.  grouped == 1: bands of 8 tile
+// rows, tm fastest inside a band (consecutive workgroups, which land on consecutive XCDs, take
+// the 8 rows of one tile column: each XCD keeps one X row band for a whole column sweep).
+__device__ __forceinline__ void gemm_tile_of(int L, int tilesM, int tilesN, int grouped, int& tm, int& tn) {
+  if (!grouped) {
+    tm = L % tilesM;
+    tn = L / tilesM;
+    return;
+  }
+  const int gsz = 8 * tilesN, g = L / gsz, first = 8 * g, gm = min(8, tilesM - first), w = L - g * gsz;
+  tm = first + w % gm;
+  tn = w / gm;
+}
+
+// Tail split (tail > 0): this launch covers tiles [tile0, tile0 + tail), gridDim.y = S slices
+// each, and slab z of tile j is stored compactly at P[(z tail + j) BM BN] (tail_reduce_kernel
+// sums them) -- the last partial round of a large grid spread over S x as many workgroups.
 template <int WM, int BK>
 __global__ void __launch_bounds__(128 * WM)
 gemm_nt_f32x32_kernel(const float* __restrict__ X, int ldx, const float* __restrict__ W, int ldw,
-                      float* __restrict__ Y, int ldy, int M, int N, int K, Epi e, int kc, float* __restrict__ P) {
+                      float* __restrict__ Y, int ldy, int M, int N, int K, Epi e, int kc, float* __restrict__ P,
+                      int tile0 = 0, int tail = 0, int grouped = 0) {
   constexpr int BM = 64 * WM, BN = 128, NT = 128 * WM;
   constexpr int LD = BK + 4;
   constexpr int F4R = BK / 4;
@@ -194,7 +212,8 @@ gemm_nt_f32x32_kernel(const float* __restrict__ X, int ldx, const float* __restr
   __shared__ __attribute__((aligned(16))) float Bs[2][BN][LD];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int tilesM = (M + BM - 1) / BM;
-  const int tm = blockIdx.x % tilesM, tn = blockIdx.x / tilesM;
+  int tm, tn;
+  gemm_tile_of(tile0 + (int)blockIdx.x, tilesM, (N + BN - 1) / BN, grouped, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
   float4 ra[APER], rb[BPER];
   const __amdgpu_buffer_rsrc_t rX = gemm_rsrc(X, (int64_t)M * ldx * 4), rW = gemm_rsrc(W, (int64_t)N * ldw * 4);
@@ -275,10 +294,32 @@ gemm_nt_f32x32_kernel(const float* __restrict__ X, int ldx, const float* __restr
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
         if (m >= M) continue;
-        if (P) P[((int64_t)blockIdx.y * M + m) * N + n] = acc[i][j][r];
-        else Y[(int64_t)m * ldy + n] = apply_epi(e, acc[i][j][r], m, n);
+        if (tail > 0)
+          P[(((int64_t)blockIdx.y * tail + blockIdx.x) * BM + (m - m0)) * BN + (n - n0)] = acc[i][j][r];
+        else if (P)
+          P[((int64_t)blockIdx.y * M + m) * N + n] = acc[i][j][r];
+        else
+          Y[(int64_t)m * ldy + n] = apply_epi(e, acc[i][j][r], m, n);
       }
     }
+}
+
+// Y of the tail tiles = epi(sum of their S compact slabs, in slice order)
+template <int BM>
+__global__ void __launch_bounds__(256) tail_reduce_kernel(const float* __restrict__ P, int S, int tail, int tile0,
+                                                          float* __restrict__ Y, int ldy, int M, int N, Epi e,
+                                                          int grouped) {
+  constexpr int BN = 128;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (int64_t)tail * BM * BN) return;
+  const int j = (int)(t / (BM * BN)), rc = (int)(t - (int64_t)j * BM * BN);
+  int tm, tn;
+  gemm_tile_of(tile0 + j, (M + BM - 1) / BM, (N + BN - 1) / BN, grouped, tm, tn);
+  const int m = tm * BM + rc / BN, n = tn * BN + rc % BN;
+  if (m >= M || n >= N) return;
+  float v = P[t];
+  for (int z = 1; z < S; ++z) v += P[(int64_t)z * tail * BM * BN + t];
+  Y[(int64_t)m * ldy + n] = apply_epi(e, v, m, n);
 }
 
 // NN layout for the data gradient of many rows: dX[M, K] = mask(dZ[M, R] . W[R, K]) (W as
@@ -417,7 +458,8 @@ hipError_t gemm_nn_dgrad(const float* dZ, int ldz, const float* W, int ldw, cons
   if (t2 > 0x7fffffff) return hipErrorInvalidValue;
   int S = 1;
   if (ws == nullptr) ws_elems = 0;
-  while (S < 8 && t2 * S * 2 <= 640 && R / (S * 2) >= 256 && (int64_t)S * 2 * M * K <= ws_elems) S *= 2;
+  const int rmin = t2 < 32 ? 64 : 256;   // a grid of a few tiles: shorter slices (as gemm_nt_rows)
+  while (S < 8 && t2 * S * 2 <= 640 && R / (S * 2) >= rmin && (int64_t)S * 2 * M * K <= ws_elems) S *= 2;
   const int kc = S > 1 ? ((R + S - 1) / S + 15) / 16 * 16 : R;
   gemm_nn_f32x32_kernel<2><<<dim3((unsigned)t2, S), 256, 0, st>>>(dZ, ldz, W, ldw, dX, ldx, M, K, R, hprev, ldh,
                                                                  scale, kc, S > 1 ? ws : nullptr);
@@ -461,6 +503,19 @@ static hipError_t launch_gemm(const float* X, int ldx, const float* W, int ldw, 
 static hipError_t gemm_nt_rows(const float* X, int ldx, const float* W, int ldw, float* Y, int ldy, int M, int N,
                                int K, Epi e, bool bf16, float* ws, int64_t ws_elems, hipStream_t st);
 
+// compute units of the current device (cached per device)
+static int gemm_cus() {
+  static int cache[16] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return 256;
+  if (cache[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cache[dev] = n;
+  }
+  return cache[dev];
+}
+
 hipError_t gemm_nt(const float* X, int ldx, const float* W, int ldw, float* Y, int ldy, int M, int N, int K, Epi e,
                    bool bf16, float* ws, int64_t ws_elems, hipStream_t st) {
   if (M <= 0 || N <= 0) return hipSuccess;
@@ -493,11 +548,39 @@ static hipError_t gemm_nt_rows(const float* X, int ldx, const float* W, int ldw,
   // fp32: the 32 x 32 x 2 form.  256 x 128 tiles when they fill the chip (>= 1.5 per CU:
   // M 14000, N 1000 measured 108.8 vs 104.4 TF/s against 128 x 128 tiles), else 128 x 128
   // tiles, split over K until ~2 workgroups per CU (slices >= 512 deep, >= 256 when fewer
-  // tiles than CUs: M 14000, N 100, K 1000 ran 110 workgroups; <= 8 slices)
+  // tiles than CUs: M 14000, N 100, K 1000 ran 110 workgroups; <= 8 slices; a grid of a few
+  // tiles, whose time is its stage count times a loaded round trip, down to 64 deep:
+  // M 1000, N 100, K 1000 is 8 tiles)
   const int64_t t4 = (int64_t)((M + 255) / 256) * ((N + 127) / 128);
-  if (t4 >= 384) return launch_gemm_f32x32<4, 16>(X, ldx, W, ldw, Y, ldy, M, N, K, e, 1, nullptr, st);
+  if (t4 >= 384) {
+    // whole rounds of the resident slots (2 workgroups per CU) as full-K tiles; a last round
+    // under 3/4 full is instead split over K into up to S x its tiles (tail_reduce_kernel sums
+    // them): M 14000, N 5000 is 4 rounds of 512 plus 152 tiles
+    const int64_t slots = 2LL * gemm_cus();
+    const int64_t rem = t4 % slots, full = t4 - rem;
+    int S = 1;
+    if (full > 0 && rem > 0 && 4 * rem < 3 * slots) {
+      S = (int)std::min<int64_t>(8, slots / rem);
+      while (S > 1 && (K / S < 512 || (int64_t)S * rem * 256 * 128 > ws_elems)) --S;
+    }
+    const int grp = g_variant[9] == 1 ? 1 : 0;   // A/B of the tile order (scripts/gemm_bench.py)
+    if (S == 1) {
+      gemm_nt_f32x32_kernel<4, 16><<<(unsigned)t4, 512, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e, K, nullptr, 0, 0,
+                                                                 grp);
+      return hipGetLastError();
+    }
+    gemm_nt_f32x32_kernel<4, 16><<<(unsigned)full, 512, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e, K, nullptr, 0, 0,
+                                                                 grp);
+    const int kc = ((K + S - 1) / S + 15) / 16 * 16;
+    gemm_nt_f32x32_kernel<4, 16><<<dim3((unsigned)rem, S), 512, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e, kc, ws,
+                                                                        (int)full, (int)rem, grp);
+    const int64_t tot = rem * 256 * 128;
+    tail_reduce_kernel<256><<<(unsigned)((tot + 255) / 256), 256, 0, st>>>(ws, S, (int)rem, (int)full, Y, ldy, M, N,
+                                                                          e, grp);
+    return hipGetLastError();
+  }
   const int64_t t2 = (int64_t)((M + 127) / 128) * ((N + 127) / 128);
-  const int kmin = t2 < 256 ? 256 : 512;
+  const int kmin = t2 < 32 ? 64 : t2 < 256 ? 256 : 512;
   int S = 1;
   while (S < 8 && t2 * S * 2 <= 640 && K / (S * 2) >= kmin && (int64_t)S * 2 * M * N <= ws_elems) S *= 2;
   return launch_gemm_f32x32<2, 16>(X, ldx, W, ldw, Y, ldy, M, N, K, e, S, ws, st);

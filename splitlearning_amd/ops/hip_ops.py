@@ -230,7 +230,8 @@ def linear_fwd(x, w, b, relu: bool, drop_p: float, seed: int, col_offset: int = 
     elif ((M + 255) // 256) * ((N + 127) // 128) < 512:
         ws = _workspace(x.device, 8 * M * N, "gemm")     # split-K slabs of the tiled GEMM (csrc/gemm.hip)
     else:
-        ws = None
+        # a large grid's last partial round split over K: at most one round of 256 x 128 slabs
+        ws = _workspace(x.device, 1024 * 256 * 128, "gemm")
     C().linear_fwd(x, w, bias, out, relu, float(drop_p), seed & M64, col_offset, _ptr(dseed), ws)
     return out
 
