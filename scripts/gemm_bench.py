@@ -36,8 +36,6 @@ def main():
     ap.add_argument("--reps", type=int, default=8)
     ap.add_argument("--shapes", default="all", choices=("all", "eval", "big"))
     ap.add_argument("--dgrad", action="store_true")
-    ap.add_argument("--order", type=int, nargs="+", default=[0],
-                    help="tile orders to A/B on the large-grid form (variant slot 9: 0 tm fastest, 1 row bands)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     C = H.C()
@@ -75,16 +73,12 @@ def main():
         C.set_variant(11, 1)                  # the in-tree GEMM for fp32 too
         try:
             for f in a.forms:
-                for o in (a.order if f == 0 else [0]):
-                    C.set_variant(10, f)
-                    C.set_variant(9, o)
-                    y = H.linear_fwd(x, w, b, True, 0.0, 0)
-                    err = (y - ref).abs().max().item()
-                    t = bench(lambda: H.linear_fwd(x, w, b, True, 0.0, 0), a.reps)
-                    tag = f"form {f}" + (f" order {o}" if len(a.order) > 1 and f == 0 else "")
-                    line.append(f"{tag} {fl / t / 1e12:.1f} TF ({100 * t_mm / t:.0f} %, err {err:.1e})")
+                C.set_variant(10, f)
+                y = H.linear_fwd(x, w, b, True, 0.0, 0)
+                err = (y - ref).abs().max().item()
+                t = bench(lambda: H.linear_fwd(x, w, b, True, 0.0, 0), a.reps)
+                line.append(f"form {f} {fl / t / 1e12:.1f} TF ({100 * t_mm / t:.0f} %, err {err:.1e})")
             C.set_variant(10, 0)
-            C.set_variant(9, 0)
             C.set_compute_dtype("bf16")
             t = bench(lambda: H.linear_fwd(x, w, b, True, 0.0, 0), a.reps)
             line.append(f"bf16 {fl / t / 1e12:.1f} TF")

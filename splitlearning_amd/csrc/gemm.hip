@@ -179,20 +179,6 @@ gemm_nt_kernel(const float* __restrict__ X, int ldx, const float* __restrict__ W
 // Split-K (gridDim.y = S > 1, for grids of few tiles): slice z = blockIdx.y covers k in
 // [z kc, z kc + kc) and stores its raw partial sums into slab z of P ([S][M][N]); the slabs are
 // then reduced with the epilogue applied (linear_epilogue).
-// Logical tile index -> (tm, tn).  grouped == 0: tm fastest.  grouped == 1: bands of 8 tile
-// rows, tm fastest inside a band (consecutive workgroups, which land on consecutive XCDs, take
-// the 8 rows of one tile column: each XCD keeps one X row band for a whole column sweep).
-__device__ __forceinline__ void gemm_tile_of(int L, int tilesM, int tilesN, int grouped, int& tm, int& tn) {
-  if (!grouped) {
-    tm = L % tilesM;
-    tn = L / tilesM;
-    return;
-  }
-  const int gsz = 8 * tilesN, g = L / gsz, first = 8 * g, gm = min(8, tilesM - first), w = L - g * gsz;
-  tm = first + w % gm;
-  tn = w / gm;
-}
-
 // Tail split (tail > 0): this launch covers tiles [tile0, tile0 + tail), gridDim.y = S slices
 // each, and slab z of tile j is stored compactly at P[(z tail + j) BM BN] (tail_reduce_kernel
 // sums them) -- the last partial round of a large grid spread over S x as many workgroups.
@@ -200,7 +186,7 @@ template <int WM, int BK>
 __global__ void __launch_bounds__(128 * WM)
 gemm_nt_f32x32_kernel(const float* __restrict__ X, int ldx, const float* __restrict__ W, int ldw,
                       float* __restrict__ Y, int ldy, int M, int N, int K, Epi e, int kc, float* __restrict__ P,
-                      int tile0 = 0, int tail = 0, int grouped = 0) {
+                      int tile0 = 0, int tail = 0) {
   constexpr int BM = 64 * WM, BN = 128, NT = 128 * WM;
   constexpr int LD = BK + 4;
   constexpr int F4R = BK / 4;
@@ -212,8 +198,8 @@ gemm_nt_f32x32_kernel(const float* __restrict__ X, int ldx, const float* __restr
   __shared__ __attribute__((aligned(16))) float Bs[2][BN][LD];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int tilesM = (M + BM - 1) / BM;
-  int tm, tn;
-  gemm_tile_of(tile0 + (int)blockIdx.x, tilesM, (N + BN - 1) / BN, grouped, tm, tn);
+  const int tix = tile0 + (int)blockIdx.x;
+  const int tm = tix % tilesM, tn = tix / tilesM;
   const int m0 = tm * BM, n0 = tn * BN;
   float4 ra[APER], rb[BPER];
   const __amdgpu_buffer_rsrc_t rX = gemm_rsrc(X, (int64_t)M * ldx * 4), rW = gemm_rsrc(W, (int64_t)N * ldw * 4);
@@ -307,15 +293,13 @@ gemm_nt_f32x32_kernel(const float* __restrict__ X, int ldx, const float* __restr
 // Y of the tail tiles = epi(sum of their S compact slabs, in slice order)
 template <int BM>
 __global__ void __launch_bounds__(256) tail_reduce_kernel(const float* __restrict__ P, int S, int tail, int tile0,
-                                                          float* __restrict__ Y, int ldy, int M, int N, Epi e,
-                                                          int grouped) {
+                                                          float* __restrict__ Y, int ldy, int M, int N, Epi e) {
   constexpr int BN = 128;
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= (int64_t)tail * BM * BN) return;
   const int j = (int)(t / (BM * BN)), rc = (int)(t - (int64_t)j * BM * BN);
-  int tm, tn;
-  gemm_tile_of(tile0 + j, (M + BM - 1) / BM, (N + BN - 1) / BN, grouped, tm, tn);
-  const int m = tm * BM + rc / BN, n = tn * BN + rc % BN;
+  const int tilesM = (M + BM - 1) / BM, tix = tile0 + j;
+  const int m = (tix % tilesM) * BM + rc / BN, n = (tix / tilesM) * BN + rc % BN;
   if (m >= M || n >= N) return;
   float v = P[t];
   for (int z = 1; z < S; ++z) v += P[(int64_t)z * tail * BM * BN + t];
@@ -563,20 +547,16 @@ static hipError_t gemm_nt_rows(const float* X, int ldx, const float* W, int ldw,
       S = (int)std::min<int64_t>(8, slots / rem);
       while (S > 1 && (K / S < 512 || (int64_t)S * rem * 256 * 128 > ws_elems)) --S;
     }
-    const int grp = g_variant[9] == 1 ? 1 : 0;   // A/B of the tile order (scripts/gemm_bench.py)
-    if (S == 1) {
-      gemm_nt_f32x32_kernel<4, 16><<<(unsigned)t4, 512, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e, K, nullptr, 0, 0,
-                                                                 grp);
-      return hipGetLastError();
-    }
-    gemm_nt_f32x32_kernel<4, 16><<<(unsigned)full, 512, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e, K, nullptr, 0, 0,
-                                                                 grp);
+    // (a row-band tile order for L2 reuse within an XCD measured the same: 127.4 vs 127.2 TF at
+    // 14000 x 5000 x 5408, profiles/r4h_gemm_tile_order_ab.txt)
+    if (S == 1) return launch_gemm_f32x32<4, 16>(X, ldx, W, ldw, Y, ldy, M, N, K, e, 1, nullptr, st);
+    gemm_nt_f32x32_kernel<4, 16><<<(unsigned)full, 512, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e, K, nullptr);
     const int kc = ((K + S - 1) / S + 15) / 16 * 16;
     gemm_nt_f32x32_kernel<4, 16><<<dim3((unsigned)rem, S), 512, 0, st>>>(X, ldx, W, ldw, Y, ldy, M, N, K, e, kc, ws,
-                                                                        (int)full, (int)rem, grp);
+                                                                        (int)full, (int)rem);
     const int64_t tot = rem * 256 * 128;
     tail_reduce_kernel<256><<<(unsigned)((tot + 255) / 256), 256, 0, st>>>(ws, S, (int)rem, (int)full, Y, ldy, M, N,
-                                                                          e, grp);
+                                                                          e);
     return hipGetLastError();
   }
   const int64_t t2 = (int64_t)((M + 127) / 128) * ((N + 127) / 128);
