@@ -106,6 +106,19 @@ def main():
                   f"{dur.min():.1f}/{dur.median():.1f}/{dur.max():.1f}; stream end {en.min():.1f}/{en.median():.1f}/"
                   f"{en.max():.1f}; flush end {fl.min():.1f}/{fl.median():.1f}/{fl.max():.1f}; next F released "
                   f"{nx.min():.1f}/{nx.median():.1f}/{nx.max():.1f}", flush=True)
+            # is a workgroup's stream length a property of the workgroup within a launch (the same
+            # slow ones every step) or of the step?  correlation between steps of one launch
+            tall4 = torch.zeros(8, G, 4, dtype=torch.int64, device=dev)
+            ex.run(acts, labels, loss, tail.seed_base, tail.fwd_count, slot.t, None, tall4, 40)
+            torch.cuda.synchronize()
+            t4s = tall4.cpu().double() / 100.0
+            d4 = t4s[:, :, 1] - t4s[:, :, 0]
+            cc = [torch.corrcoef(torch.stack([d4[0], d4[k]]))[0, 1].item() for k in range(1, 8)]
+            slow = [set(torch.argsort(d4[k], descending=True)[:16].tolist()) for k in range(8)]
+            common = len(set.intersection(*slow[:4]))
+            print(f"tp={tp} per-workgroup stream length, steps 40..47 of one launch: correlation with step 40 "
+                  + " ".join(f"{c:.2f}" for c in cc) + f"; workgroups among the 16 slowest in all of steps 40-43: "
+                  f"{common}", flush=True)
             xcd = [dur[x::8].mean().item() for x in range(8)]
             print(f"tp={tp} stream length by w % 8: " + " ".join(f"{v:.1f}" for v in xcd), flush=True)
             order = torch.argsort(dur, descending=True)[:8].tolist()

@@ -66,8 +66,8 @@ struct HyArgs {
   IpcStep ipc;            // tensor-parallel fc2 exchange (ipc.T == 0: single shard)
   int64_t* trace;         // optional [2][trace_steps][16] phase stamps of workgroups 0 and G - 1
   int trace_steps;
-  int64_t* tall;          // optional [G][4] stamps of every workgroup at step tall_step: stream
-  int tall_step;          // start, stream end, flush end, and the next step's F wait end
+  int64_t* tall;          // optional [tall_n][G][4] stamps of every workgroup at steps tall_step ..:
+  int tall_step, tall_n;  // stream start, stream end, flush end, and the next step's F wait end
   int coop;               // cooperative launch (see resident.h)
 };
 

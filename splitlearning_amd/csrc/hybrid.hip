@@ -182,8 +182,8 @@ static_assert(kHyThreads / 64 * 10 * 256 >= kHyMaxWR * 4 * kHyMaxWC4, "10 W2 16 
 
 #define HY_ALL(i_, k)                                                                           \
   do {                                                                                           \
-    if (a.tall != nullptr && (i_) == a.tall_step && threadIdx.x == 0)                           \
-      a.tall[w * 4 + (k)] = (int64_t)wall_clock64();                                            \
+    if (a.tall != nullptr && (i_) >= a.tall_step && (i_) < a.tall_step + a.tall_n && threadIdx.x == 0) \
+      a.tall[((int64_t)((i_) - a.tall_step) * G + w) * 4 + (k)] = (int64_t)wall_clock64();       \
   } while (0)
 
 #define HY_MARK(k)                                                                               \

@@ -219,11 +219,13 @@ class HybridEpoch {
     }
     a.tall = nullptr;
     a.tall_step = (int)trace_all_step;
+    a.tall_n = 0;
     if (trace_all.has_value()) {
       TORCH_CHECK(trace_all->is_cuda() && trace_all->scalar_type() == at::kLong && trace_all->is_contiguous() &&
-                      trace_all->numel() >= 4LL * a.G,
-                  "trace_all int64 [G, 4]");
+                      trace_all->numel() >= 4LL * a.G && trace_all->numel() % (4LL * a.G) == 0,
+                  "trace_all int64 [steps, G, 4]");
       a.tall = trace_all->data_ptr<int64_t>();
+      a.tall_n = (int)(trace_all->numel() / (4LL * a.G));
     }
     const std::string why = sl::hybrid_check(a);
     TORCH_CHECK(why.empty(), "HybridEpoch: ", why);

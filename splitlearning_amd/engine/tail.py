@@ -35,6 +35,14 @@ from ..ops.rng import step_seed
 from .slots import OptSlot
 
 
+
+def _persist_workgroups(tail) -> int:
+    """Workgroups of a persistent epoch launch: 0 = one per CU, launched cooperatively; a
+    positive count (the ranks-share-one-GPU rehearsal, or SL_PERSIST_WORKGROUPS for profiling
+    tools that cannot follow a cooperative launch) = that many, plain launch."""
+    n = int(getattr(tail, "resident_workgroups", 0))
+    return n if n > 0 else int(os.environ.get("SL_PERSIST_WORKGROUPS", "0"))
+
 @dataclass
 class _Layer:
     spec: LinearSpec
@@ -462,7 +470,7 @@ class TailEngine:
              "p1": L1.spec.dropout, "p2": L2.spec.dropout, "col_off1": L1.col_off, "B": B,
              "ipc": getattr(self.allreduce, "ipc", None) if L2.style == "row" else None,
              "timeout_s": float(getattr(self, "resident_timeout_s", 10.0)),
-             "workgroups": int(getattr(self, "resident_workgroups", 0))}
+             "workgroups": _persist_workgroups(self)}
         ex = self.ops.C().ResidentEpoch(d)
         self._resident = (slot, B, ex, d)
         return ex
@@ -517,7 +525,7 @@ class TailEngine:
              "p1": L1.spec.dropout, "p2": L2.spec.dropout, "col_off1": L1.col_off, "B": B,
              "ipc": getattr(self.allreduce, "ipc", None) if L2.style == "row" else None,
              "timeout_s": float(getattr(self, "resident_timeout_s", 10.0)),
-             "workgroups": int(getattr(self, "resident_workgroups", 0))}
+             "workgroups": _persist_workgroups(self)}
         ex = self.ops.C().HybridEpoch(d)
         self._hybrid = (slot, B, ex, d)
         return ex
