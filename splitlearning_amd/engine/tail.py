@@ -25,6 +25,7 @@ MI355X design:
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import torch
@@ -35,13 +36,13 @@ from ..ops.rng import step_seed
 from .slots import OptSlot
 
 
-
 def _persist_workgroups(tail) -> int:
     """Workgroups of a persistent epoch launch: 0 = one per CU, launched cooperatively; a
     positive count (the ranks-share-one-GPU rehearsal, or SL_PERSIST_WORKGROUPS for profiling
     tools that cannot follow a cooperative launch) = that many, plain launch."""
     n = int(getattr(tail, "resident_workgroups", 0))
     return n if n > 0 else int(os.environ.get("SL_PERSIST_WORKGROUPS", "0"))
+
 
 @dataclass
 class _Layer:
