@@ -183,3 +183,25 @@ def test_reference_data_api(tmp_path):
         tr, te = load_shard(str(d), 1)
         assert tuple(tr["x"].shape[1:]) == shape and len(tr["y"]) == sizes[1][0]
         assert DeviceShard(tr["x"], tr["y"], torch.device("cpu")).x.shape[1] == 784
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B", [1, 5, 16])
+def test_act_label_message_pack_roundtrip(dtype, B):
+    """The per-batch [activation | labels] message (protocols/base.py Session.pack, the layout the
+    native split executor sends: labels as int64 words behind the rows, 16-byte padded) carries
+    the labels bit-exactly in any wire dtype and the activation unchanged."""
+    from splitlearning_amd.config import CUT_FEATURES
+    from splitlearning_amd.protocols.base import Session
+    g = torch.Generator().manual_seed(B)
+    act = torch.randn(B, CUT_FEATURES, generator=g).to(dtype)
+    labels = torch.randint(0, 10, (B,), generator=g)
+    labels[0] = 9
+    buf = Session.pack(act, labels)
+    assert buf.dtype == dtype and buf.numel() == Session.packed_len(B, dtype)
+    assert (buf.numel() * buf.element_size()) % 16 == 0
+    a2, l2 = Session.unpack(buf, B)
+    assert torch.equal(a2, act) and torch.equal(l2, labels) and l2.dtype == torch.int64
+    if dtype == torch.float32:
+        # csrc/split.cpp act_msg_words: M * 5408 + 2 M floats rounded up to 4
+        assert Session.packed_len(B, dtype) == (B * CUT_FEATURES + 2 * B + 3) // 4 * 4
