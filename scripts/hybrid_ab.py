@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--epochs", type=int, default=1)
     ap.add_argument("--trace", action="store_true")
     ap.add_argument("--only", choices=("both", "hybrid", "native"), default="both")
+    ap.add_argument("--wb", type=int, nargs="+", default=[-1],
+                    help="hybrid fc1 state stores to A/B: 0 write-through, 1 write-back, -1 the default rule")
     a = ap.parse_args()
     C = H.C()
     dev = torch.device("cuda", 0)
@@ -52,19 +54,23 @@ def main():
             ipc = C.IpcAllReduce(1, 0, 64 * 1024)
             ipc.open([ipc.handle()])
             ar = ipc_allreduce(ipc)
-        kinds = ("native", "hybrid") if a.only == "both" else (a.only,)
+        kinds = (["native"] if a.only != "hybrid" else []) + \
+            ([f"hybrid{'' if len(a.wb) == 1 else f'_wb{v}'}" for v in a.wb] if a.only != "native" else [])
         mods = {}
         for kind in kinds:
             torch.manual_seed(1)
             tail = TailEngine(ServerTailSisa(), sisa_server_spec(), dev, tp_rank=0, tp_size=tp, allreduce=ar,
                               ws_tag="#" + kind)
+            wbv = int(kind.split("_wb")[1]) if "_wb" in kind else a.wb[0]
+            tail.hybrid_wb = None if wbv < 0 else wbv
             slot = OptSlot(adam(1e-3, 1e-5))
             mods[kind] = (tail, slot)
-        if "hybrid" in mods:
-            tail, slot = mods["hybrid"]
-            if not tail.hybrid_ok(slot, B):
-                print(f"tp={tp}: hybrid epoch does not fit: {tail._hybrid_executor(slot, B).why()}", flush=True)
-                continue
+        hk = [k for k in mods if k.startswith("hybrid")]
+        bad = [k for k in hk if not mods[k][0].hybrid_ok(mods[k][1], B)]
+        if bad:
+            t0, s0 = mods[bad[0]]
+            print(f"tp={tp}: hybrid epoch does not fit: {t0._hybrid_executor(s0, B).why()}", flush=True)
+            continue
 
         def run(kind, k):
             tail, slot = mods[kind]
@@ -87,8 +93,8 @@ def main():
         for kind, xs in res.items():
             print(f"tp={tp} {kind:8s} median {statistics.median(xs):7.2f} us/step  min {min(xs):7.2f}  "
                   f"({' '.join(f'{x:.1f}' for x in xs)})", flush=True)
-        if a.trace and "hybrid" in mods:
-            tail, slot = mods["hybrid"]
+        if a.trace and hk:
+            tail, slot = mods[hk[-1]]
             ex = tail._hybrid_executor(slot, B)
             ts = 64
             tr = torch.zeros(2, ts, 16, dtype=torch.int64, device=dev)

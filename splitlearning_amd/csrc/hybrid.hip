@@ -339,6 +339,15 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
     }
   };
 
+  // fc1 state stores: write-through (the hand-off form) or plain write-back (a.wb; the same
+  // workgroup reads the tile again next step, through the same L2)
+  auto sst4 = [&](__amdgpu_buffer_rsrc_t rs, int boff, f32x4 v) {
+    if (a.wb)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(res_i32x4, v), rs, boff, 0, 0);
+    else
+      hst4(rs, boff, v);
+  };
+
   // One pass over this workgroup's tile run.  UPD: dW = dz1^T x_t and the optimizer step
   // (false: the prologue's read-only pass); LOOK: the look-ahead product with xn, per wave an
   // MFMA accumulator per row block, stored to ZP when the run leaves the row block.  sp / sm /
@@ -396,16 +405,16 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
         if (kin && n1 < N1) {
           res_update4<ADAM>(a.o, ss, ib, sp[cur][0], g0, sm[cur][0], sv[cur][0]);
           const int boff = (n1 * K1 + k) * 4;
-          hst4(rW1, boff, sp[cur][0]);
-          hst4(rM1, boff, sm[cur][0]);
-          if (ADAM) hst4(rV1, boff, sv[cur][0]);
+          sst4(rW1, boff, sp[cur][0]);
+          sst4(rM1, boff, sm[cur][0]);
+          if (ADAM) sst4(rV1, boff, sv[cur][0]);
         }
         if (kin && n1 + 8 < N1) {
           res_update4<ADAM>(a.o, ss, ib, sp[cur][1], g1, sm[cur][1], sv[cur][1]);
           const int boff = ((n1 + 8) * K1 + k) * 4;
-          hst4(rW1, boff, sp[cur][1]);
-          hst4(rM1, boff, sm[cur][1]);
-          if (ADAM) hst4(rV1, boff, sv[cur][1]);
+          sst4(rW1, boff, sp[cur][1]);
+          sst4(rM1, boff, sm[cur][1]);
+          if (ADAM) sst4(rV1, boff, sv[cur][1]);
         }
         if (j + 1 < nt) {
           sa[nb * 1024 + r * 64 + lane] = xa[0];
