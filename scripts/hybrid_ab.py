@@ -36,8 +36,8 @@ def main():
     ap.add_argument("--epochs", type=int, default=1)
     ap.add_argument("--trace", action="store_true")
     ap.add_argument("--only", choices=("both", "hybrid", "native"), default="both")
-    ap.add_argument("--wb", type=int, nargs="+", default=[-1],
-                    help="hybrid fc1 state stores to A/B: 0 write-through, 1 write-back, -1 the default rule")
+    ap.add_argument("--nt", type=int, nargs="+", default=[-1],
+                    help="hybrid fc1 state stores to A/B: 1 non-temporal, 0 write-through, -1 the default rule")
     a = ap.parse_args()
     C = H.C()
     dev = torch.device("cuda", 0)
@@ -54,15 +54,15 @@ def main():
             ipc = C.IpcAllReduce(1, 0, 64 * 1024)
             ipc.open([ipc.handle()])
             ar = ipc_allreduce(ipc)
-        kinds = (["native"] if a.only != "hybrid" else []) + \
-            ([f"hybrid{'' if len(a.wb) == 1 else f'_wb{v}'}" for v in a.wb] if a.only != "native" else [])
+        hyk = [f"hybrid{'' if len(a.nt) == 1 else f'_nt{v}'}" for v in a.nt]
+        kinds = (["native"] if a.only != "hybrid" else []) + (hyk if a.only != "native" else [])
         mods = {}
         for kind in kinds:
             torch.manual_seed(1)
             tail = TailEngine(ServerTailSisa(), sisa_server_spec(), dev, tp_rank=0, tp_size=tp, allreduce=ar,
                               ws_tag="#" + kind)
-            wbv = int(kind.split("_wb")[1]) if "_wb" in kind else a.wb[0]
-            tail.hybrid_wb = None if wbv < 0 else wbv
+            ntv = int(kind.split("_nt")[1]) if "_nt" in kind else a.nt[0]
+            tail.hybrid_nt_stores = None if ntv < 0 else ntv
             slot = OptSlot(adam(1e-3, 1e-5))
             mods[kind] = (tail, slot)
         hk = [k for k in mods if k.startswith("hybrid")]

@@ -192,7 +192,9 @@ static_assert(kHyThreads / 64 * 10 * 256 >= kHyMaxWR * 4 * kHyMaxWC4, "10 W2 16 
       a.trace[((int64_t)(w == 0 ? 0 : 1) * a.trace_steps + i) * 16 + (k)] = (int64_t)wall_clock64(); \
   } while (0)
 
-template <bool ADAM>
+// NTST: fc1 state stores non-temporal (a shard whose streamed state is larger than the 256 MB
+// Infinity Cache) or write-through (one that fits)
+template <bool ADAM, bool NTST>
 __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* sw2 = reinterpret_cast<float*>(smem + OFF_W2);
@@ -339,13 +341,13 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
     }
   };
 
-  // fc1 state stores: write-through (the hand-off form) or plain write-back (a.wb; the same
-  // workgroup reads the tile again next step, through the same L2)
+  // fc1 state stores: non-temporal (NTST: TP = 1, 150.1 vs 159.3 us per step write-through and
+  // 154.8 write-back) or write-through (TP = 2 / 4, where the state fits the Infinity Cache:
+  // 84.6 / 57.3 vs 96.9 / 63.4 non-temporal; profiles/r4o_hybrid_load_store_hints_ab.txt, with
+  // non-temporal loads never faster).  The same workgroup reads the tile again next step.
   auto sst4 = [&](__amdgpu_buffer_rsrc_t rs, int boff, f32x4 v) {
-    if (a.wb)
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(res_i32x4, v), rs, boff, 0, 0);
-    else
-      hst4(rs, boff, v);
+    constexpr int SP = NTST ? 2 : 16;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(res_i32x4, v), rs, boff, 0, SP);
   };
 
   // One pass over this workgroup's tile run.  UPD: dW = dz1^T x_t and the optimizer step
@@ -1005,6 +1007,15 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
 
 int hybrid_lds_bytes() { return kHyLds; }
 
+// the instantiation a launch uses: Adam / SGD-momentum, non-temporal or write-through state stores
+static const void* hybrid_fn(const HyArgs& a) {
+  if (a.o.kind == 2)
+    return a.ntst ? reinterpret_cast<const void*>(&hybrid_epoch_kernel<true, true>)
+                  : reinterpret_cast<const void*>(&hybrid_epoch_kernel<true, false>);
+  return a.ntst ? reinterpret_cast<const void*>(&hybrid_epoch_kernel<false, true>)
+                : reinterpret_cast<const void*>(&hybrid_epoch_kernel<false, false>);
+}
+
 std::string hybrid_check(const HyArgs& a) {
   if (a.M < 1 || a.M > 16) return "rows per step 1..16";
   if (a.G < 8 || a.G % kHyNR || a.NC != a.G / kHyNR || a.NC > kHyMaxNC) return "workgroups (8 x column blocks)";
@@ -1029,8 +1040,7 @@ bool hybrid_fits(const HyArgs& a, int device, std::string* why) {
     if (hipGetDeviceProperties(&pr, device) != hipSuccess) {
       s = "device properties";
     } else {
-      const void* fn = a.o.kind == 2 ? reinterpret_cast<const void*>(&hybrid_epoch_kernel<true>)
-                                     : reinterpret_cast<const void*>(&hybrid_epoch_kernel<false>);
+      const void* fn = hybrid_fn(a);
       int nb = 0;
       hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kHyLds);
       if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, kHyThreads, kHyLds);
@@ -1045,19 +1055,15 @@ bool hybrid_fits(const HyArgs& a, int device, std::string* why) {
 hipError_t hybrid_epoch_launch(const HyArgs& a, hipStream_t st) {
   if (!hybrid_check(a).empty()) return hipErrorInvalidValue;
   if (a.S <= 0) return hipSuccess;
-  const void* fn = a.o.kind == 2 ? reinterpret_cast<const void*>(&hybrid_epoch_kernel<true>)
-                                 : reinterpret_cast<const void*>(&hybrid_epoch_kernel<false>);
+  const void* fn = hybrid_fn(a);
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kHyLds);
   if (e != hipSuccess) return e;
   e = hipMemsetAsync(a.cnt, 0, (size_t)kHyCounters * kHyStride * sizeof(unsigned), st);
   if (e != hipSuccess) return e;
   HyArgs arg = a;
   if (!a.coop) {
-    if (a.o.kind == 2)
-      hybrid_epoch_kernel<true><<<a.G, kHyThreads, kHyLds, st>>>(arg);
-    else
-      hybrid_epoch_kernel<false><<<a.G, kHyThreads, kHyLds, st>>>(arg);
-    return hipGetLastError();
+    void* params[] = {&arg};
+    return hipLaunchKernel(fn, dim3(a.G), dim3(kHyThreads), params, (size_t)kHyLds, st);
   }
   void* params[] = {&arg};
   return hipLaunchCooperativeKernel(fn, dim3(a.G), dim3(kHyThreads), params, (unsigned)kHyLds, st);

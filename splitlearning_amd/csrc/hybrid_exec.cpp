@@ -90,14 +90,13 @@ class HybridEpoch {
     G -= G % sl::kHyNR;
     a.G = G;
     a.coop = wg > 0 ? 0 : 1;
-    // fc1 state stores: write-back when the shard's streamed state is larger than the 256 MB
-    // Infinity Cache (TP = 1: 158.6 vs 160.7 us per step), write-through when it fits (TP = 2:
-    // 86.9 vs 87.5, TP = 4: 58.4 vs 61.0; profiles/r4n_hybrid_store_policy_ab.txt); cfg "wb"
-    // (0 / 1) overrides for the A/B
+    // fc1 state stores non-temporal when the shard's streamed state is larger than the 256 MB
+    // Infinity Cache (TP = 1), write-through when it fits (csrc/hybrid.hip sst4); cfg
+    // "nt_stores" (0 / 1) overrides for the A/B
     {
       const int64_t state = (int64_t)L_[0].W.numel() * 4 * (kind_ == 2 ? 3 : 2);
-      const int wbc = cfg.contains("wb") && !cfg["wb"].is_none() ? cfg["wb"].cast<int>() : -1;
-      a.wb = wbc >= 0 ? wbc : (state > (256LL << 20) ? 1 : 0);
+      const int o = cfg.contains("nt_stores") && !cfg["nt_stores"].is_none() ? cfg["nt_stores"].cast<int>() : -1;
+      a.ntst = o >= 0 ? o : (state > (256LL << 20) ? 1 : 0);
     }
     a.NC = G / sl::kHyNR;
     a.HW = a.N2 / 4;

@@ -526,7 +526,7 @@ class TailEngine:
              "p1": L1.spec.dropout, "p2": L2.spec.dropout, "col_off1": L1.col_off, "B": B,
              "ipc": getattr(self.allreduce, "ipc", None) if L2.style == "row" else None,
              "timeout_s": float(getattr(self, "resident_timeout_s", 10.0)),
-             "workgroups": _persist_workgroups(self), "wb": getattr(self, "hybrid_wb", None)}
+             "workgroups": _persist_workgroups(self), "nt_stores": getattr(self, "hybrid_nt_stores", None)}
         ex = self.ops.C().HybridEpoch(d)
         self._hybrid = (slot, B, ex, d)
         return ex
