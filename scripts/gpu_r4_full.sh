@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-4 rehearsal of the driver's round-end GPU tiers: the whole GPU suite, smoke(), the
-# N = 1 bench at its defaults, and a rocprofv3 kernel table of one bench step.
+# N = 1 bench at its defaults, and a rocprofv3 kernel table of one bench step (persistent
+# epochs as plain launches: rocprofv3 crashes at exit after a cooperative launch).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" && mkdir -p gpurun_out/r4f
@@ -12,6 +13,6 @@ echo smoke ok
 timeout -k 10 600 python bench.py > gpurun_out/r4f/bench.json 2> gpurun_out/r4f/bench.err || { echo BENCH_FAIL; tail -20 gpurun_out/r4f/bench.err; exit 1; }
 tail -1 gpurun_out/r4f/bench.json | cut -c1-400
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/r4f/prof" -o run -- \
+SL_PERSIST_WORKGROUPS=256 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/r4f/prof" -o run -- \
   python3 "$R/bench.py" --steps 1 --warmup 0 > "$R/gpurun_out/r4f/prof.log" 2>&1 || { echo PROF_FAIL; tail -20 "$R/gpurun_out/r4f/prof.log"; exit 1; }
 echo prof-done
