@@ -137,10 +137,16 @@ def main():
                 d = (t[wgi, 8:ts - 1, 1:] - t[wgi, 8:ts - 1, :-1]) / khz * 1e3
                 valid = (t[wgi, 8:ts - 1, 1:] > 0) & (t[wgi, 8:ts - 1, :-1] > 0)
                 parts = []
-                for k in range(15):
+                for k in range(14):
                     v = d[:, k][valid[:, k]]
                     if v.numel():
                         parts.append(f"{PHASES[k]} {v.mean().item():.2f}")
+                fl = t[wgi, 8:ts - 1]
+                okf = (fl[:, 15] > 0) & (fl[:, 13] > 0) & (fl[:, 14] > 0)
+                if okf.any():
+                    dr = ((fl[:, 15] - fl[:, 13]) / khz * 1e3)[okf].mean().item()
+                    rest = ((fl[:, 14] - fl[:, 15]) / khz * 1e3)[okf].mean().item()
+                    parts.append(f"(flush: drain {dr:.2f} + publish {rest:.2f})")
                 step = (t[wgi, 9:ts - 1, 0] - t[wgi, 8:ts - 2, 0]) / khz * 1e3
                 print(f"tp={tp} trace {name}: step {step.mean().item():.2f} us | " + ", ".join(parts), flush=True)
         del mods, acts

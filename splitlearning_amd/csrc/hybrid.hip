@@ -463,6 +463,10 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     {
+      const int i = so - 1;   // trace: the drain of the run's last stores ends (stamp 15)
+      HY_MARK(15);
+    }
+    {
       HY_IDX();
       for (int e = tid; e < nruns * 256; e += kHyThreads) {
         const int k = e >> 8, m = (e >> 4) & 15, nn = e & 15;
