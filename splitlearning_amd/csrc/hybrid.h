@@ -69,7 +69,7 @@ struct HyArgs {
   int64_t* tall;          // optional [tall_n][G][4] stamps of every workgroup at steps tall_step ..:
   int tall_step, tall_n;  // stream start, stream end, flush end, and the next step's F wait end
   int coop;               // cooperative launch (see resident.h)
-  int ntst;               // fc1 state stores non-temporal (1) or write-through (0)
+  int ntst;               // fc1 state policy: over-cache form (1: W plain, m / v non-temporal) or write-through (0)
 };
 
 hipError_t hybrid_epoch_launch(const HyArgs& a, hipStream_t st);

@@ -135,6 +135,19 @@ __device__ __forceinline__ bool hy_seam_wait(const HyArgs& a, int seam, unsigned
   return *s_ok != 0;
 }
 
+// fc1 state cache policy (buffer aux bits: 2 = non-temporal, 16 = write-through, 0 = plain).
+// When the shard's state exceeds the 256 MB Infinity Cache (NTST, TP = 1: 325 MB with Adam),
+// W is stored and loaded plain and m / v non-temporal, both ways: W's 108 MB then stay in the
+// Infinity Cache from one step to the next while m / v stream past it without evicting it
+// (TP = 1 144.7 us per step against 151.4 with every store non-temporal, 159.3 with every
+// store write-through; W and m kept 149.2, W write-through 148.0;
+// profiles/r4w_hybrid_per_array_cache_policy_ab.txt).  When it fits (TP = 2 / 4), every
+// array write-through: 85.5 / 58.6 against 87.1 / 60.7 plain and 96.9 / 63.4 non-temporal.
+// The same workgroup (same CU) reads a tile again next step.
+constexpr int kStW = 0, kStM = 2, kStV = 2;
+constexpr int kLdW = 0, kLdM = 2, kLdV = 2;
+constexpr int kStFit = 16;
+
 // fc2 column block of fc2 column (= fc1 shard row) float4 group n4: blocks [q0_b, q0_{b+1})
 // with q0_b = floor(b Q4 / NC)
 __device__ __forceinline__ int hy_colblk(int n4, int NC, int Q4) { return ((n4 + 1) * NC + Q4 - 1) / Q4 - 1; }
@@ -307,10 +320,10 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
       const int n = 16 * rb + r + 8 * h;
       const bool act = n < N1 && k < K1;
       const int boff = (n * K1 + k) * 4;
-      p[h] = act ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rW1, boff, 0, 0)) : zv;
+      p[h] = act ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rW1, boff, 0, NTST ? kLdW : 0)) : zv;
       if (upd) {
-        mm[h] = act ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rM1, boff, 0, 0)) : zv;
-        vv[h] = (act && ADAM) ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rV1, boff, 0, 0)) : zv;
+        mm[h] = act ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rM1, boff, 0, NTST ? kLdM : 0)) : zv;
+        vv[h] = (act && ADAM) ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rV1, boff, 0, NTST ? kLdV : 0)) : zv;
       }
     }
   };
@@ -341,14 +354,14 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
     }
   };
 
-  // fc1 state stores: non-temporal (NTST: TP = 1, 150.1 vs 159.3 us per step write-through and
-  // 154.8 write-back) or write-through (TP = 2 / 4, where the state fits the Infinity Cache:
-  // 84.6 / 57.3 vs 96.9 / 63.4 non-temporal; profiles/r4o_hybrid_load_store_hints_ab.txt, with
-  // non-temporal loads never faster).  The same workgroup reads the tile again next step.
-  auto sst4 = [&](__amdgpu_buffer_rsrc_t rs, int boff, f32x4 v) {
-    constexpr int SP = NTST ? 2 : 16;
+  // fc1 state stores: the policy above (kSt*, kStFit)
+  auto sst4 = [&](auto sp_c, __amdgpu_buffer_rsrc_t rs, int boff, f32x4 v) {
+    constexpr int SP = NTST ? decltype(sp_c)::value : kStFit;
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(res_i32x4, v), rs, boff, 0, SP);
   };
+  using StW = std::integral_constant<int, kStW>;
+  using StM = std::integral_constant<int, kStM>;
+  using StV = std::integral_constant<int, kStV>;
 
   // One pass over this workgroup's tile run.  UPD: dW = dz1^T x_t and the optimizer step
   // (false: the prologue's read-only pass); LOOK: the look-ahead product with xn, per wave an
@@ -407,16 +420,16 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
         if (kin && n1 < N1) {
           res_update4<ADAM>(a.o, ss, ib, sp[cur][0], g0, sm[cur][0], sv[cur][0]);
           const int boff = (n1 * K1 + k) * 4;
-          sst4(rW1, boff, sp[cur][0]);
-          sst4(rM1, boff, sm[cur][0]);
-          if (ADAM) sst4(rV1, boff, sv[cur][0]);
+          sst4(StW{}, rW1, boff, sp[cur][0]);
+          sst4(StM{}, rM1, boff, sm[cur][0]);
+          if (ADAM) sst4(StV{}, rV1, boff, sv[cur][0]);
         }
         if (kin && n1 + 8 < N1) {
           res_update4<ADAM>(a.o, ss, ib, sp[cur][1], g1, sm[cur][1], sv[cur][1]);
           const int boff = ((n1 + 8) * K1 + k) * 4;
-          sst4(rW1, boff, sp[cur][1]);
-          sst4(rM1, boff, sm[cur][1]);
-          if (ADAM) sst4(rV1, boff, sv[cur][1]);
+          sst4(StW{}, rW1, boff, sp[cur][1]);
+          sst4(StM{}, rM1, boff, sm[cur][1]);
+          if (ADAM) sst4(StV{}, rV1, boff, sv[cur][1]);
         }
         if (j + 1 < nt) {
           sa[nb * 1024 + r * 64 + lane] = xa[0];

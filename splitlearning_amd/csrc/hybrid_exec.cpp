@@ -90,9 +90,9 @@ class HybridEpoch {
     G -= G % sl::kHyNR;
     a.G = G;
     a.coop = wg > 0 ? 0 : 1;
-    // fc1 state stores non-temporal when the shard's streamed state is larger than the 256 MB
-    // Infinity Cache (TP = 1), write-through when it fits (csrc/hybrid.hip sst4); cfg
-    // "nt_stores" (0 / 1) overrides for the A/B
+    // fc1 state cache policy: the over-cache form (W plain, m / v non-temporal) when the
+    // shard's streamed state is larger than the 256 MB Infinity Cache (TP = 1), write-through
+    // when it fits (csrc/hybrid.hip kStW ..); cfg "nt_stores" (0 / 1) overrides for the A/B
     {
       const int64_t state = (int64_t)L_[0].W.numel() * 4 * (kind_ == 2 ? 3 : 2);
       const int o = cfg.contains("nt_stores") && !cfg["nt_stores"].is_none() ? cfg["nt_stores"].cast<int>() : -1;
