@@ -143,9 +143,12 @@ __device__ __forceinline__ bool hy_seam_wait(const HyArgs& a, int seam, unsigned
 // store write-through; W and m kept 149.2, W write-through 148.0;
 // profiles/r4w_hybrid_per_array_cache_policy_ab.txt).  When it fits (TP = 2 / 4), every
 // array write-through: 85.5 / 58.6 against 87.1 / 60.7 plain and 96.9 / 63.4 non-temporal.
-// The same workgroup (same CU) reads a tile again next step.
+// The same workgroup (same CU) reads a tile again next step.  On top, one workgroup in 8
+// keeps its m tiles plain as well (13.5 MB more in the cache): 142.5-142.8 vs 144.8-145.0
+// (one in 2 or 4: 143.3-143.8).
 constexpr int kStW = 0, kStM = 2, kStV = 2;
 constexpr int kLdW = 0, kLdM = 2, kLdV = 2;
+constexpr int kKeepM = 7;
 constexpr int kStFit = 16;
 
 // fc2 column block of fc2 column (= fc1 shard row) float4 group n4: blocks [q0_b, q0_{b+1})
@@ -311,6 +314,8 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
 
   // ---------------------------------------------------------------- fc1 tile stream
   // state of tile t (rows n0 + r + 8h, float4 column kb + 4 lane) into p / m / v
+  // over the cache (NTST): the workgroups w % (kKeepM + 1) == 0 keep their m tiles plain too
+  const bool mkeep = NTST && (w & kKeepM) == 0;
   auto load_state = [&](int t, f32x4 (&p)[2], f32x4 (&mm)[2], f32x4 (&vv)[2], bool upd) {
     HY_IDX();
     const int rb = t / ncb, cb = t - (t / ncb) * ncb;
@@ -322,7 +327,9 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
       const int boff = (n * K1 + k) * 4;
       p[h] = act ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rW1, boff, 0, NTST ? kLdW : 0)) : zv;
       if (upd) {
-        mm[h] = act ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rM1, boff, 0, NTST ? kLdM : 0)) : zv;
+        mm[h] = act ? (mkeep ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rM1, boff, 0, 0))
+                             : __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rM1, boff, 0, NTST ? kLdM : 0)))
+                    : zv;
         vv[h] = (act && ADAM) ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rV1, boff, 0, NTST ? kLdV : 0)) : zv;
       }
     }
@@ -421,14 +428,16 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
           res_update4<ADAM>(a.o, ss, ib, sp[cur][0], g0, sm[cur][0], sv[cur][0]);
           const int boff = (n1 * K1 + k) * 4;
           sst4(StW{}, rW1, boff, sp[cur][0]);
-          sst4(StM{}, rM1, boff, sm[cur][0]);
+          if (mkeep) sst4(std::integral_constant<int, 0>{}, rM1, boff, sm[cur][0]);
+          else sst4(StM{}, rM1, boff, sm[cur][0]);
           if (ADAM) sst4(StV{}, rV1, boff, sv[cur][0]);
         }
         if (kin && n1 + 8 < N1) {
           res_update4<ADAM>(a.o, ss, ib, sp[cur][1], g1, sm[cur][1], sv[cur][1]);
           const int boff = ((n1 + 8) * K1 + k) * 4;
           sst4(StW{}, rW1, boff, sp[cur][1]);
-          sst4(StM{}, rM1, boff, sm[cur][1]);
+          if (mkeep) sst4(std::integral_constant<int, 0>{}, rM1, boff, sm[cur][1]);
+          else sst4(StM{}, rM1, boff, sm[cur][1]);
           if (ADAM) sst4(StV{}, rV1, boff, sv[cur][1]);
         }
         if (j + 1 < nt) {
