@@ -304,6 +304,9 @@ def main(argv=None):
                 if sargs.mode in ("sisa", "control") else None,
                 # why: adopted, or the fit / self-test outcome that kept launch-per-stage
                 "server_executor_reason": (getattr(sess, "resident_status", None) or {}).get("reason"),
+                # a persistent epoch that failed mid-launch: rolled back, the job continued on
+                # launch-per-stage from that client epoch on ({from, epoch, reason}; None: none)
+                "server_executor_fallback": (getattr(sess, "resident_status", None) or {}).get("fallback"),
                 "calib": calib,
                 # vanilla / U-shape: the native split epochs this rank ran (co-located, or its
                 # side of a remote Alice's) and the per-batch link of the remote ones

@@ -28,6 +28,48 @@ PHASES = ["F wait", "F h1 load+mma", "H wait", "H+L", "S wait", "S", "H2 wait", 
           "W2 update", "U wait P", "U dz1+stream", "flush", "end"]
 
 
+# stamps of csrc/hybrid.hip HY_MARK: (index, label, who runs it)
+STAMPS = [(14, "flush end", "all"), (1, "F wait end (h1 published)", "all"), (2, "F arrive", "all"),
+          (3, "H wait end", "head"), (4, "H arrive", "head"), (5, "S wait end", "rows"), (6, "S arrive", "rows"),
+          (7, "H2 wait end", "head"), (8, "H2 arrive", "head"), (9, "B wait end", "all"), (10, "B arrive", "all"),
+          (11, "W2 update end", "all"), (12, "P wait end (stream start)", "all"), (13, "stream end", "all")]
+
+
+def critical_path(tp, ta, G):
+    """Per-seam latency table of one launch: every workgroup's phase stamps for consecutive
+    steps, each boundary as min / median / max over the workgroups that run it, in us after the
+    previous step's LAST stream end (T0), averaged over the step pairs.  A seam's latency is the
+    gap between the last producer's arrival (max of the arrive row) and the first consumer's
+    release (min of the next wait-end row)."""
+    NS = ta.shape[0]
+    rows = {k: [] for k, _, _ in STAMPS}
+    slen, spread = [], []
+    for s in range(NS - 1):
+        t0 = ta[s, :, 13].max()
+        for k, _, _ in STAMPS:
+            src = ta[s] if k == 14 else ta[s + 1]
+            v = src[:, k]
+            v = v[v > 0] - t0
+            if v.numel():
+                rows[k].append((v.min().item(), v.median().item(), v.max().item()))
+        d = ta[s, :, 13] - ta[s, :, 12]
+        slen.append((d.min().item(), d.median().item(), d.max().item()))
+        spread.append((ta[s + 1, :, 13].max() - t0).item())
+    print(f"tp={tp} critical path (us after the previous step's last stream end; min / median / max over "
+          f"workgroups, mean of {NS - 1} step pairs):", flush=True)
+    prev_max = None
+    for k, label, who in STAMPS:
+        if not rows[k]:
+            continue
+        mn, md, mx = (statistics.mean(r[i] for r in rows[k]) for i in range(3))
+        gap = f"  (+{mn - prev_max:5.2f} from the last arrival above)" if prev_max is not None and "wait" in label else ""
+        print(f"tp={tp}   {label:28s} [{who:4s}] {mn:7.2f} {md:7.2f} {mx:7.2f}{gap}", flush=True)
+        prev_max = mx
+    mn, md, mx = (statistics.mean(r[i] for r in slen) for i in range(3))
+    print(f"tp={tp}   stream length min / median / max {mn:.2f} / {md:.2f} / {mx:.2f}; step (last stream end to "
+          f"last stream end) {statistics.mean(spread):.2f}", flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tp", type=int, nargs="+", default=[1])
@@ -100,37 +142,11 @@ def main():
             tr = torch.zeros(2, ts, 16, dtype=torch.int64, device=dev)
             loss = torch.empty(n, device=dev)
             G = ex.workgroups()
-            tall = torch.zeros(G, 4, dtype=torch.int64, device=dev)
+            NS = 8
+            tall = torch.zeros(NS, G, 16, dtype=torch.int64, device=dev)
             ex.run(acts, labels, loss, tail.seed_base, tail.fwd_count, slot.t, tr, tall, 40)
             torch.cuda.synchronize()
-            ta = tall.cpu().double() / 100.0   # us (100 MHz wall clock)
-            s0 = ta[:, 0].min()
-            st, en, fl, nx = ta[:, 0] - s0, ta[:, 1] - s0, ta[:, 2] - s0, ta[:, 3] - s0
-            dur = en - st
-            print(f"tp={tp} per-workgroup (step 40, us from the first stream start): stream start "
-                  f"min/med/max {st.min():.1f}/{st.median():.1f}/{st.max():.1f}; stream length "
-                  f"{dur.min():.1f}/{dur.median():.1f}/{dur.max():.1f}; stream end {en.min():.1f}/{en.median():.1f}/"
-                  f"{en.max():.1f}; flush end {fl.min():.1f}/{fl.median():.1f}/{fl.max():.1f}; next F released "
-                  f"{nx.min():.1f}/{nx.median():.1f}/{nx.max():.1f}", flush=True)
-            # is a workgroup's stream length a property of the workgroup within a launch (the same
-            # slow ones every step) or of the step?  correlation between steps of one launch
-            tall4 = torch.zeros(8, G, 4, dtype=torch.int64, device=dev)
-            ex.run(acts, labels, loss, tail.seed_base, tail.fwd_count, slot.t, None, tall4, 40)
-            torch.cuda.synchronize()
-            t4s = tall4.cpu().double() / 100.0
-            d4 = t4s[:, :, 1] - t4s[:, :, 0]
-            cc = [torch.corrcoef(torch.stack([d4[0], d4[k]]))[0, 1].item() for k in range(1, 8)]
-            slow = [set(torch.argsort(d4[k], descending=True)[:16].tolist()) for k in range(8)]
-            common = len(set.intersection(*slow[:4]))
-            print(f"tp={tp} per-workgroup stream length, steps 40..47 of one launch: correlation with step 40 "
-                  + " ".join(f"{c:.2f}" for c in cc) + f"; workgroups among the 16 slowest in all of steps 40-43: "
-                  f"{common}", flush=True)
-            xcd = [dur[x::8].mean().item() for x in range(8)]
-            print(f"tp={tp} stream length by w % 8: " + " ".join(f"{v:.1f}" for v in xcd), flush=True)
-            order = torch.argsort(dur, descending=True)[:8].tolist()
-            print(f"tp={tp} slowest workgroups: " + " ".join(f"{w}:{dur[w]:.1f}" for w in order), flush=True)
-            blk = [dur[i:i + 32].mean().item() for i in range(0, G, 32)]
-            print(f"tp={tp} stream length by w // 32: " + " ".join(f"{v:.1f}" for v in blk), flush=True)
+            critical_path(tp, tall.cpu().double() / 100.0, G)   # us (100 MHz wall clock)
             khz = 100000.0
             t = tr.cpu().double()
             for wgi, name in ((0, "wg 0"), (1, "wg G-1")):

@@ -138,6 +138,11 @@ def build_parser() -> argparse.ArgumentParser:
                         "fc1's weights / Adam state streamed through the launch (csrc/hybrid.hip); "
                         "'auto' uses it where it fits and, tensor-parallel, after a cross-rank "
                         "self-test passed; 'off' = the launch-per-stage executor")
+    g.add_argument("--persistent_failsafe", choices=("on", "off"), default="on",
+                   help="copy Bob's shard (weights, optimizer state) before each persistent server "
+                        "epoch; if the launch fails mid-epoch on any Bob rank, restore it on every "
+                        "rank and continue on the launch-per-stage executor (about 0.1 ms per client "
+                        "epoch at TP = 1); 'off' = a failed launch ends the job")
     g.add_argument("--split_channel", choices=("auto", "ipc", "rccl"), default="auto",
                    help="vanilla / U-shape with the Alice remote from a one-shard Bob: the native "
                         "split epoch's per-batch link.  'auto' / 'ipc' = one-kernel messages over "

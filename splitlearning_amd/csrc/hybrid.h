@@ -66,10 +66,11 @@ struct HyArgs {
   IpcStep ipc;            // tensor-parallel fc2 exchange (ipc.T == 0: single shard)
   int64_t* trace;         // optional [2][trace_steps][16] phase stamps of workgroups 0 and G - 1
   int trace_steps;
-  int64_t* tall;          // optional [tall_n][G][4] stamps of every workgroup at steps tall_step ..:
-  int tall_step, tall_n;  // stream start, stream end, flush end, and the next step's F wait end
+  int64_t* tall;          // optional [tall_n][G][16] phase stamps (as trace) of every workgroup at
+  int tall_step, tall_n;  // steps tall_step .. tall_step + tall_n - 1
   int coop;               // cooperative launch (see resident.h)
   int ntst;               // fc1 state policy: over-cache form (1: W plain, m / v non-temporal) or write-through (0)
+  int fault_step;         // fault injection (tests): every workgroup stops at this step with err |= 8 (-1: off)
 };
 
 hipError_t hybrid_epoch_launch(const HyArgs& a, hipStream_t st);

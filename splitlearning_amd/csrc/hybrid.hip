@@ -196,16 +196,17 @@ static_assert(kHyThreads / 64 * 10 * 256 >= kHyMaxWR * 4 * kHyMaxWC4, "10 W2 16 
   const int tid = tid_l_, r = tid >> 6, lane = tid & 63, li = lane & 15, lq = lane >> 4; \
   (void)r; (void)lane; (void)li; (void)lq
 
-#define HY_ALL(i_, k)                                                                           \
-  do {                                                                                           \
-    if (a.tall != nullptr && (i_) >= a.tall_step && (i_) < a.tall_step + a.tall_n && threadIdx.x == 0) \
-      a.tall[((int64_t)((i_) - a.tall_step) * G + w) * 4 + (k)] = (int64_t)wall_clock64();       \
-  } while (0)
-
+// phase stamps (wall clock): workgroups 0 and G - 1 for the first trace_steps steps (trace), and
+// every workgroup for steps tall_step .. tall_step + tall_n - 1 (tall [tall_n][G][16]: the
+// critical-path table of scripts/hybrid_ab.py --trace)
 #define HY_MARK(k)                                                                               \
   do {                                                                                           \
-    if (a.trace != nullptr && i < a.trace_steps && threadIdx.x == 0 && (w == 0 || w == G - 1))  \
-      a.trace[((int64_t)(w == 0 ? 0 : 1) * a.trace_steps + i) * 16 + (k)] = (int64_t)wall_clock64(); \
+    if (threadIdx.x == 0) {                                                                      \
+      if (a.trace != nullptr && i < a.trace_steps && (w == 0 || w == G - 1))                     \
+        a.trace[((int64_t)(w == 0 ? 0 : 1) * a.trace_steps + i) * 16 + (k)] = (int64_t)wall_clock64(); \
+      if (a.tall != nullptr && i >= a.tall_step && i < a.tall_step + a.tall_n)                   \
+        a.tall[((int64_t)(i - a.tall_step) * G + w) * 16 + (k)] = (int64_t)wall_clock64();       \
+    }                                                                                            \
   } while (0)
 
 // NTST: fc1 state stores non-temporal (a shard whose streamed state is larger than the 256 MB
@@ -563,6 +564,10 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
   flush(0, 1u);
 
   for (int i = 0; i < a.S; ++i) {
+    if (i == a.fault_step) {   // uniform: every workgroup stops here (tests: mid-epoch failure)
+      if (w == 0 && threadIdx.x == 0) __hip_atomic_fetch_or(a.err, 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
     const int par = i & 1;
     const bool more = i + 1 < a.S;
     const uint32_t sd2 = a.seeds[4 * i + 2], sd3 = a.seeds[4 * i + 3];
@@ -578,7 +583,6 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
       if (!hy_wait(a, 1, idx, tgt, s_ok)) break;
     }
     HY_MARK(1);
-    HY_ALL(i - 1, 3);
     {
       HY_IDX();
 #pragma unroll
@@ -925,7 +929,6 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
       if (nruns > 0 && *s_ok == 0) break;
     }
     HY_MARK(12);
-    HY_ALL(i, 0);
     {
       HY_IDX();
       for (int e = tid; e < kHyRuns * 256; e += kHyThreads) {
@@ -963,9 +966,7 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
     if (more) {
       stream(std::true_type{}, std::true_type{}, xt, xn, ss, ib);
       HY_MARK(13);
-      HY_ALL(i, 1);
       flush(i + 1, (unsigned)(i + 2));
-      HY_ALL(i, 2);
     } else {
       stream(std::true_type{}, std::false_type{}, xt, xn, ss, ib);
     }
@@ -1029,7 +1030,6 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
 }
 #undef HY_IDX
 #undef HY_MARK
-#undef HY_ALL
 
 int hybrid_lds_bytes() { return kHyLds; }
 

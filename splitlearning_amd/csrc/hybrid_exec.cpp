@@ -90,6 +90,12 @@ class HybridEpoch {
     G -= G % sl::kHyNR;
     a.G = G;
     a.coop = wg > 0 ? 0 : 1;
+    a.fault_step = -1;
+    // steps per launch: the inputs of one launch are addressed with 32-bit buffer offsets
+    // (S * M * K1 * 4 < 2 GB); cfg "chunk_steps" lowers the bound (tests)
+    max_steps_ = (int64_t)(2147483647LL / ((int64_t)std::max(B_, 1) * std::max<int64_t>(L_[0].W.size(1), 1) * 4));
+    if (cfg.contains("chunk_steps") && !cfg["chunk_steps"].is_none())
+      max_steps_ = std::max<int64_t>(1, std::min<int64_t>(max_steps_, cfg["chunk_steps"].cast<int64_t>()));
     // fc1 state cache policy: the over-cache form (W plain, m / v non-temporal) when the
     // shard's streamed state is larger than the 256 MB Infinity Cache (TP = 1), write-through
     // when it fits (csrc/hybrid.hip kStW ..); cfg "nt_stores" (0 / 1) overrides for the A/B
@@ -175,8 +181,13 @@ class HybridEpoch {
   std::string why() const { return why_; }
   int workgroups() const { return a_.G; }
 
-  // Every full batch of acts [n, K1] / labels [n] (the first n - n % B rows) in ONE launch;
-  // losses into loss_rows [n].  Returns (fwd_count, t, rows done).
+  // Every full batch of acts [n, K1] / labels [n] (the first n - n % B rows): ONE launch, or
+  // consecutive launches of at most max_steps_ steps when the epoch's inputs exceed the 32-bit
+  // buffer offsets (each launch re-forms its first step's fc1 product in its prologue; one
+  // launch of S steps is bitwise S one-step launches, tests/test_hybrid_gpu.py, so the chunked
+  // epoch is bitwise the single launch).  Losses into loss_rows [n].  Returns (fwd_count, t,
+  // rows done).  Raises when an in-launch wait gave up (the shard's state is then partly
+  // updated: the caller restores it, protocols/sisa.py).
   py::tuple run(const at::Tensor& acts, const at::Tensor& labels, at::Tensor& loss_rows, int64_t seed_base,
                 int64_t fwd_count, int64_t t, const c10::optional<at::Tensor>& trace,
                 const c10::optional<at::Tensor>& trace_all, int64_t trace_all_step) {
@@ -207,45 +218,64 @@ class HybridEpoch {
     const at::Device dev = acts.device();
     adam_ = at::from_blob(adam.data(), {2 * S}, at::TensorOptions().dtype(at::kFloat)).to(dev);
     seeds_ = at::from_blob(seeds.data(), {4 * S}, at::TensorOptions().dtype(at::kInt)).to(dev);
-    sl::HyArgs a = a_;
-    a.S = (int)S;
-    a.X = acts.data_ptr<float>();
-    a.Y = labels.data_ptr<int64_t>();
-    a.loss = loss_rows.data_ptr<float>();
-    a.adam = adam_.data_ptr<float>();
-    a.seeds = reinterpret_cast<const uint32_t*>(seeds_.data_ptr<int32_t>());
-    a.ipc.T = 0;
-    if (ipc_ != nullptr) a.ipc = ipc_->begin_steps(S);
-    a.trace = nullptr;
-    a.trace_steps = 0;
+    int64_t* tr = nullptr;
+    int trs = 0;
     if (trace.has_value()) {
       TORCH_CHECK(trace->is_cuda() && trace->scalar_type() == at::kLong && trace->is_contiguous() &&
                       trace->numel() % 32 == 0,
                   "trace int64 [2, steps, 16]");
-      a.trace = trace->data_ptr<int64_t>();
-      a.trace_steps = (int)(trace->numel() / 32);
+      tr = trace->data_ptr<int64_t>();
+      trs = (int)(trace->numel() / 32);
     }
-    a.tall = nullptr;
-    a.tall_step = (int)trace_all_step;
-    a.tall_n = 0;
+    int64_t* ta = nullptr;
+    int tan = 0;
     if (trace_all.has_value()) {
       TORCH_CHECK(trace_all->is_cuda() && trace_all->scalar_type() == at::kLong && trace_all->is_contiguous() &&
-                      trace_all->numel() >= 4LL * a.G && trace_all->numel() % (4LL * a.G) == 0,
-                  "trace_all int64 [steps, G, 4]");
-      a.tall = trace_all->data_ptr<int64_t>();
-      a.tall_n = (int)(trace_all->numel() / (4LL * a.G));
+                      trace_all->numel() >= 16LL * a_.G && trace_all->numel() % (16LL * a_.G) == 0,
+                  "trace_all int64 [steps, G, 16]");
+      ta = trace_all->data_ptr<int64_t>();
+      tan = (int)(trace_all->numel() / (16LL * a_.G));
     }
-    const std::string why = sl::hybrid_check(a);
-    TORCH_CHECK(why.empty(), "HybridEpoch: ", why);
     const hipStream_t st = c10::hip::getCurrentHIPStream().stream();
-    TORCH_CHECK(hipMemsetAsync(a.err, 0, sizeof(int), st) == hipSuccess, "hybrid error word");
-    const hipError_t le = sl::hybrid_epoch_launch(a, st);
-    TORCH_CHECK(le == hipSuccess, "hybrid epoch launch: ", hipGetErrorString(le));
+    // one clear of the error word per epoch: a chunk whose wait gave up leaves it set, and every
+    // later chunk's waits then give up at once (no work is done on a half-updated shard)
+    TORCH_CHECK(hipMemsetAsync(a_.err, 0, sizeof(int), st) == hipSuccess, "hybrid error word");
+    const int64_t cs = std::max<int64_t>(1, max_steps_);
+    for (int64_t s0 = 0; s0 < S; s0 += cs) {
+      const int64_t n = std::min(cs, S - s0);
+      sl::HyArgs a = a_;
+      a.S = (int)n;
+      a.X = acts.data_ptr<float>() + s0 * B_ * a_.K1;
+      a.Y = labels.data_ptr<int64_t>() + s0 * B_;
+      a.loss = loss_rows.data_ptr<float>() + s0 * B_;
+      a.adam = adam_.data_ptr<float>() + 2 * s0;
+      a.seeds = reinterpret_cast<const uint32_t*>(seeds_.data_ptr<int32_t>()) + 4 * s0;
+      a.ipc.T = 0;
+      if (ipc_ != nullptr) a.ipc = ipc_->begin_steps(n);
+      // trace stamps: the first chunk only
+      a.trace = s0 == 0 ? tr : nullptr;
+      a.trace_steps = s0 == 0 ? trs : 0;
+      a.tall = s0 == 0 ? ta : nullptr;
+      a.tall_step = (int)trace_all_step;
+      a.tall_n = s0 == 0 ? tan : 0;
+      a.fault_step = (fault_step_ >= s0 && fault_step_ < s0 + n) ? (int)(fault_step_ - s0) : -1;
+      const std::string why = sl::hybrid_check(a);
+      TORCH_CHECK(why.empty(), "HybridEpoch: ", why);
+      const hipError_t le = sl::hybrid_epoch_launch(a, st);
+      TORCH_CHECK(le == hipSuccess, "hybrid epoch launch: ", hipGetErrorString(le));
+    }
+    ++launches_;
+    if (fault_step_ >= 0) fault_step_ = -1;   // one injected fault per arming
     const int e = err_.item<int>();   // one sync per client epoch
     TORCH_CHECK(e == 0, "hybrid server epoch: an in-launch wait gave up (error word ", e,
-                "; 2 = a hand-off timed out, 4 = the peer-mapped fc2 exchange failed)");
+                "; 2 = a hand-off timed out, 4 = the peer-mapped fc2 exchange failed, 8 = fault injected)");
     return py::make_tuple(fwd_count + S, t + S, S * B_);
   }
+
+  // tests: the next run stops every workgroup at step `step` of the epoch (err 8), as an
+  // in-launch failure would; -1 disarms
+  void set_fault_step(int64_t step) { fault_step_ = step; }
+  int64_t max_steps() const { return max_steps_; }
 
   // the device table (tile runs, row-block owners / counts, column-block counts) for checks
   at::Tensor table() const { return tab_.clone(); }
@@ -297,6 +327,7 @@ class HybridEpoch {
   sl::HyArgs a_{};
   bool ok_ = false;
   std::string why_;
+  int64_t max_steps_ = 1, fault_step_ = -1, launches_ = 0;
   at::Tensor HB_, cnt_, err_, shard_n_, tab_, adam_, seeds_;
 };
 
@@ -309,6 +340,8 @@ void sl_register_hybrid(py::module& m) {
       .def("why", &HybridEpoch::why)
       .def("workgroups", &HybridEpoch::workgroups)
       .def("table", &HybridEpoch::table)
+      .def("set_fault_step", &HybridEpoch::set_fault_step)
+      .def("max_steps", &HybridEpoch::max_steps)
       .def("run", &HybridEpoch::run, py::arg("acts"), py::arg("labels"), py::arg("loss_rows"),
            py::arg("seed_base"), py::arg("fwd_count"), py::arg("t"), py::arg("trace") = py::none(),
            py::arg("trace_all") = py::none(), py::arg("trace_all_step") = 0);

@@ -378,6 +378,10 @@ __global__ void __launch_bounds__(kResThreads) resident_epoch_kernel(ResArgs a) 
   }
 
   for (int i = 0; i < a.S && !fc1_failed; ++i) {
+    if (i == a.fault_step) {   // uniform: every workgroup stops here (tests: mid-epoch failure)
+      if (blockIdx.x == 0 && threadIdx.x == 0) __hip_atomic_fetch_or(a.err, 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
     const int par = i & 1, nxt = par ^ 1;
     const uint32_t sd2 = a.seeds[4 * i + 2], sd3 = a.seeds[4 * i + 3];
     const SlOpt o = a.o;

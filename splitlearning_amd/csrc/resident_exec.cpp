@@ -91,6 +91,7 @@ class ResidentEpoch {
     const int wg = cfg.contains("workgroups") ? cfg["workgroups"].cast<int>() : 0;
     a.G = wg > 0 ? std::min(wg, std::min(256, cus)) : std::min(256, cus);
     a.coop = wg > 0 ? 0 : 1;
+    a.fault_step = -1;
     a.nrb = (a.N1 + 15) / 16;
     a.ncb = (a.K1 + 255) / 256;
     a.ngrp = (a.ncb + sl::kResTiles - 1) / sl::kResTiles;
@@ -156,6 +157,8 @@ class ResidentEpoch {
   std::string why() const { return why_; }
   int workgroups() const { return a_.G; }
   int clock_khz() const { return clock_khz_; }
+  // tests: the next run stops every workgroup at step `step` (err 8), as an in-launch failure would
+  void set_fault_step(int64_t step) { fault_step_ = step; }
 
   // Every full batch of acts [n, K1] / labels [n] (the first n - n % B rows) in ONE launch;
   // losses into loss_rows [n].  Returns (fwd_count, t, rows done).
@@ -212,11 +215,13 @@ class ResidentEpoch {
     // the executor's own error word starts clear on every launch: a wait that gave up in an
     // earlier run (whose exception the caller handled) must not make this launch give up
     TORCH_CHECK(hipMemsetAsync(a.err, 0, sizeof(int), st) == hipSuccess, "resident error word");
+    a.fault_step = fault_step_ < S ? (int)fault_step_ : -1;
+    fault_step_ = -1;                  // one injected fault per arming
     const hipError_t le = sl::resident_epoch_launch(a, st);
     TORCH_CHECK(le == hipSuccess, "resident epoch launch: ", hipGetErrorString(le));
     const int e = err_.item<int>();   // one sync per client epoch
     TORCH_CHECK(e == 0, "resident server epoch: an in-launch wait gave up (error word ", e,
-                "; 2 = a seam timed out, 4 = the peer-mapped fc2 exchange failed)");
+                "; 2 = a seam timed out, 4 = the peer-mapped fc2 exchange failed, 8 = fault injected)");
     return py::make_tuple(fwd_count + S, t + S, S * B_);
   }
 
@@ -226,6 +231,7 @@ class ResidentEpoch {
   double lr_ = 0, beta1_ = 0, beta2_ = 0, eps_ = 0, wd_ = 0, mom_ = 0, p1_ = 0, p2_ = 0, timeout_s_ = 30.0;
   sl::IpcAllReduce* ipc_ = nullptr;
   sl::ResArgs a_{};
+  int64_t fault_step_ = -1;
   bool ok_ = false;
   std::string why_;
   at::Tensor LA_, H1_, LP_, DL_, DZ2_, W2B_, cnt_, err_, shard_n_, adam_, seeds_;
@@ -237,6 +243,7 @@ void sl_register_resident(py::module& m) {
   py::class_<ResidentEpoch>(m, "ResidentEpoch")
       .def(py::init<const py::dict&>())
       .def("ok", &ResidentEpoch::ok)
+      .def("set_fault_step", &ResidentEpoch::set_fault_step)
       .def("why", &ResidentEpoch::why)
       .def("workgroups", &ResidentEpoch::workgroups)
       .def("clock_khz", [](const ResidentEpoch& e) { return e.clock_khz(); })

@@ -24,6 +24,24 @@ import warnings
 import torch
 
 PROBE_TIMEOUT_S = 5.0
+# the probe's fc3 may differ from the launch-per-stage executor's by this fraction of the
+# epoch's whole fc3 update (fp32 sum order: ~1e-4 of it; a wrong exchange: O(1))
+PROBE_REL_TOL = 0.02
+
+
+def _launch_per_stage_epoch(t, slot, x, y, B):
+    """The scratch epoch on the launch-per-stage executor (as SisaSession.server_epoch runs it
+    when no persistent executor is adopted).  Returns the per-row losses."""
+    n = x.shape[0]
+    if t.lookahead_ok(B) and t.native_epoch_ok(B):
+        t.lookahead_prologue(x[:B])
+        return t.run_native_epoch(x.contiguous(), y.contiguous(), slot, B, True)
+    losses = []
+    for s in range(0, n, B):
+        lo, _ = t.train_fwd_bwd3(x[s:s + B], y[s:s + B], need_dx=False)
+        t.fused_step(slot)
+        losses.append(lo)
+    return torch.cat(losses)
 # fault injection (tests): the TP rank named here skips its probe launch, so every peer's
 # in-launch exchange times out
 FAULT_ENV = "SL_FAULT_RESIDENT_PROBE"
@@ -48,6 +66,11 @@ def probe(tail, slot, B: int, kind: str = "resident") -> int:
     pt.resident_timeout_s = PROBE_TIMEOUT_S
     pt.resident_workgroups = int(getattr(tail, "resident_workgroups", 0))
     pslot = type(slot)(slot.cfg)
+    # the same scratch shard on the launch-per-stage executor: the reference result
+    rt = TailEngine(copy.deepcopy(mod), tail.spec, dev, tail.tp_rank, tail.tp_size, allreduce=tail.allreduce,
+                    seed_base=77, ws_tag="#resident_probe_ref")
+    rslot = type(slot)(slot.cfg)
+    w0 = rt.layers[2].W.detach().clone()
     n = 8 * B
     x = (torch.rand(n, pt.layers[0].W.shape[1], generator=g) * 4).to(dev)
     y = torch.randint(0, pt.layers[2].W.shape[0], (n,), generator=g).to(dev)
@@ -59,11 +82,24 @@ def probe(tail, slot, B: int, kind: str = "resident") -> int:
         run = pt.run_hybrid_epoch if kind == "hybrid" else pt.run_resident_epoch
         loss = run(x, y, pslot, B)
         torch.cuda.synchronize(dev)
+        ref_loss = _launch_per_stage_epoch(rt, rslot, x, y, B)
+        torch.cuda.synchronize(dev)
     finally:
         if ipc is not None:
             ipc.set_timeout_s(old)
     if not bool(torch.isfinite(loss).all().item()):
         raise RuntimeError("non-finite losses")
+    # every rank checks its own result against the reference executor: a rank-consistent but
+    # wrong exchange (e.g. every rank reading the same stale granule) fails here, where the
+    # cross-rank fingerprint agreement alone would adopt it
+    if not torch.allclose(loss, ref_loss, rtol=1e-3, atol=1e-3):
+        d = (loss - ref_loss).abs().max().item()
+        raise RuntimeError(f"losses differ from the launch-per-stage executor's (max |d| {d:.3g})")
+    upd = (rt.layers[2].W - w0).norm().item()
+    dev_w = (pt.layers[2].W - rt.layers[2].W).norm().item()
+    if not dev_w <= PROBE_REL_TOL * upd + 1e-12:
+        raise RuntimeError(f"fc3 after the probe epoch differs from the launch-per-stage executor's "
+                           f"({dev_w:.3g} vs an update of {upd:.3g})")
     bits = pt.layers[2].W.detach().reshape(-1).view(torch.int32).to(torch.int64)
     mult = torch.arange(1, bits.numel() + 1, device=dev, dtype=torch.int64) % 1000003
     return int(((bits * mult) % ((1 << 61) - 1)).sum().item())
@@ -77,6 +113,11 @@ def _coll_device():
 KINDS = ("resident", "hybrid")
 
 
+def _wanted(w) -> bool:
+    """An executor flag: True / False, or a string naming why it is unwanted (= False)."""
+    return bool(w) and not isinstance(w, str)
+
+
 def decide(tail, slot, B: int, distributed: bool, want: bool = True, want_hybrid: bool = True) -> tuple[str, str]:
     """Collective over every process of the default group when `distributed` (ranks that are
     not Bob pass tail=None): which persistent executor Bob's server epochs run on, and why (the
@@ -84,18 +125,26 @@ def decide(tail, slot, B: int, distributed: bool, want: bool = True, want_hybrid
     kind "resident" (the whole shard on-chip: TP >= 7), "hybrid" (a wide shard: fc2 / fc3 on-
     chip, fc1 streamed) or "launch_per_stage".
 
+    `want` gates the resident executor (`--resident`), `want_hybrid` the hybrid one (`--hybrid`):
+    the two flags are independent.  Passing a string instead of False gives the reason the
+    executor is unwanted (e.g. "dtype bf16"); it is reported when nothing was adopted.
+
     Single shard: the first that fits.  Tensor-parallel: every Bob rank probes that executor;
-    adopted only if every rank chose the same one and passed with the same fc3 fingerprint.
-    When not adopted after any probe ran, every rank re-arms the peer-mapped region at the
-    largest generation any rank reserved."""
-    kind, fp, why = None, None, "" if want else "off"
+    adopted only if every rank chose the same one and passed with the same fc3 fingerprint
+    and, per rank, the probe's result agreed with the launch-per-stage executor's on the same
+    scratch epoch (`probe`).  When not adopted after any probe ran, every rank re-arms the
+    peer-mapped region at the largest generation any rank reserved."""
+    kind, fp = None, None
+    on_r, on_h = _wanted(want), _wanted(want_hybrid)
+    off = [w for w in (want, want_hybrid) if isinstance(w, str) and w]
+    why = off[0] if off else ("off" if not on_r and not on_h else "")
     ran_probe = False
-    if tail is not None and want:
-        if tail.resident_ok(slot, B):
+    if tail is not None and (on_r or on_h):
+        if on_r and tail.resident_ok(slot, B):
             kind = "resident"
-        elif want_hybrid and tail.hybrid_ok(slot, B):
+        elif on_h and tail.hybrid_ok(slot, B):
             kind = "hybrid"
-        else:
+        elif not why:
             why = "no persistent executor fits this shard"
         if kind is not None and tail.tp_size > 1:
             ran_probe = True
@@ -130,15 +179,80 @@ def decide(tail, slot, B: int, distributed: bool, want: bool = True, want_hybrid
     return "launch_per_stage", why
 
 
-def rearm(tail):
-    """Collective over the default group: clear the peer-mapped region's error word on every
-    Bob rank and continue all of them at one generation (the MAX of the generations reserved)."""
+FAULT_EPOCH_ENV = "SL_FAULT_PERSIST_EPOCH"
+
+
+class Failsafe:
+    """Client epochs on a persistent executor that survive an in-launch failure.
+
+    Before each epoch the shard's weights, optimizer state and step / dropout counters are
+    copied device-to-device (`TailEngine.snapshot_state`, one buffer reused).  A launch whose
+    in-launch waits gave up (a hand-off timeout; across GPUs, the peer-mapped fc2 exchange
+    failing; an injected fault) raises after updating part of the shard.  `run` then agrees
+    with the other Bob ranks (a MAX all-reduce of one flag over `group`, every epoch, since a
+    rank whose launch finished before its peer failed has nothing to report by itself), and if
+    ANY rank failed, every rank restores its copy, re-arms the peer-mapped region collectively
+    (`rearm`) and returns False: the caller runs that epoch, and every later one, on the
+    launch-per-stage executor.  The restored shard is bitwise the pre-epoch one, so the job's
+    result is exactly that of a job which switched executors at that epoch.
+
+    Fault injection (tests): SL_FAULT_PERSIST_EPOCH="TP_RANK:EPOCH:STEP" stops every workgroup
+    of TP rank TP_RANK's launch at step STEP of its EPOCH-th persistent epoch (0-based), as an
+    in-launch failure would (the kernels' `fault_step`, error word 8)."""
+
+    def __init__(self, tail, slot, B: int, group=None, enabled: bool = True):
+        self.tail, self.slot, self.B, self.group, self.enabled = tail, slot, B, group, enabled
+        self.snap = None
+        self.epochs = 0
+        self.fallback = None
+
+    def run(self, kind: str, acts: torch.Tensor, labels: torch.Tensor) -> bool:
+        tail, slot, B = self.tail, self.slot, self.B
+        idx = self.epochs
+        self.epochs += 1
+        if self.enabled:
+            self.snap = tail.snapshot_state(slot, self.snap)
+        ex = tail._resident_executor(slot, B) if kind == "resident" else tail._hybrid_executor(slot, B)
+        f = os.environ.get(FAULT_EPOCH_ENV, "").split(":")
+        if len(f) == 3 and int(f[0]) == tail.tp_rank and int(f[1]) == idx:
+            ex.set_fault_step(int(f[2]))
+        err = None
+        try:
+            if kind == "resident":
+                tail.run_resident_epoch(acts, labels, slot, B)
+            else:
+                tail.run_hybrid_epoch(acts, labels, slot, B)
+        except RuntimeError as e:
+            if "in-launch wait gave up" not in str(e) or not self.enabled:
+                raise
+            err = str(e).splitlines()[0][:200]
+        failed = err is not None
+        if tail.tp_size > 1:
+            import torch.distributed as dist
+            flag = torch.tensor([1 if failed else 0], dtype=torch.int32, device=_coll_device())
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
+            failed = int(flag.item()) > 0
+        if not failed:
+            return True
+        tail.restore_state(slot, self.snap)
+        if tail.tp_size > 1:
+            rearm(tail, group=self.group)
+        why = err if err is not None else "another Bob rank's persistent epoch failed"
+        warnings.warn(f"{kind} server epoch {idx} failed ({why}); shard restored, continuing on launch-per-stage")
+        self.fallback = {"from": kind, "epoch": idx, "reason": why}
+        return False
+
+
+def rearm(tail, group=None):
+    """Collective over `group` (default: the default group; a mid-epoch fallback passes the Bob
+    ranks' group): clear the peer-mapped region's error word on every Bob rank and continue all
+    of them at one generation (the MAX of the generations reserved)."""
     import torch.distributed as dist
     ipc = getattr(getattr(tail, "allreduce", None), "ipc", None) if tail is not None else None
     if ipc is not None:
         torch.cuda.synchronize()
     gen = int(ipc.generation) if ipc is not None else 0
     t = torch.tensor([gen], dtype=torch.int64, device=_coll_device())
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     if ipc is not None:
         ipc.rearm(int(t.item()))

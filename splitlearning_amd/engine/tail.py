@@ -526,10 +526,41 @@ class TailEngine:
              "p1": L1.spec.dropout, "p2": L2.spec.dropout, "col_off1": L1.col_off, "B": B,
              "ipc": getattr(self.allreduce, "ipc", None) if L2.style == "row" else None,
              "timeout_s": float(getattr(self, "resident_timeout_s", 10.0)),
-             "workgroups": _persist_workgroups(self), "nt_stores": getattr(self, "hybrid_nt_stores", None)}
+             "workgroups": _persist_workgroups(self), "nt_stores": getattr(self, "hybrid_nt_stores", None),
+             "chunk_steps": getattr(self, "hybrid_chunk_steps", None)}
         ex = self.ops.C().HybridEpoch(d)
         self._hybrid = (slot, B, ex, d)
         return ex
+
+    # ------------------------------------------------------------------ persistent-epoch rollback
+    def snapshot_state(self, slot: OptSlot, buf: dict | None = None) -> dict:
+        """Device-to-device copy of this shard's weights, biases and optimizer state in `slot`
+        plus the step / dropout counters, into `buf` (reused across epochs: one allocation of
+        the shard's size, ~390 MB at TP = 1, copied at HBM rate, ~0.1 ms).  A persistent epoch
+        that fails mid-launch has updated part of W / m / v; `restore_state` undoes it."""
+        buf = {} if buf is None else buf
+        ts = []
+        for L in self.layers:
+            ts += [L.W, L.b]
+            for nm, p in ((f"{L.spec.name}.weight", L.W), (f"{L.spec.name}.bias", L.b)):
+                ts += [slot.state(nm, p)[k] for k in sorted(slot.state(nm, p))]
+        with torch.no_grad():
+            for i, t in enumerate(ts):
+                c = buf.get(i)
+                if c is None or c.shape != t.shape or c.device != t.device:
+                    c = buf[i] = torch.empty_like(t)
+                c.copy_(t)
+        buf["tensors"] = ts
+        buf["counters"] = (self.fwd_count, slot.t)
+        return buf
+
+    def restore_state(self, slot: OptSlot, buf: dict):
+        with torch.no_grad():
+            for i, t in enumerate(buf["tensors"]):
+                t.copy_(buf[i])
+        self.fwd_count, slot.t = buf["counters"]
+        self._pre = None
+        self.acts, self.dz, self._wg = [], [], []
 
     # ------------------------------------------------------------------ TP emulation
     @staticmethod

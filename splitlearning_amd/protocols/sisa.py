@@ -30,6 +30,16 @@ from ..models import ServerTailSisa, sisa_server_spec
 from .base import AliceState, Session, _progress
 
 
+def executor_wants(args):
+    """(resident, hybrid) wants for engine/resident.decide from the CLI: `--resident` and
+    `--hybrid` gate their own executor only; both persistent executors compute in fp32, so
+    `--dtype bf16` turns both off with that reason (reported as `server_executor_reason`)."""
+    if getattr(args, "dtype", "fp32") != "fp32":
+        why = f"dtype {args.dtype}: the persistent executors compute in fp32 only"
+        return why, why
+    return getattr(args, "resident", "auto") != "off", getattr(args, "hybrid", "auto") != "off"
+
+
 class SisaSession(Session):
     mode = "sisa"
 
@@ -286,13 +296,38 @@ class SisaSession(Session):
         and its reason land in `server_executor` / `resident_status` (bench JSON).  Returns
         whether the register-resident executor was adopted."""
         from ..engine import resident
-        want = getattr(self.args, "resident", "auto") != "off" and getattr(self.args, "dtype", "fp32") == "fp32"
-        want_h = getattr(self.args, "hybrid", "auto") != "off"
+        want, want_h = executor_wants(self.args)
         kind, why = resident.decide(self.tail if self.is_bob else None, self.bob_slot if self.is_bob else None,
                                     self.B, self.comm.distributed, want, want_h)
         self.server_executor = kind
         self.resident_status = {"executor": kind, "reason": why, "adopted": kind == "resident"}
         return kind == "resident"
+
+    def _persistent_epoch(self, acts, labels) -> bool:
+        """One client epoch on the adopted persistent executor, made un-killable: the shard's
+        weights / optimizer state / counters are copied first (`TailEngine.snapshot_state`);
+        if the launch's in-launch waits gave up on ANY Bob rank (a hand-off timeout, the peer-
+        mapped fc2 exchange across xGMI failing, an injected fault), every Bob rank restores
+        its copy, the peer-mapped region is re-armed collectively, and the job continues on the
+        launch-per-stage executor from this epoch on (reported as `server_executor_fallback`).
+        Returns False when the caller must run this epoch on launch-per-stage.  Collective over
+        the Bob ranks (one small all-reduce per client epoch when tensor-parallel).
+
+        Fault injection (tests): SL_FAULT_PERSIST_EPOCH="TP_RANK:EPOCH:STEP" stops every
+        workgroup of TP rank TP_RANK's launch at step STEP of its EPOCH-th persistent epoch
+        (0-based), as an in-launch failure would."""
+        from ..engine import resident
+        if not hasattr(self, "_failsafe"):
+            self._failsafe = resident.Failsafe(self.tail, self.bob_slot, self.B, group=self.comm.tp_group,
+                                               enabled=getattr(self.args, "persistent_failsafe", "on") != "off")
+        fs = self._failsafe
+        if fs.run(self.server_executor, acts, labels):
+            return True
+        self.server_executor = "launch_per_stage"
+        st = getattr(self, "resident_status", None) or {}
+        st["fallback"] = fs.fallback
+        self.resident_status = st
+        return False
 
     def server_epoch(self, acts, labels):
         """One pass of Bob's optimizer over one client's cached activations (batch order as
@@ -304,18 +339,14 @@ class SisaSession(Session):
         G = self.GRAPH_STEPS
         la = self.tail.lookahead_ok(B)
         pre = False
-        if n >= B and self._use_resident():
-            # a narrow (tensor-parallel) shard: every full batch in one persistent launch with
-            # the shard's weights and Adam state on-chip (csrc/resident.hip)
-            self.tail.run_resident_epoch(acts.contiguous(), labels.contiguous(), self.bob_slot, B)
-            self.comm.progress()
-            return
-        if n >= B and self._use_hybrid():
-            # a wide shard: every full batch in one persistent launch with fc2 / fc3 on-chip and
-            # fc1 streamed (csrc/hybrid.hip)
-            self.tail.run_hybrid_epoch(acts.contiguous(), labels.contiguous(), self.bob_slot, B)
-            self.comm.progress()
-            return
+        if n >= B and (self._use_resident() or self._use_hybrid()):
+            # one persistent launch for every full batch: a narrow (tensor-parallel) shard with
+            # its weights and Adam state on-chip (csrc/resident.hip), or a wide shard with fc2 /
+            # fc3 on-chip and fc1 streamed (csrc/hybrid.hip); on an in-launch failure the shard
+            # is rolled back and this epoch (and every later one) runs launch-per-stage below
+            if self._persistent_epoch(acts.contiguous(), labels.contiguous()):
+                self.comm.progress()
+                return
         if self._use_graphs() and n // B >= G:
             key = (B, G, acts.shape[1])
             gs = getattr(self, "_graphed", {}).get(key)

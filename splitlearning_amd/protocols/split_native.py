@@ -18,6 +18,8 @@ from __future__ import annotations
 import torch
 
 _KIND = {"sgd": 1, "adam": 2}
+# rows per batch `_C.SplitEpoch` accepts on every role (csrc/split.cpp, the constructor's check)
+SPLIT_MIN_B, SPLIT_MAX_B = 1, 64
 
 
 def _opt(cfg) -> dict:
@@ -131,8 +133,11 @@ def _remote_placement_ok(sess, cid: int) -> bool:
 
 def _remote_side_ok(sess, cid: int, mode: str) -> bool:
     """This rank's side of the pair can run natively (the same per-side rules as
-    `native_split_ok`)."""
+    `native_split_ok`), including `_C.SplitEpoch`'s batch bound (csrc/split.cpp: 1..64 rows on
+    every role), so a larger `--batch_size` keeps the Python loop instead of raising."""
     B = sess.B
+    if not SPLIT_MIN_B <= B <= SPLIT_MAX_B:
+        return False
     if sess.hosts(cid):
         a = sess.alices[cid]
         if a.front.frozen or a.train.x.dtype != torch.uint8:

@@ -38,6 +38,42 @@ def test_server_executor_flags():
         parse_args(["--resident", "on"])
 
 
+class _FakeTail:
+    """decide()'s view of a single-shard tail: which persistent executors fit."""
+    tp_size = 1
+
+    def __init__(self, res_ok, hy_ok):
+        self.res_ok, self.hy_ok = res_ok, hy_ok
+
+    def resident_ok(self, slot, B):
+        return self.res_ok
+
+    def hybrid_ok(self, slot, B):
+        return self.hy_ok
+
+
+@pytest.mark.parametrize("argv,res_ok,hy_ok,kind,why", [
+    (["--sisa"], True, True, "resident", "adopted"),
+    (["--sisa"], False, True, "hybrid", "adopted"),
+    (["--sisa"], False, False, "launch_per_stage", "no persistent executor fits this shard"),
+    # --resident off leaves the hybrid on (round-4 bug: it turned both off)
+    (["--sisa", "--resident", "off"], True, True, "hybrid", "adopted"),
+    (["--sisa", "--resident", "off"], True, False, "launch_per_stage", "no persistent executor fits this shard"),
+    (["--sisa", "--hybrid", "off"], False, True, "launch_per_stage", "no persistent executor fits this shard"),
+    (["--sisa", "--hybrid", "off"], True, True, "resident", "adopted"),
+    (["--sisa", "--resident", "off", "--hybrid", "off"], True, True, "launch_per_stage", "off"),
+    # bf16 compute: both persistent executors are fp32-only, and the reason says so
+    (["--sisa", "--dtype", "bf16"], True, True, "launch_per_stage", "dtype bf16"),
+])
+def test_server_executor_decision_table(argv, res_ok, hy_ok, kind, why):
+    from splitlearning_amd.engine.resident import decide
+    from splitlearning_amd.protocols.sisa import executor_wants
+    want, want_h = executor_wants(parse_args(argv))
+    k, w = decide(_FakeTail(res_ok, hy_ok), None, 16, distributed=False, want=want, want_hybrid=want_h)
+    assert k == kind
+    assert w.startswith(why)
+
+
 @pytest.mark.parametrize("argv,msg", [
     (["--concat"], "--concat option can only be used with the --sisa"),
     (["--vanilla", "--sisa"], "--vanilla option cannot be used"),

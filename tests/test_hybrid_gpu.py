@@ -202,3 +202,116 @@ def test_hybrid_tensor_parallel_across_processes_on_one_gpu(T):
     text = out.stdout + out.stderr
     assert out.returncode == 0, text[-3000:]
     assert out.stdout.count("PASS") == T, text[-3000:]
+
+
+def test_hybrid_chunked_epoch_is_bitwise_one_launch(cuda):
+    """An epoch whose inputs exceed the launch's 32-bit buffer offsets runs as consecutive
+    launches (csrc/hybrid_exec.cpp max_steps): forced here with chunks of 5 steps over 23 steps
+    (the last chunk short), bitwise the single launch."""
+    B, steps, seed_base = 16, 23, 4
+    spec = _spec(n1=1252, p=0.5)
+    g = torch.Generator().manual_seed(5)
+    acts = (torch.rand(B * steps + 7, 5408, generator=g) * 20).to(cuda)
+    labels = torch.randint(0, 100, (B * steps + 7,), generator=g).to(cuda)
+    torch.manual_seed(14)
+    base = _MLP(spec)
+    one, s1 = _engine(base, spec, cuda, seed_base, "#hyc1")
+    chunked, s2 = _engine(base, spec, cuda, seed_base, "#hyc2")
+    chunked.hybrid_chunk_steps = 5
+    assert chunked._hybrid_executor(s2, B).max_steps() == 5
+    l1 = one.run_hybrid_epoch(acts, labels, s1, B)
+    l2 = chunked.run_hybrid_epoch(acts, labels, s2, B)
+    torch.cuda.synchronize()
+    assert torch.equal(l1, l2)
+    for La, Lb in zip(one.layers, chunked.layers):
+        assert torch.equal(La.W, Lb.W) and torch.equal(La.b, Lb.b)
+    for k in s1.states:
+        for kk in s1.states[k]:
+            assert torch.equal(s1.states[k][kk], s2.states[k][kk]), (k, kk)
+    assert (one.fwd_count, s1.t) == (chunked.fwd_count, s2.t) == (steps + 1, steps + 1)
+
+
+def test_hybrid_sgd_momentum_close_to_torch(cuda):
+    """The SGD-momentum instantiation (hybrid_epoch_kernel<false, *>: one state array, `buf`)
+    against torch.optim.SGD(momentum=0.9) over free-running steps (the vanilla optimizer,
+    data_entities_vanilla.py:37-42)."""
+    from splitlearning_amd.engine import sgd_momentum
+    B, rows, lr, seed_base = 16, 16 * 10, 1e-3, 6
+    spec = _spec(n1=1252, p=0.5)
+    g = torch.Generator().manual_seed(6)
+    acts = (torch.rand(rows, 5408, generator=g) * 4).to(cuda)
+    labels = torch.randint(0, 100, (rows,), generator=g).to(cuda)
+    torch.manual_seed(15)
+    base = _MLP(spec)
+    te = TailEngine(copy.deepcopy(base), spec, cuda, seed_base=seed_base, ws_tag="#hysgd")
+    slot = OptSlot(sgd_momentum(lr))
+    for L in te.layers:
+        slot.state(f"{L.spec.name}.weight", L.W)
+        slot.state(f"{L.spec.name}.bias", L.b)
+    assert te.hybrid_ok(slot, B), te._hybrid_executor(slot, B).why()
+    loss_e = te.run_hybrid_epoch(acts, labels, slot, B)
+    ref = copy.deepcopy(base).to(cuda)
+    opt = torch.optim.SGD(ref.parameters(), lr=lr, momentum=0.9)
+    losses = []
+    for i, s in enumerate(range(0, rows, B)):
+        x, y = acts[s:s + B], labels[s:s + B]
+        opt.zero_grad()
+        loss_r = F.cross_entropy(_ref_forward(ref, x, seed_base, i + 1), y, reduction="none")
+        loss_r.mean().backward()
+        opt.step()
+        losses.append(loss_r.detach())
+    torch.testing.assert_close(loss_e, torch.cat(losses), rtol=1e-3, atol=1e-3)
+    for name, p in ref.named_parameters():
+        L = te.layers[int(name[2]) - 1]
+        e = L.W if name.endswith("weight") else L.b
+        torch.testing.assert_close(e, p.detach(), rtol=1e-4, atol=1e-5, msg=name)
+        torch.testing.assert_close(slot.states[name]["buf"], opt.state[p]["momentum_buffer"], rtol=1e-3,
+                                   atol=1e-6 + 1e-4 * opt.state[p]["momentum_buffer"].abs().max().item(), msg=name)
+
+
+def test_hybrid_mid_epoch_failure_rolls_back_to_launch_per_stage(cuda, monkeypatch):
+    """`engine.resident.Failsafe` (the path SisaSession.server_epoch takes): a launch stopped
+    at step 5 of the second client epoch (injected: the kernel's fault_step) raises after
+    updating part of the shard; the shard is restored and the epoch re-runs launch-per-stage.
+    The result is bitwise a job that switched executors at that epoch with no failure."""
+    from splitlearning_amd.engine.resident import FAULT_EPOCH_ENV, Failsafe, _launch_per_stage_epoch
+    B, rows, seed_base = 16, 16 * 12, 8
+    spec = _spec(n1=1252, p=0.5)
+    g = torch.Generator().manual_seed(9)
+    acts = (torch.rand(rows, 5408, generator=g) * 20).to(cuda)
+    labels = torch.randint(0, 100, (rows,), generator=g).to(cuda)
+    torch.manual_seed(16)
+    base = _MLP(spec)
+    ta, sa = _engine(base, spec, cuda, seed_base, "#hyfa")
+    tb, sb = _engine(base, spec, cuda, seed_base, "#hyfb")
+    monkeypatch.setenv(FAULT_EPOCH_ENV, "0:1:5")
+    fs = Failsafe(ta, sa, B)
+    assert fs.run("hybrid", acts, labels)
+    assert not fs.run("hybrid", acts, labels)
+    assert fs.fallback["epoch"] == 1 and "error word 8" in fs.fallback["reason"]
+    la = _launch_per_stage_epoch(ta, sa, acts, labels, B)
+    monkeypatch.delenv(FAULT_EPOCH_ENV)
+    tb.run_hybrid_epoch(acts, labels, sb, B)
+    lb = _launch_per_stage_epoch(tb, sb, acts, labels, B)
+    torch.cuda.synchronize()
+    assert torch.equal(la, lb)
+    for La, Lb in zip(ta.layers, tb.layers):
+        assert torch.equal(La.W, Lb.W) and torch.equal(La.b, Lb.b)
+    for k in sa.states:
+        for kk in sa.states[k]:
+            assert torch.equal(sa.states[k][kk], sb.states[k][kk]), (k, kk)
+    assert (ta.fwd_count, sa.t) == (tb.fwd_count, sb.t) == (2 * rows // B, 2 * rows // B)
+
+
+@pytest.mark.parametrize("kind", ["hybrid", "resident"])
+def test_tensor_parallel_mid_epoch_failure_survived_across_processes(kind):
+    """T = 2 real processes on the one GPU: rank 0's persistent launch stops mid-epoch, rank 1's
+    in-launch exchange times out; both ranks roll back, re-arm the peer-mapped region and finish
+    on launch-per-stage; nothing raises, the state is bitwise a clean switch at that epoch and
+    close to fp32 torch (scripts/persist_fallback_one_gpu.py)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, os.path.join(root, "scripts", "persist_fallback_one_gpu.py"), "2", kind],
+                         capture_output=True, text=True, timeout=110, cwd=root)
+    text = out.stdout + out.stderr
+    assert out.returncode == 0, text[-3000:]
+    assert out.stdout.count("PASS") == 2, text[-3000:]

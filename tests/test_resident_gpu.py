@@ -241,7 +241,7 @@ def test_sisa_session_runs_its_server_epochs_on_the_resident_executor(cuda, tmp_
     runs = {}
     for res in ("auto", "off"):
         args = parse_args(["--sisa", "--world_size", "2", "--seed", "5", "--num_samples", "1400", "--no_tqdm",
-                           "--server_epochs", "1", "--resident", res,
+                           "--server_epochs", "1", "--resident", res, "--hybrid", res,
                            "--datapath", str(tmp_path / f"d{res}"), "--log_dir", str(tmp_path / f"l{res}")])
         write_shards(args, verbose=False)
         sess = Narrow(args, Comm(0, 1, cuda, Placement.make(2, 1, 1)), cuda)

@@ -73,3 +73,24 @@ def test_bob_tp_policy():
         assert choose_bob_tp("vanilla", n) == n
         assert choose_bob_tp("ushape", n) == 1
     assert choose_bob_tp("vanilla", 6) in (1, 2, 6) and 6 % choose_bob_tp("vanilla", 6) == 0
+
+
+@pytest.mark.parametrize("B,ok", [(16, True), (64, True), (65, False), (128, False)])
+def test_remote_native_split_respects_executor_batch_bound(B, ok):
+    """A remote Alice's epoch runs on `_C.SplitEpoch` only within its batch bound (1..64 rows on
+    every role, csrc/split.cpp); beyond it both sides of the pair report "not native", so the
+    Python loop runs it instead of both ranks raising in the executor's constructor."""
+    from types import SimpleNamespace
+
+    from splitlearning_amd.protocols import split_native as sn
+
+    class _Tail:
+        layers = [0, 0, 0]
+
+        def fused3_ok(self):
+            return True
+
+    alice = SimpleNamespace(front=SimpleNamespace(frozen=False), train=SimpleNamespace(x=torch.zeros(1, dtype=torch.uint8)))
+    for hosts in (True, False):   # the Alice's side and Bob's side of the pair
+        s = SimpleNamespace(B=B, alices={1: alice}, tail=_Tail(), hosts=lambda cid, h=hosts: h)
+        assert sn._remote_side_ok(s, 1, "vanilla") is ok
