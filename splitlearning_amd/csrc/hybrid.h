@@ -49,13 +49,15 @@ struct HyArgs {
   int col_off1;           // global index of this shard's fc1 row 0 (dropout hash column)
   // hand-off buffers, double-buffered by step parity, in ONE allocation HB (one buffer
   // resource for all of them); offsets in floats:
-  //   LA [2][nrb][kHySlots][16][16] look-ahead partials (slot = w - rbw0)
-  //   H1 [2][16][N1] h1 rows
-  //   FP [2][NC][16][N2] fc2 product partials per column block
+  // (the MFMA-produced ones batch-row fastest, [..][n][16 m]: a lane's accumulator is four
+  // consecutive rows of one column, so every hand-off store and load is 16 B)
+  //   LA [2][nrb][kHySlots][16 n][16 m] look-ahead partials (slot = w - rbw0)
+  //   H1 [2][N1][16 m] h1 (rows m >= M zero)
+  //   FP [2][NC][N2][16 m] fc2 product partials per column block
   //   LP [2][HW][16][C4] logit partials
   //   DL [2][16][C4] dlogits
   //   DZ [2][16][N2] dz2
-  //   DP [2][8][16][N1] dz1 partials per fc2 row block
+  //   DP [2][8][N1][16 m] dz1 partials per fc2 row block
   //   ZP [G][kHyRuns][8 waves][64] f32x4 per-wave look-ahead accumulators
   float* HB;
   int oLA, oH1, oFP, oLP, oDL, oDZ, oDP, oZP;
@@ -70,7 +72,7 @@ struct HyArgs {
   int tall_step, tall_n;  // steps tall_step .. tall_step + tall_n - 1
   int coop;               // cooperative launch (see resident.h)
   int ntst;               // fc1 state policy: over-cache form (1: W plain, m / v non-temporal) or write-through (0)
-  int fault_step;         // fault injection (tests): every workgroup stops at this step with err |= 8 (-1: off)
+  int fault_step;         // fault injection (tests): this step's first wait is never met (times out, err 2); -1: off
 };
 
 hipError_t hybrid_epoch_launch(const HyArgs& a, hipStream_t st);

@@ -172,8 +172,7 @@ constexpr int U_RED = U_SDZ2 + ((16 * PD * 4 + 15) & ~15);   // [16][32] f32x4
 constexpr int U_SDL = U_RED + 16 * 32 * 16;            // dlogits [16][kHyMaxC]
 constexpr int U_SH2 = U_SDL + 16 * kHyMaxC * 4;        // h2 [16][4]
 constexpr int U_SDZH = U_SH2 + 16 * 4 * 4;             // dz2 of the head rows [16][4]
-constexpr int U_SP2 = U_SDZH + 16 * 4 * 4;             // P2 of the head rows [16] f32x4
-constexpr int kUFc2 = U_SP2 + 16 * 16;
+constexpr int kUFc2 = U_SDZH + 16 * 4 * 4;
 constexpr int kU = kUStream > kUFc2 ? kUStream : kUFc2;
 constexpr int OFF_W3 = OFF_U + kU;                     // W3 columns {W, m, v}[4][kHyMaxC]
 constexpr int OFF_B3 = OFF_W3 + 3 * 4 * kHyMaxC * 4;   // b3 {W, m, v}[kHyMaxC]
@@ -223,7 +222,6 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
   float* sdl = reinterpret_cast<float*>(smem + OFF_U + U_SDL);
   float* sh2 = reinterpret_cast<float*>(smem + OFF_U + U_SH2);
   float* sdzh = reinterpret_cast<float*>(smem + OFF_U + U_SDZH);
-  f32x4* sp2 = reinterpret_cast<f32x4*>(smem + OFF_U + U_SP2);
   float* sW3 = reinterpret_cast<float*>(smem + OFF_W3);
   float* sb3 = reinterpret_cast<float*>(smem + OFF_B3);
   float* sb2 = reinterpret_cast<float*>(smem + OFF_B2);
@@ -491,23 +489,23 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
     }
     {
       HY_IDX();
-      for (int e = tid; e < nruns * 256; e += kHyThreads) {
-        const int k = e >> 8, m = (e >> 4) & 15, nn = e & 15;
+      // (row nn, rows m = 4 mg ..): the waves' accumulators are already in that layout
+      for (int e = tid; e < nruns * 64; e += kHyThreads) {
+        const int k = e >> 6, nn = (e >> 2) & 15, mg = e & 3;
         const int rb = rbA + k, slot = w - a.tab[a.G + 1 + rb], n = 16 * rb + nn;
-        float parts[8];
+        f32x4 parts[8];
         if (k == nruns - 1) {
 #pragma unroll
-          for (int ww = 0; ww < 8; ++ww) parts[ww] = sa[ww * 64 + 16 * (m >> 2) + nn][m & 3];
+          for (int ww = 0; ww < 8; ++ww) parts[ww] = sa[ww * 64 + 16 * mg + nn];
         } else {
 #pragma unroll
-          for (int ww = 0; ww < 8; ++ww)
-            parts[ww] = hld1(rHB, bZP + ((((w * kHyRuns + k) * 8 + ww) * 64 + 16 * (m >> 2) + nn) * 4 + (m & 3)) * 4);
+          for (int ww = 0; ww < 8; ++ww) parts[ww] = hld4(rHB, bZP + (((w * kHyRuns + k) * 8 + ww) * 64 + 16 * mg + nn) * 16);
         }
-        float v = parts[0];
+        f32x4 v = parts[0];
 #pragma unroll
         for (int ww = 1; ww < 8; ++ww) v += parts[ww];
         if (slot == 0) v += sb1[(k * 3) * 16 + nn];
-        if (m < M && n < N1) hst1(rHB, bLA + (((par * a.nrb + rb) * kHySlots + slot) * 256 + m * 16 + nn) * 4, v);
+        if (n < N1) hst4(rHB, bLA + (((par * a.nrb + rb) * kHySlots + slot) * 256 + nn * 16 + 4 * mg) * 4, v);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -521,23 +519,28 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
     __syncthreads();
     bool any = false;
     for (int k = 0; k < nruns; ++k) any = any || s_ok[1 + k] != 0;
-    // the row blocks this workgroup arrived last on, two at a time (256 lanes each)
-    for (int e0 = 0; e0 < nruns * 256; e0 += kHyThreads) {
+    // the row blocks this workgroup arrived last on (64 lanes each: row nn, rows m = 4 mg ..;
+    // rows m >= M published as zero)
+    for (int e0 = 0; e0 < nruns * 64; e0 += kHyThreads) {
       HY_IDX();
-      const int e = e0 + tid, k = e >> 8;
+      const int e = e0 + tid, k = e >> 6;
       if (k < nruns && s_ok[1 + k]) {
         const int rb = rbA + k, ns = a.tab[a.G + 1 + a.nrb + rb];
-        const int m = (e >> 4) & 15, nn = e & 15, n = 16 * rb + nn;
-        if (m < M && n < N1) {
-          float parts[kHySlots];
+        const int nn = (e >> 2) & 15, mg = e & 3, n = 16 * rb + nn;
+        if (n < N1) {
+          f32x4 parts[kHySlots];
 #pragma unroll
           for (int s = 0; s < kHySlots; ++s)
-            parts[s] = s < ns ? hld1(rHB, bLA + (((par * a.nrb + rb) * kHySlots + s) * 256 + m * 16 + nn) * 4) : 0.f;
-          float v = parts[0];
+            parts[s] = s < ns ? hld4(rHB, bLA + (((par * a.nrb + rb) * kHySlots + s) * 256 + nn * 16 + 4 * mg) * 4) : zv;
+          f32x4 v = parts[0];
 #pragma unroll
           for (int s = 1; s < kHySlots; ++s) v += parts[s];
-          v = drop_relu(v, a.seeds[4 * so], a.seeds[4 * so + 1], m, a.col_off1 + n, a.thr1, a.dsc1);
-          hst1(rHB, bH1 + ((par * 16 + m) * N1 + n) * 4, v);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int m = 4 * mg + j;
+            v[j] = m < M ? drop_relu(v[j], a.seeds[4 * so], a.seeds[4 * so + 1], m, a.col_off1 + n, a.thr1, a.dsc1) : 0.f;
+          }
+          hst4(rHB, bH1 + ((par * N1 + n) * 16 + 4 * mg) * 4, v);
         }
       }
     }
@@ -564,10 +567,6 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
   flush(0, 1u);
 
   for (int i = 0; i < a.S; ++i) {
-    if (i == a.fault_step) {   // uniform: every workgroup stops here (tests: mid-epoch failure)
-      if (w == 0 && threadIdx.x == 0) __hip_atomic_fetch_or(a.err, 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      break;
-    }
     const int par = i & 1;
     const bool more = i + 1 < a.S;
     const uint32_t sd2 = a.seeds[4 * i + 2], sd3 = a.seeds[4 * i + 3];
@@ -579,7 +578,9 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
     HY_MARK(0);
     {
       int idx[1] = {hy_H(tb)};
-      unsigned tgt[1] = {(unsigned)(i + 1) * (unsigned)a.tab[a.G + 1 + 2 * a.nrb + tb]};
+      // fault injection (tests): at step fault_step this wait cannot be met, times out (err 2)
+      // and every other wait gives up, as a hand-off that never arrives would make them
+      unsigned tgt[1] = {i == a.fault_step ? 0xffffffffu : (unsigned)(i + 1) * (unsigned)a.tab[a.G + 1 + 2 * a.nrb + tb]};
       if (!hy_wait(a, 1, idx, tgt, s_ok)) break;
     }
     HY_MARK(1);
@@ -587,11 +588,13 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
       HY_IDX();
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        const int e = tid + u * kHyThreads;   // 16 rows x kHyMaxWC4 float4
-        const int m = e / kHyMaxWC4, q = e - m * kHyMaxWC4;
-        if (e < 16 * kHyMaxWC4) {
-          const f32x4 v = (m < M && q < WC4) ? hld4(rHB, bH1 + ((par * 16 + m) * N1 + c0 + 4 * q) * 4) : zv;
-          *reinterpret_cast<f32x4*>(sh1 + m * PH + 4 * q) = v;
+        // 4 kHyMaxWC4 columns x 4 float4 of rows (H1 is [N1][16]; columns >= WC zero)
+        const int e = tid + u * kHyThreads;
+        const int kc = e >> 2, mg = e & 3;
+        if (kc < 4 * kHyMaxWC4) {
+          const f32x4 v = kc < WC ? hld4(rHB, bH1 + ((par * N1 + c0 + kc) * 16 + 4 * mg) * 4) : zv;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) sh1[(4 * mg + j) * PH + kc] = v[j];
         }
       }
     }
@@ -609,12 +612,8 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
         }
         const f32x4 acc = acc0 + acc1;
         const int n = 16 * r + li;
-        if (n < WR)
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int m = 4 * lq + k;
-            if (m < M) hst1(rHB, bFP + (((par * NC + tb) * 16 + m) * N2 + r0 + n) * 4, acc[k]);
-          }
+        // FP is [NC][N2][16]: the lane's four rows m = 4 lq .. as one 16-B store
+        if (n < WR) hst4(rHB, bFP + (((par * NC + tb) * N2 + r0 + n) * 16 + 4 * lq) * 4, acc);
       }
     }
     hy_arrive(a, hy_seam(0, w & 7));
@@ -625,23 +624,19 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
       if (!hy_seam_wait(a, 0, (unsigned)(i + 1), s_ok)) break;
       HY_MARK(3);
       {
+        // partial cq of fc2 row 4 w + ii, rows m = 4 mg .. (FP is [NC][N2][16])
         HY_IDX();
-        const int m = tid >> 5, cq = tid & 31;
-        red[m * 32 + cq] = (m < M && cq < NC) ? hld4(rHB, bFP + (((par * NC + cq) * 16 + m) * N2 + 4 * w) * 4) : zv;
-      }
-      __syncthreads();
-      if (threadIdx.x < 16) {
-        const int m = threadIdx.x;
-        f32x4 s = red[m * 32];
-#pragma unroll
-        for (int cq = 1; cq < kHyMaxNC; ++cq) s += red[m * 32 + cq];   // partials >= NC are zero
-        sp2[m] = s;
+        const int cq = tid >> 4, ii = (tid >> 2) & 3, mg = tid & 3;
+        red[tid] = cq < NC ? hld4(rHB, bFP + (((par * NC + cq) * N2 + 4 * w + ii) * 16 + 4 * mg) * 4) : zv;
       }
       __syncthreads();
       if (threadIdx.x < 64) {
         HY_IDX();
         const int m = tid >> 2, ii = tid & 3;
-        float pv = sp2[m][ii];
+        // the NC partials in order (partials >= NC are zero)
+        float pv = red[ii * 4 + (m >> 2)][m & 3];
+#pragma unroll
+        for (int cq = 1; cq < kHyMaxNC; ++cq) pv += red[cq * 16 + ii * 4 + (m >> 2)][m & 3];
         if (a.ipc.T > 0) {
           // tensor-parallel fc2 (row-parallel): this workgroup's 16 x 4 product block to every
           // rank as 8-byte granules {generation, value}, summed in rank order on every rank
@@ -873,12 +868,8 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
           if (h == 1 && !two) break;
           const f32x4 acc = h == 0 ? a0 + a1 : b0 + b1;
           const int j = 16 * (h == 0 ? jt0 : jt1) + li;
-          if (j < WC)
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              const int m = 4 * lq + k;
-              if (m < M) hst1(rHB, bDP + (((par * kHyNR + ta) * 16 + m) * N1 + c0 + j) * 4, acc[k]);
-            }
+          // DP is [8][N1][16]: the lane's four rows m = 4 lq .. as one 16-B store
+          if (j < WC) hst4(rHB, bDP + (((par * kHyNR + ta) * N1 + c0 + j) * 16 + 4 * lq) * 4, acc);
         }
       }
     }
@@ -931,21 +922,24 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
     HY_MARK(12);
     {
       HY_IDX();
-      for (int e = tid; e < kHyRuns * 256; e += kHyThreads) {
-        const int k = e >> 8, m = (e >> 4) & 15, nn = e & 15;
+      // (row nn, rows m = 4 mg ..): DP is [8][N1][16], H1 [N1][16]
+      for (int e = tid; e < kHyRuns * 64; e += kHyThreads) {
+        const int k = e >> 6, nn = (e >> 2) & 15, mg = e & 3;
         const int n = 16 * (rbA + k) + nn;
-        float v = 0.f;
-        if (k < nruns && m < M && n < N1) {
-          float parts[kHyNR];
+        f32x4 v = zv;
+        if (k < nruns && n < N1) {
+          f32x4 parts[kHyNR];
 #pragma unroll
-          for (int b = 0; b < kHyNR; ++b) parts[b] = hld1(rHB, bDP + (((par * kHyNR + b) * 16 + m) * N1 + n) * 4);
-          const float h = hld1(rHB, bH1 + ((par * 16 + m) * N1 + n) * 4);
+          for (int b = 0; b < kHyNR; ++b) parts[b] = hld4(rHB, bDP + (((par * kHyNR + b) * N1 + n) * 16 + 4 * mg) * 4);
+          const f32x4 h = hld4(rHB, bH1 + ((par * N1 + n) * 16 + 4 * mg) * 4);
           v = parts[0];
 #pragma unroll
           for (int b = 1; b < kHyNR; ++b) v += parts[b];
-          v = h > 0.f ? v * a.dsc1 : 0.f;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = (4 * mg + j < M && h[j] > 0.f) ? v[j] * a.dsc1 : 0.f;
         }
-        sdz1[e] = v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sdz1[k * 256 + (4 * mg + j) * 16 + nn] = v[j];
       }
     }
     __syncthreads();

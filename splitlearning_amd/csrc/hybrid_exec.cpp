@@ -268,12 +268,12 @@ class HybridEpoch {
     if (fault_step_ >= 0) fault_step_ = -1;   // one injected fault per arming
     const int e = err_.item<int>();   // one sync per client epoch
     TORCH_CHECK(e == 0, "hybrid server epoch: an in-launch wait gave up (error word ", e,
-                "; 2 = a hand-off timed out, 4 = the peer-mapped fc2 exchange failed, 8 = fault injected)");
+                "; 2 = a hand-off timed out, 4 = the peer-mapped fc2 exchange failed)");
     return py::make_tuple(fwd_count + S, t + S, S * B_);
   }
 
-  // tests: the next run stops every workgroup at step `step` of the epoch (err 8), as an
-  // in-launch failure would; -1 disarms
+  // tests: in the next run, step `step`'s first hand-off wait is never met (it times out,
+  // err 2, and every other wait gives up), as a lost hand-off would; -1 disarms
   void set_fault_step(int64_t step) { fault_step_ = step; }
   int64_t max_steps() const { return max_steps_; }
 

@@ -64,7 +64,7 @@ struct ResArgs {
   // plain launch, for ranks that deliberately share one GPU with a partial grid each (the
   // one-GPU multi-process rehearsal), where the device-wide check does not describe the split
   int coop;
-  int fault_step;         // fault injection (tests): every workgroup stops at this step with err |= 8 (-1: off)
+  int fault_step;         // fault injection (tests): this step's first wait is never met (times out, err 2); -1: off
 };
 
 hipError_t resident_epoch_launch(const ResArgs& a, hipStream_t st);

@@ -82,7 +82,7 @@ __device__ __forceinline__ bool seam_wait(const ResArgs& a, int seam, unsigned m
     if (lane < 8) {
       const int n = a.shard_n[seam * 8 + lane];
       const unsigned* p = a.cnt + (seam * 8 + lane) * kResShardStride;
-      const unsigned tgt = mult * (unsigned)n;
+      const unsigned tgt = mult == 0xffffffffu ? mult : mult * (unsigned)n;   // ~0u: never met
       if (n > 0 && poll(p) < tgt) {
         const uint64_t t0 = wall_clock64();
         while (poll(p) < tgt) {
@@ -378,10 +378,6 @@ __global__ void __launch_bounds__(kResThreads) resident_epoch_kernel(ResArgs a) 
   }
 
   for (int i = 0; i < a.S && !fc1_failed; ++i) {
-    if (i == a.fault_step) {   // uniform: every workgroup stops here (tests: mid-epoch failure)
-      if (blockIdx.x == 0 && threadIdx.x == 0) __hip_atomic_fetch_or(a.err, 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      break;
-    }
     const int par = i & 1, nxt = par ^ 1;
     const uint32_t sd2 = a.seeds[4 * i + 2], sd3 = a.seeds[4 * i + 3];
     const SlOpt o = a.o;
@@ -390,7 +386,9 @@ __global__ void __launch_bounds__(kResThreads) resident_epoch_kernel(ResArgs a) 
 
     // ================= A: h1_t, fc2 rows, logit partials
     RES_MARK(0);
-    if (!seam_wait(a, 0, (unsigned)(i + 1), s_ok)) break;
+    // fault injection (tests): at step fault_step this wait cannot be met, times out (err 2) and
+    // every other wait gives up, as a hand-off that never arrives would make them
+    if (!seam_wait(a, 0, i == a.fault_step ? 0xffffffffu : (unsigned)(i + 1), s_ok)) break;
     RES_MARK(1);
     {
       RES_IDX();

@@ -157,7 +157,7 @@ class ResidentEpoch {
   std::string why() const { return why_; }
   int workgroups() const { return a_.G; }
   int clock_khz() const { return clock_khz_; }
-  // tests: the next run stops every workgroup at step `step` (err 8), as an in-launch failure would
+  // tests: in the next run, step `step`'s first hand-off wait is never met (times out, err 2)
   void set_fault_step(int64_t step) { fault_step_ = step; }
 
   // Every full batch of acts [n, K1] / labels [n] (the first n - n % B rows) in ONE launch;
@@ -221,7 +221,7 @@ class ResidentEpoch {
     TORCH_CHECK(le == hipSuccess, "resident epoch launch: ", hipGetErrorString(le));
     const int e = err_.item<int>();   // one sync per client epoch
     TORCH_CHECK(e == 0, "resident server epoch: an in-launch wait gave up (error word ", e,
-                "; 2 = a seam timed out, 4 = the peer-mapped fc2 exchange failed, 8 = fault injected)");
+                "; 2 = a seam timed out, 4 = the peer-mapped fc2 exchange failed)");
     return py::make_tuple(fwd_count + S, t + S, S * B_);
   }
 

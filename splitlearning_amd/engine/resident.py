@@ -7,13 +7,18 @@ the survivors inconsistent (split_nn.py:183-186, mp.spawn join=True).
 Tensor-parallel, the resident executor exchanges fc2 product rows between the ranks inside its
 persistent launch, through the same peer-mapped region as the launch-per-stage executor's fused
 all-reduce (csrc/ipc_ar.h).  Before adopting it every Bob rank runs a short self-test epoch on a
-scratch copy of its shard (`probe`); the ranks adopt it only if every one finished and the
-replicated fc3 came out bitwise equal.  A probe whose exchange timed out has raised the region's
+scratch copy of its shard (`probe`); the ranks adopt it only if every one finished, its result
+agreed with the launch-per-stage executor's on the same scratch epoch, and the replicated fc3
+came out bitwise equal across ranks.  A probe whose exchange timed out has raised the region's
 error word, which would make every later wait of the launch-per-stage executor give up at once;
 so when the agreement is "no", every rank re-arms the region collectively (`rearm`): device
 synchronised, error word and host mirror cleared, all ranks continue at one agreed generation
 above anything already in the region.  The job then trains on the launch-per-stage executor
 instead of dying (tests/test_resident_gpu.py::test_failed_probe_falls_back_on_every_rank).
+
+After adoption, every client epoch goes through `Failsafe`: a launch that fails mid-epoch is
+rolled back on every Bob rank and the job continues on launch-per-stage
+(tests/test_hybrid_gpu.py::test_tensor_parallel_mid_epoch_failure_survived_across_processes).
 """
 from __future__ import annotations
 
@@ -42,6 +47,8 @@ def _launch_per_stage_epoch(t, slot, x, y, B):
         t.fused_step(slot)
         losses.append(lo)
     return torch.cat(losses)
+
+
 # fault injection (tests): the TP rank named here skips its probe launch, so every peer's
 # in-launch exchange times out
 FAULT_ENV = "SL_FAULT_RESIDENT_PROBE"
@@ -197,8 +204,10 @@ class Failsafe:
     result is exactly that of a job which switched executors at that epoch.
 
     Fault injection (tests): SL_FAULT_PERSIST_EPOCH="TP_RANK:EPOCH:STEP" stops every workgroup
-    of TP rank TP_RANK's launch at step STEP of its EPOCH-th persistent epoch (0-based), as an
-    in-launch failure would (the kernels' `fault_step`, error word 8)."""
+    of TP rank TP_RANK's launch at step STEP of its EPOCH-th persistent epoch (0-based): that
+    step's first hand-off wait is never met, times out (error word 2) and every other wait of
+    the launch gives up, as a hand-off that never arrives would make them (the kernels'
+    `fault_step`)."""
 
     def __init__(self, tail, slot, B: int, group=None, enabled: bool = True):
         self.tail, self.slot, self.B, self.group, self.enabled = tail, slot, B, group, enabled

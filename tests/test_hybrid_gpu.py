@@ -270,9 +270,9 @@ def test_hybrid_sgd_momentum_close_to_torch(cuda):
 
 
 def test_hybrid_mid_epoch_failure_rolls_back_to_launch_per_stage(cuda, monkeypatch):
-    """`engine.resident.Failsafe` (the path SisaSession.server_epoch takes): a launch stopped
-    at step 5 of the second client epoch (injected: the kernel's fault_step) raises after
-    updating part of the shard; the shard is restored and the epoch re-runs launch-per-stage.
+    """`engine.resident.Failsafe` (the path SisaSession.server_epoch takes): a launch whose
+    hand-off at step 5 of the second client epoch never arrives (injected: the kernel's
+    fault_step) times out and raises after updating part of the shard; the shard is restored and the epoch re-runs launch-per-stage.
     The result is bitwise a job that switched executors at that epoch with no failure."""
     from splitlearning_amd.engine.resident import FAULT_EPOCH_ENV, Failsafe, _launch_per_stage_epoch
     B, rows, seed_base = 16, 16 * 12, 8
@@ -283,12 +283,13 @@ def test_hybrid_mid_epoch_failure_rolls_back_to_launch_per_stage(cuda, monkeypat
     torch.manual_seed(16)
     base = _MLP(spec)
     ta, sa = _engine(base, spec, cuda, seed_base, "#hyfa")
+    ta.resident_timeout_s = 1.0          # the injected stall times out after 1 s
     tb, sb = _engine(base, spec, cuda, seed_base, "#hyfb")
     monkeypatch.setenv(FAULT_EPOCH_ENV, "0:1:5")
     fs = Failsafe(ta, sa, B)
     assert fs.run("hybrid", acts, labels)
     assert not fs.run("hybrid", acts, labels)
-    assert fs.fallback["epoch"] == 1 and "error word 8" in fs.fallback["reason"]
+    assert fs.fallback["epoch"] == 1 and "error word 2" in fs.fallback["reason"]
     la = _launch_per_stage_epoch(ta, sa, acts, labels, B)
     monkeypatch.delenv(FAULT_EPOCH_ENV)
     tb.run_hybrid_epoch(acts, labels, sb, B)
