@@ -10,7 +10,8 @@ two boxes), so a variant is only ever compared with the others of the same call.
         --cmd 'python -u {root}/scripts/hybrid_ab.py --tp 1 --steps 500 --rounds 3 --only hybrid' --passes 2
     gpurun --timeout 900 -- 'mkdir -p gpurun_out && bash ab/run.sh'   # -> gpurun_out/ab.log
 
-Each substitution is FILE|OLD|NEW (OLD must occur in FILE; every occurrence is replaced).  The
+Each substitution is FILE|OLD|NEW (OLD must occur in FILE; every occurrence is replaced) or
+FILE<SRC (the variant's FILE becomes a copy of SRC, e.g. a saved earlier version of a kernel).  The
 timing command runs with `{root}` = the variant's tree, whose scripts put that tree first on
 sys.path.  `ab/` is git-ignored; delete it after the call (it ships with every gpurun call).
 """
@@ -31,6 +32,10 @@ def build_variant(out, name, subs):
         shutil.copytree(os.path.join(REPO, d), os.path.join(root, d),
                         ignore=shutil.ignore_patterns("__pycache__", "build"))
     for spec in subs:
+        if "<" in spec and "|" not in spec:     # FILE<SRC: the variant's FILE is a copy of SRC
+            path, src = spec.split("<", 1)
+            shutil.copyfile(src, os.path.join(root, path))
+            continue
         path, old, new = spec.split("|", 2)
         p = os.path.join(root, path)
         with open(p) as f:

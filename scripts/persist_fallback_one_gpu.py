@@ -84,17 +84,36 @@ def worker(rank, world, port, kind):
             fs = Failsafe(ta, sa, B, group=None)
             ex_a = kind
             la = []
+            la_all = []
+            canary = (acts.clone(), labels.clone())
+
+            def intact(where):
+                ok_a, ok_y = torch.equal(acts, canary[0]), torch.equal(labels, canary[1])
+                if not (ok_a and ok_y):
+                    print(f"rank {rank}: INPUTS CORRUPTED {where}: acts {ok_a} labels {ok_y}; "
+                          f"{int((acts != canary[0]).sum().item())} act elements differ", flush=True)
             for e in range(epochs):
+                intact(f"before A epoch {e}")
                 if ex_a != "launch_per_stage" and fs.run(ex_a, acts, labels):
+                    la_all.append(fs.loss)
                     continue
                 ex_a = "launch_per_stage"
                 la.append(_launch_per_stage_epoch(ta, sa, acts, labels, B))
+                la_all.append(la[-1])
+                print(f"rank {rank}: A epoch {e} on launch-per-stage; ipc error word {ipc.error()}", flush=True)
             os.environ.pop(FAULT_EPOCH_ENV)
             print(f"rank {rank}: engine A fallback {fs.fallback}", flush=True)
+            intact("after A")
             run_b = tb.run_hybrid_epoch if kind == "hybrid" else tb.run_resident_epoch
-            run_b(acts, labels, sb, B)
+            lb_all = [run_b(acts, labels, sb, B)]
+            intact("after B epoch 0")
             lb = [_launch_per_stage_epoch(tb, sb, acts, labels, B) for _ in range(epochs - 1)]
+            lb_all += lb
             torch.cuda.synchronize()
+            for e, (x, y) in enumerate(zip(la_all, lb_all)):
+                print(f"rank {rank}: epoch {e} losses A vs B max |d| {(x - y).abs().max().item():.3g}", flush=True)
+            for nm, (La, Lb) in zip(("fc1", "fc2", "fc3"), zip(ta.layers, tb.layers)):
+                print(f"rank {rank}: {nm} W A vs B max |d| {(La.W - Lb.W).abs().max().item():.3g}", flush=True)
         except Exception as e:                          # the test's point: nothing raises
             raised = e
             print(f"rank {rank}: raised {type(e).__name__}: {e}", flush=True)
@@ -114,6 +133,7 @@ def worker(rank, world, port, kind):
         step = 0
         last = []
         for e in range(epochs):
+            ep = []
             for i in range(n // B):
                 step += 1
                 x, y = acts[i * B:(i + 1) * B], labels[i * B:(i + 1) * B]
@@ -131,8 +151,15 @@ def worker(rank, world, port, kind):
                 lr_ = F.cross_entropy(h, y, reduction="none")
                 lr_.mean().backward()
                 opt.step()
+                ep.append(lr_.detach())
                 if e == epochs - 1:
                     last.append(lr_.detach())
+            ep = torch.cat(ep)
+            print(f"rank {rank}: epoch {e} vs torch max |d|: A {(la_all[e] - ep).abs().max().item():.3g} "
+                  f"B {(lb_all[e] - ep).abs().max().item():.3g}", flush=True)
+        nan_a = sum(int(torch.isnan(L.W).sum().item()) for L in ta.layers)
+        nan_b = sum(int(torch.isnan(L.W).sum().item()) for L in tb.layers)
+        print(f"rank {rank}: NaN in W: A {nan_a} B {nan_b}", flush=True)
         close = torch.allclose(la[-1], torch.cat(last), rtol=2e-3, atol=2e-3)
         print(f"rank {rank}: last epoch's losses close to torch {close} (max diff "
               f"{(la[-1] - torch.cat(last)).abs().max().item():.2e})", flush=True)

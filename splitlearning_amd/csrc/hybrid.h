@@ -21,9 +21,9 @@ constexpr int kHySlots = 8;         // workgroups whose runs may touch one fc1 r
 constexpr int kHyMaxRB = 320;       // fc1 row blocks of 16 rows (N1 <= 5120)
 constexpr int kHyStride = 32;       // counter words 128 B apart
 constexpr int kHySeams = 4;         // F: fc2 partials, L: logit partials, D: dlogits, Z: dz2
-// counter words: the seams' 8 shards each, then H[NC] (h1 column blocks published), P[NC]
-// (dz1 partials per fc2 column block), R[nrb] (look-ahead partials per fc1 row block)
-constexpr int kHyCounters = kHySeams * 8 + 2 * kHyMaxNC + kHyMaxRB;
+// counter words: the seams' 8 shards each, then P[NC] (dz1 partials per fc2 column block),
+// R[nrb] (look-ahead partials per fc1 row block)
+constexpr int kHyCounters = kHySeams * 8 + kHyMaxNC + kHyMaxRB;
 
 struct HyArgs {
   ResLayer L1, L2, L3;
@@ -52,7 +52,7 @@ struct HyArgs {
   // (the MFMA-produced ones batch-row fastest, [..][n][16 m]: a lane's accumulator is four
   // consecutive rows of one column, so every hand-off store and load is 16 B)
   //   LA [2][nrb][kHySlots][16 n][16 m] look-ahead partials (slot = w - rbw0)
-  //   H1 [2][N1][16 m] h1 (rows m >= M zero)
+  //   H1 [2][N1][16 m] h1 (rows m >= M zero), written by the F phase's ta == 0 workgroups
   //   FP [2][NC][N2][16 m] fc2 product partials per column block
   //   LP [2][HW][16][C4] logit partials
   //   DL [2][16][C4] dlogits

@@ -19,14 +19,17 @@
 // 650 MB at TP = 1 instead of 770 + 40) plus hand-offs.
 //
 // Step i, workgroup w = (ta, tb) = (w / NC, w % NC):
-//   F  wait until every fc1 row block overlapping fc2 column block tb has published h1_i
-//      (counter H[tb]); h1[:, slice] -> LDS; the tile's fc2 partial FP[tb][m][r0 + n] =
-//      h1[m, slice] . W2[r0 + n, slice] (exact-fp32 MFMA)                       -> seam F
+//   F  wait until every fc1 row block overlapping fc2 column block tb has published its
+//      look-ahead partials (counters R[rb]); h1[:, slice] = drop(relu(the partials summed in
+//      workgroup order)) -> LDS (ta == 0 also -> H1 for the U phase's mask); the tile's fc2
+//      partial FP[tb][r0 + n][m] = h1[m, slice] . W2[r0 + n, slice] (exact-fp32 MFMA) -> seam F
 //   H  head w < N2 / 4 (fc2 rows 4w .. 4w + 3): P2 = the NC partials in order (tensor-
 //      parallel: resident.hip's peer-mapped granule exchange, summed in rank order); h2 =
 //      drop(relu(P2 + b2)); logit partials of these rows                      -> seam L
-//   S  w < M: row w's logits (partials in order, + b3), softmax-CE, dlogits, loss -> seam D
-//   H2 head: dz2 of its rows (dlogits . W3[:, rows], ReLU / dropout mask)        -> seam Z;
+//   S  w < 4 M: quarter w % 4 of row w / 4's logits (partials in order, + b3) and its softmax
+//      statistics {max, sum exp}                                                  -> seam D
+//   H2 head: the softmax-CE from the logits and the quarters' statistics (loss by w = 0),
+//      dz2 of its rows (dlogits . W3[:, rows], ReLU / dropout mask)              -> seam Z;
 //      then the Adam steps of b3, its W3 columns and b2 (off the critical path)
 //   B  the tile's dz1 partial DP[ta][m][c0 + j] = dz2[m, tile rows] . W2_i[tile rows, c0 + j]
 //      (MFMA)                                                          -> counter P[tb];
@@ -37,10 +40,11 @@
 //      look-ahead product x_{i+1} W1_{i+1}^T accumulated per row block (MFMA, the updated
 //      tile staged through LDS as wgrad_group_kernel); the loads of the next tile are in
 //      flight while a tile computes (first tile: issued before W2's update).  After the
-//      run, each row block's partial -> LA; the row block's last-arriving workgroup sums the
-//      partials in workgroup order (+ b1_{i+1}), applies ReLU and step i + 1's dropout,
-//      publishes h1_{i+1} rows and counts them into H[] of the fc2 column blocks they cover.
-// A prologue pass (W1 read only) forms h1_0 the same way.  Arithmetic is fp32 (exact-fp32
+//      run, each row block's partial (+ b1_{i+1} from its first workgroup) -> LA and one
+//      arrival on R[rb]; step i + 1's F phases sum them (a last-arriving workgroup reducing
+//      them first put a returning atomic, a cold read, a second publication and a second
+//      counter on the critical path: 139.3 -> see docs/PERF.md round 5).
+// A prologue pass (W1 read only) forms h1_0's partials the same way.  Arithmetic is fp32 (exact-fp32
 // MFMA for the three products that use it); every sum runs in a fixed order, so a launch is
 // deterministic and one launch of S steps is bitwise S one-step launches; the order differs
 // from the launch-per-stage executor's, so results agree with it and with torch to fp32
@@ -65,9 +69,8 @@ using namespace persist;
 
 __device__ __forceinline__ unsigned* hy_cnt(const HyArgs& a, int i) { return a.cnt + i * kHyStride; }
 __device__ __forceinline__ int hy_seam(int seam, int shard) { return seam * 8 + shard; }
-__device__ __forceinline__ int hy_H(int b) { return kHySeams * 8 + b; }
-__device__ __forceinline__ int hy_P(int b) { return kHySeams * 8 + kHyMaxNC + b; }
-__device__ __forceinline__ int hy_R(int rb) { return kHySeams * 8 + 2 * kHyMaxNC + rb; }
+__device__ __forceinline__ int hy_P(int b) { return kHySeams * 8 + b; }
+__device__ __forceinline__ int hy_R(int rb) { return kHySeams * 8 + kHyMaxNC + rb; }
 
 // bounded wait until *p >= tgt (one lane); false when it gave up
 __device__ __forceinline__ bool hy_spin(const HyArgs& a, const unsigned* p, unsigned tgt) {
@@ -89,20 +92,6 @@ __device__ __forceinline__ void hy_arrive(const HyArgs& a, int idx) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) __hip_atomic_fetch_add(hy_cnt(a, idx), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// lanes 0 .. n-1 of wave 0 each wait for counter idx[lane] >= tgt[lane]; the barrier then
-// releases every wave to its sc1 loads.  Uniform result over the workgroup.
-__device__ __forceinline__ bool hy_wait(const HyArgs& a, int n, const int* idx, const unsigned* tgt, int* s_ok) {
-  if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
-    bool ok = true;
-    if (lane < n) ok = hy_spin(a, hy_cnt(a, idx[lane]), tgt[lane]);
-    ok = __all(ok);
-    if (lane == 0) *s_ok = ok ? 1 : 0;
-  }
-  __syncthreads();
-  return *s_ok != 0;
 }
 
 // the 8 shards of a seam (shard s receives shard_n[seam][s] arrivals per step)
@@ -201,7 +190,7 @@ static_assert(kHyThreads / 64 * 10 * 256 >= kHyMaxWR * 4 * kHyMaxWC4, "10 W2 16 
 #define HY_MARK(k)                                                                               \
   do {                                                                                           \
     if (threadIdx.x == 0) {                                                                      \
-      if (a.trace != nullptr && i < a.trace_steps && (w == 0 || w == G - 1))                     \
+      if (a.trace != nullptr && i >= 0 && i < a.trace_steps && (w == 0 || w == G - 1))           \
         a.trace[((int64_t)(w == 0 ? 0 : 1) * a.trace_steps + i) * 16 + (k)] = (int64_t)wall_clock64(); \
       if (a.tall != nullptr && i >= a.tall_step && i < a.tall_step + a.tall_n)                   \
         a.tall[((int64_t)(i - a.tall_step) * G + w) * 16 + (k)] = (int64_t)wall_clock64();       \
@@ -467,12 +456,12 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
     zlast = z;   // the last row block's accumulators go to flush through LDS
   };
 
-  // Publish the run's look-ahead partials for step `so` (parity so & 1, generation gen of the
-  // row-block counters): each row block's partial (the 8 waves' MFMA accumulators from ZP, in
-  // wave order, + b1 by its first workgroup) -> LA; the row block's last arriver sums all
-  // partials in workgroup order, applies ReLU and step so's dropout, publishes h1 rows and
-  // counts them into H[] of the fc2 column blocks they cover.
-  auto flush = [&](int so, unsigned gen) {
+  // Publish the run's look-ahead partials for step `so` (parity so & 1): each row block's
+  // partial (the 8 waves' MFMA accumulators from ZP, in wave order, + b1 by its first
+  // workgroup) -> LA, then one arrival per row block on R[].  The consumers (step so's F) sum a
+  // row block's partials in workgroup order and apply its epilogue themselves: no last-arriver
+  // round trip, no second publication on the step's critical path.
+  auto flush = [&](int so) {
     const int par = so & 1;
     {
       // the last row block's per-wave accumulators through LDS (the stream's buffers are free
@@ -508,63 +497,17 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
         if (n < N1) hst4(rHB, bLA + (((par * a.nrb + rb) * kHySlots + slot) * 256 + nn * 16 + 4 * mg) * 4, v);
       }
     }
+    // every wave drained its LA stores; then one lane per run row block arrives
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    // one lane per run: the row blocks' arrivals in flight together (one round trip)
-    if (threadIdx.x < (unsigned)nruns) {
-      const int k = threadIdx.x, rb = rbA + k;
-      const unsigned old = __hip_atomic_fetch_add(hy_cnt(a, hy_R(rb)), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_ok[1 + k] = (old == gen * (unsigned)a.tab[a.G + 1 + a.nrb + rb] - 1u) ? 1 : 0;
-    }
-    __syncthreads();
-    bool any = false;
-    for (int k = 0; k < nruns; ++k) any = any || s_ok[1 + k] != 0;
-    // the row blocks this workgroup arrived last on (64 lanes each: row nn, rows m = 4 mg ..;
-    // rows m >= M published as zero)
-    for (int e0 = 0; e0 < nruns * 64; e0 += kHyThreads) {
-      HY_IDX();
-      const int e = e0 + tid, k = e >> 6;
-      if (k < nruns && s_ok[1 + k]) {
-        const int rb = rbA + k, ns = a.tab[a.G + 1 + a.nrb + rb];
-        const int nn = (e >> 2) & 15, mg = e & 3, n = 16 * rb + nn;
-        if (n < N1) {
-          f32x4 parts[kHySlots];
-#pragma unroll
-          for (int s = 0; s < kHySlots; ++s)
-            parts[s] = s < ns ? hld4(rHB, bLA + (((par * a.nrb + rb) * kHySlots + s) * 256 + nn * 16 + 4 * mg) * 4) : zv;
-          f32x4 v = parts[0];
-#pragma unroll
-          for (int s = 1; s < kHySlots; ++s) v += parts[s];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int m = 4 * mg + j;
-            v[j] = m < M ? drop_relu(v[j], a.seeds[4 * so], a.seeds[4 * so + 1], m, a.col_off1 + n, a.thr1, a.dsc1) : 0.f;
-          }
-          hst4(rHB, bH1 + ((par * N1 + n) * 16 + 4 * mg) * 4, v);
-        }
-      }
-    }
-    if (any) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        for (int k = 0; k < nruns; ++k) {
-          if (!s_ok[1 + k]) continue;
-          const int rb = rbA + k;
-          const int blo = hy_colblk((16 * rb) >> 2, NC, Q4);
-          const int bhi = hy_colblk((min(16 * rb + 16, N1) - 1) >> 2, NC, Q4);
-          for (int b = blo; b <= bhi; ++b)
-            __hip_atomic_fetch_add(hy_cnt(a, hy_H(b)), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-    }
-    __syncthreads();
+    if (threadIdx.x < (unsigned)nruns)
+      __hip_atomic_fetch_add(hy_cnt(a, hy_R(rbA + threadIdx.x)), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
 
   // ---- prologue: h1_0 = drop(relu(x_0 W1_0^T + b1)) by a read-only pass over the run
   if (nt > 0) load_state(t_begin, sp[0], sm[0], sv[0], false);
   stream(std::false_type{}, std::true_type{}, 0, 0, 0.f, 0.f);
-  flush(0, 1u);
+  flush(0);
 
   for (int i = 0; i < a.S; ++i) {
     const int par = i & 1;
@@ -576,23 +519,54 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
 
     // ================= F: h1 slice, the tile's fc2 partial
     HY_MARK(0);
-    {
-      int idx[1] = {hy_H(tb)};
-      // fault injection (tests): at step fault_step this wait cannot be met, times out (err 2)
-      // and every other wait gives up, as a hand-off that never arrives would make them
-      unsigned tgt[1] = {i == a.fault_step ? 0xffffffffu : (unsigned)(i + 1) * (unsigned)a.tab[a.G + 1 + 2 * a.nrb + tb]};
-      if (!hy_wait(a, 1, idx, tgt, s_ok)) break;
+    // the look-ahead partials of every fc1 row block overlapping this column block
+    // [c0, c0 + WC) published (R[rb] counts each run's arrival: (i + 1) ns[rb] by now; lane l of
+    // wave 0 polls row block rlo + l)
+    if (threadIdx.x < 64) {
+      const int lane = threadIdx.x;
+      const int rlo = c0 >> 4, rhi = (c0 + WC - 1) >> 4;
+      bool ok = true;
+      if (rlo + lane <= rhi) {
+        const int rb = rlo + lane;
+        // fault injection (tests): at step fault_step this wait cannot be met, times out (err 2)
+        // and every other wait gives up, as a hand-off that never arrives would make them
+        const unsigned tg = i == a.fault_step ? 0xffffffffu : (unsigned)(i + 1) * (unsigned)a.tab[a.G + 1 + a.nrb + rb];
+        ok = hy_spin(a, hy_cnt(a, hy_R(rb)), tg);
+      }
+      ok = __all(ok);
+      if (lane == 0) *s_ok = ok ? 1 : 0;
     }
+    __syncthreads();
+    if (*s_ok == 0) break;
     HY_MARK(1);
     {
+      // h1 of the slice from the partials (in workgroup order; slot 0 carries b1), ReLU and
+      // step i's dropout, rows m >= M zero, columns >= WC zero; the ta == 0 workgroup also
+      // publishes it to H1 ([N1][16]: the U phase's ReLU mask)
       HY_IDX();
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        // 4 kHyMaxWC4 columns x 4 float4 of rows (H1 is [N1][16]; columns >= WC zero)
         const int e = tid + u * kHyThreads;
         const int kc = e >> 2, mg = e & 3;
         if (kc < 4 * kHyMaxWC4) {
-          const f32x4 v = kc < WC ? hld4(rHB, bH1 + ((par * N1 + c0 + kc) * 16 + 4 * mg) * 4) : zv;
+          f32x4 v = zv;
+          if (kc < WC) {
+            const int n = c0 + kc, rb = n >> 4, nn = n & 15;
+            const int ns = a.tab[a.G + 1 + a.nrb + rb];
+            f32x4 parts[kHySlots];
+#pragma unroll
+            for (int sl = 0; sl < kHySlots; ++sl)
+              parts[sl] = sl < ns ? hld4(rHB, bLA + (((par * a.nrb + rb) * kHySlots + sl) * 256 + nn * 16 + 4 * mg) * 4) : zv;
+            v = parts[0];
+#pragma unroll
+            for (int sl = 1; sl < kHySlots; ++sl) v += parts[sl];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int m = 4 * mg + j;
+              v[j] = m < M ? drop_relu(v[j], a.seeds[4 * i], a.seeds[4 * i + 1], m, a.col_off1 + n, a.thr1, a.dsc1) : 0.f;
+            }
+            if (ta == 0) hst4(rHB, bH1 + ((par * N1 + n) * 16 + 4 * mg) * 4, v);
+          }
 #pragma unroll
           for (int j = 0; j < 4; ++j) sh1[(4 * mg + j) * PH + kc] = v[j];
         }
@@ -960,7 +934,7 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
     if (more) {
       stream(std::true_type{}, std::true_type{}, xt, xn, ss, ib);
       HY_MARK(13);
-      flush(i + 1, (unsigned)(i + 2));
+      flush(i + 1);
     } else {
       stream(std::true_type{}, std::false_type{}, xt, xn, ss, ib);
     }

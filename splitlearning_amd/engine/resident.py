@@ -226,11 +226,12 @@ class Failsafe:
         if len(f) == 3 and int(f[0]) == tail.tp_rank and int(f[1]) == idx:
             ex.set_fault_step(int(f[2]))
         err = None
+        self.loss = None
         try:
             if kind == "resident":
-                tail.run_resident_epoch(acts, labels, slot, B)
+                self.loss = tail.run_resident_epoch(acts, labels, slot, B)
             else:
-                tail.run_hybrid_epoch(acts, labels, slot, B)
+                self.loss = tail.run_hybrid_epoch(acts, labels, slot, B)
         except RuntimeError as e:
             if "in-launch wait gave up" not in str(e) or not self.enabled:
                 raise
