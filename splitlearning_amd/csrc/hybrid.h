@@ -42,7 +42,7 @@ struct HyArgs {
   int64_t ignore;
   float ce_scale;
   SlOpt o;
-  const float* adam;      // [S][2] {step_size, inv_bc2_sqrt}
+  const float* adam;      // [S][4] {step_size, inv_bc2_sqrt, CE scale (1 / the step's rows), -}
   const uint32_t* seeds;  // [S][4] {fc1 lo, hi, fc2 lo, hi}
   uint32_t thr1, thr2;
   float dsc1, dsc2;

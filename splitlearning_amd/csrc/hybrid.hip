@@ -514,7 +514,7 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
     const bool more = i + 1 < a.S;
     const uint32_t sd2 = a.seeds[4 * i + 2], sd3 = a.seeds[4 * i + 3];
     const SlOpt o = a.o;
-    float ss = ADAM ? a.adam[2 * i] : 0.f, ib = ADAM ? a.adam[2 * i + 1] : 0.f;
+    float ss = ADAM ? a.adam[4 * i] : 0.f, ib = ADAM ? a.adam[4 * i + 1] : 0.f;
     asm volatile("" : "+v"(ss), "+v"(ib));
 
     // ================= F: h1 slice, the tile's fc2 partial
@@ -734,7 +734,7 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
           const int cc = 4 * c4 + c;
           float pr = e[c] * inv;
           if (cc == lab) pr -= 1.f;
-          d[c] = (ign || cc >= C) ? 0.f : pr * a.ce_scale;
+          d[c] = (ign || cc >= C) ? 0.f : pr * a.adam[4 * i + 2];
         }
         if (act) hst4(rHB, bDL + ((par * 16 + m) * C4 + 4 * c4) * 4, d);
         if (tid == 0) a.loss[(int64_t)i * M + m] = ign ? 0.f : mx + logf(se) - zl;

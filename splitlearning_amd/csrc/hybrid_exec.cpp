@@ -188,9 +188,16 @@ class HybridEpoch {
   // epoch is bitwise the single launch).  Losses into loss_rows [n].  Returns (fwd_count, t,
   // rows done).  Raises when an in-launch wait gave up (the shard's state is then partly
   // updated: the caller restores it, protocols/sisa.py).
+  //
+  // step_rows (optional, [S] host ints): the batch of step i holds step_rows[i] <= B real rows
+  // (its CE mean is over them); acts / labels are then exactly S * B rows, every short batch
+  // zero-padded with ignored labels (-100), so every step of a whole server epoch over all
+  // clients' caches, short final batches included, runs in the same launch (padded rows add
+  // exact zeros to every gradient).
   py::tuple run(const at::Tensor& acts, const at::Tensor& labels, at::Tensor& loss_rows, int64_t seed_base,
                 int64_t fwd_count, int64_t t, const c10::optional<at::Tensor>& trace,
-                const c10::optional<at::Tensor>& trace_all, int64_t trace_all_step) {
+                const c10::optional<at::Tensor>& trace_all, int64_t trace_all_step,
+                const c10::optional<std::vector<int64_t>>& step_rows) {
     TORCH_CHECK(ok_, "HybridEpoch: this shard does not fit: ", why_);
     TORCH_CHECK(acts.is_cuda() && acts.scalar_type() == at::kFloat && acts.dim() == 2 && acts.is_contiguous() &&
                     acts.size(1) == a_.K1,
@@ -202,12 +209,18 @@ class HybridEpoch {
                 "loss [n]");
     const int64_t S = acts.size(0) / B_;
     if (S == 0) return py::make_tuple(fwd_count, t, (int64_t)0);
-    std::vector<float> adam(2 * S, 0.f);
+    if (step_rows.has_value())
+      TORCH_CHECK((int64_t)step_rows->size() == S && acts.size(0) == S * B_,
+                  "step_rows: one row count per step, acts exactly S * B rows");
+    std::vector<float> adam(4 * S, 0.f);
     std::vector<int32_t> seeds(4 * S);
     for (int64_t i = 0; i < S; ++i) {
       const SlOpt o = sl::make_opt_raw(kind_, lr_, beta1_, beta2_, eps_, wd_, mom_, t + 1 + i, nullptr);
-      adam[2 * i] = o.step_size;
-      adam[2 * i + 1] = o.inv_bc2_sqrt;
+      adam[4 * i] = o.step_size;
+      adam[4 * i + 1] = o.inv_bc2_sqrt;
+      const int64_t rows = step_rows.has_value() ? (*step_rows)[i] : B_;
+      TORCH_CHECK(rows >= 1 && rows <= B_, "step_rows: 1 .. B rows per step");
+      adam[4 * i + 2] = (float)(1.0 / (double)rows);
       const uint64_t s0 = sl::step_seed((uint64_t)seed_base, 0, (uint64_t)(fwd_count + 1 + i));
       const uint64_t s1 = sl::step_seed((uint64_t)seed_base, 1, (uint64_t)(fwd_count + 1 + i));
       seeds[4 * i] = (int32_t)(uint32_t)(s0 & 0xffffffffull);
@@ -216,7 +229,7 @@ class HybridEpoch {
       seeds[4 * i + 3] = (int32_t)(uint32_t)(s1 >> 32);
     }
     const at::Device dev = acts.device();
-    adam_ = at::from_blob(adam.data(), {2 * S}, at::TensorOptions().dtype(at::kFloat)).to(dev);
+    adam_ = at::from_blob(adam.data(), {4 * S}, at::TensorOptions().dtype(at::kFloat)).to(dev);
     seeds_ = at::from_blob(seeds.data(), {4 * S}, at::TensorOptions().dtype(at::kInt)).to(dev);
     int64_t* tr = nullptr;
     int trs = 0;
@@ -248,7 +261,7 @@ class HybridEpoch {
       a.X = acts.data_ptr<float>() + s0 * B_ * a_.K1;
       a.Y = labels.data_ptr<int64_t>() + s0 * B_;
       a.loss = loss_rows.data_ptr<float>() + s0 * B_;
-      a.adam = adam_.data_ptr<float>() + 2 * s0;
+      a.adam = adam_.data_ptr<float>() + 4 * s0;
       a.seeds = reinterpret_cast<const uint32_t*>(seeds_.data_ptr<int32_t>()) + 4 * s0;
       a.ipc.T = 0;
       if (ipc_ != nullptr) a.ipc = ipc_->begin_steps(n);
@@ -344,5 +357,5 @@ void sl_register_hybrid(py::module& m) {
       .def("max_steps", &HybridEpoch::max_steps)
       .def("run", &HybridEpoch::run, py::arg("acts"), py::arg("labels"), py::arg("loss_rows"),
            py::arg("seed_base"), py::arg("fwd_count"), py::arg("t"), py::arg("trace") = py::none(),
-           py::arg("trace_all") = py::none(), py::arg("trace_all_step") = 0);
+           py::arg("trace_all") = py::none(), py::arg("trace_all_step") = 0, py::arg("step_rows") = py::none());
 }

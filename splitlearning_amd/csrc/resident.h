@@ -36,7 +36,7 @@ struct ResArgs {
   int64_t ignore;
   float ce_scale;         // per-row loss scale (1 / M)
   SlOpt o;                // kind / lr / betas / eps / wd / momentum (step scalars: adam)
-  const float* adam;      // [S][2] {step_size, inv_bc2_sqrt} per step (Adam)
+  const float* adam;      // [S][4] {step_size, inv_bc2_sqrt, CE scale (1 / the step's rows), -}
   const uint32_t* seeds;  // [S][4] {fc1 lo, hi, fc2 lo, hi} dropout seeds per step
   uint32_t thr1, thr2;    // dropout thresholds (0: off)
   float dsc1, dsc2;       // 1 / (1 - p)

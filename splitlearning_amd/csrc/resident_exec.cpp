@@ -162,8 +162,11 @@ class ResidentEpoch {
 
   // Every full batch of acts [n, K1] / labels [n] (the first n - n % B rows) in ONE launch;
   // losses into loss_rows [n].  Returns (fwd_count, t, rows done).
+  // step_rows (optional): rows of each step's batch (<= B; acts exactly S * B rows, short
+  // batches zero-padded with ignored labels), as HybridEpoch::run.
   py::tuple run(const at::Tensor& acts, const at::Tensor& labels, at::Tensor& loss_rows, int64_t seed_base,
-                int64_t fwd_count, int64_t t, const c10::optional<at::Tensor>& trace) {
+                int64_t fwd_count, int64_t t, const c10::optional<at::Tensor>& trace,
+                const c10::optional<std::vector<int64_t>>& step_rows) {
     TORCH_CHECK(ok_, "ResidentEpoch: this shard does not fit: ", why_);
     TORCH_CHECK(acts.is_cuda() && acts.scalar_type() == at::kFloat && acts.dim() == 2 && acts.is_contiguous() &&
                     acts.size(1) == a_.K1,
@@ -175,14 +178,20 @@ class ResidentEpoch {
                 "loss [n]");
     const int64_t S = acts.size(0) / B_;
     if (S == 0) return py::make_tuple(fwd_count, t, (int64_t)0);
+    if (step_rows.has_value())
+      TORCH_CHECK((int64_t)step_rows->size() == S && acts.size(0) == S * B_,
+                  "step_rows: one row count per step, acts exactly S * B rows");
     // per-step tables: Adam {step_size, 1/sqrt(bc2)} at steps t+1 .. t+S and the two dropout
     // seeds at forward counts fwd_count+1 .. fwd_count+S
-    std::vector<float> adam(2 * S, 0.f);
+    std::vector<float> adam(4 * S, 0.f);
     std::vector<int32_t> seeds(4 * S);
     for (int64_t i = 0; i < S; ++i) {
       const SlOpt o = sl::make_opt_raw(kind_, lr_, beta1_, beta2_, eps_, wd_, mom_, t + 1 + i, nullptr);
-      adam[2 * i] = o.step_size;
-      adam[2 * i + 1] = o.inv_bc2_sqrt;
+      adam[4 * i] = o.step_size;
+      adam[4 * i + 1] = o.inv_bc2_sqrt;
+      const int64_t rows = step_rows.has_value() ? (*step_rows)[i] : B_;
+      TORCH_CHECK(rows >= 1 && rows <= B_, "step_rows: 1 .. B rows per step");
+      adam[4 * i + 2] = (float)(1.0 / (double)rows);
       const uint64_t s0 = sl::step_seed((uint64_t)seed_base, 0, (uint64_t)(fwd_count + 1 + i));
       const uint64_t s1 = sl::step_seed((uint64_t)seed_base, 1, (uint64_t)(fwd_count + 1 + i));
       seeds[4 * i] = (int32_t)(uint32_t)(s0 & 0xffffffffull);
@@ -191,7 +200,7 @@ class ResidentEpoch {
       seeds[4 * i + 3] = (int32_t)(uint32_t)(s1 >> 32);
     }
     const at::Device dev = acts.device();
-    adam_ = at::from_blob(adam.data(), {2 * S}, at::TensorOptions().dtype(at::kFloat)).to(dev);
+    adam_ = at::from_blob(adam.data(), {4 * S}, at::TensorOptions().dtype(at::kFloat)).to(dev);
     seeds_ = at::from_blob(seeds.data(), {4 * S}, at::TensorOptions().dtype(at::kInt)).to(dev);
     sl::ResArgs a = a_;
     a.S = (int)S;
@@ -248,5 +257,6 @@ void sl_register_resident(py::module& m) {
       .def("workgroups", &ResidentEpoch::workgroups)
       .def("clock_khz", [](const ResidentEpoch& e) { return e.clock_khz(); })
       .def("run", &ResidentEpoch::run, py::arg("acts"), py::arg("labels"), py::arg("loss_rows"),
-           py::arg("seed_base"), py::arg("fwd_count"), py::arg("t"), py::arg("trace") = py::none());
+           py::arg("seed_base"), py::arg("fwd_count"), py::arg("t"), py::arg("trace") = py::none(),
+           py::arg("step_rows") = py::none());
 }

@@ -215,7 +215,7 @@ class Failsafe:
         self.epochs = 0
         self.fallback = None
 
-    def run(self, kind: str, acts: torch.Tensor, labels: torch.Tensor) -> bool:
+    def run(self, kind: str, acts: torch.Tensor, labels: torch.Tensor, step_rows=None) -> bool:
         tail, slot, B = self.tail, self.slot, self.B
         idx = self.epochs
         self.epochs += 1
@@ -229,9 +229,9 @@ class Failsafe:
         self.loss = None
         try:
             if kind == "resident":
-                self.loss = tail.run_resident_epoch(acts, labels, slot, B)
+                self.loss = tail.run_resident_epoch(acts, labels, slot, B, step_rows)
             else:
-                self.loss = tail.run_hybrid_epoch(acts, labels, slot, B)
+                self.loss = tail.run_hybrid_epoch(acts, labels, slot, B, step_rows)
         except RuntimeError as e:
             if "in-launch wait gave up" not in str(e) or not self.enabled:
                 raise

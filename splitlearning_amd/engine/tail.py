@@ -434,16 +434,19 @@ class TailEngine:
             return False
         return self._resident_executor(slot, B).ok()
 
-    def run_resident_epoch(self, acts: torch.Tensor, labels: torch.Tensor, slot: OptSlot, B: int) -> torch.Tensor:
+    def run_resident_epoch(self, acts: torch.Tensor, labels: torch.Tensor, slot: OptSlot, B: int,
+                           step_rows=None) -> torch.Tensor:
         """One epoch over `acts` / `labels` with every full batch in ONE persistent launch that
         keeps this shard's weights and optimizer state on-chip (csrc/resident.hip); a trailing
-        partial batch runs on the launch-per-stage executor.  Same step / seed / Adam-count
-        bookkeeping as `run_native_epoch`; the sums run in another order, so results agree
-        with it to fp32 rounding, not bitwise.  Returns the per-row losses."""
+        partial batch runs on the launch-per-stage executor.  `step_rows`: the plan of
+        `padded_plan` (every step's real rows; acts / labels padded to B rows per step): every
+        step, short ones included, in the launch.  Same step / seed / Adam-count bookkeeping as
+        `run_native_epoch`; the sums run in another order, so results agree with it to fp32
+        rounding, not bitwise.  Returns the per-row losses."""
         ex = self._resident_executor(slot, B)
         n = acts.shape[0]
         loss = torch.empty(n, device=self.device)
-        fc, t, done = ex.run(acts, labels, loss, self.seed_base, self.fwd_count, slot.t)
+        fc, t, done = ex.run(acts, labels, loss, self.seed_base, self.fwd_count, slot.t, None, step_rows)
         self.fwd_count, slot.t = int(fc), int(t)
         self._pre = None
         if done < n:
@@ -489,16 +492,18 @@ class TailEngine:
             return False
         return self._hybrid_executor(slot, B).ok()
 
-    def run_hybrid_epoch(self, acts: torch.Tensor, labels: torch.Tensor, slot: OptSlot, B: int) -> torch.Tensor:
+    def run_hybrid_epoch(self, acts: torch.Tensor, labels: torch.Tensor, slot: OptSlot, B: int,
+                         step_rows=None) -> torch.Tensor:
         """One epoch over `acts` / `labels` with every full batch in ONE persistent launch that
         keeps fc2 / fc3 and the biases on-chip and streams fc1 (csrc/hybrid.hip); a trailing
-        partial batch runs on the launch-per-stage executor.  Same step / seed / Adam-count
-        bookkeeping as `run_native_epoch`; the sums run in another order, so results agree
-        with it to fp32 rounding, not bitwise.  Returns the per-row losses."""
+        partial batch runs on the launch-per-stage executor.  `step_rows`: as
+        `run_resident_epoch`.  Same step / seed / Adam-count bookkeeping as `run_native_epoch`;
+        the sums run in another order, so results agree with it to fp32 rounding, not bitwise.
+        Returns the per-row losses."""
         ex = self._hybrid_executor(slot, B)
         n = acts.shape[0]
         loss = torch.empty(n, device=self.device)
-        fc, t, done = ex.run(acts, labels, loss, self.seed_base, self.fwd_count, slot.t)
+        fc, t, done = ex.run(acts, labels, loss, self.seed_base, self.fwd_count, slot.t, None, None, 0, step_rows)
         self.fwd_count, slot.t = int(fc), int(t)
         self._pre = None
         if done < n:
@@ -561,6 +566,39 @@ class TailEngine:
         self.fwd_count, slot.t = buf["counters"]
         self._pre = None
         self.acts, self.dz, self._wg = [], [], []
+
+    @staticmethod
+    def padded_plan(caches, B: int, ignore: int = -100):
+        """One server epoch over several clients' cached (acts, labels), in order, as one
+        persistent-launch input: every client's batches of B rows, its short final batch
+        zero-padded to B rows with ignored labels.  Returns (acts [S B, K], labels [S B],
+        step_rows [S]); the persistent kernels take each step's CE mean over its real rows, and
+        a padded row adds exact zeros to every gradient, so the steps are the reference's
+        (data_entities_vanilla_sisa.py:298-313: `for cid: for batch in cid's loader: step`).
+        A single client with whole batches is returned as is (no copy)."""
+        rows = []
+        for a, y in caches:
+            n = int(y.numel())
+            rows += [B] * (n // B) + ([n % B] if n % B else [])
+        if len(caches) == 1 and caches[0][1].numel() % B == 0:
+            a, y = caches[0]
+            return a, y, rows
+        S = len(rows)
+        a0 = caches[0][0]
+        X = torch.zeros(S * B, a0.shape[1], device=a0.device, dtype=a0.dtype)
+        Y = torch.full((S * B,), ignore, device=a0.device, dtype=torch.int64)
+        s = 0
+        for a, y in caches:
+            n = int(y.numel())
+            full = n - n % B
+            X[s * B:s * B + full] = a[:full]
+            Y[s * B:s * B + full] = y[:full]
+            s += full // B
+            if n % B:
+                X[s * B:s * B + n % B] = a[full:]
+                Y[s * B:s * B + n % B] = y[full:]
+                s += 1
+        return X, Y, rows
 
     # ------------------------------------------------------------------ TP emulation
     @staticmethod

@@ -303,7 +303,7 @@ class SisaSession(Session):
         self.resident_status = {"executor": kind, "reason": why, "adopted": kind == "resident"}
         return kind == "resident"
 
-    def _persistent_epoch(self, acts, labels) -> bool:
+    def _persistent_epoch(self, acts, labels, step_rows=None) -> bool:
         """One client epoch on the adopted persistent executor, made un-killable: the shard's
         weights / optimizer state / counters are copied first (`TailEngine.snapshot_state`);
         if the launch's in-launch waits gave up on ANY Bob rank (a hand-off timeout, the peer-
@@ -321,7 +321,7 @@ class SisaSession(Session):
             self._failsafe = resident.Failsafe(self.tail, self.bob_slot, self.B, group=self.comm.tp_group,
                                                enabled=getattr(self.args, "persistent_failsafe", "on") != "off")
         fs = self._failsafe
-        if fs.run(self.server_executor, acts, labels):
+        if fs.run(self.server_executor, acts, labels, step_rows):
             return True
         self.server_executor = "launch_per_stage"
         st = getattr(self, "resident_status", None) or {}
@@ -380,17 +380,35 @@ class SisaSession(Session):
         self.switch_mode_to_train()
         samples = 0
         self.prefetch_activations(unlearn_request_from_alices, unlearn_id)
+        plan = None
         for _ in _progress(range(self.args.server_epochs), self.show, desc="Epochs", ascii=" >="):
+            caches = []
             for cid in range(1, self.k + 1):
                 if cid in unlearn_request_from_alices:
-                    got = self.get_activation_and_labels(cid, unlearned=True, unlearn_id=unlearn_id)
+                    caches.append(self.get_activation_and_labels(cid, unlearned=True, unlearn_id=unlearn_id))
                 else:
-                    got = self.get_activation_and_labels(cid, unlearned=False)
-                if self.is_bob:
-                    acts, labels = got
-                    with self.tracer.gpu_span(f"server_epoch[alice{cid}]", samples=int(labels.numel())):
-                        self.server_epoch(acts, labels)
-                    samples += labels.numel()
+                    caches.append(self.get_activation_and_labels(cid, unlearned=False))
+            if not self.is_bob:
+                continue
+            n_all = sum(int(c[1].numel()) for c in caches)
+            if (self._use_resident() or self._use_hybrid()) and n_all > 0:
+                # the whole server epoch, every client's batches in order (short final batches
+                # included), as ONE persistent-executor call: one launch (or a few, past the 2 GB
+                # input offsets) instead of one per client plus a launch-per-stage tail batch each
+                if plan is None:
+                    cs = [(a if a.dtype == torch.float32 else a.float(), y) for a, y in caches]
+                    plan = self.tail.padded_plan(cs, self.B)
+                X, Y, rows = plan
+                with self.tracer.gpu_span("server_epoch[all]", samples=n_all):
+                    ok = self._persistent_epoch(X.contiguous(), Y.contiguous(), rows)
+                self.comm.progress()
+                if ok:
+                    samples += n_all
+                    continue
+            for cid, (acts, labels) in enumerate(caches, 1):
+                with self.tracer.gpu_span(f"server_epoch[alice{cid}]", samples=int(labels.numel())):
+                    self.server_epoch(acts, labels)
+                samples += labels.numel()
         self.bob_log.info("Global training completed.")
         self.comm.barrier()
         return samples

@@ -127,3 +127,18 @@ def test_bf16_compute_rule_torch_ops():
     torch.testing.assert_close(dw, r(dz).t() @ r(x))
     torch.testing.assert_close(db, r(dz).sum(0))
     assert not torch.allclose(y, x @ w.t() + b, rtol=1e-5, atol=1e-5)
+
+
+def test_padded_plan_layout():
+    """`TailEngine.padded_plan`: each client's whole batches in order, its short final batch
+    zero-padded to B rows with ignored labels; a single whole-batch client is passed through."""
+    import torch
+    from splitlearning_amd.engine.tail import TailEngine
+    a1, y1 = torch.arange(5 * 3, dtype=torch.float32).view(5, 3), torch.arange(5)
+    a2, y2 = -torch.ones(4, 3), torch.full((4,), 7)
+    X, Y, rows = TailEngine.padded_plan([(a1, y1), (a2, y2)], 2)
+    assert rows == [2, 2, 1, 2, 2] and X.shape == (10, 3)
+    assert torch.equal(X[:5], a1) and torch.equal(X[5], torch.zeros(3)) and torch.equal(X[6:], a2)
+    assert Y.tolist() == [0, 1, 2, 3, 4, -100, 7, 7, 7, 7]
+    X1, Y1, r1 = TailEngine.padded_plan([(a2, y2)], 2)
+    assert X1 is a2 and Y1 is y2 and r1 == [2, 2]
