@@ -358,9 +358,11 @@ def test_resident_mid_epoch_failure_rolls_back_to_launch_per_stage(cuda, monkeyp
 def test_whole_server_epoch_with_short_batches_in_one_launch(cuda, kind, n1):
     """One server epoch over three clients' caches with short final batches (50, 37, 64 rows at
     B = 16) as ONE persistent call (`TailEngine.padded_plan`: every short batch zero-padded
-    with ignored labels, its CE mean over its real rows) against torch replaying the
-    reference loop `for cid: for batch in cid's cached batches: step`
-    (data_entities_vanilla_sisa.py:298-313), partial batches as themselves."""
+    with ignored labels, its CE mean over its real rows).  Every step of the plan, launched on
+    its own from torch's synced state, matches torch replaying the reference loop
+    `for cid: for batch in cid's cached batches: step` (data_entities_vanilla_sisa.py:298-313)
+    on the batch's real rows; and the whole plan in one call is bitwise those per-step launches
+    (an unsynced 11-step Adam comparison would only measure how fast fp32 rounding amplifies)."""
     B, lr, seed_base = 16, 1e-3, 3
     spec = _spec(n1=n1, p=0.5)
     g = torch.Generator().manual_seed(11)
@@ -369,32 +371,44 @@ def test_whole_server_epoch_with_short_batches_in_one_launch(cuda, kind, n1):
         caches.append(((torch.rand(n, 5408, generator=g) * 20).to(cuda), torch.randint(0, 100, (n,), generator=g).to(cuda)))
     torch.manual_seed(18)
     base = _MLP(spec)
-    te, slot = _engine(base, spec, cuda, seed_base, f"#plan{kind}")
-    assert (te.resident_ok(slot, B) if kind == "resident" else te.hybrid_ok(slot, B))
     X, Y, rows = TailEngine.padded_plan(caches, B)
     assert rows == [16, 16, 16, 2, 16, 16, 5, 16, 16, 16, 16] and X.shape[0] == 16 * len(rows)
-    run = te.run_resident_epoch if kind == "resident" else te.run_hybrid_epoch
-    loss = run(X, Y, slot, B, rows)
-    torch.cuda.synchronize()
-    assert (te.fwd_count, slot.t) == (len(rows), len(rows))
+    # per step, each from torch's synced state
+    te, slot = _engine(base, spec, cuda, seed_base, f"#plan{kind}a")
+    assert (te.resident_ok(slot, B) if kind == "resident" else te.hybrid_ok(slot, B))
+    ex = te._resident_executor(slot, B) if kind == "resident" else te._hybrid_executor(slot, B)
     ref = copy.deepcopy(base).to(cuda)
     opt = torch.optim.Adam(ref.parameters(), lr=lr, weight_decay=1e-5)
-    step, got, want = 0, [], []
-    for (a, y) in caches:
-        for s in range(0, y.numel(), B):
-            x, yy = a[s:s + B], y[s:s + B]
-            step += 1
-            opt.zero_grad()
-            lr_ = F.cross_entropy(_ref_forward(ref, x, seed_base, step), yy, reduction="none")
-            lr_.mean().backward()
-            opt.step()
-            want.append(lr_.detach())
-            got.append(loss[(step - 1) * B:(step - 1) * B + yy.numel()])
-            assert torch.all(loss[(step - 1) * B + yy.numel():step * B] == 0), "padded rows carry no loss"
-    torch.testing.assert_close(torch.cat(got), torch.cat(want), rtol=1e-3, atol=1e-3)
-    for name, p in ref.named_parameters():
-        L = te.layers[int(name[2]) - 1]
-        e = L.W if name.endswith("weight") else L.b
-        d = (e - p.detach()).abs()
-        assert d.max().item() <= 2 * lr * step + 1e-6, (name, d.max().item())
-        assert (d > 1e-4).float().mean().item() < 1e-3, (name, (d > 1e-4).float().mean().item())
+    per_step = []
+    for i, r in enumerate(rows):
+        x, y = X[i * B:(i + 1) * B], Y[i * B:(i + 1) * B]
+        assert torch.all(y[r:] == -100) and torch.all(x[r:] == 0)
+        _sync_torch(ref, opt, te, slot, i)
+        opt.zero_grad()
+        loss_r = F.cross_entropy(_ref_forward(ref, x[:r], seed_base, i + 1), y[:r], reduction="none")
+        loss_r.mean().backward()
+        opt.step()
+        loss_e = torch.empty(B, device=cuda)
+        fc, t, done = ex.run(x.contiguous(), y.contiguous(), loss_e, seed_base, te.fwd_count, slot.t, step_rows=[r])
+        te.fwd_count, slot.t = int(fc), int(t)
+        assert done == B
+        per_step.append(loss_e)
+        assert torch.all(loss_e[r:] == 0), "padded rows carry no loss"
+        torch.testing.assert_close(loss_e[:r], loss_r.detach(), rtol=2e-4, atol=1e-4, msg=f"step {i} loss")
+        for name, p in ref.named_parameters():
+            L = te.layers[int(name[2]) - 1]
+            e = L.W if name.endswith("weight") else L.b
+            d = (e - p.detach()).abs()
+            assert d.max().item() <= 2 * lr + 1e-6, (i, name, d.max().item())
+            # Adam's first steps move a near-zero-gradient entry by about +-lr whichever way its
+            # fp32 gradient rounds: a few such entries per tensor, however small the tensor
+            assert (d > 1e-6).sum().item() <= max(2, 1e-4 * d.numel()), (i, name, (d > 1e-6).sum().item())
+    # the whole plan in one call
+    tw, sw = _engine(base, spec, cuda, seed_base, f"#plan{kind}b")
+    run = tw.run_resident_epoch if kind == "resident" else tw.run_hybrid_epoch
+    loss = run(X, Y, sw, B, rows)
+    torch.cuda.synchronize()
+    assert (tw.fwd_count, sw.t) == (len(rows), len(rows))
+    assert torch.equal(loss, torch.cat(per_step))
+    for La, Lb in zip(te.layers, tw.layers):
+        assert torch.equal(La.W, Lb.W) and torch.equal(La.b, Lb.b)
