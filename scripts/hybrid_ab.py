@@ -68,6 +68,15 @@ def critical_path(tp, ta, G):
     mn, md, mx = (statistics.mean(r[i] for r in slen) for i in range(3))
     print(f"tp={tp}   stream length min / median / max {mn:.2f} / {md:.2f} / {mx:.2f}; step (last stream end to "
           f"last stream end) {statistics.mean(spread):.2f}", flush=True)
+    # where the slow streams are: by w % 8 (the XCD under round-robin dispatch) and by w // 32
+    d = (ta[:-1, :, 13] - ta[:-1, :, 12]).mean(0)
+    e = (ta[:-1, :, 13] - ta[:-1, :, 13].max(1, keepdim=True).values).mean(0)
+    print(f"tp={tp}   stream length by w % 8: " + " ".join(f"{d[x::8].mean().item():6.2f}" for x in range(8)), flush=True)
+    print(f"tp={tp}   stream length by w // 32: " + " ".join(f"{d[32 * x:32 * x + 32].mean().item():6.2f}"
+                                                       for x in range((G + 31) // 32)), flush=True)
+    print(f"tp={tp}   stream end - last end by w % 8: " + " ".join(f"{e[x::8].mean().item():6.2f}" for x in range(8)), flush=True)
+    os.makedirs("gpurun_out", exist_ok=True)
+    torch.save(ta.float(), f"gpurun_out/hybrid_tall_tp{tp}.pt")
 
 
 def main():
