@@ -1,7 +1,9 @@
 """Is the co-located U-shape epoch bound by the host's launch issue or by the GPU?  Times one
 native split epoch (`_C.SplitEpoch.run`, csrc/split.cpp) twice: the host returns once every
 launch is issued (t_issue), the GPU finishes at the synchronize (t_done).  t_issue ~ t_done:
-the GPU waits on the host.  Usage: python scripts/ushape_host_probe.py [variant20]"""
+the GPU waits on the host.  Usage: python scripts/ushape_host_probe.py [variant20] [ushape|vanilla]
+(variant 20 selected the fused U-shape middle + head launch of an A/B that was removed:
+profiles/r5w_misc/ushape_fused_mid_head_ab.txt)."""
 import os
 import sys
 import tempfile

@@ -37,6 +37,7 @@ struct WgGroup {
   int wt;               // write-through (sc1) W/m/v stores (set by wgrad_group)
   int bf16;             // bf16 compute: dZ / A / look-ahead operands rounded to bf16 (set by wgrad_group)
   int afirst;           // load the first chunk's A / dZ before W / m / v (set by wgrad_group)
+  int pol;              // W / state load and store cache policy preset (set by wgrad_group; variant 21)
 };
 
 int head3_slices(int N2);

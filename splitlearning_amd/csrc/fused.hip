@@ -355,6 +355,33 @@ __device__ __forceinline__ void st_wt(float* base, int N, int ld, int boff, f32x
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), rs, boff, 0, 16);
 }
 
+// Per-array cache-policy presets of the W / m / v stream (grp.pol, variant 21; buffer aux bits
+// 0 plain, 2 non-temporal, 16 write-through): {W load, state load, W store, state store}.
+// Preset 0 is the shipped form (plain loads, write-through stores).
+__device__ __forceinline__ f32x4 ld_pol(const float* base, int bytes, int boff, int aux) {
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, bytes, 0x00020000);
+  if (aux == 2) return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, boff, 0, 2));
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, boff, 0, 0));
+}
+__device__ __forceinline__ void st_pol(float* base, int bytes, int boff, f32x4 v, int aux) {
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, bytes, 0x00020000);
+  if (aux == 2) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), rs, boff, 0, 2);
+  else if (aux == 16) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), rs, boff, 0, 16);
+  else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), rs, boff, 0, 0);
+}
+__device__ __forceinline__ void pol_aux(int pol, int& lw, int& ls, int& sw, int& ss) {
+  switch (pol) {
+    case 1: lw = 0; ls = 2; sw = 0; ss = 2; break;     // the hybrid's over-the-cache form
+    case 2: lw = 2; ls = 2; sw = 2; ss = 2; break;     // all non-temporal
+    case 3: lw = 0; ls = 0; sw = 0; ss = 0; break;     // all plain
+    case 4: lw = 0; ls = 2; sw = 16; ss = 16; break;   // nt state loads, write-through stores
+    case 5: lw = 0; ls = 0; sw = 0; ss = 16; break;    // W plain, state write-through
+    default: lw = 0; ls = 0; sw = 16; ss = 16; break;  // shipped (cache-resident state)
+  }
+}
+
 template <bool ADAM, int FWDC, bool BF = false>
 __global__ void __launch_bounds__(1024)
 wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
@@ -393,10 +420,19 @@ wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
     if (tid < 256 && (tid >> 4) < M && n0 + (tid & 15) < L.N) dzv0 = L.dz[(int64_t)(tid >> 4) * L.ldz + n0 + (tid & 15)];
   }
   f32x4 p = zv, q0 = zv, q1 = zv;
+  int plw = 0, pls = 0, psw = 16, pss = 16;
+  pol_aux(grp.pol, plw, pls, psw, pss);
+  const int lbytes = L.N * L.ldw * 4;   // grp.pol != 0 only for layers under 2 GB
   if (act) {
-    p = *reinterpret_cast<const f32x4*>(L.W + off);
-    q0 = *reinterpret_cast<const f32x4*>(L.s0 + off);
-    if (ADAM) q1 = *reinterpret_cast<const f32x4*>(L.s1 + off);
+    if (grp.pol == 0) {
+      p = *reinterpret_cast<const f32x4*>(L.W + off);
+      q0 = *reinterpret_cast<const f32x4*>(L.s0 + off);
+      if (ADAM) q1 = *reinterpret_cast<const f32x4*>(L.s1 + off);
+    } else {
+      p = ld_pol(L.W, lbytes, (int)(off * 4), plw);
+      q0 = ld_pol(L.s0, lbytes, (int)(off * 4), pls);
+      if (ADAM) q1 = ld_pol(L.s1, lbytes, (int)(off * 4), pls);
+    }
   }
   // look-ahead A operand in MFMA layout: lane (li, lq) holds x_next[li][kb + 16*wave + 4*lq .. +3]
   const int li = lane & 15, lq = lane >> 4;
@@ -463,7 +499,12 @@ wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
   }
   if (act) {
     sl_opt_update4<ADAM>(o, p, g, q0, q1);
-    if (grp.wt) {
+    if (grp.pol != 0) {
+      const int boff = (int)(off * 4);
+      if (o.kind != 0) st_pol(L.W, lbytes, boff, p, psw);
+      st_pol(L.s0, lbytes, boff, q0, pss);
+      if (ADAM) st_pol(L.s1, lbytes, boff, q1, pss);
+    } else if (grp.wt) {
       const int boff = (int)(off * 4);
       if (o.kind != 0) st_wt(L.W, L.N, L.ldw, boff, p);
       st_wt(L.s0, L.N, L.ldw, boff, q0);
@@ -574,6 +615,15 @@ static void set_traversal(WgGroup& gg) {
   gg.bf16 = g_bf16;
   for (int i = 0; i < gg.n; ++i)
     if ((int64_t)gg.d[i].N * gg.d[i].ldw * 4 > 2147483647LL) gg.wt = 0;
+  // a layer-0 stream larger than the 256 MB Infinity Cache (concat's fc1, SISA's TP = 1 fc1 on
+  // launch-per-stage) takes the hybrid's over-the-cache policy: W plain both ways (it stays
+  // cached from one step to the next), the optimizer state non-temporal both ways.  ws = 9
+  // concat on one GPU 88.1-88.4 k -> 90.0 k; vanilla and U-shape, whose state fits, are
+  // fastest as shipped (profiles/r5w_misc/wgrad_group_cache_policy_ab.txt).  Variant 21 forces
+  // a preset (pol_aux; 6 = the shipped one).
+  const int64_t st0 = (int64_t)gg.d[0].N * gg.d[0].ldw * 4 * (gg.d[0].s1 ? 3 : 2);
+  const int v21 = g_variant[21];
+  gg.pol = !gg.wt ? 0 : (v21 == 6 ? 0 : (v21 != 0 ? v21 : (st0 > (256ll << 20) ? 1 : 0)));
 }
 
 hipError_t wgrad_group(const WgGroup& g, int M, SlOpt o, hipStream_t st) {

@@ -95,13 +95,14 @@ __device__ __forceinline__ void hy_arrive(const HyArgs& a, int idx) {
 }
 
 // the 8 shards of a seam (shard s receives shard_n[seam][s] arrivals per step)
-__device__ __forceinline__ bool hy_seam_wait(const HyArgs& a, int seam, unsigned mult, int* s_ok) {
+// (s_sn: a.shard_n staged in LDS at the start, so the poll's target costs no global round trip)
+__device__ __forceinline__ bool hy_seam_wait(const HyArgs& a, int seam, unsigned mult, int* s_ok, const int* s_sn) {
   int idx[8];
   unsigned tgt[8];
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
     idx[s] = hy_seam(seam, s);
-    tgt[s] = mult * (unsigned)a.shard_n[seam * 8 + s];
+    tgt[s] = mult * (unsigned)s_sn[seam * 8 + s];
   }
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
@@ -169,7 +170,11 @@ constexpr int OFF_B2 = OFF_B3 + 3 * kHyMaxC * 4;       // b2 {W, m, v}[4]
 constexpr int OFF_B1 = OFF_B2 + 64;                    // b1 {W, m, v}[kHyRuns][16]
 constexpr int OFF_DZ1 = OFF_B1 + kHyRuns * 3 * 16 * 4; // dz1 [kHyRuns][16 m][16 rows]
 constexpr int OFF_OK = OFF_DZ1 + kHyRuns * 256 * 4;    // ints
-constexpr int kHyLds = OFF_OK + 64;
+// per-workgroup tile-table values the step loop needs, read from LDS instead of a global
+// round trip on the critical path: the arrival counts of the F slice's row blocks [32] and
+// this run's slots in its row blocks' partial lists [kHyRuns]
+constexpr int OFF_TABC = OFF_OK + 64;
+constexpr int kHyLds = OFF_TABC + (32 + kHyRuns + kHySeams * 8) * 4 + 4;
 static_assert(kHyLds <= 160 * 1024, "LDS");
 static_assert(kHyThreads / 64 * 10 * 256 >= kHyMaxWR * 4 * kHyMaxWC4, "10 W2 16 x 16 blocks per wave");
 
@@ -217,6 +222,9 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
   float* sb1 = reinterpret_cast<float*>(smem + OFF_B1);
   float* sdz1 = reinterpret_cast<float*>(smem + OFF_DZ1);
   int* s_ok = reinterpret_cast<int*>(smem + OFF_OK);
+  int* s_fns = reinterpret_cast<int*>(smem + OFF_TABC);        // [32]: ns of row block rlo + j
+  int* s_slot = s_fns + 32;                                     // [kHyRuns]: w - first toucher
+  int* s_sn = s_slot + kHyRuns;                                 // [kHySeams * 8]: a.shard_n
   constexpr int MC = kHyMaxC;
   const f32x4 zv = {0.f, 0.f, 0.f, 0.f};
 
@@ -290,6 +298,12 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
       sb2[4 + tid] = a.L2.mb[n];
       sb2[8 + tid] = ADAM ? a.L2.vb[n] : 0.f;
     }
+    if (tid < 32) {
+      const int rb = (c0 >> 4) + tid;
+      s_fns[tid] = rb <= ((c0 + WC - 1) >> 4) && rb < a.nrb ? a.tab[a.G + 1 + a.nrb + rb] : 0;
+    }
+    if (tid < kHyRuns) s_slot[tid] = tid < nruns ? w - a.tab[a.G + 1 + rbA + tid] : -1;
+    if (tid < kHySeams * 8) s_sn[tid] = a.shard_n[tid];
     if (tid < 16 * kHyRuns) {
       const int k = tid >> 4, j = tid & 15;
       const int rb = rbA + k, n = 16 * rb + j;
@@ -481,7 +495,7 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
       // (row nn, rows m = 4 mg ..): the waves' accumulators are already in that layout
       for (int e = tid; e < nruns * 64; e += kHyThreads) {
         const int k = e >> 6, nn = (e >> 2) & 15, mg = e & 3;
-        const int rb = rbA + k, slot = w - a.tab[a.G + 1 + rb], n = 16 * rb + nn;
+        const int rb = rbA + k, slot = s_slot[k], n = 16 * rb + nn;
         f32x4 parts[8];
         if (k == nruns - 1) {
 #pragma unroll
@@ -530,7 +544,7 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
         const int rb = rlo + lane;
         // fault injection (tests): at step fault_step this wait cannot be met, times out (err 2)
         // and every other wait gives up, as a hand-off that never arrives would make them
-        const unsigned tg = i == a.fault_step ? 0xffffffffu : (unsigned)(i + 1) * (unsigned)a.tab[a.G + 1 + a.nrb + rb];
+        const unsigned tg = i == a.fault_step ? 0xffffffffu : (unsigned)(i + 1) * (unsigned)s_fns[lane];
         ok = hy_spin(a, hy_cnt(a, hy_R(rb)), tg);
       }
       ok = __all(ok);
@@ -552,7 +566,7 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
           f32x4 v = zv;
           if (kc < WC) {
             const int n = c0 + kc, rb = n >> 4, nn = n & 15;
-            const int ns = a.tab[a.G + 1 + a.nrb + rb];
+            const int ns = s_fns[rb - (c0 >> 4)];
             f32x4 parts[kHySlots];
 #pragma unroll
             for (int sl = 0; sl < kHySlots; ++sl)
@@ -595,7 +609,7 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
 
     // ================= H: P2 of the head rows, h2, logit partials
     if (head) {
-      if (!hy_seam_wait(a, 0, (unsigned)(i + 1), s_ok)) break;
+      if (!hy_seam_wait(a, 0, (unsigned)(i + 1), s_ok, s_sn)) break;
       HY_MARK(3);
       {
         // partial cq of fc2 row 4 w + ii, rows m = 4 mg .. (FP is [NC][N2][16])
@@ -675,7 +689,7 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
 
     // ================= S: row m's logits, softmax-CE, dlogits (workgroups m < M)
     if (w < M) {
-      if (!hy_seam_wait(a, 1, (unsigned)(i + 1), s_ok)) break;
+      if (!hy_seam_wait(a, 1, (unsigned)(i + 1), s_ok, s_sn)) break;
       HY_MARK(5);
       const int m = w;
       const int nc4 = C4 >> 2;
@@ -745,7 +759,7 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
 
     // ================= H2: dz2 of the head rows; b3 / W3 / b2 steps
     if (head) {
-      if (!hy_seam_wait(a, 2, (unsigned)(i + 1), s_ok)) break;
+      if (!hy_seam_wait(a, 2, (unsigned)(i + 1), s_ok, s_sn)) break;
       HY_MARK(7);
       {
         HY_IDX();
@@ -804,7 +818,7 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
     }
 
     // ================= B: the tile's dz1 partial, then W2's step
-    if (!hy_seam_wait(a, 3, (unsigned)(i + 1), s_ok)) break;
+    if (!hy_seam_wait(a, 3, (unsigned)(i + 1), s_ok, s_sn)) break;
     HY_MARK(9);
     {
       HY_IDX();
@@ -922,7 +936,7 @@ __global__ void __launch_bounds__(kHyThreads) hybrid_epoch_kernel(HyArgs a) {
       if (tid < 16 * nruns) {
         const int k = tid >> 4, jj = tid & 15;
         const int rb = rbA + k;
-        if (a.tab[a.G + 1 + rb] == w && 16 * rb + jj < N1) {
+        if (s_slot[k] == 0 && 16 * rb + jj < N1) {
           float g = 0.f;
 #pragma unroll
           for (int m = 0; m < 16; ++m) g += sdz1[k * 256 + m * 16 + jj];

@@ -57,7 +57,11 @@ class IpcChannel {
   std::string handle() const;
   void open(const std::vector<std::string>& handles);
   // n floats from x (16-B aligned, n % 4 == 0, n <= cap) to / from rank `peer`, on stream st.
-  // Stream-ordered; every call of a pair advances that pair's generation on both sides.
+  // Stream-ordered; every call of a pair advances that pair's generation on both sides.  All
+  // sends to one peer must be issued on ONE stream, and all receives from one peer on one
+  // stream: a chunk beyond the previous message's chunk count waits on chunk 0's ack, which
+  // is only ordered after that message's receive if the receives are stream-ordered.  The
+  // first call binds the stream; a call on another stream throws.
   void send(const float* x, int64_t n, int peer, hipStream_t st);
   void recv(float* x, int64_t n, int peer, hipStream_t st);
   bool serves(const void* p, int64_t n) const {
@@ -93,6 +97,10 @@ class IpcChannel {
   std::vector<void*> mapped_;
   std::vector<uint32_t> send_gen_, recv_gen_;
   std::vector<int> hist_;      // [peer][parity]: chunk count of the last message sent on it
+  std::vector<hipStream_t> send_st_, recv_st_;   // the stream bound per peer (first call)
+  std::vector<char> send_bound_, recv_bound_;
+  void bind_stream(std::vector<hipStream_t>& sts, std::vector<char>& bound, int peer, hipStream_t st,
+                   const char* what);
   bool opened_ = false;
   int64_t timeout_ = 0;
   int clock_khz_ = 100000;

@@ -155,9 +155,25 @@ void IpcChannel::check(const void* x, int64_t n, int peer) const {
                              " floats (needs n % 4 == 0, n <= cap, a 16-B aligned buffer)");
 }
 
+void IpcChannel::bind_stream(std::vector<hipStream_t>& sts, std::vector<char>& bound, int peer, hipStream_t st,
+                             const char* what) {
+  if (sts.size() < (size_t)nranks_) {
+    sts.assign(nranks_, nullptr);
+    bound.assign(nranks_, 0);
+  }
+  if (!bound[peer]) {
+    bound[peer] = 1;
+    sts[peer] = st;
+  } else if (sts[peer] != st) {
+    throw std::runtime_error(std::string("IpcChannel.") + what + ": every message of a pair must be issued on one "
+                             "stream (the per-chunk acks are ordered by it)");
+  }
+}
+
 void IpcChannel::send(const float* x, int64_t n, int peer, hipStream_t st) {
   if (n == 0) return;
   check(x, n, peer);
+  bind_stream(send_st_, send_bound_, peer, st, "send");
   const uint32_t g = ++send_gen_[peer];
   const int par = (int)(g & 1u);
   const int chunks = (int)((n + kIpcChunk - 1) / kIpcChunk);
@@ -172,6 +188,7 @@ void IpcChannel::send(const float* x, int64_t n, int peer, hipStream_t st) {
 void IpcChannel::recv(float* x, int64_t n, int peer, hipStream_t st) {
   if (n == 0) return;
   check(x, n, peer);
+  bind_stream(recv_st_, recv_bound_, peer, st, "recv");
   const uint32_t g = ++recv_gen_[peer];
   const int par = (int)(g & 1u);
   const int chunks = (int)((n + kIpcChunk - 1) / kIpcChunk);

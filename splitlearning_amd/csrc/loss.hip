@@ -8,7 +8,6 @@
 // SURVEY §2.7 K9, K10.  One wave64 per row; all reductions are in-register
 // shuffles, no LDS.
 #include "common.h"
-#include "head_core.h"
 
 namespace sl {
 
@@ -258,8 +257,12 @@ head_step_kernel(const float* __restrict__ X, const float* __restrict__ W, const
 }
 
 // head_step_mfma_kernel: the same step for M <= 16 rows, C <= 16 classes, K <= 128 (% 4)
-// features -- the U-shape head (16 x 100 -> 10) -- on exact-fp32 MFMA (head_core.h, shared
-// with the fused U-shape middle + head launch of ushape.hip).  One 256-thread workgroup.
+// features — the U-shape head (16 x 100 -> 10) — with its three products on exact-fp32 MFMA
+// (v_mfma_f32_16x16x4f32, 16 x 16 tiles) instead of per-thread FMA chains: logits (wave 0,
+// K / 4 steps), data gradient (one 16-column tile of K per wave step, C padded to 16) and
+// weight gradient (M = 16 as the reduction), the softmax-CE on DPP row reductions over the
+// 16 class lanes of each row.  bf16 compute is a template parameter.  One 256-thread
+// workgroup; the optimizer update keeps head_step_kernel's thread mapping (state loads first).
 template <bool BF>
 __global__ void __launch_bounds__(256)
 head_step_mfma_kernel(const float* __restrict__ X, const float* __restrict__ W, const float* __restrict__ bias,
@@ -267,11 +270,128 @@ head_step_mfma_kernel(const float* __restrict__ X, const float* __restrict__ W, 
                       float* __restrict__ dX, float* __restrict__ Wout, float* __restrict__ bout,
                       float* __restrict__ s0w, float* __restrict__ s1w, float* __restrict__ s0b,
                       float* __restrict__ s1b, int M, int K, int C, SlOpt o, int mask_dx) {
-  __shared__ __attribute__((aligned(16))) HeadLds L;
-  HeadPre P;
-  head_preload(P, W, bias, s0w, s1w, s0b, s1b, K, C);
-  head_core<BF>(L, P, false, X, bias, y, ignore, scale, loss_rows, dX, Wout, bout, s0w, s1w, s0b, s1b, M, K, C, o,
-                mask_dx);
+  constexpr int KP = 132;                      // padded LDS row (K <= 128)
+  __shared__ __attribute__((aligned(16))) float sx[16][KP];
+  __shared__ __attribute__((aligned(16))) float sw[16][KP];
+  __shared__ __attribute__((aligned(16))) float sg[16][KP];    // dW [C][K]
+  __shared__ float sd[16][17];                 // dlogits [M][C]
+  auto R = [](float v) { return BF ? bfr(v) : v; };
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, li = lane & 15, lq = lane >> 4;
+  constexpr int PF = 8;                        // state elements per thread (C K <= 2048)
+  float r0[PF], r1[PF];
+#pragma unroll
+  for (int j = 0; j < PF; ++j) {
+    const int i = tid + 256 * j;
+    r0[j] = i < C * K ? s0w[i] : 0.f;
+    r1[j] = (i < C * K && s1w) ? s1w[i] : 0.f;
+  }
+  float rb0 = 0.f, rb1 = 0.f, rbp = 0.f;
+  if (bias && tid < C) {
+    rbp = bias[tid];
+    rb0 = s0b[tid];
+    rb1 = s1b ? s1b[tid] : 0.f;
+  }
+  // operands into LDS, zero-padded to 16 rows and 16-column tiles: every float4 load of X and
+  // W is issued before anything is stored (one memory round trip), the zero fill meanwhile
+  const int K4 = K >> 2;
+  f32x4 xr[2], wr[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int f = tid + 256 * j, r = f / K4, q = f - r * K4;
+    const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+    xr[j] = r < M ? reinterpret_cast<const f32x4*>(X)[f] : z4;
+    wr[j] = r < C ? reinterpret_cast<const f32x4*>(W)[f] : z4;
+  }
+  for (int i = tid; i < 16 * KP; i += 256) {
+    (&sx[0][0])[i] = 0.f;
+    (&sw[0][0])[i] = 0.f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int f = tid + 256 * j, r = f / K4, q = f - r * K4;
+    if (r < 16) {
+      *reinterpret_cast<f32x4*>(&sx[r][4 * q]) = xr[j];
+      *reinterpret_cast<f32x4*>(&sw[r][4 * q]) = wr[j];
+    }
+  }
+  __syncthreads();
+  // logits D[m][c] = sum_k X[m][k] W[c][k] (wave 0): A lane (m = li, k = 4s + lq), B (k, c = li)
+  if (wv == 0) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int s4 = 0; s4 < K; s4 += 4)
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(R(sx[li][s4 + lq]), R(sw[li][s4 + lq]), acc, 0, 0, 0);
+    // lane (c = li, lq) holds rows m = 4 lq + r; softmax over the 16 class lanes of each row
+    const bool vc = li < C;
+    const float bc = (bias && vc) ? bias[li] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = 4 * lq + r;
+      const float z = vc ? acc[r] + bc : -INFINITY;
+      const float mx = sl_row16_max(z);
+      const float e = vc ? expf(z - mx) : 0.f;
+      const float se = sl_row16_sum(e);
+      float dl = 0.f;
+      if (m < M) {
+        const int64_t lab = y[m];
+        if (lab == ignore) {
+          if (li == 0) loss_rows[m] = 0.f;
+        } else {
+          const float zl = sl_dpp_pick(z, (int)lab);
+          if (li == 0) loss_rows[m] = mx + logf(se) - zl;
+          if (vc) dl = (e / se - (li == lab ? 1.f : 0.f)) * scale;
+        }
+      }
+      sd[m][li] = dl;
+    }
+  }
+  __syncthreads();
+  // data gradient dX[m][k] = sum_c dlog[m][c] W[c][k]: wave w takes 16-column tiles w, w+4, ..
+  for (int kt = wv; kt * 16 < K; kt += 4) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s4 = 0; s4 < 16; s4 += 4)
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(R(sd[li][s4 + lq]), R(sw[s4 + lq][16 * kt + li]), acc, 0, 0, 0);
+    const int k = 16 * kt + li;
+    if (k < K) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = 4 * lq + r;
+        if (m < M) dX[m * K + k] = (mask_dx && !(sx[m][k] > 0.f)) ? 0.f : acc[r];
+      }
+    }
+  }
+  // weight gradient dW[c][k] = sum_m dlog[m][c] X[m][k] -> LDS
+  for (int kt = wv; kt * 16 < K; kt += 4) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s4 = 0; s4 < 16; s4 += 4)
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(R(sd[s4 + lq][li]), R(sx[s4 + lq][16 * kt + li]), acc, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sg[4 * lq + r][16 * kt + li] = acc[r];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < PF; ++j) {
+    const int i = tid + 256 * j;
+    if (i < C * K) {
+      const int c = i / K, k = i - c * K;
+      float pp = sw[c][k], a0 = r0[j], a1 = r1[j];
+      sl_opt_update(o, pp, sg[c][k], a0, a1);
+      if (o.kind != 0) Wout[i] = pp;
+      s0w[i] = a0;
+      if (s1w) s1w[i] = a1;
+    }
+  }
+  if (bias && tid < C) {
+    float g = 0.f;
+    for (int m = 0; m < M; ++m) g += sd[m][tid];
+    float pp = rbp, a0 = rb0, a1 = rb1;
+    sl_opt_update(o, pp, g, a0, a1);
+    if (o.kind != 0) bout[tid] = pp;
+    s0b[tid] = a0;
+    if (s1b) s1b[tid] = a1;
+  }
 }
 
 hipError_t head_step(const float* X, float* W, float* b, const int64_t* y, int64_t ignore, float scale,

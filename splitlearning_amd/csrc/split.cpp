@@ -51,7 +51,6 @@
 #include "fused.h"
 #include "host.h"
 #include "ipc_p2p.h"
-#include "ushape.h"
 
 namespace sl {
 hipError_t conv_fwd(const void* x, bool x_u8, const int64_t* idx, int64_t row0, int B, const float* w,
@@ -256,11 +255,6 @@ class SplitEpoch {
                   "SplitEpoch: the U-shape head needs B * 100 <= 4096 (B <= 40)");
     }
     if (!bob) return;
-    if (alice && mode_ == 2) {
-      // the fused middle + head launch's partials and arrival counter (ushape.hip)
-      mid_part_ = f32(sl::ushape_mid_part_floats((int)L_[0].w.p.size(0), (int)N2));
-      mid_cnt_ = at::zeros({1}, at::TensorOptions().dtype(at::kInt).device(dev));
-    }
     const int64_t S1 = (kCut + 255) / 256;
     pn_ = f32(S1 * B_ * N1);
     h1_ = f32((int64_t)B_ * N1);
@@ -510,48 +504,7 @@ class SplitEpoch {
   // step count (the head and the front share the tick of this batch).
   int64_t bob_ushape(const float* act, const int64_t* lab, int M, bool pre, int64_t t_a, hipStream_t st) {
     const int N1 = (int)L_[0].w.p.size(0), N2 = (int)L_[1].w.p.size(0), C = (int)hw_.p.size(0);
-    const Epi e1 = sl::make_epi_raw(L_[0].b.p.data_ptr<float>(), true, 0.0, 0, 0, nullptr);
-    // (variant 20 = 1: the three launches, for A/B)
-    if (mid_cnt_.defined() && sl::g_variant[20] == 0 && sl::ushape_mid_ok(M, N1, N2, C)) {
-      // one launch for the fc1 epilogue, fc2 forward and Alice's head step (ushape.hip; the
-      // same bits as the three launches below)
-      if (!pre) fc1(act, M, e1, false, st);
-      ++t_a;
-      sl::MidArgs m{};
-      m.pn = pre ? pn_.data_ptr<float>() : nullptr;
-      m.S = (int)((kCut + 255) / 256);
-      m.slab = (int64_t)M * N1;
-      m.e1 = e1;
-      m.h1 = h1_.data_ptr<float>();
-      m.W2 = L_[1].w.p.data_ptr<float>();
-      m.e2 = sl::make_epi_raw(L_[1].b.p.data_ptr<float>(), true, 0.0, 0, 0, nullptr);
-      m.h2 = h2_.data_ptr<float>();
-      m.hw = hw_.p.data_ptr<float>();
-      m.hb = hb_.p.data_ptr<float>();
-      m.s0w = hw_.s0;
-      m.s1w = hw_.s1;
-      m.s0b = hb_.s0;
-      m.s1b = hb_.s1;
-      m.y = lab;
-      m.ignore = -100;
-      m.scale = (float)(1.0 / M);
-      m.loss_rows = loss_.data_ptr<float>();
-      m.dz2 = dz2_.data_ptr<float>();
-      m.o = fopt_.at(t_a);
-      m.part = mid_part_.data_ptr<float>();
-      m.cnt = reinterpret_cast<unsigned*>(mid_cnt_.data_ptr<int>());
-      m.M = M;
-      m.N1 = N1;
-      m.N2 = N2;
-      m.C = C;
-      ck(sl::ushape_mid(m, st), "U-shape middle + head");
-      ck(sl::linear_dgrad(dz2_.data_ptr<float>(), N2, L_[1].w.p.data_ptr<float>(), N1, h1_.data_ptr<float>(), N1,
-                          1.f, dz1_.data_ptr<float>(), N1, dgws_.data_ptr<float>(), dgws_.numel(), M, N2, N1, st),
-         "fc2 dgrad");
-      cut_grad(M, st);
-      return t_a;
-    }
-    fc1(act, M, e1, pre, st);
+    fc1(act, M, sl::make_epi_raw(L_[0].b.p.data_ptr<float>(), true, 0.0, 0, 0, nullptr), pre, st);
     ck(sl::linear_fwd(h1_.data_ptr<float>(), N1, L_[1].w.p.data_ptr<float>(), N1, h2_.data_ptr<float>(), N2, M, N2,
                       N1, sl::make_epi_raw(L_[1].b.p.data_ptr<float>(), true, 0.0, 0, 0, nullptr),
                       fwdws_.data_ptr<float>(), fwdws_.numel(), st),
@@ -615,7 +568,7 @@ class SplitEpoch {
   Opt fopt_, bopt_;
   std::vector<Layer> L_;
   at::Tensor act_[2], am_[2], lab_[2], slab_[2];
-  at::Tensor pn_, h1_, h2_, dz1_, dz2_, dx_, dlog_, loss_, fwdws_, p2ws_, dgws_, headws_, mid_part_, mid_cnt_;
+  at::Tensor pn_, h1_, h2_, dz1_, dz2_, dx_, dlog_, loss_, fwdws_, p2ws_, dgws_, headws_;
 };
 
 }  // namespace
