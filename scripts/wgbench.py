@@ -41,7 +41,13 @@ def main():
     ap.add_argument("--tps", type=int, nargs="+", default=[1, 2, 4, 8])
     ap.add_argument("--iters", type=int, default=100)
     ap.add_argument("--variant", action="append", default=[])
+    ap.add_argument("--case", choices=("tp", "ushape", "vanilla", "concat"), default="tp",
+                    help="tp: the SISA tail's shards; ushape: fc1 1000 x 5408 + fc2 100 x 1000 (Adam); "
+                         "vanilla: 5000 x 5408 / 1000 x 5000 / 100 x 1000 (SGD-momentum); concat: "
+                         "fc1 5000 x 43264 (k = 8, Adam)")
     a = ap.parse_args()
+    if a.case != "tp":
+        return other_case(a)
     C = H.C()
     for kv in a.variant:
         slot, val = (int(v) for v in kv.split("="))
@@ -89,6 +95,49 @@ def main():
               "group+la": 24 * (n_par + W2.numel() + W3.numel())}
         for k, us in res.items():
             print(f"tp={T} {k:9s} {us:8.2f} us  {gb[k] / us / 1e3:7.0f} GB/s", flush=True)
+
+
+def other_case(a):
+    """wgrad_group over the split modes' / concat's layers, with the look-ahead: us per call and
+    the state bytes moved (W + states read and written) per us."""
+    C = H.C()
+    for kv in a.variant:
+        slot, val = (int(v) for v in kv.split("="))
+        C.set_variant(slot, val)
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    M = 16
+    if a.case == "ushape":
+        shapes, cfg = [(1000, 5408), (100, 1000)], OptimCfg("adam", 1e-3, weight_decay=1e-5)
+    elif a.case == "vanilla":
+        shapes, cfg = [(5000, 5408), (1000, 5000), (100, 1000)], OptimCfg("sgd", 1e-2, momentum=0.9)
+    else:
+        shapes, cfg = [(5000, 43264), (1000, 5000), (800, 1000)], OptimCfg("adam", 1e-3, weight_decay=1e-5)
+    adam = cfg.kind == "adam"
+    Ls, nbytes = [], 0
+    for n, k in shapes:
+        W = torch.randn(n, k, device=dev) * 0.01
+        b = torch.zeros(n, device=dev)
+        st = {"m": torch.zeros_like(W), "v": torch.zeros_like(W)} if adam else {"buf": torch.zeros_like(W)}
+        sb = {"m": torch.zeros_like(b), "v": torch.zeros_like(b)} if adam else {"buf": torch.zeros_like(b)}
+        Ls.append((torch.randn(M, n, device=dev), torch.rand(M, k, device=dev), W, st, b, sb))
+        nbytes += W.numel() * 4 * 2 * (3 if adam else 2)
+    xn = torch.rand(M, shapes[0][1], device=dev)
+    pn = H.lookahead_slabs(dev, shapes[0][1], M, shapes[0][0])
+    us = timeit(lambda: H.wgrad_group_(Ls, M, cfg, 5, x_next=xn, p_next=pn), a.iters)
+    print(f"{a.case} variants {a.variant}: {us:8.2f} us  {nbytes / us / 1e3:7.0f} GB/s of state traffic", flush=True)
+    if a.case == "concat":
+        # ceilings for the same bytes: a device copy of W (read + write) and the plain
+        # optimizer stream (opt_flat: p, g, m, v read; p, m, v written) over fc1
+        W1, st1 = Ls[0][2], Ls[0][3]
+        dst = torch.empty_like(W1)
+        cu = timeit(lambda: dst.copy_(W1), a.iters)
+        print(f"  copy of fc1 W ({W1.numel() * 4 / 1e6:.0f} MB): {cu:8.2f} us  {2 * W1.numel() * 4 / cu / 1e3:7.0f} GB/s",
+              flush=True)
+        g1 = torch.randn_like(W1)
+        so = timeit(lambda: H.apply_update_(W1.view(-1), g1.view(-1), {"m": st1["m"].view(-1), "v": st1["v"].view(-1)},
+                                            cfg, 5), a.iters)
+        print(f"  opt_flat over fc1: {so:8.2f} us  {28 * W1.numel() / so / 1e3:7.0f} GB/s", flush=True)
 
 
 if __name__ == "__main__":
