@@ -126,6 +126,11 @@ def other_case(a):
     pn = H.lookahead_slabs(dev, shapes[0][1], M, shapes[0][0])
     us = timeit(lambda: H.wgrad_group_(Ls, M, cfg, 5, x_next=xn, p_next=pn), a.iters)
     print(f"{a.case} variants {a.variant}: {us:8.2f} us  {nbytes / us / 1e3:7.0f} GB/s of state traffic", flush=True)
+    n1b = Ls[0][2].numel() * 4 * 2 * (3 if adam else 2)
+    u1 = timeit(lambda: H.wgrad_group_(Ls[:1], M, cfg, 5), a.iters)
+    u2 = timeit(lambda: H.wgrad_group_(Ls[:1], M, cfg, 5, x_next=xn, p_next=pn), a.iters)
+    print(f"  fc1 alone: {u1:8.2f} us  {n1b / u1 / 1e3:7.0f} GB/s;  fc1 + look-ahead: {u2:8.2f} us  "
+          f"{n1b / u2 / 1e3:7.0f} GB/s", flush=True)
     if a.case == "concat":
         # ceilings for the same bytes: a device copy of W (read + write) and the plain
         # optimizer stream (opt_flat: p, g, m, v read; p, m, v written) over fc1
