@@ -126,6 +126,8 @@ def main(argv=None):
     ap.add_argument("--resident", choices=("auto", "off"), default="auto",
                     help="SISA server epochs of a narrow Bob shard (TP >= 7) on the register-resident "
                          "persistent executor (csrc/resident.hip) after its cross-rank self-test")
+    ap.add_argument("--split_persist", choices=("auto", "off"), default="auto",
+                    help="vanilla: co-located epochs as one persistent launch (csrc/vanilla.hip)")
     ap.add_argument("--tp_allreduce", choices=("auto", "rccl"), default="auto",
                     help="Bob's TP all-reduce: peer-mapped one-kernel path when it passes set-up (auto) or RCCL")
     ap.add_argument("--act_dtype", choices=("fp32", "bf16"), default="fp32")
@@ -181,7 +183,7 @@ def main(argv=None):
         "--server_epochs", str(a.server_epochs), "--seed", str(a.seed), "--num_samples", str(a.num_samples),
         "--kernels", a.kernels, "--graphs", a.graphs, "--act_dtype", a.act_dtype, "--dtype", a.dtype, "--no_tqdm",
         "--tp_allreduce", a.tp_allreduce, "--resident", a.resident, "--hybrid", a.hybrid,
-        "--log_dir", log_dir, "--watchdog", "off"]
+        "--split_persist", a.split_persist, "--log_dir", log_dir, "--watchdog", "off"]
     if a.mode == "concat" and a.concat_unlearn:
         argv_s.append("--concat_unlearn")
     if a.python_epoch:
@@ -311,6 +313,8 @@ def main(argv=None):
                 # vanilla / U-shape: the native split epochs this rank ran (co-located, or its
                 # side of a remote Alice's) and the per-batch link of the remote ones
                 "split_epochs": _gathered_split(sess) if sargs.mode in ("vanilla", "ushape") else None,
+                "split_persist_fallback": (getattr(sess, "split_persist_fallback", None)
+                                           or getattr(sess, "split_persist_reason", None)),
                 "split_channel": _channel_kind(sess) if sargs.mode in ("vanilla", "ushape") else None,
             },
         }

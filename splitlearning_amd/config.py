@@ -138,6 +138,10 @@ def build_parser() -> argparse.ArgumentParser:
                         "fc1's weights / Adam state streamed through the launch (csrc/hybrid.hip); "
                         "'auto' uses it where it fits and, tensor-parallel, after a cross-rank "
                         "self-test passed; 'off' = the launch-per-stage executor")
+    g.add_argument("--split_persist", choices=("auto", "off"), default="auto",
+                   help="vanilla epochs of an Alice co-located with a one-shard Bob as ONE persistent "
+                        "launch per epoch: her conv front and Bob's whole tail, fc2 / fc3 on-chip, "
+                        "fc1 streamed (csrc/vanilla.hip); 'off' = the per-batch native executor")
     g.add_argument("--persistent_failsafe", choices=("on", "off"), default="on",
                    help="copy Bob's shard (weights, optimizer state) before each persistent server "
                         "epoch; if the launch fails mid-epoch on any Bob rank, restore it on every "

@@ -1,0 +1,293 @@
+// Host side of the vanilla persistent split epoch (`_C.VanillaEpoch`, csrc/vanilla.hip).
+//
+// Reference: the vanilla hot loop, data_entities_vanilla.py:66-76.  One `run` call = ONE
+// cooperative launch over every batch of a co-located Alice's epoch order, a short final batch
+// included (its rows padded to B with ignored labels and zero activations, its CE mean over its
+// real rows).  The host builds the per-step tables (batch rows, labels, CE scales, dropout
+// seeds: host.h step_seed == ops/rng.py), the two fc1 tile-run tables, zeroes the counters (in
+// the launch), launches and reads the kernel's error word once.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+
+#include <string>
+#include <vector>
+
+#include "host.h"
+#include "vanilla.h"
+
+namespace py = pybind11;
+
+namespace {
+
+at::Tensor va_get(const py::dict& d, const char* k) {
+  TORCH_CHECK(d.contains(k) && !d[k].is_none(), "VanillaEpoch: missing '", k, "'");
+  return d[k].cast<at::Tensor>();
+}
+
+void va_f32(const at::Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous(), "VanillaEpoch: ", what, " f32 GPU");
+}
+
+class VanillaEpoch {
+ public:
+  // cfg: layers = [3 dicts {W, b, s0, sb0}] (Bob's model2_sisa, SGD-momentum buffers), lr /
+  // momentum / wd (Bob), alice = {w [32, 1, 3, 3], b [32], s0w, s0b} + alice_lr / alice_momentum /
+  // alice_wd, x (uint8 shard [N, 784]), y (int64 labels [N]), p1 / p2, B, timeout_s,
+  // workgroups (0: cooperative launch of 256)
+  explicit VanillaEpoch(const py::dict& cfg) {
+    auto layers = cfg["layers"].cast<std::vector<py::dict>>();
+    TORCH_CHECK(layers.size() == 3, "VanillaEpoch drives model2_sisa's 3 layers");
+    for (int i = 0; i < 3; ++i) {
+      const py::dict& d = layers[i];
+      W_[i] = va_get(d, "W");
+      b_[i] = va_get(d, "b");
+      s0_[i] = va_get(d, "s0");
+      sb0_[i] = va_get(d, "sb0");
+      for (const at::Tensor* t : {&W_[i], &b_[i], &s0_[i], &sb0_[i]}) va_f32(*t, "layer tensors");
+      TORCH_CHECK(W_[i].dim() == 2 && s0_[i].sizes() == W_[i].sizes() && b_[i].numel() == W_[i].size(0) &&
+                      sb0_[i].numel() == W_[i].size(0),
+                  "layer shapes");
+    }
+    TORCH_CHECK(W_[1].size(1) == W_[0].size(0) && W_[2].size(1) == W_[1].size(0), "layer chain shapes");
+    py::dict al = cfg["alice"].cast<py::dict>();
+    cw_ = va_get(al, "w");
+    cb_ = va_get(al, "b");
+    cmw_ = va_get(al, "s0w");
+    cmb_ = va_get(al, "s0b");
+    for (const at::Tensor* t : {&cw_, &cb_, &cmw_, &cmb_}) va_f32(*t, "conv tensors");
+    TORCH_CHECK(cw_.numel() == 288 && cb_.numel() == 32 && cmw_.numel() == 288 && cmb_.numel() == 32,
+                "conv 32 x 1 x 3 x 3");
+    x_ = va_get(cfg, "x");
+    y_ = va_get(cfg, "y");
+    TORCH_CHECK(x_.is_cuda() && x_.scalar_type() == at::kByte && x_.is_contiguous() && x_.numel() % 784 == 0,
+                "shard pixels uint8 [N, 784]");
+    TORCH_CHECK(y_.is_cuda() && y_.scalar_type() == at::kLong && y_.numel() * 784 == x_.numel(), "labels int64 [N]");
+    B_ = cfg["B"].cast<int>();
+    const double p1 = cfg["p1"].cast<double>(), p2 = cfg["p2"].cast<double>();
+    timeout_s_ = cfg.contains("timeout_s") ? cfg["timeout_s"].cast<double>() : 30.0;
+
+    dev_ = W_[0].device().index();
+    int cus = 0;
+    TORCH_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev_) == hipSuccess, "CU count");
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev_) != hipSuccess || khz <= 0) khz = 100000;
+
+    sl::VaArgs& a = a_;
+    a = sl::VaArgs{};
+    a.N1 = (int)W_[0].size(0);
+    a.K1 = (int)W_[0].size(1);
+    a.N2 = (int)W_[1].size(0);
+    a.C = (int)W_[2].size(0);
+    a.C4 = (a.C + 3) & ~3;
+    a.M = B_;
+    a.G = sl::kVaG;
+    const int wg = cfg.contains("workgroups") ? cfg["workgroups"].cast<int>() : 0;
+    a.coop = wg > 0 ? 0 : 1;
+    a.fault_step = -1;
+    a.NC = a.G / sl::kVaNR;
+    a.HW = a.N2 / 4;
+    a.nrb = (a.N1 + 15) / 16;
+    a.ncb = (a.K1 + 255) / 256;
+    a.ntile = a.nrb * a.ncb;
+    a.ignore = -100;
+    a.thr1 = p1 > 0 ? (uint32_t)(p1 * 4294967296.0) : 0u;
+    a.thr2 = p2 > 0 ? (uint32_t)(p2 * 4294967296.0) : 0u;
+    a.dsc1 = p1 > 0 ? (float)(1.0 / (1.0 - p1)) : 1.f;
+    a.dsc2 = p2 > 0 ? (float)(1.0 / (1.0 - p2)) : 1.f;
+    a.o = sl::make_opt_raw(1, cfg["lr"].cast<double>(), 0, 0, 0, cfg["wd"].cast<double>(),
+                           cfg["momentum"].cast<double>(), 0, nullptr);
+    a.oa = sl::make_opt_raw(1, cfg["alice_lr"].cast<double>(), 0, 0, 0, cfg["alice_wd"].cast<double>(),
+                            cfg["alice_momentum"].cast<double>(), 0, nullptr);
+    why_ = cus < a.G ? "fewer than 256 CUs" : "";
+    if (why_.empty()) why_ = sl::vanilla_check(a);
+    if (why_.empty()) why_ = tables();
+    if (why_.empty()) {
+      auto opt = at::TensorOptions().dtype(at::kFloat).device(W_[0].device());
+      int64_t off = 0;
+      auto take = [&](int64_t n) {
+        const int64_t o = off;
+        off += (n + 3) & ~3LL;
+        return (int)o;
+      };
+      a.oLA = take(2LL * a.nrb * sl::kVaSlots * 256);
+      a.oH1 = take(2LL * 16 * a.N1);
+      a.oFP = take(2LL * a.NC * 16 * a.N2);
+      a.oLP = take(2LL * a.HW * 16 * a.C4);
+      a.oDL = take(2LL * 16 * a.C4);
+      a.oDZ = take(2LL * 16 * a.N2);
+      a.oDP = take(2LL * sl::kVaNR * 16 * a.N1);
+      a.oZP = take((int64_t)a.G * sl::kVaRuns * 8 * 64 * 4);
+      a.oDX = take((int64_t)a.ncb * sl::kVaDxSlots * 16 * 256);
+      a.oX = take(2LL * 16 * a.K1);
+      a.oCWP = take(2LL * 32 * 8 * 16);
+      HB_ = at::zeros({off}, opt);
+      a.HB = HB_.data_ptr<float>();
+      cnt_ = at::zeros({(int64_t)sl::kVaCounters * sl::kVaStride}, opt.dtype(at::kInt));
+      err_ = at::zeros({1}, opt.dtype(at::kInt));
+      std::vector<int> sn(sl::kVaSeams * 8, 0);
+      for (int w = 0; w < a.G; ++w) {
+        ++sn[0 * 8 + (w & 7)];                 // F: every tile
+        if (w < a.HW) ++sn[1 * 8 + (w & 7)];   // L: head workgroups
+        if (w < a.M) ++sn[2 * 8 + (w & 7)];    // D: softmax workgroups
+        if (w < a.HW) ++sn[3 * 8 + (w & 7)];   // Z: head workgroups
+        ++sn[4 * 8 + (w & 7)];                 // X: every conv job
+      }
+      shard_n_ = at::tensor(sn, at::TensorOptions().dtype(at::kInt)).to(W_[0].device());
+      a.cnt = reinterpret_cast<unsigned*>(cnt_.data_ptr<int>());
+      a.shard_n = shard_n_.data_ptr<int>();
+      a.err = err_.data_ptr<int>();
+      a.tab = tab_.data_ptr<int>();
+      a.timeout = (int64_t)(timeout_s_ * 1000.0 * khz);
+      auto setL = [&](sl::ResLayer& r, int i) {
+        r.W = W_[i].data_ptr<float>();
+        r.b = b_[i].data_ptr<float>();
+        r.m = s0_[i].data_ptr<float>();
+        r.mb = sb0_[i].data_ptr<float>();
+        r.v = nullptr;
+        r.vb = nullptr;
+      };
+      setL(a.L1, 0);
+      setL(a.L2, 1);
+      setL(a.L3, 2);
+      a.img = x_.data_ptr<uint8_t>();
+      a.cw = cw_.data_ptr<float>();
+      a.cb = cb_.data_ptr<float>();
+      a.cmw = cmw_.data_ptr<float>();
+      a.cmb = cmb_.data_ptr<float>();
+      std::string why;
+      sl::vanilla_fits(a, dev_, &why);
+      why_ = why;
+    }
+    ok_ = why_.empty();
+  }
+
+  bool ok() const { return ok_; }
+  std::string why() const { return why_; }
+
+  // One epoch over `order` (int64 shard rows [n], on the device): ceil(n / B) steps in one
+  // launch.  Per-row losses -> loss_rows [>= S * B] (padding rows 0).  t_a / t_b: optimizer
+  // steps so far; fwd_count: Bob's forward counter (dropout hash).  Returns (t_a, t_b,
+  // fwd_count) advanced by the step count.  Raises when an in-launch wait gave up.
+  py::tuple run(const at::Tensor& order, at::Tensor& loss_rows, int64_t t_a, int64_t t_b, int64_t fwd_count,
+                int64_t seed_base) {
+    TORCH_CHECK(ok_, "VanillaEpoch: ", why_);
+    TORCH_CHECK(order.is_cuda() && order.scalar_type() == at::kLong && order.dim() == 1, "order int64 [n] on the GPU");
+    const int64_t n = order.numel();
+    const int64_t S = (n + B_ - 1) / B_;
+    if (S == 0) return py::make_tuple(t_a, t_b, fwd_count);
+    TORCH_CHECK(loss_rows.is_cuda() && loss_rows.scalar_type() == at::kFloat && loss_rows.numel() >= S * B_,
+                "loss_rows f32 [>= S * B]");
+    const at::Device dev = order.device();
+    auto lopt = at::TensorOptions().dtype(at::kLong).device(dev);
+    rows_ = at::full({S * B_}, -1, lopt);
+    rows_.narrow(0, 0, n).copy_(order);
+    labels_ = at::full({S * B_}, -100, lopt);
+    labels_.narrow(0, 0, n).copy_(y_.index_select(0, order));
+    std::vector<float> tabf(4 * S, 0.f);
+    std::vector<int32_t> seeds(4 * S);
+    for (int64_t i = 0; i < S; ++i) {
+      const int64_t rows = std::min<int64_t>(B_, n - i * B_);
+      tabf[4 * i + 2] = (float)(1.0 / (double)rows);
+      const uint64_t s0 = sl::step_seed((uint64_t)seed_base, 0, (uint64_t)(fwd_count + 1 + i));
+      const uint64_t s1 = sl::step_seed((uint64_t)seed_base, 1, (uint64_t)(fwd_count + 1 + i));
+      seeds[4 * i] = (int32_t)(uint32_t)(s0 & 0xffffffffull);
+      seeds[4 * i + 1] = (int32_t)(uint32_t)(s0 >> 32);
+      seeds[4 * i + 2] = (int32_t)(uint32_t)(s1 & 0xffffffffull);
+      seeds[4 * i + 3] = (int32_t)(uint32_t)(s1 >> 32);
+    }
+    tabf_ = at::from_blob(tabf.data(), {4 * S}, at::TensorOptions().dtype(at::kFloat)).to(dev);
+    seeds_ = at::from_blob(seeds.data(), {4 * S}, at::TensorOptions().dtype(at::kInt)).to(dev);
+    sl::VaArgs a = a_;
+    a.S = (int)S;
+    a.rows = rows_.data_ptr<int64_t>();
+    a.Y = labels_.data_ptr<int64_t>();
+    a.loss = loss_rows.data_ptr<float>();
+    a.adam = tabf_.data_ptr<float>();
+    a.seeds = reinterpret_cast<const uint32_t*>(seeds_.data_ptr<int32_t>());
+    a.fault_step = fault_step_;
+    fault_step_ = -1;
+    const hipStream_t st = c10::hip::getCurrentHIPStream().stream();
+    TORCH_CHECK(hipMemsetAsync(a_.err, 0, sizeof(int), st) == hipSuccess, "vanilla error word");
+    const hipError_t le = sl::vanilla_epoch_launch(a, st);
+    TORCH_CHECK(le == hipSuccess, "vanilla epoch launch: ", hipGetErrorString(le));
+    const int e = err_.item<int>();
+    TORCH_CHECK(e == 0, "vanilla split epoch: an in-launch wait gave up (error word ", e, ")");
+    return py::make_tuple(t_a + S, t_b + S, fwd_count + S);
+  }
+
+  void set_fault_step(int64_t s) { fault_step_ = (int)s; }
+  at::Tensor table() const { return tab_.clone(); }
+
+ private:
+  // forward (row-major, hybrid_exec.cpp's) and update (column-major) tile runs
+  std::string tables() {
+    sl::VaArgs& a = a_;
+    const int G = a.G, nrb = a.nrb, ncb = a.ncb, NC = a.NC, T = a.ntile;
+    const int Q4 = a.N1 / 4;
+    if (T < G) return "fewer fc1 tiles than workgroups";
+    std::vector<int> tab(G + 1 + 2 * nrb + NC, 0);
+    for (int w = 0; w <= G; ++w) tab[w] = (int)((int64_t)w * T / G);
+    auto wg_of = [&](const std::vector<int>& t0, int base, int t) {
+      int lo = 0, hi = G - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) / 2;
+        if (t0[base + mid] <= t) lo = mid;
+        else hi = mid - 1;
+      }
+      return lo;
+    };
+    auto colblk = [&](int n4) { return (int)(((int64_t)(n4 + 1) * NC + Q4 - 1) / Q4) - 1; };
+    for (int rb = 0; rb < nrb; ++rb) {
+      const int w0 = wg_of(tab, 0, rb * ncb), w1 = wg_of(tab, 0, std::min((rb + 1) * ncb, T) - 1);
+      tab[G + 1 + rb] = w0;
+      tab[G + 1 + nrb + rb] = w1 - w0 + 1;
+      if (w1 - w0 + 1 > sl::kVaSlots) return "an fc1 row block spans more workgroups than the forward slots";
+      const int blo = colblk((16 * rb) / 4), bhi = colblk((std::min(16 * rb + 16, a.N1) - 1) / 4);
+      for (int b = blo; b <= bhi; ++b) ++tab[G + 1 + 2 * nrb + b];
+    }
+    for (int w = 0; w < G; ++w) {
+      if (tab[w + 1] <= tab[w]) continue;
+      const int runs = (tab[w + 1] - 1) / ncb - tab[w] / ncb + 1;
+      if (runs > sl::kVaRuns) return "a forward run touches more than 3 fc1 row blocks";
+    }
+    for (int b = 0; b < NC; ++b)
+      if (tab[G + 1 + 2 * nrb + b] < 1) return "an fc2 column block without fc1 rows";
+    // update runs: u0[G + 1], cbw0[ncb], cbn[ncb]
+    a.oU = (int)tab.size();
+    const int base = a.oU;
+    tab.resize(base + G + 1 + 2 * ncb, 0);
+    for (int w = 0; w <= G; ++w) tab[base + w] = (int)((int64_t)w * T / G);
+    for (int w = 0; w < G; ++w)
+      if (tab[base + w + 1] - tab[base + w] > sl::kVaMaxRun) return "an update run longer than 28 tiles";
+    for (int cb = 0; cb < ncb; ++cb) {
+      const int w0 = wg_of(tab, base, cb * nrb), w1 = wg_of(tab, base, (cb + 1) * nrb - 1);
+      tab[base + G + 1 + cb] = w0;
+      tab[base + G + 1 + ncb + cb] = w1 - w0 + 1;
+      if (w1 - w0 + 1 > sl::kVaDxSlots) return "an fc1 column block spans more workgroups than the dx slots";
+    }
+    tab_ = at::tensor(tab, at::TensorOptions().dtype(at::kInt)).to(W_[0].device());
+    return "";
+  }
+
+  at::Tensor W_[3], b_[3], s0_[3], sb0_[3];
+  at::Tensor cw_, cb_, cmw_, cmb_, x_, y_;
+  int B_ = 16, dev_ = 0, fault_step_ = -1;
+  double timeout_s_ = 30.0;
+  sl::VaArgs a_{};
+  bool ok_ = false;
+  std::string why_;
+  at::Tensor HB_, cnt_, err_, shard_n_, tab_, tabf_, seeds_, rows_, labels_;
+};
+
+}  // namespace
+
+void sl_register_vanilla(py::module& m) {
+  py::class_<VanillaEpoch>(m, "VanillaEpoch")
+      .def(py::init<const py::dict&>())
+      .def("ok", &VanillaEpoch::ok)
+      .def("why", &VanillaEpoch::why)
+      .def("table", &VanillaEpoch::table)
+      .def("set_fault_step", &VanillaEpoch::set_fault_step)
+      .def("run", &VanillaEpoch::run, py::arg("order"), py::arg("loss_rows"), py::arg("t_a"), py::arg("t_b"),
+           py::arg("fwd_count"), py::arg("seed_base"));
+}

@@ -15,6 +15,8 @@ Reference hot loops: data_entities_vanilla.py:66-76 and data_entities.py:65-81.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 _KIND = {"sgd": 1, "adam": 2}
@@ -119,6 +121,83 @@ def run_native_split_epoch(sess, cid: int, order: torch.Tensor, mode: str):
     if a.head is not None:
         a.head.fwd_count += nb
     return ex
+
+
+# ---------------------------------------------------------------------- persistent vanilla epoch
+def persistent_vanilla_ok(sess, cid: int) -> bool:
+    """Whether `run_persistent_vanilla_epoch` may drive this epoch: the co-located native
+    conditions, fp32 SGD-momentum on both sides, batches of at most 16 rows, the flag, and no
+    earlier failure of the persistent executor in this session."""
+    if getattr(sess.args, "split_persist", "auto") == "off" or sess.__dict__.get("_va_off"):
+        return False
+    if not native_split_ok(sess, cid, "vanilla") or not hasattr(sess.ops.C(), "VanillaEpoch"):
+        return False
+    a = sess.alices[cid]
+    return (1 <= sess.B <= 16 and a.slot.cfg.kind == "sgd" and sess.bob_slot(cid).cfg.kind == "sgd"
+            and len(sess.tail.layers) == 3 and all(L.W.dtype == torch.float32 for L in sess.tail.layers))
+
+
+def _va_cfg(sess, cid: int) -> dict:
+    a = sess.alices[cid]
+    a.front.flush()
+    w, b = a.front.params
+    aw, ab = _param(a.slot, "conv.weight", w), _param(a.slot, "conv.bias", b)
+    bslot = sess.bob_slot(cid)
+    layers = []
+    for L in sess.tail.layers:
+        pw, pb = _param(bslot, f"{L.spec.name}.weight", L.W), _param(bslot, f"{L.spec.name}.bias", L.b)
+        layers.append({"W": pw["p"], "b": pb["p"], "s0": pw["s0"], "sb0": pb["s0"]})
+    bo, ao = bslot.cfg, a.slot.cfg
+    return {"layers": layers, "lr": bo.lr, "momentum": bo.momentum, "wd": bo.weight_decay,
+            "alice": {"w": aw["p"], "b": ab["p"], "s0w": aw["s0"], "s0b": ab["s0"]},
+            "alice_lr": ao.lr, "alice_momentum": ao.momentum, "alice_wd": ao.weight_decay,
+            "x": a.train.x, "y": a.train.y, "B": sess.B,
+            "p1": sess.tail.layers[0].spec.dropout, "p2": sess.tail.layers[1].spec.dropout,
+            "timeout_s": float(getattr(sess.args, "persist_timeout_s", 30.0)),
+            # a plain (non-cooperative) launch of the same grid for rocprofv3, whose process dies at
+            # exit after any cooperative launch (docs/PERF.md, tools/coop_repro.hip)
+            "workgroups": int(os.environ.get("SL_PERSIST_WORKGROUPS", "0"))}
+
+
+def run_persistent_vanilla_epoch(sess, cid: int, order: torch.Tensor) -> bool:
+    """One vanilla epoch of a co-located Alice_cid as ONE launch (`_C.VanillaEpoch`,
+    csrc/vanilla.hip).  Fail-safe: the Alice's and Bob's parameters and momentum buffers are
+    copied first; if the launch fails they are restored, the persistent executor is switched
+    off for the session (`split_persist_fallback`) and False is returned, so the caller runs
+    the epoch on the per-batch executor instead."""
+    cfg = _va_cfg(sess, cid)
+    ex = sess.ops.C().VanillaEpoch(cfg)
+    if not ex.ok():
+        sess.__dict__["_va_off"] = True
+        sess.__dict__["split_persist_reason"] = ex.why()
+        return False
+    a = sess.alices[cid]
+    order = order.to(sess.device, torch.int64).contiguous()
+    state = [L["W"] for L in cfg["layers"]] + [L["b"] for L in cfg["layers"]]
+    state += [L["s0"] for L in cfg["layers"]] + [L["sb0"] for L in cfg["layers"]] + list(cfg["alice"].values())
+    snap = [t.clone() for t in state] if getattr(sess.args, "persistent_failsafe", "on") != "off" else None
+    B = sess.B
+    nb = -(-int(order.numel()) // B)
+    loss = torch.empty(max(nb, 1) * B, dtype=torch.float32, device=sess.device)
+    sess.tail._pre = None
+    fault = sess.__dict__.pop("_va_fault_step", None)
+    if fault is not None:
+        ex.set_fault_step(int(fault))
+    try:
+        t_a, t_b, fc = ex.run(order, loss, a.slot.t, sess.bob_slot(cid).t, sess.tail.fwd_count, sess.tail.seed_base)
+    except RuntimeError as e:
+        if snap is None:
+            raise
+        for t, s in zip(state, snap):
+            t.copy_(s)
+        sess.__dict__["_va_off"] = True
+        sess.__dict__["split_persist_fallback"] = str(e).splitlines()[0][:200]
+        return False
+    _count(sess, "persistent")
+    a.slot.t = int(t_a)
+    _bob_done(sess, cid, t_b, fc)
+    sess.__dict__["last_split_losses"] = loss[:order.numel()]
+    return True
 
 
 # ---------------------------------------------------------------------- remote placements

@@ -19,7 +19,8 @@ from ..config import CUT_FEATURES
 from ..engine.slots import OptSlot, sgd_momentum
 from ..models import ServerTailSisa, sisa_server_spec
 from .base import Session, _progress
-from .split_native import native_remote_role, native_split_ok, run_native_remote_epoch, run_native_split_epoch
+from .split_native import (native_remote_role, native_split_ok, persistent_vanilla_ok, run_native_remote_epoch,
+                           run_native_split_epoch, run_persistent_vanilla_epoch)
 
 
 class VanillaSession(Session):
@@ -90,6 +91,8 @@ class VanillaSession(Session):
         spans = [(s, min(s + B, n)) for s in range(0, n, B)]
         if not spans:
             return
+        if order is not None and persistent_vanilla_ok(self, cid) and run_persistent_vanilla_epoch(self, cid, order):
+            return                                # the whole epoch in one launch (csrc/vanilla.hip)
         if order is not None and native_split_ok(self, cid, "vanilla"):
             run_native_split_epoch(self, cid, order, "vanilla")   # the same launches, issued from C++
             return

@@ -14,11 +14,13 @@ from splitlearning_amd.parallel.dist import Comm, Placement
 pytestmark = pytest.mark.gpu
 
 
-def _session(kind, tmp_path, native, dev, B=16):
+def _session(kind, tmp_path, native, dev, B=16, persist=False):
     from splitlearning_amd.protocols import UShapeSession, VanillaSession
     flags = ["--vanilla"] if kind == "vanilla" else []
     if not native:
         flags.append("--python_epoch")
+    if not persist:
+        flags += ["--split_persist", "off"]   # the per-batch executor (csrc/vanilla.hip has its own tests)
     args = parse_args(flags + ["--world_size", "2", "--seed", "11", "--num_samples", "900", "--no_tqdm",
                                "--batch_size", str(B), "--datapath", str(tmp_path / "d"),
                                "--log_dir", str(tmp_path / ("logs_n" if native else "logs_p"))])
