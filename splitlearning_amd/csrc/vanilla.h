@@ -28,6 +28,7 @@ constexpr int kVaSeams = 5;         // F: fc2 partials, L: logit partials, D: dl
 // counter words: the seams' 8 shards each, then P[NC] (dz1 partials per fc2 column block),
 // R[nrb] (forward partials per fc1 row block), XD[ncb] (cut-gradient partials per fc1 column
 // block), CW[32] (conv gradient partials per channel)
+constexpr int kVaMaxS = 6000;      // steps per launch (the activation slots' 32-bit offsets)
 constexpr int kVaCounters = kVaSeams * 8 + kVaMaxNC + kVaMaxRB + kVaMaxCB + 32;
 
 struct VaArgs {
@@ -62,16 +63,21 @@ struct VaArgs {
   //   FP [2][NC][N2][16 m] fc2 partials                      LP [2][HW][16][C4] logit partials
   //   DL [2][16][C4] dlogits                                 DZ [2][16][N2] dz2
   //   DP [2][8][N1][16 m] dz1 partials                       ZP [G][kVaRuns][8][64] f32x4
-  //   DX [ncb][kVaDxSlots][16 m][256] cut-gradient partials  X [2][16][K1] the batch's activation
+  //   DX [ncb][kVaDxSlots][16 m][256] cut-gradient partials
   //   CWP [2][32][8][16] conv gradient partials per (channel, image pair)
+  // the batches' activations, one [16][K1] slot per step of the launch (each written once,
+  // before any read, so the forward and update passes read it with plain L2-cached loads)
+  float* Xr;
   float* HB;
-  int oLA, oH1, oFP, oLP, oDL, oDZ, oDP, oZP, oDX, oX, oCWP;
+  int oLA, oH1, oFP, oLP, oDL, oDZ, oDP, oZP, oDX, oCWP;
   unsigned* cnt;          // [kVaCounters][kVaStride] (zeroed per launch)
   const int* shard_n;     // [kVaSeams][8] arrivals per seam shard and step
   int* err;               // nonzero after a wait gave up (2 timeout)
   int64_t timeout;        // wall-clock ticks per wait
   int coop;               // cooperative launch
   int fault_step;         // tests: this step's first wait is never met; -1 off
+  int64_t* tall;          // optional [tall_n][G][16] phase stamps (wall clock) of every workgroup
+  int tall_step, tall_n;  // for steps tall_step .. tall_step + tall_n - 1
 };
 
 hipError_t vanilla_epoch_launch(const VaArgs& a, hipStream_t st);

@@ -157,6 +157,13 @@ static_assert(kVaThreads / 64 * 10 * 256 >= kVaMaxWR * 4 * kVaMaxWC4, "10 W2 16 
   const int tid = tid_l_, r = tid >> 6, lane = tid & 63, li = lane & 15, lq = lane >> 4; \
   (void)r; (void)lane; (void)li; (void)lq
 
+// phase stamps of every workgroup for steps tall_step .. (scripts/vanilla_trace.py)
+#define VA_MARK(k)                                                                             \
+  do {                                                                                         \
+    if (threadIdx.x == 0 && a.tall != nullptr && i >= a.tall_step && i < a.tall_step + a.tall_n) \
+      a.tall[((int64_t)(i - a.tall_step) * G + w) * 16 + (k)] = (int64_t)wall_clock64();     \
+  } while (0)
+
 __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* sw2 = reinterpret_cast<float*>(smem + OFF_W2);
@@ -205,7 +212,8 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
   const int cc = w & 31, cg = w >> 5;
   const __amdgpu_buffer_rsrc_t rHB = rs_of(a.HB);
   const int bLA = 4 * a.oLA, bH1 = 4 * a.oH1, bFP = 4 * a.oFP, bLP = 4 * a.oLP, bDL = 4 * a.oDL, bDZ = 4 * a.oDZ,
-            bDP = 4 * a.oDP, bZP = 4 * a.oZP, bDX = 4 * a.oDX, bX = 4 * a.oX, bCW = 4 * a.oCWP;
+            bDP = 4 * a.oDP, bZP = 4 * a.oZP, bDX = 4 * a.oDX, bCW = 4 * a.oCWP;
+  const __amdgpu_buffer_rsrc_t rX = rs_of(a.Xr);
   const __amdgpu_buffer_rsrc_t rW1 = rs_of(a.L1.W), rM1 = rs_of(a.L1.m);
 
   // ---- resident state: the W2 tile (LDS), its momentum (VGPRs), head columns, biases, conv channel
@@ -332,7 +340,7 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
       if (valid) conv_at(step & 1, bl, p, y, arg);
       cy = y;
       carg = arg;
-      hst1(rHB, bX + (((step & 1) * 16 + m) * K1 + cc * 169 + p) * 4, y);
+      hst1(rX, ((step * 16 + m) * K1 + cc * 169 + p) * 4, y);
     }
   };
 
@@ -350,13 +358,13 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
                  : zv;
     }
   };
-  auto load_xv = [&](int xpar, int t, f32x4 (&xv)[2]) {
+  auto load_xv = [&](int step, int t, f32x4 (&xv)[2]) {
     VA_IDX();
     const int cb = t - (t / ncb) * ncb;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int k = cb * 256 + 16 * (r + 8 * h) + 4 * lq;
-      xv[h] = k < K1 ? hld4(rHB, bX + ((xpar * 16 + li) * K1 + k) * 4) : zv;
+      xv[h] = k < K1 ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rX, ((step * 16 + li) * K1 + k) * 4, 0, 0)) : zv;
     }
   };
   f32x4 zlast = zv;
@@ -364,9 +372,13 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
     VA_IDX();
     hst4(rHB, bZP + (((w * kVaRuns + k) * 8 + r) * 64 + lane) * 16, z);
   };
-  auto fwd_pass = [&](int xpar) {
+  auto fwd_pass = [&](int step) {
     if (nt <= 0) return;
+    // the x operand too is loaded one tile ahead (loaded in its own tile, its latency was
+    // exposed once per tile)
+    f32x4 xv2[2][2];
     load_w(t_begin, sp[0]);
+    load_xv(step, t_begin, xv2[0]);
     __syncthreads();
     f32x4 z = zv;
     int kz = 0;
@@ -380,9 +392,10 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
         z = zv;
         kz = kr;
       }
-      f32x4 xv[2];
-      load_xv(xpar, t, xv);
-      if (j + 1 < nt) load_w(t + 1, sp[nb]);
+      if (j + 1 < nt) {
+        load_w(t + 1, sp[nb]);
+        load_xv(step, t + 1, xv2[nb]);
+      }
       VA_IDX();
       const int n1 = 16 * rb + r;
       const int k = cb * 256 + 4 * lane;
@@ -394,7 +407,7 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
       for (int h = 0; h < 2; ++h) {
         const f32x4 wv4 = sw[cur * 1040 + li * 65 + 4 * (r + 8 * h) + lq];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) z = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[h][c], wv4[c], z, 0, 0, 0);
+        for (int c = 0; c < 4; ++c) z = __builtin_amdgcn_mfma_f32_16x16x4f32(xv2[cur][h][c], wv4[c], z, 0, 0, 0);
       }
     };
     int j = 0;
@@ -459,13 +472,13 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
       mm[s] = act ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rM1, boff, 0, kSt)) : zv;
     }
   };
-  auto stage_x = [&](int cb, int xpar) {
+  auto stage_x = [&](int cb, int step) {
     VA_IDX();
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int e = tid + u * kVaThreads;
       const int m = e >> 6, k = cb * 256 + 4 * (e & 63);
-      sa[e] = k < K1 ? hld4(rHB, bX + ((xpar * 16 + m) * K1 + k) * 4) : zv;
+      sa[e] = k < K1 ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rX, ((step * 16 + m) * K1 + k) * 4, 0, 0)) : zv;
     }
   };
   f32x4 dacc[4];
@@ -502,10 +515,10 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
     for (int c = 0; c < 4; ++c) dacc[c] = zv;
     va_arrive(a, va_XD(cb));
   };
-  auto upd_pass = [&](int xpar, float ss, float ib) {
+  auto upd_pass = [&](int step, float ss, float ib) {
     if (unt <= 0) return;
     int ccb = u_begin / nrb;
-    stage_x(ccb, xpar);
+    stage_x(ccb, step);
 #pragma unroll
     for (int c = 0; c < 4; ++c) dacc[c] = zv;
     __syncthreads();
@@ -516,7 +529,7 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
       if (cb != ccb) {   // uniform: the run enters its next column block
         flush_dx(ccb);
         ccb = cb;
-        stage_x(cb, xpar);
+        stage_x(cb, step);
         __syncthreads();
       }
       if (j + 1 < unt) load_u(t + 1, sp[nb], sm[nb]);
@@ -580,6 +593,7 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
     const SlOpt o = a.o;
     float ss = 0.f, ib = 0.f;
     asm volatile("" : "+v"(ss), "+v"(ib));
+    VA_MARK(0);
     // the next batch's images, in flight across the step (written to LDS in the conv phase)
     const uint32_t pimg = more ? img_word(i + 1) : 0u;
 
@@ -598,6 +612,7 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
     }
     __syncthreads();
     if (*s_ok == 0) break;
+    VA_MARK(1);
     {
       VA_IDX();
 #pragma unroll
@@ -647,6 +662,7 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
     }
     va_arrive(a, va_seam(0, w & 7));
 
+    VA_MARK(2);
     // ================= H: the head rows' fc2 sums, h2, logit partials
     if (head) {
       if (!va_seam_wait(a, 0, (unsigned)(i + 1), s_ok, s_sn)) break;
@@ -808,8 +824,10 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
       }
     }
 
+    VA_MARK(3);
     // ================= B: the tile's dz1 partial, then W2's step
     if (!va_seam_wait(a, 3, (unsigned)(i + 1), s_ok, s_sn)) break;
+    VA_MARK(3);
     {
       VA_IDX();
       const int m = tid >> 5, k4 = tid & 31;
@@ -850,6 +868,7 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
       }
     }
     va_arrive(a, va_P(tb));
+    VA_MARK(4);
     // the first update tile's state in flight under W2's update and the dz1 wait
     if (unt > 0) load_u(u_begin, sp[0], sm[0]);
     {
@@ -874,6 +893,7 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
       }
     }
 
+    VA_MARK(5);
     // ================= U: dz1 of the update run and the forward run, b1's step, the update pass
     {
       // every fc2 column block's dz1 partials (the update run spans ~27 row blocks, possibly
@@ -884,16 +904,21 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
           }))
         break;
     }
+    VA_MARK(6);
     {
       VA_IDX();
-      // (row nn, rows m = 4 mg ..): DP is [8][N1][16], H1 [N1][16]
-      for (int e = tid; e < (unt + nruns) * 64; e += kVaThreads) {
+      // (row nn, rows m = 4 mg ..): DP is [8][N1][16], H1 [N1][16]; up to 4 items per thread,
+      // unrolled so that all their loads are in flight together (a rolled loop took 4.5 us)
+#pragma unroll
+      for (int u = 0; u < (kVaMaxRun + kVaRuns + 7) / 8; ++u) {
+        const int e = tid + u * kVaThreads;
+        const bool item = e < (unt + nruns) * 64;
         const int j = e >> 6, nn = (e >> 2) & 15, mg = e & 3;
         const bool upd = j < unt;
         const int rb = upd ? (u_begin + j) - ((u_begin + j) / nrb) * nrb : rbA + (j - unt);
         const int n = 16 * rb + nn;
         f32x4 v = zv;
-        if (n < N1) {
+        if (item && n < N1) {
           f32x4 parts[kVaNR];
 #pragma unroll
           for (int b = 0; b < kVaNR; ++b) parts[b] = hld4(rHB, bDP + (((par * kVaNR + b) * N1 + n) * 16 + 4 * mg) * 4);
@@ -905,8 +930,10 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
           for (int q = 0; q < 4; ++q) v[q] = (4 * mg + q < M && h[q] > 0.f) ? v[q] * a.dsc1 : 0.f;
         }
         float* dst = upd ? sdz1 + j * 256 : sdzb + (j - unt) * 256;
+        if (item) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) dst[(4 * mg + q) * 16 + nn] = v[q];
+          for (int q = 0; q < 4; ++q) dst[(4 * mg + q) * 16 + nn] = v[q];
+        }
       }
     }
     __syncthreads();
@@ -924,7 +951,9 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
       }
     }
     __syncthreads();   // sdzb (union) is read before the update pass stages x over it
-    upd_pass(par, ss, ib);
+    VA_MARK(7);
+    upd_pass(i, ss, ib);
+    VA_MARK(8);
 
     // ================= C: Alice's backward + step (conv job), her forward of batch i + 1
     {
@@ -935,6 +964,7 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
           }))
         break;
     }
+    VA_MARK(9);
     img_put(par ^ 1, pimg);
     {
       VA_IDX();
@@ -947,8 +977,13 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
         if (m < M && cy > 0.f) {
           const int k = cc * 169 + p, cb = k >> 8, kk = k & 255;
           const int ns = a.tab[a.oU + G + 1 + ncb + cb];
-          float gx = 0.f;
-          for (int s = 0; s < ns; ++s) gx += hld1(rHB, bDX + (((cb * kVaDxSlots + s) * 16 + m) * 256 + kk) * 4);
+          float parts[kVaDxSlots];
+#pragma unroll
+          for (int s = 0; s < kVaDxSlots; ++s)
+            parts[s] = s < ns ? hld1(rHB, bDX + (((cb * kVaDxSlots + s) * 16 + m) * 256 + kk) * 4) : 0.f;
+          float gx = parts[0];
+#pragma unroll
+          for (int s = 1; s < kVaDxSlots; ++s) gx += parts[s];
           const uint8_t* im = simg + par * 1568 + bl * 784;
           const int ph = p / 13, pw = p - (p / 13) * 13;
           const int rr = 2 * ph + (carg >> 1), c2 = 2 * pw + (carg & 1);
@@ -974,11 +1009,13 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
       hst1(rHB, bCW + (((par * 32 + cc) * 8 + cg) * 16 + j) * 4, g);
     }
     va_arrive(a, va_CW(cc));
+    VA_MARK(10);
     if (!va_wait_many(a, 1, s_ok, [&](int, int& idx) {
           idx = va_CW(cc);
           return (unsigned)(i + 1) * 8u;
         }))
       break;
+    VA_MARK(11);
     if (threadIdx.x < 10) {
       const int j = threadIdx.x;
       float parts[8];
@@ -996,10 +1033,14 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
     if (more) {
       conv_fwd(i + 1);
       va_arrive(a, va_seam(4, w & 7));
+      VA_MARK(12);
       if (!va_seam_wait(a, 4, (unsigned)(i + 2), s_ok, s_sn)) break;
+      VA_MARK(13);
       // ================= V: the forward pass of batch i + 1 over the updated fc1
-      fwd_pass(par ^ 1);
+      fwd_pass(i + 1);
+      VA_MARK(14);
       flush(i + 1);
+      VA_MARK(15);
     }
   }
 
@@ -1057,6 +1098,7 @@ done:
   }
 }
 #undef VA_IDX
+#undef VA_MARK
 
 int vanilla_lds_bytes() { return kVaLds; }
 
@@ -1072,6 +1114,7 @@ std::string vanilla_check(const VaArgs& a) {
     return "fc2 width % 4, <= 1024";
   if (a.C < 1 || a.C > kVaMaxC || a.C4 != ((a.C + 3) & ~3)) return "classes <= 128";
   if (a.o.kind != 1 || a.oa.kind != 1) return "SGD-momentum on both sides";
+  if (a.S > kVaMaxS) return "more than 6000 steps in one launch";
   return "";
 }
 

@@ -118,7 +118,6 @@ class VanillaEpoch {
       a.oDP = take(2LL * sl::kVaNR * 16 * a.N1);
       a.oZP = take((int64_t)a.G * sl::kVaRuns * 8 * 64 * 4);
       a.oDX = take((int64_t)a.ncb * sl::kVaDxSlots * 16 * 256);
-      a.oX = take(2LL * 16 * a.K1);
       a.oCWP = take(2LL * 32 * 8 * 16);
       HB_ = at::zeros({off}, opt);
       a.HB = HB_.data_ptr<float>();
@@ -169,7 +168,7 @@ class VanillaEpoch {
   // steps so far; fwd_count: Bob's forward counter (dropout hash).  Returns (t_a, t_b,
   // fwd_count) advanced by the step count.  Raises when an in-launch wait gave up.
   py::tuple run(const at::Tensor& order, at::Tensor& loss_rows, int64_t t_a, int64_t t_b, int64_t fwd_count,
-                int64_t seed_base) {
+                int64_t seed_base, const c10::optional<at::Tensor>& trace_all, int64_t trace_step) {
     TORCH_CHECK(ok_, "VanillaEpoch: ", why_);
     TORCH_CHECK(order.is_cuda() && order.scalar_type() == at::kLong && order.dim() == 1, "order int64 [n] on the GPU");
     const int64_t n = order.numel();
@@ -197,25 +196,41 @@ class VanillaEpoch {
     }
     tabf_ = at::from_blob(tabf.data(), {4 * S}, at::TensorOptions().dtype(at::kFloat)).to(dev);
     seeds_ = at::from_blob(seeds.data(), {4 * S}, at::TensorOptions().dtype(at::kInt)).to(dev);
-    sl::VaArgs a = a_;
-    a.S = (int)S;
-    a.rows = rows_.data_ptr<int64_t>();
-    a.Y = labels_.data_ptr<int64_t>();
-    a.loss = loss_rows.data_ptr<float>();
-    a.adam = tabf_.data_ptr<float>();
-    a.seeds = reinterpret_cast<const uint32_t*>(seeds_.data_ptr<int32_t>());
-    a.fault_step = fault_step_;
-    fault_step_ = -1;
     const hipStream_t st = c10::hip::getCurrentHIPStream().stream();
     TORCH_CHECK(hipMemsetAsync(a_.err, 0, sizeof(int), st) == hipSuccess, "vanilla error word");
-    const hipError_t le = sl::vanilla_epoch_launch(a, st);
-    TORCH_CHECK(le == hipSuccess, "vanilla epoch launch: ", hipGetErrorString(le));
+    // launches of at most kVaMaxS steps (one launch of S steps is bitwise S one-step launches)
+    const int64_t cs = std::min<int64_t>(S, max_steps_);
+    xr_ = at::empty({cs * 16 * a_.K1}, at::TensorOptions().dtype(at::kFloat).device(dev));
+    for (int64_t s0 = 0; s0 < S; s0 += cs) {
+      const int64_t ns = std::min(cs, S - s0);
+      sl::VaArgs a = a_;
+      a.S = (int)ns;
+      a.Xr = xr_.data_ptr<float>();
+      a.rows = rows_.data_ptr<int64_t>() + s0 * B_;
+      a.Y = labels_.data_ptr<int64_t>() + s0 * B_;
+      a.loss = loss_rows.data_ptr<float>() + s0 * B_;
+      a.adam = tabf_.data_ptr<float>() + 4 * s0;
+      a.seeds = reinterpret_cast<const uint32_t*>(seeds_.data_ptr<int32_t>()) + 4 * s0;
+      if (trace_all.has_value() && s0 == 0) {
+        TORCH_CHECK(trace_all->is_cuda() && trace_all->scalar_type() == at::kLong && trace_all->is_contiguous() &&
+                        trace_all->numel() % (16LL * a_.G) == 0,
+                    "trace_all int64 [steps, G, 16]");
+        a.tall = trace_all->data_ptr<int64_t>();
+        a.tall_n = (int)(trace_all->numel() / (16LL * a_.G));
+        a.tall_step = (int)(trace_step - s0);
+      }
+      a.fault_step = fault_step_ >= s0 && fault_step_ < s0 + ns ? (int)(fault_step_ - s0) : -1;
+      const hipError_t le = sl::vanilla_epoch_launch(a, st);
+      TORCH_CHECK(le == hipSuccess, "vanilla epoch launch: ", hipGetErrorString(le));
+    }
+    fault_step_ = -1;
     const int e = err_.item<int>();
     TORCH_CHECK(e == 0, "vanilla split epoch: an in-launch wait gave up (error word ", e, ")");
     return py::make_tuple(t_a + S, t_b + S, fwd_count + S);
   }
 
   void set_fault_step(int64_t s) { fault_step_ = (int)s; }
+  void set_max_steps(int64_t s) { max_steps_ = std::max<int64_t>(1, std::min<int64_t>(s, sl::kVaMaxS)); }
   at::Tensor table() const { return tab_.clone(); }
 
  private:
@@ -272,11 +287,12 @@ class VanillaEpoch {
   at::Tensor W_[3], b_[3], s0_[3], sb0_[3];
   at::Tensor cw_, cb_, cmw_, cmb_, x_, y_;
   int B_ = 16, dev_ = 0, fault_step_ = -1;
+  int64_t max_steps_ = sl::kVaMaxS;
   double timeout_s_ = 30.0;
   sl::VaArgs a_{};
   bool ok_ = false;
   std::string why_;
-  at::Tensor HB_, cnt_, err_, shard_n_, tab_, tabf_, seeds_, rows_, labels_;
+  at::Tensor HB_, cnt_, err_, shard_n_, tab_, tabf_, seeds_, rows_, labels_, xr_;
 };
 
 }  // namespace
@@ -288,6 +304,7 @@ void sl_register_vanilla(py::module& m) {
       .def("why", &VanillaEpoch::why)
       .def("table", &VanillaEpoch::table)
       .def("set_fault_step", &VanillaEpoch::set_fault_step)
+      .def("set_max_steps", &VanillaEpoch::set_max_steps)
       .def("run", &VanillaEpoch::run, py::arg("order"), py::arg("loss_rows"), py::arg("t_a"), py::arg("t_b"),
-           py::arg("fwd_count"), py::arg("seed_base"));
+           py::arg("fwd_count"), py::arg("seed_base"), py::arg("trace_all") = py::none(), py::arg("trace_step") = 0);
 }

@@ -180,6 +180,8 @@ def run_persistent_vanilla_epoch(sess, cid: int, order: torch.Tensor) -> bool:
     nb = -(-int(order.numel()) // B)
     loss = torch.empty(max(nb, 1) * B, dtype=torch.float32, device=sess.device)
     sess.tail._pre = None
+    if sess.__dict__.get("_va_max_steps"):
+        ex.set_max_steps(int(sess._va_max_steps))      # tests: the epoch as several launches
     fault = sess.__dict__.pop("_va_fault_step", None)
     if fault is not None:
         ex.set_fault_step(int(fault))

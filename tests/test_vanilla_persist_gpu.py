@@ -52,16 +52,20 @@ def test_persistent_vanilla_one_launch_is_bitwise_step_launches(cuda, tmp_path):
     B = 16
     s1 = _session("vanilla", tmp_path, True, cuda, B, persist=True)
     s2 = _session("vanilla", tmp_path, True, cuda, B, persist=True)
+    s3 = _session("vanilla", tmp_path, True, cuda, B, persist=True)
+    s3._va_max_steps = 2          # the executor's own chunking: launches of at most 2 steps
     order = s1.alices[1].train.shuffled_order(torch.Generator().manual_seed(7))[:B * 5 + 7].to(cuda)
     s1.split_epoch(1, order, order.numel())
+    s3.split_epoch(1, order, order.numel())
     for i in range(0, order.numel(), B):
         part = order[i:i + B]
         s2.split_epoch(1, part, part.numel())
     torch.cuda.synchronize()
     assert s1.native_split_epochs["persistent"] == 1 and s2.native_split_epochs["persistent"] == 6
-    a, b = _states(s1, "vanilla"), _states(s2, "vanilla")
+    a, b, c = _states(s1, "vanilla"), _states(s2, "vanilla"), _states(s3, "vanilla")
     for k in a:
         assert torch.equal(a[k], b[k]), k
+        assert torch.equal(a[k], c[k]), k
     assert s1.tail.fwd_count == s2.tail.fwd_count and s1.bob_slot(1).t == s2.bob_slot(1).t
 
 
