@@ -88,6 +88,7 @@ __device__ __forceinline__ bool va_seam_wait(const VaArgs& a, int seam, unsigned
     if (lane == 0) *s_ok = ok ? 1 : 0;
   }
   __syncthreads();
+  asm volatile("" ::: "memory");   // no load of the handed-off bytes is hoisted above the wait
   return *s_ok != 0;
 }
 
@@ -106,6 +107,7 @@ __device__ __forceinline__ bool va_wait_many(const VaArgs& a, int n, int* s_ok, 
     if (lane == 0) *s_ok = ok ? 1 : 0;
   }
   __syncthreads();
+  asm volatile("" ::: "memory");   // no load of the handed-off bytes is hoisted above the wait
   return *s_ok != 0;
 }
 
