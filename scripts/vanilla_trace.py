@@ -65,6 +65,10 @@ def main():
     ex.run(order, loss, 0, 0, 0, 1, tall, a.trace_step)
     torch.cuda.synchronize()
     t = tall.cpu().double() / 100.0   # wall clock 100 MHz -> us
+    tab = ex.table().cpu()
+    nrb = (s.tail.layers[0].W.shape[0] + 15) // 16
+    ncb = (s.tail.layers[0].W.shape[1] + 255) // 256
+    oU = G + 1 + 2 * nrb + G // 8
     per = []
     for k in range(T - 1):
         per.append(float(t[k + 1, :, 0].median() - t[k, :, 0].median()))
@@ -81,6 +85,27 @@ def main():
         if rows:
             mid = sorted(rows, key=lambda x: x[1])[len(rows) // 2]
             print(f"{m:2d} {NAMES[m]:>11s} {mid[0]:8.1f} {mid[1]:8.1f} {mid[2]:8.1f}")
+    spread(t[:T - 1], tab, G, nrb, oU)
+
+
+def spread(t, tab, G, nrb, oU):
+    """Stamp 8 (update pass done) relative to stamp 7 per workgroup: by XCD (w % 8) and by run
+    shape (tiles, column blocks touched)."""
+    import collections
+    d = (t[:, :, 8] - t[:, :, 7]).median(dim=0).values   # per workgroup, median over steps
+    by_x = collections.defaultdict(list)
+    by_shape = collections.defaultdict(list)
+    for w in range(G):
+        u0, u1 = int(tab[oU + w]), int(tab[oU + w + 1])
+        ncbs = (u1 - 1) // nrb - u0 // nrb + 1
+        by_x[w % 8].append(float(d[w]))
+        by_shape[(u1 - u0, ncbs, u0 // nrb == 21 or (u1 - 1) // nrb == 21)].append(float(d[w]))
+    print("update pass (stamp 7 -> 8) by XCD: " + "  ".join(f"{x}: {sorted(v)[len(v) // 2]:.1f}/{max(v):.1f}" for x, v in sorted(by_x.items())))
+    for k, v in sorted(by_shape.items()):
+        print(f"  run {k[0]} tiles, {k[1]} column block(s), touches the 32-wide block: {k[2]!s:5s} "
+              f"n={len(v):3d} median {sorted(v)[len(v) // 2]:.1f} max {max(v):.1f}")
+    slow = sorted(range(G), key=lambda w: -float(d[w]))[:8]
+    print("slowest: " + ", ".join(f"w{w} ({float(d[w]):.1f})" for w in slow))
 
 
 if __name__ == "__main__":
