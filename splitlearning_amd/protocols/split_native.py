@@ -130,6 +130,8 @@ def persistent_vanilla_ok(sess, cid: int) -> bool:
     earlier failure of the persistent executor in this session."""
     if getattr(sess.args, "split_persist", "auto") == "off" or sess.__dict__.get("_va_off"):
         return False
+    if getattr(sess.comm, "host_staging", False):
+        return False   # ranks share this GPU (--ranks_share_gpu): 256 co-resident workgroups are not assured
     if not native_split_ok(sess, cid, "vanilla") or not hasattr(sess.ops.C(), "VanillaEpoch"):
         return False
     a = sess.alices[cid]

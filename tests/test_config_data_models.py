@@ -241,3 +241,22 @@ def test_act_label_message_pack_roundtrip(dtype, B):
     if dtype == torch.float32:
         # csrc/split.cpp act_msg_words: M * 5408 + 2 M floats rounded up to 4
         assert Session.packed_len(B, dtype) == (B * CUT_FEATURES + 2 * B + 3) // 4 * 4
+
+
+def test_split_persist_flag_and_cpu_decision(tmp_path):
+    """--split_persist defaults to auto; the persistent vanilla epoch is never chosen off the GPU
+    (csrc/vanilla.hip needs 256 co-resident workgroups), so CPU sessions keep the Python loop."""
+    import torch
+    from splitlearning_amd.config import parse_args
+    from splitlearning_amd.data.mnist import write_shards
+    from splitlearning_amd.parallel.dist import Comm, Placement
+    from splitlearning_amd.protocols import VanillaSession
+    from splitlearning_amd.protocols.split_native import persistent_vanilla_ok
+    assert parse_args(["--vanilla"]).split_persist == "auto"
+    assert parse_args(["--vanilla", "--split_persist", "off"]).split_persist == "off"
+    args = parse_args(["--vanilla", "--world_size", "2", "--num_samples", "300", "--no_tqdm",
+                       "--datapath", str(tmp_path / "d"), "--log_dir", str(tmp_path / "l")])
+    write_shards(args, verbose=False)
+    dev = torch.device("cpu")
+    s = VanillaSession(args, Comm(0, 1, dev, Placement.make(2, 1, 1)), dev)
+    assert not persistent_vanilla_ok(s, 1)
