@@ -30,13 +30,15 @@
 //      the pool / ReLU backward (the argmax and value kept in VGPRs since the forward), the
 //      10 conv gradients of (c, g) -> CWP, arrival on CW[c]; every job of channel c then sums
 //      the 8 pairs' partials in order and applies the same SGD-momentum step (no owner, no
-//      second hand-off), and runs the forward of batch i + 1 for (c, g) -> X, seam X.
+//      second hand-off), and runs the forward of batch i + 1 for (c, g) -> its activation
+//      slot, seam X.
 //   V  the forward pass of batch i + 1 (row-major runs, hybrid.hip's look-ahead product on
 //      the updated tiles staged through LDS) -> LA partials, arrivals on R[rb].
 // A prologue runs Alice's forward of batch 0 and the forward pass V of it.  Tiles written by
 // one workgroup's update run are read by another's forward run: every fc1 store is write-
-// through (sc1) and drained before the arrival that orders it, and every fc1 / X load is an
-// sc1 load (MI355X_MICROARCH.md, the valid-forms table row 1).  All sums run in a fixed order:
+// through (sc1) and drained before the arrival that orders it, and every fc1 load is an sc1
+// load (MI355X_MICROARCH.md, the valid-forms table row 1).  Each step's activation has its own
+// slot in the launch (written once, before any read), so it is read with plain loads.  All sums run in a fixed order:
 // a launch is deterministic and one launch of S steps is bitwise S one-step launches.
 #include "vanilla.h"
 #include "persist.h"
@@ -328,7 +330,7 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
       }
     y = fmaxf(best, 0.f);
   };
-  // forward of step `step` for this job -> X[step & 1]; keeps (y, arg) for the backward
+  // forward of step `step` for this job -> activation slot `step`; keeps (y, arg) for the backward
   float cy = 0.f;
   int carg = 0;
   auto conv_fwd = [&](int step) {
