@@ -330,6 +330,10 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
       }
     y = fmaxf(best, 0.f);
   };
+  // activation slot layout [K1 / 16][16 m][16 k] per step: the forward pass's MFMA A operand
+  // (row m = lane % 16, four consecutive k) is then one contiguous 1 KB per wave load (row-major
+  // [16][K1], 16 rows x 64 B per load, cost ~7 us of the 32 us forward pass)
+  auto xoff = [&](int step, int m, int k) { return ((step * (K1 >> 4) + (k >> 4)) * 16 + m) * 16 + (k & 15); };
   // forward of step `step` for this job -> activation slot `step`; keeps (y, arg) for the backward
   float cy = 0.f;
   int carg = 0;
@@ -344,7 +348,7 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
       if (valid) conv_at(step & 1, bl, p, y, arg);
       cy = y;
       carg = arg;
-      hst1(rX, ((step * 16 + m) * K1 + cc * 169 + p) * 4, y);
+      hst1(rX, xoff(step, m, cc * 169 + p) * 4, y);
     }
   };
 
@@ -368,7 +372,7 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int k = cb * 256 + 16 * (r + 8 * h) + 4 * lq;
-      xv[h] = k < K1 ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rX, ((step * 16 + li) * K1 + k) * 4, 0, 0)) : zv;
+      xv[h] = k < K1 ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rX, xoff(step, li, k) * 4, 0, 0)) : zv;
     }
   };
   f32x4 zlast = zv;
@@ -482,7 +486,7 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
     for (int u = 0; u < 2; ++u) {
       const int e = tid + u * kVaThreads;
       const int m = e >> 6, k = cb * 256 + 4 * (e & 63);
-      sa[e] = k < K1 ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rX, ((step * 16 + m) * K1 + k) * 4, 0, 0)) : zv;
+      sa[e] = k < K1 ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rX, xoff(step, m, k) * 4, 0, 0)) : zv;
     }
   };
   f32x4 dacc[4];
