@@ -17,7 +17,7 @@ for spec in "n1:" "va:--mode vanilla --steps 3" "vaoff:--mode vanilla --split_pe
   tail -1 gpurun_out/$OUT/bench_$name.json | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$name', d['value'], d['ms_per_step'], d['config'].get('split_epochs'), d['config'].get('phase_seconds'))"
 done
 cd /tmp && export TMPDIR=/tmp
-for c in FETCH_SIZE WRITE_SIZE; do
+for c in ${PMC-FETCH_SIZE WRITE_SIZE}; do
   SL_PERSIST_WORKGROUPS=256 timeout -s KILL 150 rocprofv3 --pmc $c --kernel-trace --output-format csv -d "$R/gpurun_out/$OUT/pmc_$c" -o va -- \
     python3 "$R/scripts/vanilla_trace.py" --reps 1 --batches 400 > "$R/gpurun_out/$OUT/pmc_$c.log" 2>&1 || { echo PMC_FAIL $c; tail -5 "$R/gpurun_out/$OUT/pmc_$c.log"; exit 1; }
   echo pmc $c done
