@@ -3,7 +3,8 @@
 * the native SISA server epoch (`_C.ServerEpoch`: fc1 look-ahead inside the fused
   wgrad+Adam kernel, 128 optimizer steps) against `model2_sisa` trained by
   `torch.optim.Adam(lr, weight_decay=1e-5)` (data_entities_vanilla_sisa.py:266,305-313);
-* the vanilla `split_epoch` (Alice's deferred in-kernel update, Bob's look-ahead) against the
+* the vanilla `split_epoch` (the persistent vanilla epoch, csrc/vanilla.hip, one launch per
+  batch here) against the
   composed `model1_sisa` + `model2_sisa` with two `torch.optim.SGD(momentum=0.9)`
   (data_entities_vanilla.py:37-42,66-76).
 Dropout masks are the framework's counter hash (`ops/rng.keep_mask`), regenerated for the
@@ -182,6 +183,9 @@ def test_vanilla_split_epoch_matches_composed_torch_sgd(cuda, tmp_path):
             torch.testing.assert_close(e, p.detach(), rtol=1e-4, atol=1e-4, msg=f"batch {i} {name}")
     torch.cuda.synchronize()
     assert bslot.t == -(-n // 16)
+    # every batch above ran as a one-step launch of the persistent vanilla epoch
+    # (csrc/vanilla.hip; the co-located default), so this pins that kernel to torch per step
+    assert sess.native_split_epochs.get("persistent") == -(-n // 16), sess.native_split_epochs
 
 
 class _BF16Linear(torch.autograd.Function):
