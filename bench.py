@@ -268,6 +268,11 @@ def main(argv=None):
         ref_t = sum(r["samples"] / rates[_phase_kind(sargs.mode, r["phase"])] for r in recs
                     if _phase_kind(sargs.mode, r["phase"]) is not None)
         base = samples / ref_t
+    # after the clock: is what the adopted server executor computed right?  (every rank joins;
+    # the persistent executor replays a slice against launch-per-stage from one snapshot, the
+    # replicated fc3 is compared across Bob ranks; the job's state is restored afterwards)
+    from splitlearning_amd.engine.resident import validate
+    val = validate(sess)
     sent = comm.gather_obj((comm.bytes_sent - b0) // max(1, a.steps), 0)
     sess._split_counts_all = comm.gather_obj(dict(getattr(sess, "native_split_epochs", {})), 0)
     if rank == 0:
@@ -309,6 +314,10 @@ def main(argv=None):
                 # a persistent epoch that failed mid-launch: rolled back, the job continued on
                 # launch-per-stage from that client epoch on ({from, epoch, reason}; None: none)
                 "server_executor_fallback": (getattr(sess, "resident_status", None) or {}).get("fallback"),
+                # the post-run self-check (engine/resident.validate): None = nothing to check
+                # for this mode; details: replayed steps, loss / fc3 gaps, fc3 replicas equal
+                "validated": val.get("validated"),
+                "validation": val,
                 "calib": calib,
                 # vanilla / U-shape: the native split epochs this rank ran (co-located, or its
                 # side of a remote Alice's) and the per-batch link of the remote ones

@@ -16,6 +16,7 @@
 
 #include "common.h"
 #include "fused.h"
+#include "handoff.h"
 #include "host.h"
 
 namespace sl {
@@ -764,5 +765,53 @@ PYBIND11_MODULE(_C, m) {
     sl::g_bf16 = d == "bf16" ? 1 : 0;
   });
   m.def("get_compute_dtype", []() { return std::string(sl::g_bf16 ? "bf16" : "fp32"); });
+  // hand-off stress test (csrc/handoff.hip, tests/test_handoff_gpu.py): G workgroups x R rounds
+  // of the persistent kernels' publication primitive in `mode`; returns {mismatching words,
+  // rounds completed by the slowest workgroup, error word, kernel ms, first mismatch [7]...}
+  m.def("handoff_stress", [](int64_t G, int64_t P, int64_t R, int64_t nsrc, int64_t src_stride, int64_t mode,
+                             double busy_us, double timeout_s) {
+    sl::HoArgs a{};
+    a.P = (int)P;
+    a.R = (int)R;
+    a.nsrc = (int)nsrc;
+    a.src_stride = (int)src_stride;
+    a.mode = (int)mode;
+    const std::string why = sl::handoff_check(a, (int)G);
+    TORCH_CHECK(why.empty(), "handoff_stress: ", why);
+    int dev = 0, khz = 0;
+    TORCH_CHECK(hipGetDevice(&dev) == hipSuccess, "device");
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) khz = 100000;
+    auto fo = at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, dev);
+    auto io = fo.dtype(at::kInt);
+    at::Tensor D = at::zeros({G * P}, fo), S = at::zeros({G * sl::kHoScratchF4 * 4}, fo);
+    at::Tensor cnt = at::zeros({2 * 8 * sl::kHoStride}, io), bad = at::zeros({G}, io), done = at::zeros({G}, io);
+    at::Tensor first = at::zeros({8}, io), err = at::zeros({1}, io);
+    a.D = D.data_ptr<float>();
+    a.scratch = S.data_ptr<float>();
+    a.cnt = reinterpret_cast<unsigned*>(cnt.data_ptr<int>());
+    a.bad = reinterpret_cast<unsigned*>(bad.data_ptr<int>());
+    a.done = reinterpret_cast<unsigned*>(done.data_ptr<int>());
+    a.first = reinterpret_cast<unsigned*>(first.data_ptr<int>());
+    a.err = err.data_ptr<int>();
+    a.timeout = (int64_t)(timeout_s * 1000.0 * khz);
+    a.busy_ticks = (int)(busy_us * khz / 1000.0);
+    const hipStream_t st = cur_stream();
+    hipEvent_t e0, e1;
+    TORCH_CHECK(hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess, "events");
+    TORCH_CHECK(hipEventRecord(e0, st) == hipSuccess, "event");
+    check(sl::handoff_stress_launch(a, (int)G, st), "handoff_stress");
+    TORCH_CHECK(hipEventRecord(e1, st) == hipSuccess, "event");
+    TORCH_CHECK(hipEventSynchronize(e1) == hipSuccess, "handoff_stress sync");
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, e0, e1);
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    const int64_t nbad = bad.to(at::kLong).sum().item<int64_t>();
+    const int64_t rmin = done.min().item<int>();
+    std::vector<int64_t> f(7);
+    auto fc = first.cpu();
+    for (int i = 0; i < 7; ++i) f[i] = (int64_t)(uint32_t)fc.data_ptr<int>()[i];
+    return pybind11::make_tuple(nbad, rmin, err.item<int>(), (double)ms, f);
+  });
   m.attr("arch") = "gfx950";
 }

@@ -250,11 +250,14 @@ class HybridEpoch {
       tan = (int)(trace_all->numel() / (16LL * a_.G));
     }
     const hipStream_t st = c10::hip::getCurrentHIPStream().stream();
-    // one clear of the error word per epoch: a chunk whose wait gave up leaves it set, and every
-    // later chunk's waits then give up at once (no work is done on a half-updated shard)
+    // one clear of the error word per epoch; a chunk whose wait gave up leaves it set, and the
+    // host reads it before issuing the next chunk (one sync per chunk of thousands of steps), so
+    // no later chunk runs on a half-updated shard (the kernels only read the word inside a wait
+    // that is not already met, so they cannot be relied on to stop by themselves)
     TORCH_CHECK(hipMemsetAsync(a_.err, 0, sizeof(int), st) == hipSuccess, "hybrid error word");
     const int64_t cs = std::max<int64_t>(1, max_steps_);
     for (int64_t s0 = 0; s0 < S; s0 += cs) {
+      if (s0 > 0 && err_.item<int>() != 0) break;
       const int64_t n = std::min(cs, S - s0);
       sl::HyArgs a = a_;
       a.S = (int)n;

@@ -114,6 +114,17 @@ __device__ __forceinline__ bool va_wait_many(const VaArgs& a, int n, int* s_ok, 
 }
 
 constexpr int kSt = 16;   // fc1 W / buf loads and stores: sc1 (write-through stores, L1-bypassing loads)
+constexpr int kVaFwdRing = 4;   // forward-pass register ring depth (tiles; kVaFwdRing - 1 in flight)
+
+// f(integral_constant<int, I>) for I in [B, E): compile-time ring and buffer indices in the
+// unrolled tile loops
+template <int B, int E, typename F>
+__device__ __forceinline__ void va_static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    va_static_for<B + 1, E>(f);
+  }
+}
 
 // LDS carve (bytes)
 constexpr int PW2 = 4 * kVaMaxWC4 + 1;
@@ -380,18 +391,28 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
     VA_IDX();
     hst4(rHB, bZP + (((w * kVaRuns + k) * 8 + r) * 64 + lane) * 16, z);
   };
+  // The forward pass keeps kVaFwdRing - 1 tiles of W (sc1 loads: tiles another workgroup's
+  // update run just wrote) and x in flight in a register ring, every load issued after the
+  // seam-X wait that orders it (all of the step's fc1 stores drained before any conv job
+  // arrived, docs/PERF.md round 6); ring slot = tile index % kVaFwdRing, LDS staging buffer =
+  // tile index % 2, both compile-time in the unrolled loop.  Same products in the same order
+  // at every depth: the depth changes timing only, never a bit of the result.
   auto fwd_pass = [&](int step) {
     if (nt <= 0) return;
-    // the x operand too is loaded one tile ahead (loaded in its own tile, its latency was
-    // exposed once per tile)
-    f32x4 xv2[2][2];
-    load_w(t_begin, sp[0]);
-    load_xv(step, t_begin, xv2[0]);
+    constexpr int D = kVaFwdRing;
+    static_assert(D >= 2 && D % 2 == 0, "ring depth: even, >= 2");
+    f32x4 wr[D][2], xr[D][2];
+#pragma unroll
+    for (int d = 0; d < D - 1; ++d)
+      if (d < nt) {
+        load_w(t_begin + d, wr[d]);
+        load_xv(step, t_begin + d, xr[d]);
+      }
     __syncthreads();
     f32x4 z = zv;
     int kz = 0;
     auto tile = [&](auto cur_c, int j) {
-      constexpr int cur = decltype(cur_c)::value, nb = cur ^ 1;
+      constexpr int cur = decltype(cur_c)::value, nx = (cur + D - 1) % D, lb = cur & 1;
       const int t = t_begin + j;
       const int rb = t / ncb, cb = t - (t / ncb) * ncb;
       const int kr = rb - rbA;
@@ -400,30 +421,29 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
         z = zv;
         kz = kr;
       }
-      if (j + 1 < nt) {
-        load_w(t + 1, sp[nb]);
-        load_xv(step, t + 1, xv2[nb]);
+      if (j + D - 1 < nt) {
+        load_w(t + D - 1, wr[nx]);
+        load_xv(step, t + D - 1, xr[nx]);
       }
       VA_IDX();
       const int n1 = 16 * rb + r;
       const int k = cb * 256 + 4 * lane;
       const bool kin = k < K1;
-      sw[cur * 1040 + r * 65 + lane] = (kin && n1 < N1) ? sp[cur][0] : zv;
-      sw[cur * 1040 + (r + 8) * 65 + lane] = (kin && n1 + 8 < N1) ? sp[cur][1] : zv;
+      sw[lb * 1040 + r * 65 + lane] = (kin && n1 < N1) ? wr[cur][0] : zv;
+      sw[lb * 1040 + (r + 8) * 65 + lane] = (kin && n1 + 8 < N1) ? wr[cur][1] : zv;
       __syncthreads();
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const f32x4 wv4 = sw[cur * 1040 + li * 65 + 4 * (r + 8 * h) + lq];
+        const f32x4 wv4 = sw[lb * 1040 + li * 65 + 4 * (r + 8 * h) + lq];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) z = __builtin_amdgcn_mfma_f32_16x16x4f32(xv2[cur][h][c], wv4[c], z, 0, 0, 0);
+        for (int c = 0; c < 4; ++c) z = __builtin_amdgcn_mfma_f32_16x16x4f32(xr[cur][h][c], wv4[c], z, 0, 0, 0);
       }
     };
     int j = 0;
-    for (; j + 1 < nt; j += 2) {
-      tile(std::integral_constant<int, 0>{}, j);
-      tile(std::integral_constant<int, 1>{}, j + 1);
-    }
-    if (j < nt) tile(std::integral_constant<int, 0>{}, j);
+    for (; j + D - 1 < nt; j += D) va_static_for<0, D>([&](auto dc) { tile(dc, j + decltype(dc)::value); });
+    va_static_for<0, D - 1>([&](auto dc) {
+      if (j + decltype(dc)::value < nt) tile(dc, j + decltype(dc)::value);
+    });
     zlast = z;
   };
   // the run's forward partials for step so (hybrid.hip's flush): each row block's partial (the

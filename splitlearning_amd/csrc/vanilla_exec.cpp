@@ -202,6 +202,8 @@ class VanillaEpoch {
     const int64_t cs = std::min<int64_t>(S, max_steps_);
     xr_ = at::empty({cs * 16 * a_.K1}, at::TensorOptions().dtype(at::kFloat).device(dev));
     for (int64_t s0 = 0; s0 < S; s0 += cs) {
+      // a chunk whose wait gave up stops the epoch here (host check between chunks, as HybridEpoch)
+      if (s0 > 0 && err_.item<int>() != 0) break;
       const int64_t ns = std::min(cs, S - s0);
       sl::VaArgs a = a_;
       a.S = (int)ns;

@@ -107,9 +107,7 @@ def probe(tail, slot, B: int, kind: str = "resident") -> int:
     if not dev_w <= PROBE_REL_TOL * upd + 1e-12:
         raise RuntimeError(f"fc3 after the probe epoch differs from the launch-per-stage executor's "
                            f"({dev_w:.3g} vs an update of {upd:.3g})")
-    bits = pt.layers[2].W.detach().reshape(-1).view(torch.int32).to(torch.int64)
-    mult = torch.arange(1, bits.numel() + 1, device=dev, dtype=torch.int64) % 1000003
-    return int(((bits * mult) % ((1 << 61) - 1)).sum().item())
+    return fingerprint(pt.layers[2].W)
 
 
 def _coll_device():
@@ -226,6 +224,7 @@ class Failsafe:
         if len(f) == 3 and int(f[0]) == tail.tp_rank and int(f[1]) == idx:
             ex.set_fault_step(int(f[2]))
         err = None
+        fatal = None
         self.loss = None
         try:
             if kind == "resident":
@@ -234,14 +233,30 @@ class Failsafe:
                 self.loss = tail.run_hybrid_epoch(acts, labels, slot, B, step_rows)
         except RuntimeError as e:
             if "in-launch wait gave up" not in str(e) or not self.enabled:
-                raise
-            err = str(e).splitlines()[0][:200]
-        failed = err is not None
+                fatal = e
+            else:
+                err = str(e).splitlines()[0][:200]
+        if fatal is None and err is None and self.enabled:
+            # a launch that finished but produced garbage (a non-finite loss, or a non-finite
+            # value anywhere in the shard) is rolled back like one that timed out: the
+            # snapshot is the pre-epoch state, and launch-per-stage re-runs the epoch
+            bad = self.nonfinite(tail, slot, self.loss)
+            if bad:
+                err = f"non-finite result after the launch ({bad})"
+        # 0 = ok, 1 = recoverable on this rank, 2 = fatal on this rank.  Every rank joins the
+        # agreement before anything is raised, so a fatal error ends every Bob rank together
+        # instead of leaving the others blocked in this all-reduce
+        code = 2 if fatal is not None else (1 if err is not None else 0)
         if tail.tp_size > 1:
             import torch.distributed as dist
-            flag = torch.tensor([1 if failed else 0], dtype=torch.int32, device=_coll_device())
+            flag = torch.tensor([code], dtype=torch.int32, device=_coll_device())
             dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
-            failed = int(flag.item()) > 0
+            code = int(flag.item())
+        if fatal is not None:
+            raise fatal
+        if code == 2:
+            raise RuntimeError(f"{kind} server epoch {idx}: another Bob rank's persistent launch failed fatally")
+        failed = code > 0
         if not failed:
             return True
         tail.restore_state(slot, self.snap)
@@ -251,6 +266,24 @@ class Failsafe:
         warnings.warn(f"{kind} server epoch {idx} failed ({why}); shard restored, continuing on launch-per-stage")
         self.fallback = {"from": kind, "epoch": idx, "reason": why}
         return False
+
+    @staticmethod
+    def nonfinite(tail, slot, loss) -> str:
+        """'' when the epoch's losses and every weight / bias / optimizer-state tensor of the
+        shard are finite, else a short description of the first offender.  One sum per tensor
+        (a NaN or an infinity anywhere makes it non-finite; no tensor-sized temporaries) and ONE
+        host sync per epoch (~0.1 ms at TP = 1 against a ~0.5 s server epoch)."""
+        ts = [("loss", loss)] if loss is not None else []
+        for L in tail.layers:
+            for nm, p in ((f"{L.spec.name}.weight", L.W), (f"{L.spec.name}.bias", L.b)):
+                ts.append((nm, p))
+                st = slot.state(nm, p)
+                ts += [(f"{nm}.{k}", st[k]) for k in sorted(st)]
+        flags = torch.isfinite(torch.stack([t.detach().sum(dtype=torch.float64) for _, t in ts])).cpu()
+        for (nm, _), ok in zip(ts, flags.tolist()):
+            if not ok:
+                return nm
+        return ""
 
 
 def rearm(tail, group=None):
@@ -266,3 +299,76 @@ def rearm(tail, group=None):
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     if ipc is not None:
         ipc.rearm(int(t.item()))
+
+
+def fingerprint(t: torch.Tensor) -> int:
+    """Integer fingerprint of a tensor's exact bits (the probe's fc3 check): equal fingerprints
+    on every rank = bitwise-equal replicas, with overwhelming probability."""
+    bits = t.detach().reshape(-1).contiguous().view(torch.int32).to(torch.int64)
+    mult = torch.arange(1, bits.numel() + 1, device=bits.device, dtype=torch.int64) % 1000003
+    return int(((bits * mult) % ((1 << 61) - 1)).sum().item())
+
+
+def validate(sess, steps: int = 32) -> dict:
+    """Self-check of a finished run (bench.py, after its timed region; collective over every
+    rank of the job): is what the adopted server executor computed right?
+
+    * Every Bob rank replays `steps` steps of its first cached client epoch twice from one
+      snapshot: on the adopted persistent executor (resident / hybrid) and on the launch-per-
+      stage executor, and compares the losses (rtol / atol 1e-3, as the adoption probe) and
+      the fc3 weight (within PROBE_REL_TOL of that slice's fc3 update); then restores the
+      snapshot, so the job's state is untouched.
+    * The replicated fc3 (identical on every TP rank by construction: rank-ordered sums) is
+      fingerprinted and compared across the Bob ranks.
+    Returns {validated, max_loss_diff, fc3_dev_over_update, fc3_replicas_equal, executor,
+    steps}; `validated` is the AND over all ranks (None when the mode has no server epochs)."""
+    import torch.distributed as dist
+    mode = getattr(sess, "mode", "")
+    if mode not in ("sisa", "control", "concat"):
+        return {"validated": None, "reason": f"mode {mode}: no server executor to validate"}
+    kind = getattr(sess, "server_executor", "launch_per_stage")
+    out = {"executor": kind, "steps": 0, "max_loss_diff": None, "fc3_dev_over_update": None,
+           "fc3_replicas_equal": None}
+    ok = True
+    tail = sess.tail if sess.is_bob else None
+    if tail is not None:
+        slot, B = sess.bob_slot, sess.B
+        cache = sess.activation_and_labels_cache
+        if kind in KINDS and cache:
+            acts, labels = cache[min(cache)]
+            n = min(int(labels.numel()) // B, steps) * B
+            if n >= B:
+                x = acts[:n].float().contiguous()
+                y = labels[:n].contiguous()
+                snap = tail.snapshot_state(slot)
+                w0 = tail.layers[2].W.detach().clone()
+                lp = (tail.run_resident_epoch if kind == "resident" else tail.run_hybrid_epoch)(x, y, slot, B)
+                wp = tail.layers[2].W.detach().clone()
+                tail.restore_state(slot, snap)
+                ll = _launch_per_stage_epoch(tail, slot, x, y, B)
+                wl = tail.layers[2].W.detach().clone()
+                tail.restore_state(slot, snap)
+                torch.cuda.synchronize(tail.device) if tail.device.type == "cuda" else None
+                d = (lp - ll).abs().max().item()
+                upd = (wl - w0).norm().item()
+                dev_w = (wp - wl).norm().item() / max(upd, 1e-30)
+                out.update(steps=n // B, max_loss_diff=d, fc3_dev_over_update=dev_w)
+                ok = (bool(torch.isfinite(lp).all().item()) and torch.allclose(lp, ll, rtol=1e-3, atol=1e-3)
+                      and dev_w <= PROBE_REL_TOL)
+        if tail.tp_size > 1:
+            fp = fingerprint(tail.layers[2].W)
+            dev = _coll_device()
+            lo = torch.tensor([fp], dtype=torch.int64, device=dev)
+            hi = lo.clone()
+            g = sess.comm.tp_group
+            dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=g)
+            dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=g)
+            same = int(lo.item()) == int(hi.item())
+            out["fc3_replicas_equal"] = same
+            ok = ok and same
+    if getattr(sess.comm, "distributed", False):
+        f = torch.tensor([1 if ok else 0], dtype=torch.int32, device=_coll_device())
+        dist.all_reduce(f, op=dist.ReduceOp.MIN)
+        ok = bool(int(f.item()))
+    out["validated"] = ok
+    return out

@@ -394,11 +394,16 @@ class SisaSession(Session):
             if (self._use_resident() or self._use_hybrid()) and n_all > 0:
                 # the whole server epoch, every client's batches in order (short final batches
                 # included), as ONE persistent-executor call: one launch (or a few, past the 2 GB
-                # input offsets) instead of one per client plus a launch-per-stage tail batch each
-                if plan is None:
+                # input offsets) instead of one per client plus a launch-per-stage tail batch each.
+                # The plan (a padded copy for several clients) is rebuilt whenever a cache tensor
+                # is not the one it was built from (storage, shape or in-place version changed),
+                # and lives only for this call
+                key = tuple((a.data_ptr(), tuple(a.shape), a._version, y.data_ptr(), y.numel(), y._version)
+                            for a, y in caches)
+                if plan is None or plan[0] != key:
                     cs = [(a if a.dtype == torch.float32 else a.float(), y) for a, y in caches]
-                    plan = self.tail.padded_plan(cs, self.B)
-                X, Y, rows = plan
+                    plan = (key, self.tail.padded_plan(cs, self.B))
+                X, Y, rows = plan[1]
                 with self.tracer.gpu_span("server_epoch[all]", samples=n_all):
                     ok = self._persistent_epoch(X.contiguous(), Y.contiguous(), rows)
                 self.comm.progress()

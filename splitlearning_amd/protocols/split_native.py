@@ -134,6 +134,14 @@ def persistent_vanilla_ok(sess, cid: int) -> bool:
         return False   # ranks share this GPU (--ranks_share_gpu): 256 co-resident workgroups are not assured
     if not native_split_ok(sess, cid, "vanilla") or not hasattr(sess.ops.C(), "VanillaEpoch"):
         return False
+    # vanilla.hip computes in exact fp32 only: a bf16 run (fp32 master weights, bf16 operands
+    # through the global compute-dtype switch) stays on the per-batch executor, whose kernels
+    # honour it, instead of silently running fp32
+    dt = getattr(sess.args, "dtype", "fp32")
+    C = sess.ops.C()
+    if dt != "fp32" or (hasattr(C, "get_compute_dtype") and C.get_compute_dtype() != "fp32"):
+        sess.__dict__["split_persist_reason"] = f"dtype {dt if dt != 'fp32' else C.get_compute_dtype()}: fp32 only"
+        return False
     a = sess.alices[cid]
     return (1 <= sess.B <= 16 and a.slot.cfg.kind == "sgd" and sess.bob_slot(cid).cfg.kind == "sgd"
             and len(sess.tail.layers) == 3 and all(L.W.dtype == torch.float32 for L in sess.tail.layers))

@@ -260,3 +260,44 @@ def test_split_persist_flag_and_cpu_decision(tmp_path):
     dev = torch.device("cpu")
     s = VanillaSession(args, Comm(0, 1, dev, Placement.make(2, 1, 1)), dev)
     assert not persistent_vanilla_ok(s, 1)
+
+
+def test_persistent_vanilla_refuses_bf16(tmp_path, monkeypatch):
+    """csrc/vanilla.hip is exact fp32 only: with --dtype bf16 (fp32 master weights, bf16 operands
+    through the global compute-dtype switch) the persistent vanilla epoch must not be chosen, and
+    the reason is reported.  The GPU-only conditions are stubbed so the dtype gate
+    itself is what decides."""
+    import torch
+    from splitlearning_amd.config import parse_args
+    from splitlearning_amd.data.mnist import write_shards
+    from splitlearning_amd.parallel.dist import Comm, Placement
+    from splitlearning_amd.protocols import VanillaSession
+    from splitlearning_amd.protocols import split_native
+
+    class _C:
+        VanillaEpoch = object
+
+        def __init__(self, dt):
+            self.dt = dt
+
+        def get_compute_dtype(self):
+            return self.dt
+
+    class _Ops:
+        def __init__(self, dt):
+            self.c = _C(dt)
+
+        def C(self):
+            return self.c
+
+    monkeypatch.setattr(split_native, "native_split_ok", lambda sess, cid, mode: True)
+    for flag, dt, want in (("fp32", "fp32", True), ("bf16", "bf16", False), ("fp32", "bf16", False)):
+        args = parse_args(["--vanilla", "--world_size", "2", "--num_samples", "300", "--no_tqdm", "--dtype", flag,
+                           "--datapath", str(tmp_path / "d"), "--log_dir", str(tmp_path / "l")])
+        write_shards(args, verbose=False)
+        dev = torch.device("cpu")
+        s = VanillaSession(args, Comm(0, 1, dev, Placement.make(2, 1, 1)), dev)
+        s.ops = _Ops(dt)
+        assert split_native.persistent_vanilla_ok(s, 1) is want, (flag, dt)
+        if not want:
+            assert "bf16" in s.__dict__.get("split_persist_reason", "")

@@ -304,7 +304,7 @@ def test_hybrid_mid_epoch_failure_rolls_back_to_launch_per_stage(cuda, monkeypat
     assert (ta.fwd_count, sa.t) == (tb.fwd_count, sb.t) == (2 * rows // B, 2 * rows // B)
 
 
-@pytest.mark.parametrize("kind", ["hybrid"])
+@pytest.mark.parametrize("kind", ["hybrid", "resident"])
 def test_tensor_parallel_mid_epoch_failure_survived_across_processes(kind):
     """T = 2 real processes on the one GPU: rank 0's persistent launch stops mid-epoch, rank 1's
     in-launch exchange times out; both ranks roll back, re-arm the peer-mapped region and finish
@@ -321,9 +321,8 @@ def test_tensor_parallel_mid_epoch_failure_survived_across_processes(kind):
 def test_resident_mid_epoch_failure_rolls_back_to_launch_per_stage(cuda, monkeypatch):
     """The same rollback on the register-resident executor (a TP = 8-wide shard's fc1, one
     process): a stalled hand-off at step 3 of the second epoch times out, the shard is restored
-    and the epoch re-runs launch-per-stage, bitwise a clean switch at that epoch.  (The T = 2
-    cross-process form of this test on the resident executor was flaky on the one-GPU box:
-    docs/PERF.md, round 5.)"""
+    and the epoch re-runs launch-per-stage, bitwise a clean switch at that epoch (the T = 2
+    cross-process form is test_tensor_parallel_mid_epoch_failure_survived_across_processes)."""
     from splitlearning_amd.engine.resident import FAULT_EPOCH_ENV, Failsafe, _launch_per_stage_epoch
     B, rows, seed_base = 16, 16 * 10, 9
     spec = _spec(n1=628, p=0.5)
@@ -412,3 +411,31 @@ def test_whole_server_epoch_with_short_batches_in_one_launch(cuda, kind, n1):
     assert torch.equal(loss, torch.cat(per_step))
     for La, Lb in zip(te.layers, tw.layers):
         assert torch.equal(La.W, Lb.W) and torch.equal(La.b, Lb.b)
+
+
+@pytest.mark.parametrize("kind,n1", [("hybrid", 1252), ("resident", 628)])
+def test_nonfinite_epoch_rolls_back(cuda, kind, n1):
+    """A NaN injected into one epoch's inputs: the launch finishes, but its losses and shard are
+    non-finite; `Failsafe` restores the pre-epoch shard (bitwise) and reports the fallback, so
+    the caller re-runs that epoch launch-per-stage instead of training on garbage."""
+    from splitlearning_amd.engine.resident import Failsafe
+    B, rows, seed_base = 16, 16 * 6, 4
+    spec = _spec(n1=n1, p=0.5)
+    g = torch.Generator().manual_seed(12)
+    acts = (torch.rand(rows, 5408, generator=g) * 20).to(cuda)
+    labels = torch.randint(0, 100, (rows,), generator=g).to(cuda)
+    torch.manual_seed(19)
+    base = _MLP(spec)
+    te, slot = _engine(base, spec, cuda, seed_base, f"#nan{kind}")
+    assert te.resident_ok(slot, B) if kind == "resident" else te.hybrid_ok(slot, B)
+    fs = Failsafe(te, slot, B)
+    assert fs.run(kind, acts, labels)                       # a clean epoch is kept
+    before = [L.W.clone() for L in te.layers] + [v.clone() for st in slot.states.values() for v in st.values()]
+    counters = (te.fwd_count, slot.t)
+    bad = acts.clone()
+    bad[3 * B + 5, 100] = float("nan")                      # one element of step 3's batch
+    assert not fs.run(kind, bad, labels)
+    assert fs.fallback["epoch"] == 1 and "non-finite" in fs.fallback["reason"], fs.fallback
+    after = [L.W for L in te.layers] + [v for st in slot.states.values() for v in st.values()]
+    assert all(torch.equal(x, y) for x, y in zip(before, after))
+    assert (te.fwd_count, slot.t) == counters

@@ -72,3 +72,6 @@ def test_bench_eight_ranks_gloo(tmp_path, mode):
               ("local_training", "server_training", "eval_breakdown", "unlearn_local", "server_retraining"))
     for p in phases:
         assert p in c["phase_seconds"], p
+    # the post-run self-check: the replicated fc3 agrees bitwise across the 8 Bob ranks
+    assert c["validated"] is True, c["validation"]
+    assert c["validation"]["fc3_replicas_equal"] is True
