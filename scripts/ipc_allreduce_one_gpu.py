@@ -22,8 +22,11 @@ def worker(rank, world, port):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    torch.cuda.set_device(0)
-    dev = torch.device("cuda", 0)
+    # SL_RANK_DEVICES=D: rank r on cuda:(r % D) (tests/test_multi_gpu.py: the same protocol across
+    # devices, over xGMI); default 1: every rank shares cuda:0
+    ndev = int(os.environ.get("SL_RANK_DEVICES", "1"))
+    torch.cuda.set_device(rank % ndev)
+    dev = torch.device("cuda", rank % ndev)
     from splitlearning_amd.parallel.rccl import make_ipc_allreduce
     ipc = make_ipc_allreduce(list(range(world)), rank)
     print(f"rank {rank}: ipc allreduce {'up' if ipc is not None else 'unavailable'}", flush=True)

@@ -35,8 +35,11 @@ def worker(rank, world, port, kind):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    torch.cuda.set_device(0)
-    dev = torch.device("cuda", 0)
+    # SL_RANK_DEVICES=D: rank r on cuda:(r % D) (tests/test_multi_gpu.py: the same protocol across
+    # devices, over xGMI); default 1: every rank shares cuda:0
+    ndev = int(os.environ.get("SL_RANK_DEVICES", "1"))
+    torch.cuda.set_device(rank % ndev)
+    dev = torch.device("cuda", rank % ndev)
     from splitlearning_amd import ops
     from splitlearning_amd.engine import OptSlot, TailEngine, adam
     from splitlearning_amd.engine.resident import FAULT_EPOCH_ENV, Failsafe, _launch_per_stage_epoch
@@ -62,7 +65,7 @@ def worker(rank, world, port, kind):
     def engine(tag):
         t = TailEngine(copy.deepcopy(base), spec, dev, tp_rank=rank, tp_size=world, allreduce=ipc_allreduce(ipc),
                        seed_base=seed_base, ws_tag=tag)
-        t.resident_workgroups = 256 // world
+        t.resident_workgroups = 256 // world if ndev == 1 else 0
         t.resident_timeout_s = 2.0
         s = OptSlot(adam(1e-3, 1e-5))
         for L in t.layers:

@@ -27,8 +27,11 @@ def worker(rank, world, port, kind):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    torch.cuda.set_device(0)
-    dev = torch.device("cuda", 0)
+    # SL_RANK_DEVICES=D: rank r on cuda:(r % D) (tests/test_multi_gpu.py: the same protocol across
+    # devices, over xGMI); default 1: every rank shares cuda:0
+    ndev = int(os.environ.get("SL_RANK_DEVICES", "1"))
+    torch.cuda.set_device(rank % ndev)
+    dev = torch.device("cuda", rank % ndev)
     from splitlearning_amd import ops
     from splitlearning_amd.engine import OptSlot, TailEngine, adam
     from splitlearning_amd.models.zoo import LinearSpec, TailSpec, _MLP
@@ -51,7 +54,7 @@ def worker(rank, world, port, kind):
         base = _MLP(spec)
         mine = TailEngine(copy.deepcopy(base), spec, dev, tp_rank=rank, tp_size=world, allreduce=ipc_allreduce(ipc),
                           seed_base=seed_base)
-        mine.resident_workgroups = 256 // world
+        mine.resident_workgroups = 256 // world if ndev == 1 else 0
         mine.resident_timeout_s = 5.0
         slot = OptSlot(adam(1e-3, 1e-5))
         ok = mine.hybrid_ok(slot, B) if kind == "hybrid" else mine.resident_ok(slot, B)

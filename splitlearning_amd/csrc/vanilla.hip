@@ -37,8 +37,10 @@
 // A prologue runs Alice's forward of batch 0 and the forward pass V of it.  Tiles written by
 // one workgroup's update run are read by another's forward run: every fc1 store is write-
 // through (sc1) and drained before the arrival that orders it, and every fc1 load is an sc1
-// load (MI355X_MICROARCH.md, the valid-forms table row 1).  Each step's activation has its own
-// slot in the launch (written once, before any read), so it is read with plain loads.  All sums run in a fixed order:
+// load (MI355X_MICROARCH.md, the valid-forms table row 1).  The activation slots are handed
+// off the same way (sc1 stores by the conv jobs, sc1 loads after seam X): every load of
+// handed-off bytes in this kernel is an sc1 load, as the row requires (plain loads of an sc1-
+// stored payload read stale L1 lines: csrc/handoff.hip mode 2).  All sums run in a fixed order:
 // a launch is deterministic and one launch of S steps is bitwise S one-step launches.
 #include "vanilla.h"
 #include "persist.h"
@@ -383,7 +385,7 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int k = cb * 256 + 16 * (r + 8 * h) + 4 * lq;
-      xv[h] = k < K1 ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rX, xoff(step, li, k) * 4, 0, 0)) : zv;
+      xv[h] = k < K1 ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rX, xoff(step, li, k) * 4, 0, kSt)) : zv;
     }
   };
   f32x4 zlast = zv;
@@ -506,7 +508,7 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
     for (int u = 0; u < 2; ++u) {
       const int e = tid + u * kVaThreads;
       const int m = e >> 6, k = cb * 256 + 4 * (e & 63);
-      sa[e] = k < K1 ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rX, xoff(step, m, k) * 4, 0, 0)) : zv;
+      sa[e] = k < K1 ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rX, xoff(step, m, k) * 4, 0, kSt)) : zv;
     }
   };
   f32x4 dacc[4];
