@@ -23,8 +23,8 @@ OBJ = os.path.join(HERE, "build")
 ARCH = os.environ.get("SL_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-KERNEL_SOURCES = ["conv.hip", "linear.hip", "loss.hip", "fused.hip", "gemm.hip", "ipc_ar.hip", "ipc_p2p.hip", "resident.hip", "hybrid.hip", "vanilla.hip", "handoff.hip"]
-BINDING_SOURCES = ["bindings.cpp", "comm.cpp", "engine.cpp", "split.cpp", "resident_exec.cpp", "hybrid_exec.cpp", "vanilla_exec.cpp"]
+KERNEL_SOURCES = ["conv.hip", "linear.hip", "loss.hip", "fused.hip", "gemm.hip", "ipc_ar.hip", "ipc_p2p.hip", "resident.hip", "hybrid.hip", "vanilla.hip", "handoff.hip", "ushape.hip"]
+BINDING_SOURCES = ["bindings.cpp", "comm.cpp", "engine.cpp", "split.cpp", "resident_exec.cpp", "hybrid_exec.cpp", "vanilla_exec.cpp", "ushape_exec.cpp"]
 
 
 def so_path() -> str:

@@ -712,6 +712,7 @@ void sl_register_split(pybind11::module& m);
 void sl_register_resident(pybind11::module& m);
 void sl_register_hybrid(pybind11::module& m);
 void sl_register_vanilla(pybind11::module& m);
+void sl_register_ushape(pybind11::module& m);
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "splitlearning_amd gfx950 (MI355X) HIP kernels";
@@ -721,6 +722,7 @@ PYBIND11_MODULE(_C, m) {
   sl_register_resident(m);
   sl_register_hybrid(m);
   sl_register_vanilla(m);
+  sl_register_ushape(m);
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_local_step", &conv_local_step);
   m.def("conv_bwd_step", &conv_bwd_step);

@@ -212,6 +212,94 @@ def run_persistent_vanilla_epoch(sess, cid: int, order: torch.Tensor) -> bool:
     return True
 
 
+# ---------------------------------------------------------------------- persistent U-shape epoch
+def persistent_ushape_ok(sess, cid: int) -> bool:
+    """Whether `run_persistent_ushape_epoch` may drive this epoch: the co-located native
+    conditions, Adam on both sides, fp32 compute, batches of at most 16 rows, the flag, and no
+    earlier failure of the persistent executor in this session."""
+    if getattr(sess.args, "split_persist", "auto") == "off" or sess.__dict__.get("_us_off"):
+        return False
+    if getattr(sess.comm, "host_staging", False):
+        return False   # ranks share this GPU (--ranks_share_gpu): 256 co-resident workgroups are not assured
+    if not native_split_ok(sess, cid, "ushape") or not hasattr(sess.ops.C(), "UShapeEpoch"):
+        return False
+    dt = getattr(sess.args, "dtype", "fp32")
+    C = sess.ops.C()
+    if dt != "fp32" or (hasattr(C, "get_compute_dtype") and C.get_compute_dtype() != "fp32"):
+        sess.__dict__["split_persist_reason"] = f"dtype {dt if dt != 'fp32' else C.get_compute_dtype()}: fp32 only"
+        return False
+    a = sess.alices[cid]
+    return (1 <= sess.B <= 16 and a.slot.cfg.kind == "adam" and sess.bob_slot(cid).cfg.kind == "adam"
+            and len(sess.tail.layers) == 2 and all(L.W.dtype == torch.float32 for L in sess.tail.layers))
+
+
+def _six(slot, name: str, W: torch.Tensor, b: torch.Tensor) -> dict:
+    sw, sb = slot.state(name + ".weight", W), slot.state(name + ".bias", b)
+    return {"W": W, "m": sw["m"], "v": sw["v"], "b": b, "mb": sb["m"], "vb": sb["v"]}
+
+
+def _adam(cfg) -> dict:
+    return {"lr": cfg.lr, "beta1": cfg.beta1, "beta2": cfg.beta2, "eps": cfg.eps, "wd": cfg.weight_decay}
+
+
+def _us_cfg(sess, cid: int) -> dict:
+    a = sess.alices[cid]
+    a.front.flush()
+    w, b = a.front.params
+    H = a.head.layers[0]
+    bslot = sess.bob_slot(cid)
+    L1, L2 = sess.tail.layers
+    return {"fc1": _six(bslot, L1.spec.name, L1.W, L1.b), "fc2": _six(bslot, L2.spec.name, L2.W, L2.b),
+            "conv": _six(a.slot, "front.conv", w, b), "head": _six(a.slot, f"head.{H.spec.name}", H.W, H.b),
+            "bob_opt": _adam(bslot.cfg), "alice_opt": _adam(a.slot.cfg),
+            "x": a.train.x, "y": a.train.y, "B": sess.B,
+            "timeout_s": float(getattr(sess.args, "persist_timeout_s", 30.0)),
+            "workgroups": int(os.environ.get("SL_PERSIST_WORKGROUPS", "0"))}
+
+
+def run_persistent_ushape_epoch(sess, cid: int, order: torch.Tensor) -> bool:
+    """One U-shape epoch of a co-located Alice_cid as ONE launch (`_C.UShapeEpoch`,
+    csrc/ushape.hip: every parameter and Adam moment of model1 / model2 / model3 on-chip).
+    Fail-safe as `run_persistent_vanilla_epoch`: parameters and moments are copied first; a
+    failed launch restores them, switches the persistent executor off for the session
+    (`split_persist_fallback`) and returns False, so the caller runs the epoch per batch."""
+    cfg = _us_cfg(sess, cid)
+    ex = sess.ops.C().UShapeEpoch(cfg)
+    if not ex.ok():
+        sess.__dict__["_us_off"] = True
+        sess.__dict__["split_persist_reason"] = ex.why()
+        return False
+    a = sess.alices[cid]
+    order = order.to(sess.device, torch.int64).contiguous()
+    state = [t for k in ("fc1", "fc2", "conv", "head") for t in cfg[k].values()]
+    snap = [t.clone() for t in state] if getattr(sess.args, "persistent_failsafe", "on") != "off" else None
+    B = sess.B
+    nb = -(-int(order.numel()) // B)
+    loss = torch.empty(max(nb, 1) * B, dtype=torch.float32, device=sess.device)
+    sess.tail._pre = None
+    if sess.__dict__.get("_us_max_steps"):
+        ex.set_max_steps(int(sess._us_max_steps))      # tests: the epoch as several launches
+    fault = sess.__dict__.pop("_us_fault_step", None)
+    if fault is not None:
+        ex.set_fault_step(int(fault))
+    try:
+        t_a, t_b = ex.run(order, loss, a.slot.t, sess.bob_slot(cid).t)
+    except RuntimeError as e:
+        if snap is None:
+            raise
+        for t, s in zip(state, snap):
+            t.copy_(s)
+        sess.__dict__["_us_off"] = True
+        sess.__dict__["split_persist_fallback"] = str(e).splitlines()[0][:200]
+        return False
+    _count(sess, "persistent")
+    a.slot.t = int(t_a)
+    _bob_done(sess, cid, t_b, sess.tail.fwd_count + nb)
+    a.head.fwd_count += nb
+    sess.__dict__["last_split_losses"] = loss[:order.numel()]
+    return True
+
+
 # ---------------------------------------------------------------------- remote placements
 def _remote_placement_ok(sess, cid: int) -> bool:
     """Conditions every rank evaluates identically (placement, flags, the link): the Alice

@@ -22,7 +22,8 @@ from ..engine.slots import OptSlot, adam
 from ..engine.tail import TailEngine
 from ..models import ClientFront, Head, ServerTailUShape, head_spec, ushape_server_spec
 from .base import AliceState, Session, _progress
-from .split_native import native_remote_role, native_split_ok, run_native_remote_epoch, run_native_split_epoch
+from .split_native import (native_remote_role, native_split_ok, persistent_ushape_ok, run_native_remote_epoch,
+                           run_native_split_epoch, run_persistent_ushape_epoch)
 
 
 class UShapeSession(Session):
@@ -140,6 +141,8 @@ class UShapeSession(Session):
         spans = [(s, min(s + B, n)) for s in range(0, n, B)]
         if not spans:
             return
+        if order is not None and persistent_ushape_ok(self, cid) and run_persistent_ushape_epoch(self, cid, order):
+            return                                # the whole epoch in one launch, state on-chip
         if order is not None and native_split_ok(self, cid, "ushape"):
             run_native_split_epoch(self, cid, order, "ushape")   # the same launches, issued from C++
             return

@@ -132,6 +132,10 @@ def test_ushape_split_epoch_matches_composed_torch_adam_every_step(cuda, tmp_pat
             _moments_close(ref.opt, p, st, f"batch {i} {name}")
     torch.cuda.synchronize()
     assert sess.bob_slot(1).t == a.slot.t == -(-n // 16)
+    # every batch above ran as a one-step launch of the persistent U-shape epoch (csrc/ushape.hip,
+    # the co-located default), so this pins that kernel to torch at every step
+    assert sess.native_split_epochs.get("persistent") == -(-n // 16), (
+        sess.native_split_epochs, sess.__dict__.get("split_persist_reason"), sess.__dict__.get("split_persist_fallback"))
 
 
 def test_ushape_lookahead_epoch_free_running_matches_torch(cuda, tmp_path):
