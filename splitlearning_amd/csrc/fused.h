@@ -38,6 +38,7 @@ struct WgGroup {
   int bf16;             // bf16 compute: dZ / A / look-ahead operands rounded to bf16 (set by wgrad_group)
   int afirst;           // load the first chunk's A / dZ before W / m / v (set by wgrad_group)
   int pol;              // W / state load and store cache policy preset (set by wgrad_group; variant 21)
+  int rt;               // row tiles per workgroup of the streaming form (set by wgrad_group; 0 = tiled form)
 };
 
 int head3_slices(int N2);

@@ -553,6 +553,152 @@ wgrad_group_kernel(WgGroup grp, int M, SlOpt o) {
   }
 }
 
+// wgrad_stream_kernel: wgrad_group_kernel's fp32 update (M <= 16 rows, look-ahead of <= 16 rows)
+// as a column walk: workgroup = (layer, 256-column block bx, a run of grp.rt consecutive 16-row
+// tiles).  The tiled form stages A (and the look-ahead's x) once per 16 x 256 tile and holds one
+// tile's W / m / v per thread, so a CU's in-flight bytes drop to nothing while a workgroup
+// stages, sums and stores; over concat's 2.6 GB fc1 state it streams at 4.4-4.7 TB/s
+// (profiles/r5w_misc/wgbench_split_concat_policy.txt).  Here A and x are staged once per run,
+// each wave takes its row's 16 dZ values in lanes 0-15 (read back with v_readlane: no LDS
+// staging, no barrier per tile without the look-ahead), and the next tile's W / m / v / dZ loads
+// are issued before the current tile's update, so every thread keeps a tile's state in flight
+// across the whole run.  Every element's sums are the tiled form's, in its order: bitwise equal.
+template <bool ADAM, bool FWDN>
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8)))
+wgrad_stream_kernel(WgGroup grp, int M, SlOpt o) {
+  __shared__ f32x4 sa[16][64];
+  __shared__ f32x4 sw[FWDN ? 16 * 65 : 1];
+  __shared__ f32x4 red[FWDN ? 16 : 1][64];
+  const int lin = (int)blockIdx.x;
+  const int li = (grp.n > 2 && lin >= grp.d[2].wb0) ? 2 : ((grp.n > 1 && lin >= grp.d[1].wb0) ? 1 : 0);
+  const int wb0 = li == 2 ? grp.d[2].wb0 : (li == 1 ? grp.d[1].wb0 : 0);
+  const bool l0 = li == 0;
+  const WgDesc L = li == 2 ? grp.d[2] : (l0 ? grp.d[0] : grp.d[1]);
+  const int kx = (L.K + 255) >> 8;
+  int local = lin - wb0;
+  if (l0 && grp.rev0) local = grp.nt0 - 1 - local;
+  const int byg = __builtin_amdgcn_readfirstlane(local / kx);
+  const int bx = local - byg * kx;
+  const int kb = bx * 256;
+  const int ny = (L.N + 15) >> 4;
+  const int t0 = byg * grp.rt, t1 = min(ny, t0 + grp.rt);
+  const int tid = threadIdx.x;
+  const int r = tid >> 6, lane = tid & 63;
+  const int k = kb + lane * 4;
+  const bool kin = k < L.K;
+  const f32x4 zv = {0.f, 0.f, 0.f, 0.f};
+  int plw = 0, pls = 0, psw = 16, pss = 16;
+  pol_aux(grp.pol, plw, pls, psw, pss);
+  const int lbytes = L.N * L.ldw * 4;   // grp.pol != 0 only for layers under 2 GB
+  // one tile's state for this thread: W / m / v of (row 16 by + r, columns k .. k + 3), and the
+  // wave's dZ[lane][16 by + r] in lanes 0-15
+  auto ld_tile = [&](int by, f32x4& p, f32x4& q0, f32x4& q1, float& dzl) {
+    const int n = by * 16 + r;
+    dzl = (lane < 16 && lane < M && n < L.N) ? L.dz[(int64_t)lane * L.ldz + n] : 0.f;
+    p = zv;
+    q0 = zv;
+    q1 = zv;
+    if (n < L.N && kin) {
+      const int64_t off = (int64_t)n * L.ldw + k;
+      if (grp.pol == 0) {
+        p = *reinterpret_cast<const f32x4*>(L.W + off);
+        q0 = *reinterpret_cast<const f32x4*>(L.s0 + off);
+        if (ADAM) q1 = *reinterpret_cast<const f32x4*>(L.s1 + off);
+      } else {
+        p = ld_pol(L.W, lbytes, (int)(off * 4), plw);
+        q0 = ld_pol(L.s0, lbytes, (int)(off * 4), pls);
+        if (ADAM) q1 = ld_pol(L.s1, lbytes, (int)(off * 4), pls);
+      }
+    }
+  };
+  f32x4 p, q0, q1;
+  float dzl;
+  ld_tile(t0, p, q0, q1, dzl);
+  // A rows (zero past M) and the look-ahead's x (MFMA A layout, lane (li, lq): x_next[li][kb +
+  // 16 wave + 4 lq ..]) of this column block, once for the whole run
+  const int xi = lane & 15, xq = lane >> 4;
+  const int kxn = kb + 16 * r + 4 * xq;
+  f32x4 xv = zv;
+  if (FWDN && l0 && xi < grp.mn && kxn < L.K) xv = *reinterpret_cast<const f32x4*>(grp.xn + (int64_t)xi * grp.ldxn + kxn);
+  sa[r][lane] = (r < M && kin) ? *reinterpret_cast<const f32x4*>(L.A + (int64_t)r * L.lda + k) : zv;
+  __syncthreads();
+  for (int by = t0; by < t1; ++by) {
+    f32x4 pn_ = zv, qn0 = zv, qn1 = zv;
+    float dzn = 0.f;
+    if (by + 1 < t1) ld_tile(by + 1, pn_, qn0, qn1, dzn);   // uniform
+    const int n0 = by * 16, n = n0 + r;
+    const bool act = n < L.N && kin;
+    f32x4 g = zv;
+    float gb = 0.f;
+    // (fully unrolled the form without the look-ahead hoists all 16 LDS reads and spills at
+    // 8 waves per SIMD; unrolled by 4 the look-ahead form spills instead)
+    if constexpr (FWDN) {
+#pragma unroll
+      for (int mm = 0; mm < 16; ++mm) {
+        const float d = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, dzl), mm));
+        g += d * sa[mm][lane];
+        gb += d;
+      }
+    } else {
+#pragma unroll 4
+      for (int mm = 0; mm < 16; ++mm) {
+        const float d = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, dzl), mm));
+        g += d * sa[mm][lane];
+        gb += d;
+      }
+    }
+    if (act) {
+      sl_opt_update4<ADAM>(o, p, g, q0, q1);
+      const int64_t off = (int64_t)n * L.ldw + k;
+      if (grp.pol != 0) {
+        const int boff = (int)(off * 4);
+        if (o.kind != 0) st_pol(L.W, lbytes, boff, p, psw);
+        st_pol(L.s0, lbytes, boff, q0, pss);
+        if (ADAM) st_pol(L.s1, lbytes, boff, q1, pss);
+      } else if (grp.wt) {
+        const int boff = (int)(off * 4);
+        if (o.kind != 0) st_wt(L.W, L.N, L.ldw, boff, p);
+        st_wt(L.s0, L.N, L.ldw, boff, q0);
+        if (ADAM) st_wt(L.s1, L.N, L.ldw, boff, q1);
+      } else {
+        if (o.kind != 0) *reinterpret_cast<f32x4*>(L.W + off) = p;
+        *reinterpret_cast<f32x4*>(L.s0 + off) = q0;
+        if (ADAM) *reinterpret_cast<f32x4*>(L.s1 + off) = q1;
+      }
+    }
+    if (FWDN && l0) {
+      // the tiled form's look-ahead, tile by tile (sw / red reuse: the barrier after red's
+      // writes follows every read of sw, the next tile's first barrier every read of red)
+      sw[r * 65 + lane] = act ? p : zv;
+      __syncthreads();
+      const f32x4 wv4 = sw[xi * 65 + 4 * r + xq];
+      f32x4 z = zv;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) z = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[i], wv4[i], z, 0, 0, 0);
+      red[r][lane] = z;
+      __syncthreads();
+      if (tid < 256) {
+        const int m = tid >> 4, nn = tid & 15;
+        float v = 0.f;
+#pragma unroll
+        for (int w = 0; w < 16; ++w) v += red[w][16 * (m >> 2) + nn][m & 3];
+        if (m < grp.mn && n0 + nn < L.N) grp.pn[((int64_t)bx * grp.mn + m) * L.N + n0 + nn] = v;
+      }
+    }
+    if (L.bias && bx == 0 && lane == 0 && n < L.N) {
+      float pb = L.bias[n], b0 = L.sb0[n], b1 = L.sb1 ? L.sb1[n] : 0.f;
+      sl_opt_update(o, pb, gb, b0, b1);
+      if (o.kind != 0) L.bias[n] = pb;
+      L.sb0[n] = b0;
+      if (L.sb1) L.sb1[n] = b1;
+    }
+    p = pn_;
+    q0 = qn0;
+    q1 = qn1;
+    dzl = dzn;
+  }
+}
+
 int head3_slices(int N2) { return max(1, (N2 / 4 + HS - 1) / HS); }
 
 static dim3 head_grid(int M, int Q) { return dim3(Q, M); }
@@ -645,6 +791,36 @@ hipError_t wgrad_group(const WgGroup& g, int M, SlOpt o, hipStream_t st) {
   if (gg.xn && (gg.mn <= 0 || gg.mn > 64 || !gg.pn)) return hipErrorInvalidValue;
   const bool fw = gg.xn != nullptr;
   const int fc = (fw && gg.mn > 16) ? 4 : (fw ? 1 : 0);
+  // The streaming form for fp32 steps of <= 16 rows: runs of 4 row tiles when that still
+  // leaves >= 1024 workgroups (2 per CU), of 2 when it leaves >= 512, else the tiled form.
+  // wgbench (us per call, tiled -> stream; profiles/r6_wg/wgbench.txt): concat's fc1 + fc2 + fc3
+  // 1,149 -> 1,002 (rt 4: 4.6 -> 5.3 TB/s of state), vanilla's 112 -> 92 (rt 4), U-shape's 30.1
+  // -> 27.5 (rt 2; rt 4 leaves 352 workgroups: 31.1).  Variant 22: -1 forces the tiled form,
+  // > 0 forces that run length.
+  int rt = g_variant[22];
+  if (rt == 0) {
+    int tiles = 0;
+    for (int i = 0; i < gg.n; ++i) tiles += ((gg.d[i].K + 255) / 256) * ((gg.d[i].N + 15) / 16);
+    rt = tiles >= 4 * 1024 ? 4 : (tiles >= 2 * 512 ? 2 : 0);
+  }
+  if (rt > 0 && !gg.bf16 && M <= 16 && fc <= 1) {
+    WgGroup gs = gg;
+    gs.rt = rt;
+    int ws = 0;
+    for (int i = 0; i < gs.n; ++i) {
+      gs.d[i].wb0 = ws;
+      ws += ((gs.d[i].K + 255) / 256) * (((gs.d[i].N + 15) / 16 + rt - 1) / rt);
+      if (i == 0) gs.nt0 = ws;
+    }
+    if (o.kind == 2) {
+      if (fw) wgrad_stream_kernel<true, true><<<ws, 1024, 0, st>>>(gs, M, o);
+      else wgrad_stream_kernel<true, false><<<ws, 1024, 0, st>>>(gs, M, o);
+    } else {
+      if (fw) wgrad_stream_kernel<false, true><<<ws, 1024, 0, st>>>(gs, M, o);
+      else wgrad_stream_kernel<false, false><<<ws, 1024, 0, st>>>(gs, M, o);
+    }
+    return hipGetLastError();
+  }
   // 2-D grid when it wastes < 10 % of its workgroups (TP = 1: 3 %, measured 1.4 us per step
   // faster there), else the 1-D grid (TP = 2 / 4 / 8: 18-55 % empty, 0.3-1.2 us faster;
   // profiles/r1_cache_ab_grid.txt)

@@ -57,6 +57,7 @@ struct UsArgs {
   int* err;                    // nonzero after a wait gave up (2: timeout)
   int64_t timeout;             // wall-clock ticks per wait
   int coop;
+  int bf16;                    // products on bf16 operands (fc1's on bf16 MFMA), fp32 accumulation and state
   int fault_step;              // tests: this step's first wait is never met; -1 off
 };
 

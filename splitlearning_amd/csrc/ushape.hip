@@ -141,7 +141,18 @@ static_assert(US_IMG % 16 == 0 && US_CV % 16 == 0 && US_W3 % 16 == 0 && US_DL % 
   const int tid = tid_l_, r = tid >> 6, lane = tid & 63, li = lane & 15, lq = lane >> 4; \
   (void)r; (void)lane; (void)li; (void)lq
 
+// BF (`--dtype bf16`): every product's operands rounded to bf16 with fp32 accumulation, as the
+// per-batch executor's bf16 kernels (linear.hip / fused.hip / loss.hip); fc1's three products on
+// bf16 MFMA (v_mfma_f32_16x16x16_bf16: one instruction per 16-column block where the fp32 form
+// issues four), the conv front in fp32 (as conv.hip), every state and moment fp32.
+typedef __bf16 us_bf16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ us_bf16x4 us_bf4(f32x4 v) {
+  return us_bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+}
+
+template <bool BF>
 __global__ void __launch_bounds__(kUsThreads) ushape_epoch_kernel(UsArgs a) {
+  auto R = [](float v) { return BF ? bfr(v) : v; };
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* sx = reinterpret_cast<float*>(smem + US_SX);
   float* sdz = reinterpret_cast<float*>(smem + US_DZ1);
@@ -329,6 +340,15 @@ __global__ void __launch_bounds__(kUsThreads) ushape_epoch_kernel(UsArgs a) {
 #pragma unroll
       for (int kb = 0; kb < kUsKB; ++kb) {
         const f32x4 xa = *reinterpret_cast<const f32x4*>(sx + li * kUsKP + 16 * kb + 4 * lq);
+        if constexpr (BF) {
+          // k = 4 lq + comp of the block: the fp32 form's four instructions as one
+          if (kb & 1)
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(us_bf4(xa), us_bf4(Wr[kb]), acc1, 0, 0, 0);
+          else
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(us_bf4(xa), us_bf4(Wr[kb]), acc0, 0, 0, 0);
+          asm volatile("" ::: "memory");
+          continue;
+        }
 #pragma unroll
         for (int comp = 0; comp < 4; ++comp) {
           if (kb & 1)
@@ -375,9 +395,9 @@ __global__ void __launch_bounds__(kUsThreads) ushape_epoch_kernel(UsArgs a) {
       f32x4 p = zv;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const float w2 = sW2[q * 128 + j];
+        const float w2 = R(sW2[q * 128 + j]);
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) p[jj] = fmaf(sh1[(4 * mg + jj) * 4 + q], w2, p[jj]);
+        for (int jj = 0; jj < 4; ++jj) p[jj] = fmaf(R(sh1[(4 * mg + jj) * 4 + q]), w2, p[jj]);
       }
       hst4(rHB, bP2 + (((par * kUsN2P + j) * kUsG + w) * 16 + 4 * mg) * 4, p);
     }
@@ -442,7 +462,7 @@ __global__ void __launch_bounds__(kUsThreads) ushape_epoch_kernel(UsArgs a) {
           const int cls = tid >> 4, part = tid & 15;
           float s = 0.f;
           if (cls < C)
-            for (int j = part; j < N2; j += 16) s = fmaf(sh2[j], sW3[cls * N2 + j], s);
+            for (int j = part; j < N2; j += 16) s = fmaf(R(sh2[j]), R(sW3[cls * N2 + j]), s);
           s = sl_row16_sum(s);
           if (part == 0) slg[cls] = s + sb3[cls];
         }
@@ -492,7 +512,7 @@ __global__ void __launch_bounds__(kUsThreads) ushape_epoch_kernel(UsArgs a) {
         const int m = 4 * mq + jj;
         float s = 0.f;
         if (j < N2)
-          for (int cls = 0; cls < C; ++cls) s = fmaf(sdl[m * kUsCP + cls], sW3[cls * N2 + j], s);
+          for (int cls = 0; cls < C; ++cls) s = fmaf(R(sdl[m * kUsCP + cls]), R(sW3[cls * N2 + j]), s);
         sdz2[m * kUsN2P + j] = sh2[m * kUsN2P + j] > 0.f ? s : 0.f;
       }
     }
@@ -502,7 +522,7 @@ __global__ void __launch_bounds__(kUsThreads) ushape_epoch_kernel(UsArgs a) {
       const int o = tid >> 3, part = tid & 7, m = o >> 2, q = o & 3;
       float s = 0.f;
 #pragma unroll
-      for (int jj = 0; jj < 16; ++jj) s = fmaf(sdz2[m * kUsN2P + part * 16 + jj], sW2[q * 128 + part * 16 + jj], s);
+      for (int jj = 0; jj < 16; ++jj) s = fmaf(R(sdz2[m * kUsN2P + part * 16 + jj]), R(sW2[q * 128 + part * 16 + jj]), s);
       s = sl_group_sum<8>(s);
       if (part == 0) sdzm[m * 4 + q] = sh1[m * 4 + q] > 0.f ? s : 0.f;
     }
@@ -526,7 +546,7 @@ __global__ void __launch_bounds__(kUsThreads) ushape_epoch_kernel(UsArgs a) {
         if (nb + 4 * cc + q < N1 && j < N2) {
           float g = 0.f;
 #pragma unroll
-          for (int m = 0; m < 16; ++m) g = fmaf(sdz2[m * kUsN2P + j], sh1[m * 4 + q], g);
+          for (int m = 0; m < 16; ++m) g = fmaf(R(sdz2[m * kUsN2P + j]), R(sh1[m * 4 + q]), g);
           res_update<true>(a.ob, ss_b, ib_b, sW2[q * 128 + j], g, sW2[512 + q * 128 + j], sW2[1024 + q * 128 + j]);
         }
       }
@@ -546,7 +566,7 @@ __global__ void __launch_bounds__(kUsThreads) ushape_epoch_kernel(UsArgs a) {
         const int cls = e / N2, j = e - cls * N2;
         float g = 0.f;
 #pragma unroll
-        for (int m = 0; m < 16; ++m) g = fmaf(sdl[m * kUsCP + cls], sh2[m * kUsN2P + j], g);
+        for (int m = 0; m < 16; ++m) g = fmaf(R(sdl[m * kUsCP + cls]), R(sh2[m * kUsN2P + j]), g);
         res_update<true>(a.oa, ss_a, ib_a, sW3[e], g, sW3[kUsW3 + e], sW3[2 * kUsW3 + e]);
       }
       if (tid >= 32 && tid < 32 + C) {
@@ -583,6 +603,19 @@ __global__ void __launch_bounds__(kUsThreads) ushape_epoch_kernel(UsArgs a) {
         const int kb = r + 8 * u;
         if (kb < kUsKB) {
           f32x4 acc0 = zv, acc1 = zv;
+          if constexpr (BF) {
+            // n = 16 t + 4 lq + c: eight bf16 instructions over the row group's 128 rows
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+              const f32x4 av = *reinterpret_cast<const f32x4*>(sdz + li * kDzP + 16 * t + 4 * lq);
+              f32x4 bv;
+#pragma unroll
+              for (int c = 0; c < 4; ++c) bv[c] = sws[(16 * t + 4 * lq + c) * kUsKP + 16 * kb + li];
+              if (t & 1) acc1 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(us_bf4(av), us_bf4(bv), acc1, 0, 0, 0);
+              else acc0 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(us_bf4(av), us_bf4(bv), acc0, 0, 0, 0);
+              asm volatile("" ::: "memory");
+            }
+          } else
 #pragma unroll
           for (int s = 0; s < 32; s += 2) {
             acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(sdz[li * kDzP + 4 * s + lq],
@@ -673,6 +706,16 @@ __global__ void __launch_bounds__(kUsThreads) ushape_epoch_kernel(UsArgs a) {
 #pragma unroll
       for (int kb = 0; kb < kUsKB; ++kb) {
         f32x4 g = zv;
+        if constexpr (BF) {
+          // the 16 batch rows m = 4 lq + c in one bf16 instruction
+          f32x4 av, bv;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            av[c] = sx[(4 * lq + c) * kUsKP + 16 * kb + li];
+            bv[c] = sdz[(4 * lq + c) * kDzP + 16 * r + li];
+          }
+          g = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(us_bf4(av), us_bf4(bv), g, 0, 0, 0);
+        } else
 #pragma unroll
         for (int t4 = 0; t4 < 4; ++t4)
           g = __builtin_amdgcn_mfma_f32_16x16x4f32(sx[(4 * t4 + lq) * kUsKP + 16 * kb + li],
@@ -766,7 +809,8 @@ bool ushape_fits(const UsArgs& a, int device, std::string* why) {
     if (hipGetDeviceProperties(&pr, device) != hipSuccess) {
       s = "device properties";
     } else {
-      const void* fn = reinterpret_cast<const void*>(&ushape_epoch_kernel);
+      const void* fn = a.bf16 ? reinterpret_cast<const void*>(&ushape_epoch_kernel<true>)
+                              : reinterpret_cast<const void*>(&ushape_epoch_kernel<false>);
       int nb = 0;
       hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kUsLds);
       if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, kUsThreads, kUsLds);
@@ -781,7 +825,8 @@ bool ushape_fits(const UsArgs& a, int device, std::string* why) {
 hipError_t ushape_epoch_launch(const UsArgs& a, hipStream_t st) {
   if (!ushape_check(a).empty()) return hipErrorInvalidValue;
   if (a.S <= 0) return hipSuccess;
-  const void* fn = reinterpret_cast<const void*>(&ushape_epoch_kernel);
+  const void* fn = a.bf16 ? reinterpret_cast<const void*>(&ushape_epoch_kernel<true>)
+                          : reinterpret_cast<const void*>(&ushape_epoch_kernel<false>);
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kUsLds);
   if (e != hipSuccess) return e;
   e = hipMemsetAsync(a.cnt, 0, (size_t)kUsCounters * kUsStride * sizeof(unsigned), st);

@@ -75,6 +75,7 @@ class UShapeEpoch {
     a.C = (int)hd_.W.size(0);
     a.M = B_;
     a.coop = wg > 0 ? 0 : 1;
+    a.bf16 = cfg.contains("bf16") && cfg["bf16"].cast<bool>() ? 1 : 0;
     a.fault_step = -1;
     a.ignore = -100;
     a.ob = us_opt(bo_, 1);

@@ -215,7 +215,7 @@ def run_persistent_vanilla_epoch(sess, cid: int, order: torch.Tensor) -> bool:
 # ---------------------------------------------------------------------- persistent U-shape epoch
 def persistent_ushape_ok(sess, cid: int) -> bool:
     """Whether `run_persistent_ushape_epoch` may drive this epoch: the co-located native
-    conditions, Adam on both sides, fp32 compute, batches of at most 16 rows, the flag, and no
+    conditions, Adam on both sides, fp32 or bf16 compute (as --dtype), batches of at most 16 rows, the flag, and no
     earlier failure of the persistent executor in this session."""
     if getattr(sess.args, "split_persist", "auto") == "off" or sess.__dict__.get("_us_off"):
         return False
@@ -225,8 +225,11 @@ def persistent_ushape_ok(sess, cid: int) -> bool:
         return False
     dt = getattr(sess.args, "dtype", "fp32")
     C = sess.ops.C()
-    if dt != "fp32" or (hasattr(C, "get_compute_dtype") and C.get_compute_dtype() != "fp32"):
-        sess.__dict__["split_persist_reason"] = f"dtype {dt if dt != 'fp32' else C.get_compute_dtype()}: fp32 only"
+    cdt = C.get_compute_dtype() if hasattr(C, "get_compute_dtype") else "fp32"
+    if dt not in ("fp32", "bf16") or cdt != dt:
+        # bf16 runs the kernel's bf16 instantiation (bf16 operands, fp32 state), but only when the
+        # compute dtype the per-batch kernels use agrees with --dtype
+        sess.__dict__["split_persist_reason"] = f"dtype {dt} with compute dtype {cdt}"
         return False
     a = sess.alices[cid]
     return (1 <= sess.B <= 16 and a.slot.cfg.kind == "adam" and sess.bob_slot(cid).cfg.kind == "adam"
@@ -254,7 +257,8 @@ def _us_cfg(sess, cid: int) -> dict:
             "bob_opt": _adam(bslot.cfg), "alice_opt": _adam(a.slot.cfg),
             "x": a.train.x, "y": a.train.y, "B": sess.B,
             "timeout_s": float(getattr(sess.args, "persist_timeout_s", 30.0)),
-            "workgroups": int(os.environ.get("SL_PERSIST_WORKGROUPS", "0"))}
+            "workgroups": int(os.environ.get("SL_PERSIST_WORKGROUPS", "0")),
+            "bf16": getattr(sess.args, "dtype", "fp32") == "bf16"}
 
 
 def run_persistent_ushape_epoch(sess, cid: int, order: torch.Tensor) -> bool:

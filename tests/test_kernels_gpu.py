@@ -288,6 +288,47 @@ def test_wgrad_group_alternating_walk_is_bit_identical(cuda, kind):
 
 
 @pytest.mark.parametrize("kind", ["sgd", "adam"])
+@pytest.mark.parametrize("rt,pol", [(1, 0), (3, 0), (8, 0), (8, 1), (40, 1)])
+@pytest.mark.parametrize("M,shapes,mn", [(16, [(1000, 5408), (200, 1000), (100, 200)], 16),
+                                         (7, [(36, 300), (10, 36)], 5), (16, [(300, 1000)], 0)])
+def test_wgrad_stream_form_is_bitwise_the_tiled_form(cuda, kind, rt, pol, M, shapes, mn):
+    """The streaming wgrad form (variant 22 = row tiles per workgroup, -1 the tiled form: A staged
+    once per column walk, the next tile's state in flight; csrc/fused.hip wgrad_stream_kernel) computes every
+    element's sums in the tiled form's order: W / states / biases / look-ahead slabs bitwise
+    equal, under the shipped and the over-the-cache store policies (variant 21)."""
+    C = hip_ops.C()
+    cfg = OptimCfg("adam", 1e-3, weight_decay=1e-5) if kind == "adam" else OptimCfg("sgd", 1e-2, momentum=0.9)
+    g = torch.Generator().manual_seed(5)
+    base = [(torch.randn(M, N, generator=g), torch.randn(M, K, generator=g), torch.randn(N, K, generator=g),
+             torch.randn(N, generator=g)) for N, K in shapes]
+    xn = torch.randn(max(mn, 1), shapes[0][1], generator=g).to(cuda)
+    outs = []
+    try:
+        for v22 in (-1, rt):
+            C.set_variant(22, v22)
+            C.set_variant(21, pol)
+            layers = []
+            for dz, a, w, b in base:
+                w, b = w.to(cuda), b.to(cuda)
+                sw = {"m": torch.full_like(w, 0.01), "v": torch.full_like(w, 0.02)} if kind == "adam" else \
+                    {"buf": torch.full_like(w, 0.01)}
+                sb = {k: torch.full_like(b, 0.01) for k in sw}
+                layers.append((dz.to(cuda), a.to(cuda), w, sw, b, sb))
+            kw = {}
+            if mn:
+                kw = {"x_next": xn[:mn], "p_next": hip_ops.lookahead_slabs(cuda, shapes[0][1], mn, shapes[0][0])}
+            hip_ops.wgrad_group_(layers, M, cfg, 3, **kw)
+            torch.cuda.synchronize()
+            outs.append([t.clone() for L in layers for t in (L[2], L[4], *L[3].values(), *L[5].values())] +
+                        ([kw["p_next"].clone()] if mn else []))
+    finally:
+        C.set_variant(22, 0)
+        C.set_variant(21, 0)
+    for x, y in zip(outs[0], outs[1]):
+        assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("kind", ["sgd", "adam"])
 def test_conv_local_epoch_matches_steps(cuda, kind):
     """The C++-looped epoch == the per-step calls (bitwise), incl. a partial last batch."""
     x = _shard(300, cuda)

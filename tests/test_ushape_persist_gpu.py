@@ -15,6 +15,10 @@ import torch
 
 from test_split_native_gpu import _session, _states
 
+from splitlearning_amd.config import parse_args
+from splitlearning_amd.data.mnist import write_shards
+from splitlearning_amd.parallel.dist import Comm, Placement
+
 pytestmark = pytest.mark.gpu
 
 
@@ -113,3 +117,55 @@ def test_persistent_ushape_long_launch_is_bitwise_chunks(cuda, tmp_path):
         assert torch.equal(a[k], b[k]), k
         assert torch.isfinite(a[k]).all(), k
     assert torch.equal(s1.last_split_losses, s2.last_split_losses)
+
+
+def _session_bf16(tmp_path, dev, persist, B=16):
+    """A U-shape session under --dtype bf16 (the per-batch kernels and the persistent kernel's
+    bf16 instantiation: bf16 operands, fp32 accumulation, state and moments)."""
+    from splitlearning_amd.protocols import UShapeSession
+    flags = ["--dtype", "bf16"] + ([] if persist else ["--split_persist", "off"])
+    args = parse_args(flags + ["--world_size", "2", "--seed", "11", "--num_samples", "900", "--no_tqdm",
+                               "--batch_size", str(B), "--datapath", str(tmp_path / "d"),
+                               "--log_dir", str(tmp_path / "logs_bf")])
+    if not (tmp_path / "d").exists():
+        write_shards(args, verbose=False)
+    return UShapeSession(args, Comm(0, 1, dev, Placement.make(2, 1, 1)), dev)
+
+
+def test_persistent_ushape_bf16_matches_per_batch_bf16(cuda, tmp_path):
+    """--dtype bf16: the persistent epoch runs (bf16 instantiation), agrees with the per-batch
+    bf16 executor within the Adam bound, differs from the fp32 persistent epoch (the bf16
+    products really ran), and one launch is bitwise its one-step launches."""
+    from splitlearning_amd.ops import hip_ops
+    from splitlearning_amd.protocols.split_native import persistent_ushape_ok
+    B = 16
+    try:
+        sp = _session_bf16(tmp_path, cuda, False)
+        sq = _session_bf16(tmp_path, cuda, True)
+        s1 = _session_bf16(tmp_path, cuda, True)
+        assert hip_ops.C().get_compute_dtype() == "bf16"
+        assert persistent_ushape_ok(sq, 1) and not persistent_ushape_ok(sp, 1)
+        order = sp.alices[1].train.shuffled_order(torch.Generator().manual_seed(4))[:B * 6 + 3].to(cuda)
+        for s in (sp, sq):
+            _epochs(s, order, B)
+        for i in range(0, order.numel(), B):
+            part = order[i:i + B]
+            s1.split_epoch(1, part, part.numel())
+        torch.cuda.synchronize()
+        assert sq.native_split_epochs.get("persistent") == 3, (sq.__dict__.get("split_persist_reason"),
+                                                               sq.__dict__.get("split_persist_fallback"))
+        _close_adam(_states(sq, "ushape"), _states(sp, "ushape"), sq.args.lr, 2 * 7 + 3, "bf16", frac=2e-2)
+        # one launch (the first epoch of sq) vs one-step launches: replay the first epoch alone
+        s2 = _session_bf16(tmp_path, cuda, True)
+        s2.split_epoch(1, order, order.numel())
+        torch.cuda.synchronize()
+        a, b = _states(s2, "ushape"), _states(s1, "ushape")
+        for k in a:
+            assert torch.equal(a[k], b[k]), k
+    finally:
+        hip_ops.C().set_compute_dtype("fp32")
+    sf = _session("ushape", tmp_path, True, cuda, B, persist=True)
+    sf.split_epoch(1, order, order.numel())
+    torch.cuda.synchronize()
+    f = _states(sf, "ushape")
+    assert any(not torch.equal(f[k], a[k]) for k in a if k.endswith(".W"))
