@@ -41,10 +41,11 @@ def main():
     ap.add_argument("--tps", type=int, nargs="+", default=[1, 2, 4, 8])
     ap.add_argument("--iters", type=int, default=100)
     ap.add_argument("--variant", action="append", default=[])
-    ap.add_argument("--case", choices=("tp", "ushape", "vanilla", "concat"), default="tp",
+    ap.add_argument("--case", choices=("tp", "ushape", "vanilla", "concat", "concat_tp8"), default="tp",
                     help="tp: the SISA tail's shards; ushape: fc1 1000 x 5408 + fc2 100 x 1000 (Adam); "
                          "vanilla: 5000 x 5408 / 1000 x 5000 / 100 x 1000 (SGD-momentum); concat: "
-                         "fc1 5000 x 43264 (k = 8, Adam)")
+                         "fc1 5000 x 43264 (k = 8, Adam); concat_tp8: its TP = 8 shard (fc1 625 x 43264, fc2 "
+                         "1000 x 625, fc3 800 x 1000)")
     a = ap.parse_args()
     if a.case != "tp":
         return other_case(a)
@@ -111,6 +112,8 @@ def other_case(a):
         shapes, cfg = [(1000, 5408), (100, 1000)], OptimCfg("adam", 1e-3, weight_decay=1e-5)
     elif a.case == "vanilla":
         shapes, cfg = [(5000, 5408), (1000, 5000), (100, 1000)], OptimCfg("sgd", 1e-2, momentum=0.9)
+    elif a.case == "concat_tp8":
+        shapes, cfg = [(628, 43264), (1000, 628), (800, 1000)], OptimCfg("adam", 1e-3, weight_decay=1e-5)
     else:
         shapes, cfg = [(5000, 43264), (1000, 5000), (800, 1000)], OptimCfg("adam", 1e-3, weight_decay=1e-5)
     adam = cfg.kind == "adam"

@@ -791,17 +791,18 @@ hipError_t wgrad_group(const WgGroup& g, int M, SlOpt o, hipStream_t st) {
   if (gg.xn && (gg.mn <= 0 || gg.mn > 64 || !gg.pn)) return hipErrorInvalidValue;
   const bool fw = gg.xn != nullptr;
   const int fc = (fw && gg.mn > 16) ? 4 : (fw ? 1 : 0);
-  // The streaming form for fp32 steps of <= 16 rows: runs of 4 row tiles when that still
-  // leaves >= 1024 workgroups (2 per CU), of 2 when it leaves >= 512, else the tiled form.
-  // wgbench (us per call, tiled -> stream; profiles/r6_wg/wgbench.txt): concat's fc1 + fc2 + fc3
-  // 1,149 -> 1,002 (rt 4: 4.6 -> 5.3 TB/s of state), vanilla's 112 -> 92 (rt 4), U-shape's 30.1
-  // -> 27.5 (rt 2; rt 4 leaves 352 workgroups: 31.1).  Variant 22: -1 forces the tiled form,
-  // > 0 forces that run length.
+  // The streaming form for fp32 steps of <= 16 rows: runs of 4 row tiles from 8,000 tiles
+  // (>= 2,000 workgroups), of 2 from 1,280, else the tiled form.  wgbench (us per call, tiled ->
+  // stream; profiles/r6_wg/): concat's fc1 + fc2 + fc3 1,149 -> 1,002 (rt 4: 4.6 -> 5.3 TB/s of
+  // state), vanilla's 112 -> 92 (rt 4), the SISA tail at TP = 1 / 2 / 4 151 / 66.5 / 37.4 -> 137 /
+  // 62.9 / 36.7 (rt 4 / 2 / 2; rt 4 at TP = 2: 68), U-shape's 30.1 -> 27.5 (rt 2); a TP = 8 shard
+  // (1,097 tiles) keeps the tiled form (22.2 against 23.8 at rt 2).  Variant 22: -1 forces the
+  // tiled form, > 0 forces that run length.
   int rt = g_variant[22];
   if (rt == 0) {
     int tiles = 0;
     for (int i = 0; i < gg.n; ++i) tiles += ((gg.d[i].K + 255) / 256) * ((gg.d[i].N + 15) / 16);
-    rt = tiles >= 4 * 1024 ? 4 : (tiles >= 2 * 512 ? 2 : 0);
+    rt = tiles >= 8000 ? 4 : (tiles >= 1280 ? 2 : 0);
   }
   if (rt > 0 && !gg.bf16 && M <= 16 && fc <= 1) {
     WgGroup gs = gg;
