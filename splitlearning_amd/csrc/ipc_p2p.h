@@ -47,6 +47,23 @@ struct P2PMsg {
   int64_t timeout;      // wall-clock ticks
 };
 
+// The pair's regions and generations handed to a persistent kernel that sends and receives a
+// run of messages itself (csrc/vanilla.hip's remote-Alice epoch): send j of the run carries
+// generation sgen0 + 1 + j, receive j rgen0 + 1 + j, each on the slot of its generation's parity
+struct P2PRun {
+  float* sdata[2];
+  uint32_t* sflag[2];
+  uint32_t* sack[2];
+  float* rdata[2];
+  uint32_t* rflag[2];
+  uint32_t* rack[2];
+  uint32_t sgen0, rgen0;
+  int sprev[2];        // chunk counts of the messages two generations before sends 0 and 1
+  int* err;
+  int* herr;
+  int64_t timeout;
+};
+
 class IpcChannel {
  public:
   // cap: the largest message (floats) this channel carries
@@ -64,6 +81,11 @@ class IpcChannel {
   // first call binds the stream; a call on another stream throws.
   void send(const float* x, int64_t n, int peer, hipStream_t st);
   void recv(float* x, int64_t n, int peer, hipStream_t st);
+  // A run of messages with `peer` that ONE kernel on stream st sends / receives itself: the
+  // floats of each send and receive, in issue order.  Checks them as send / recv would, binds
+  // the streams, and advances the pair's generations and slot history exactly as that many
+  // send / recv calls, so the channel's later messages continue the sequence.
+  P2PRun run(int peer, hipStream_t st, const std::vector<int64_t>& sends, const std::vector<int64_t>& recvs);
   bool serves(const void* p, int64_t n) const {
     return n <= cap_ && n % 4 == 0 && (reinterpret_cast<uintptr_t>(p) & 15) == 0;
   }

@@ -198,6 +198,35 @@ void IpcChannel::recv(float* x, int64_t n, int peer, hipStream_t st) {
   SL_HIP_THROW(hipGetLastError());
 }
 
+P2PRun IpcChannel::run(int peer, hipStream_t st, const std::vector<int64_t>& sends,
+                       const std::vector<int64_t>& recvs) {
+  for (int64_t n : sends) check(data_, n, peer);
+  for (int64_t n : recvs) check(data_, n, peer);
+  if (!sends.empty()) bind_stream(send_st_, send_bound_, peer, st, "send");
+  if (!recvs.empty()) bind_stream(recv_st_, recv_bound_, peer, st, "recv");
+  P2PRun r{};
+  for (int par = 0; par < 2; ++par) {
+    r.sdata[par] = peer_data_[peer] + ((int64_t)rank_ * 2 + par) * cap_;
+    r.sflag[par] = sync_[peer] + flag_off(rank_, par);
+    r.sack[par] = syncw_ + ack_off(peer, par);
+    r.rdata[par] = data_ + ((int64_t)peer * 2 + par) * cap_;
+    r.rflag[par] = syncw_ + flag_off(peer, par);
+    r.rack[par] = sync_[peer] + ack_off(rank_, par);
+  }
+  r.sgen0 = send_gen_[peer];
+  r.rgen0 = recv_gen_[peer];
+  for (int j = 0; j < 2; ++j) r.sprev[j] = hist_[2 * peer + (int)((r.sgen0 + 1u + (uint32_t)j) & 1u)];
+  for (int64_t n : sends) {
+    const uint32_t g = ++send_gen_[peer];
+    hist_[2 * peer + (int)(g & 1u)] = (int)((n + kIpcChunk - 1) / kIpcChunk);
+  }
+  recv_gen_[peer] += (uint32_t)recvs.size();
+  r.err = err_;
+  r.herr = herr_dev_;
+  r.timeout = timeout_;
+  return r;
+}
+
 int IpcChannel::error() const {
   int e = 0;
   SL_HIP_THROW(hipMemcpy(&e, err_, sizeof(int), hipMemcpyDeviceToHost));

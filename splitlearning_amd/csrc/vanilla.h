@@ -31,6 +31,24 @@ constexpr int kVaSeams = 5;         // F: fc2 partials, L: logit partials, D: dl
 constexpr int kVaMaxS = 6000;      // steps per launch (the activation slots' 32-bit offsets)
 constexpr int kVaCounters = kVaSeams * 8 + kVaMaxNC + kVaMaxRB + kVaMaxCB + 32;
 
+// A REMOTE Alice (VaArgs::rem): her conv front runs in her own process (csrc/split.cpp
+// run_alice, unchanged) and the launch speaks the peer-mapped channel's protocol
+// (csrc/ipc_p2p.h) itself: per step i it receives her activation message of step i (generation
+// rgen0 + 1 + i) and sends her the cut gradient of step i (generation sgen0 + 1 + i), each on
+// the parity slot of its generation -- the same messages, sizes and order as run_bob.
+struct VaLink {
+  float* sdata[2];          // her slot data[bob][par]: the cut gradients land there
+  uint32_t* sflag[2];       // her flag words [bob][par][chunk]
+  const uint32_t* sack[2];  // own ack words [alice][par][chunk] (she acks a cut gradient read)
+  const float* rdata[2];    // own slot data[alice][par]: her activation messages
+  const uint32_t* rflag[2]; // own flag words [alice][par][chunk]
+  uint32_t* rack[2];        // her ack words [bob][par][chunk] (acks of her activations)
+  uint32_t sgen0, rgen0;    // the pair's generations before the launch's first message
+  int sprev[2];             // chunk counts of the messages sent two generations before sends 0, 1
+  int* err;                 // the channel's error word (uncached) and its host-pinned mirror
+  int* herr;
+};
+
 struct VaArgs {
   ResLayer L1, L2, L3;    // Bob's tail (v unused: SGD-momentum)
   int N1, K1, N2, C, C4;  // fc1 rows, fc1 width (5408), fc2 rows, classes, C rounded up to 4
@@ -53,7 +71,7 @@ struct VaArgs {
   float* loss;            // [S * M] per-row losses
   int64_t ignore;
   SlOpt o;                // Bob's optimizer (SGD-momentum)
-  const float* adam;      // [S][4] {-, -, CE scale (1 / the step's rows), -}
+  const float* adam;      // [S][4] {the step's rows, -, CE scale (1 / the step's rows), -}
   const uint32_t* seeds;  // [S][4] {fc1 lo, hi, fc2 lo, hi}
   uint32_t thr1, thr2;
   float dsc1, dsc2;
@@ -78,6 +96,12 @@ struct VaArgs {
   int fault_step;         // tests: this step's first wait is never met; -1 off
   int64_t* tall;          // optional [tall_n][G][16] phase stamps (wall clock) of every workgroup
   int tall_step, tall_n;  // for steps tall_step .. tall_step + tall_n - 1
+  // remote Alice: the kernel's <true> instantiation; no conv jobs, so G may be any multiple of
+  // 8 up to 256 that the fc2 tiling allows (a one-GPU test leaves CUs to the Alice's kernels).
+  // Yrem: the launch-local [S * M] labels the kernel fills from the messages (Y unused).
+  int rem;
+  int64_t* Yrem;
+  VaLink lk;
 };
 
 hipError_t vanilla_epoch_launch(const VaArgs& a, hipStream_t st);

@@ -42,7 +42,25 @@
 // handed-off bytes in this kernel is an sc1 load, as the row requires (plain loads of an sc1-
 // stored payload read stale L1 lines: csrc/handoff.hip mode 2).  All sums run in a fixed order:
 // a launch is deterministic and one launch of S steps is bitwise S one-step launches.
+//
+// REMOTE Alice (the <true> instantiation; BASELINE config 3, where 3 of 4
+// Alices live on other GPUs; reference data_entities_vanilla.py:56-76 with split_nn.py:49-52's
+// round-robin).  Her conv front runs in her process (csrc/split.cpp run_alice, unchanged) and
+// this launch speaks the peer-mapped channel's protocol (csrc/ipc_p2p.h) in place of the C
+// phase's conv jobs:
+//   C_send  workgroup c < the message's chunks: wait every column block's cut-gradient
+//           partials (XD), the ack of the message two generations back, then its 1,024 floats
+//           of dx_i (the partials in slot order, as the conv jobs sum them) as system-scope
+//           write-through stores into her slot over xGMI -> drain -> release -> flag = gen;
+//   C_recv  (batch i + 1) every workgroup its 1 / G share of the [16][K1] activation slot:
+//           poll the flags of the chunks it reads (relaxed system loads, then one acquire),
+//           system-scope loads of her message, sc1 stores into the step's slot in the MFMA A
+//           layout (padding rows zero), workgroup 0 the labels -> Yrem -> seam X; after seam X
+//           the message's chunks are acked (every read of it has drained).
+// So her messages, their sizes and their order are run_bob's: she cannot tell which executor
+// served her, and the per-batch Bob path stays the fallback with no change on her side.
 #include "vanilla.h"
+#include "ipc_ar.h"
 #include "persist.h"
 
 #include <string>
@@ -115,8 +133,25 @@ __device__ __forceinline__ bool va_wait_many(const VaArgs& a, int n, int* s_ok, 
   return *s_ok != 0;
 }
 
+// one lane: bounded wait until the channel flag / ack word *f reaches generation `want`
+// (remote Alice); a timeout raises the launch's error word and the channel's
+__device__ __forceinline__ bool va_pwait(const VaArgs& a, const uint32_t* f, uint32_t want) {
+  if ((int32_t)(ipc_poll_flag(f) - want) >= 0) return true;
+  const uint64_t t0 = wall_clock64();
+  while ((int32_t)(ipc_poll_flag(f) - want) < 0) {
+    if (failed(a.err)) return false;
+    __builtin_amdgcn_s_sleep(1);
+    if ((int64_t)(wall_clock64() - t0) > a.timeout) {
+      __hip_atomic_fetch_or(a.err, 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ipc_fail(a.lk.err, a.lk.herr);
+      return false;
+    }
+  }
+  return true;
+}
+
 constexpr int kSt = 16;   // fc1 W / buf loads and stores: sc1 (write-through stores, L1-bypassing loads)
-constexpr int kVaFwdRing = 4;   // forward-pass register ring depth (tiles; kVaFwdRing - 1 in flight)
+constexpr int kVaFwdRing = 6;   // forward-pass register ring depth (tiles; kVaFwdRing - 1 in flight)
 
 // f(integral_constant<int, I>) for I in [B, E): compile-time ring and buffer indices in the
 // unrolled tile loops
@@ -134,9 +169,6 @@ constexpr int PH = 4 * kVaMaxWC4 + 4;
 constexpr int PD = kVaMaxWR + 1;
 constexpr int OFF_W2 = 0;
 constexpr int OFF_U = OFF_W2 + ((kVaMaxWR * PW2 * 4 + 15) & ~15);
-// union, forward-pass view: updated W1 tile [2][16][65] f32x4
-constexpr int U_SW = 0;
-constexpr int kUFwd = 2 * 16 * 65 * 16;
 // union, update-pass view: x_i column block [16][64] f32x4 (also the dx flush scratch), dz1 of
 // the forward run's row blocks [kVaRuns][16 m][16] (b1's step)
 constexpr int U_SA = 0;
@@ -150,8 +182,7 @@ constexpr int U_SDL = U_RED + 16 * 32 * 16;
 constexpr int U_SH2 = U_SDL + 16 * kVaMaxC * 4;
 constexpr int U_SDZH = U_SH2 + 16 * 4 * 4;
 constexpr int kUFc2 = U_SDZH + 16 * 4 * 4;
-constexpr int kU0 = kUFwd > kUUpd ? kUFwd : kUUpd;
-constexpr int kU = kU0 > kUFc2 ? kU0 : kUFc2;
+constexpr int kU = kUUpd > kUFc2 ? kUUpd : kUFc2;
 constexpr int OFF_W3 = OFF_U + kU;                       // W3 columns {W, buf}[4][kVaMaxC]
 constexpr int OFF_B3 = OFF_W3 + 2 * 4 * kVaMaxC * 4;     // b3 {W, buf}[kVaMaxC]
 constexpr int OFF_B2 = OFF_B3 + 2 * kVaMaxC * 4;         // b2 {W, buf}[4] (+ pad)
@@ -181,10 +212,11 @@ static_assert(kVaThreads / 64 * 10 * 256 >= kVaMaxWR * 4 * kVaMaxWC4, "10 W2 16 
       a.tall[((int64_t)(i - a.tall_step) * G + w) * 16 + (k)] = (int64_t)wall_clock64();     \
   } while (0)
 
+// REM: the Alice is remote (the channel phases above in place of the conv jobs)
+template <bool REM>
 __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* sw2 = reinterpret_cast<float*>(smem + OFF_W2);
-  f32x4* sw = reinterpret_cast<f32x4*>(smem + OFF_U + U_SW);
   f32x4* sa = reinterpret_cast<f32x4*>(smem + OFF_U + U_SA);
   float* sdzb = reinterpret_cast<float*>(smem + OFF_U + U_DZB);
   float* sh1 = reinterpret_cast<float*>(smem + OFF_U + U_SH1);
@@ -288,7 +320,7 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
       sb1[(k * 3 + 1) * 16 + j] = own ? a.L1.mb[n] : 0.f;
       sb1[(k * 3 + 2) * 16 + j] = 0.f;
     }
-    if (tid < 20) {
+    if (!REM && tid < 20) {
       // {w[9], b, buf w[9], buf b} of channel cc
       const int j = tid < 10 ? tid : tid - 10;
       const float* src = tid < 10 ? (j < 9 ? a.cw + cc * 9 + j : a.cb + cc) : (j < 9 ? a.cmw + cc * 9 + j : a.cmb + cc);
@@ -367,13 +399,16 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
 
   // ---------------------------------------------------------------- fc1 forward pass
   f32x4 sp[2][2], sm[2][2];
+  // W1 tile t straight in the MFMA B layout (no LDS staging): lane (li, lq) of wave r holds row
+  // 16 rb + li, columns 256 cb + 16 (r + 8 h) + 4 lq .. + 3 -- the operand the wave's MFMAs take
+  // (a wave's load: 16 rows x 64 B; two waves share each 128-B line)
   auto load_w = [&](int t, f32x4 (&p)[2]) {
     VA_IDX();
     const int rb = t / ncb, cb = t - (t / ncb) * ncb;
-    const int k = cb * 256 + 4 * lane;
+    const int n = 16 * rb + li;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int n = 16 * rb + r + 8 * h;
+      const int k = cb * 256 + 16 * (r + 8 * h) + 4 * lq;
       p[h] = (n < N1 && k < K1)
                  ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rW1, (n * K1 + k) * 4, 0, kSt))
                  : zv;
@@ -396,9 +431,11 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
   // The forward pass keeps kVaFwdRing - 1 tiles of W (sc1 loads: tiles another workgroup's
   // update run just wrote) and x in flight in a register ring, every load issued after the
   // seam-X wait that orders it (all of the step's fc1 stores drained before any conv job
-  // arrived, docs/PERF.md round 6); ring slot = tile index % kVaFwdRing, LDS staging buffer =
-  // tile index % 2, both compile-time in the unrolled loop.  Same products in the same order
-  // at every depth: the depth changes timing only, never a bit of the result.
+  // arrived, docs/PERF.md round 6); ring slot = tile index % kVaFwdRing, compile-time in the
+  // unrolled loop.  Both operands are loaded in their MFMA layouts, so every wave streams its
+  // own k-slice of each tile with no LDS staging and no workgroup barrier per tile (the staged
+  // form: a 16 KB LDS round trip and a barrier per tile, 4.3 TB/s).  Same products in the same
+  // order at every depth and in both forms: the form and the depth change timing only.
   auto fwd_pass = [&](int step) {
     if (nt <= 0) return;
     constexpr int D = kVaFwdRing;
@@ -410,13 +447,12 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
         load_w(t_begin + d, wr[d]);
         load_xv(step, t_begin + d, xr[d]);
       }
-    __syncthreads();
     f32x4 z = zv;
     int kz = 0;
     auto tile = [&](auto cur_c, int j) {
-      constexpr int cur = decltype(cur_c)::value, nx = (cur + D - 1) % D, lb = cur & 1;
+      constexpr int cur = decltype(cur_c)::value, nx = (cur + D - 1) % D;
       const int t = t_begin + j;
-      const int rb = t / ncb, cb = t - (t / ncb) * ncb;
+      const int rb = t / ncb;
       const int kr = rb - rbA;
       if (kr != kz) {
         zp_store(kz, z);
@@ -427,19 +463,10 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
         load_w(t + D - 1, wr[nx]);
         load_xv(step, t + D - 1, xr[nx]);
       }
-      VA_IDX();
-      const int n1 = 16 * rb + r;
-      const int k = cb * 256 + 4 * lane;
-      const bool kin = k < K1;
-      sw[lb * 1040 + r * 65 + lane] = (kin && n1 < N1) ? wr[cur][0] : zv;
-      sw[lb * 1040 + (r + 8) * 65 + lane] = (kin && n1 + 8 < N1) ? wr[cur][1] : zv;
-      __syncthreads();
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const f32x4 wv4 = sw[lb * 1040 + li * 65 + 4 * (r + 8 * h) + lq];
+      for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int c = 0; c < 4; ++c) z = __builtin_amdgcn_mfma_f32_16x16x4f32(xr[cur][h][c], wv4[c], z, 0, 0, 0);
-      }
+        for (int c = 0; c < 4; ++c) z = __builtin_amdgcn_mfma_f32_16x16x4f32(xr[cur][h][c], wr[cur][h][c], z, 0, 0, 0);
     };
     int j = 0;
     for (; j + D - 1 < nt; j += D) va_static_for<0, D>([&](auto dc) { tile(dc, j + decltype(dc)::value); });
@@ -607,12 +634,119 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
     flush_dx(ccb);
   };
 
-  // ---- prologue: Alice's forward of batch 0, then the forward pass over it
-  img_put(0, img_word(0));
-  __syncthreads();
-  conv_fwd(0);
+  // ---------------------------------------------------------------- remote Alice (REM)
+  auto rows_of = [&](int s) { return (int)a.adam[4 * s]; };
+  // her activation message of step s -> the step's slot (all 16 rows, padding rows zero), the
+  // labels -> Yrem (workgroup 0); false when a wait gave up
+  auto recv_act = [&](int s) -> bool {
+    const int Ms = rows_of(s);
+    const uint32_t rg = a.lk.rgen0 + 1u + (uint32_t)s;
+    const int par = (int)(rg & 1u);
+    const int K4 = K1 >> 2, NQ = 16 * K4;   // float4 groups of a row / of the slot
+    const int q0 = (int)((int64_t)w * NQ / G), q1 = (int)((int64_t)(w + 1) * NQ / G);
+    const int qm = Ms * K4;                  // float4 groups the message carries
+    const int qe = q1 < qm ? q1 : qm;
+    const int ca0 = 4 * q0 / kIpcChunk, na = qe > q0 ? (4 * qe - 1) / kIpcChunk - ca0 + 1 : 0;
+    const int fl = Ms * K1;                  // the labels' first word
+    const int cl0 = fl / kIpcChunk, nl = w == 0 ? (fl + 2 * Ms - 1) / kIpcChunk - cl0 + 1 : 0;
+    if (threadIdx.x < 64) {
+      const int lane = threadIdx.x;
+      int c = -1;
+      if (lane < na) c = ca0 + lane;
+      else if (lane >= 32 && lane - 32 < nl) c = cl0 + lane - 32;
+      bool ok = true;
+      if (c >= 0) ok = va_pwait(a, a.lk.rflag[par] + c, rg);
+      ok = __all(ok);
+      ipc_acquire();
+      if (lane == 0) *s_ok = ok ? 1 : 0;
+    }
+    __syncthreads();
+    if (*s_ok == 0) return false;
+    const __amdgpu_buffer_rsrc_t rR = ipc_rsrc(a.lk.rdata[par]);
+    for (int q = q0 + (int)threadIdx.x; q < q1; q += kVaThreads) {
+      const int m = q / K4, k = 4 * (q - m * K4);
+      const f32x4 v = q < qm ? __builtin_bit_cast(f32x4, ipc_ld4(rR, 4 * (int64_t)q)) : zv;
+      hst4(rX, xoff(s, m, k) * 4, v);
+    }
+    if (w == 0 && (int)threadIdx.x < M) {
+      const int m = threadIdx.x;
+      uint32_t lo = 0xffffff9cu, hi = 0xffffffffu;   // -100: a padding row, ignored
+      if (m < Ms) {
+        lo = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rR, (fl + 2 * m) * 4, 0, 17);
+        hi = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rR, (fl + 2 * m + 1) * 4, 0, 17);
+      }
+      const __amdgpu_buffer_rsrc_t rY = rs_of(a.Yrem);
+      hst1(rY, (s * M + m) * 8, __builtin_bit_cast(float, lo));
+      hst1(rY, (s * M + m) * 8 + 4, __builtin_bit_cast(float, hi));
+    }
+    return true;
+  };
+  // after seam X every read of step s's message has drained: ack its chunks
+  auto ack_act = [&](int s) {
+    if (threadIdx.x == 0) {
+      const int Ms = rows_of(s);
+      const uint32_t rg = a.lk.rgen0 + 1u + (uint32_t)s;
+      const int par = (int)(rg & 1u);
+      const int nch = (((Ms * K1 + 2 * Ms + 3) & ~3) + kIpcChunk - 1) / kIpcChunk;
+      for (int c = w; c < nch; c += G) ipc_raise_flag(a.lk.rack[par] + c, rg, 0);
+    }
+  };
+  // the cut gradient of step i -> her slot (workgroup c: chunk c, 1,024 floats); false when a
+  // wait gave up
+  auto send_dx = [&](int i) -> bool {
+    const int len = rows_of(i) * K1;
+    const int nch = (len + kIpcChunk - 1) / kIpcChunk;
+    if (w >= nch) return true;
+    if (!va_wait_many(a, ncb, s_ok, [&](int l, int& idx) {
+          idx = va_XD(l);
+          return (unsigned)(i + 1) * (unsigned)a.tab[a.oU + G + 1 + ncb + l];
+        }))
+      return false;
+    const uint32_t sg = a.lk.sgen0 + 1u + (uint32_t)i;
+    const int par = (int)(sg & 1u);
+    const int prev = i >= 2 ? (rows_of(i - 2) * K1 + kIpcChunk - 1) / kIpcChunk : a.lk.sprev[i];
+    const __amdgpu_buffer_rsrc_t rS = ipc_rsrc(a.lk.sdata[par]);
+    for (int c = w; c < nch; c += G) {
+      if (threadIdx.x == 0) {
+        // chunks beyond the message two generations back wait on its chunk 0 (ipc_p2p.hip)
+        const bool ok = prev == 0 || va_pwait(a, a.lk.sack[par] + (c < prev ? c : 0), sg - 2u);
+        ipc_acquire();
+        *s_ok = ok ? 1 : 0;
+      }
+      __syncthreads();
+      if (*s_ok == 0) return false;
+      const int e = c * kIpcChunk + 4 * (int)threadIdx.x;
+      if ((int)threadIdx.x < kIpcThreads && e < len) {
+        const int m = e / K1, k = e - m * K1, cb = k >> 8, kk = k & 255;
+        const int ns = a.tab[a.oU + G + 1 + ncb + cb];
+        f32x4 parts[kVaDxSlots];
+#pragma unroll
+        for (int sl = 0; sl < kVaDxSlots; ++sl)
+          parts[sl] = sl < ns ? hld4(rHB, bDX + (((cb * kVaDxSlots + sl) * 16 + m) * 256 + kk) * 4) : zv;
+        f32x4 v = parts[0];
+#pragma unroll
+        for (int sl = 1; sl < kVaDxSlots; ++sl) v += parts[sl];
+        ipc_st4(rS, e, __builtin_bit_cast(float4, v));
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) ipc_raise_flag(a.lk.sflag[par] + c, sg);
+      __syncthreads();   // s_ok is rewritten by the next chunk
+    }
+    return true;
+  };
+
+  // ---- prologue: Alice's forward of batch 0 (REM: her message of it), then the forward pass
+  if constexpr (REM) {
+    if (!recv_act(0)) goto done;
+  } else {
+    img_put(0, img_word(0));
+    __syncthreads();
+    conv_fwd(0);
+  }
   va_arrive(a, va_seam(4, w & 7));
   if (!va_seam_wait(a, 4, 1u, s_ok, s_sn)) goto done;
+  if constexpr (REM) ack_act(0);
   fwd_pass(0);
   flush(0);
 
@@ -625,7 +759,7 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
     asm volatile("" : "+v"(ss), "+v"(ib));
     VA_MARK(0);
     // the next batch's images, in flight across the step (written to LDS in the conv phase)
-    const uint32_t pimg = more ? img_word(i + 1) : 0u;
+    const uint32_t pimg = (!REM && more) ? img_word(i + 1) : 0u;
 
     // ================= F: h1 slice, the tile's fc2 partial
     if (threadIdx.x < 64) {
@@ -761,7 +895,15 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
           for (int gq = 0; gq < NG; ++gq) lg += red[gq * 32 + c4];
           lg += *reinterpret_cast<const f32x4*>(sb3 + 4 * c4);
         }
-        const int64_t lab = a.Y[(int64_t)i * M + m];
+        int64_t lab;
+        if constexpr (REM) {   // handed off by workgroup 0's receive: sc1 loads
+          const __amdgpu_buffer_rsrc_t rY = rs_of(a.Yrem);
+          const uint32_t lo = __builtin_bit_cast(uint32_t, hld1(rY, (i * M + m) * 8));
+          const uint32_t hi = __builtin_bit_cast(uint32_t, hld1(rY, (i * M + m) * 8 + 4));
+          lab = (int64_t)(((uint64_t)hi << 32) | lo);
+        } else {
+          lab = a.Y[(int64_t)i * M + m];
+        }
         const bool ign = lab == a.ignore || lab < 0 || lab >= C;
         float mx = -INFINITY;
 #pragma unroll
@@ -985,6 +1127,24 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
     upd_pass(i, ss, ib);
     VA_MARK(8);
 
+    if constexpr (REM) {
+      // ================= C (remote Alice): dx_i to her, her activation of batch i + 1 in
+      if (!send_dx(i)) break;
+      VA_MARK(9);
+      if (more) {
+        if (!recv_act(i + 1)) break;
+        va_arrive(a, va_seam(4, w & 7));
+        VA_MARK(12);
+        if (!va_seam_wait(a, 4, (unsigned)(i + 2), s_ok, s_sn)) break;
+        VA_MARK(13);
+        ack_act(i + 1);
+        fwd_pass(i + 1);
+        VA_MARK(14);
+        flush(i + 1);
+        VA_MARK(15);
+      }
+      continue;
+    }
     // ================= C: Alice's backward + step (conv job), her forward of batch i + 1
     {
       const int k0 = cc * 169, cblo = k0 >> 8, cbhi = (k0 + 168) >> 8;
@@ -1120,7 +1280,7 @@ done:
         a.L1.mb[n] = sb1[(k * 3 + 1) * 16 + j];
       }
     }
-    if (cg == 0 && tid < 20) {
+    if (!REM && cg == 0 && tid < 20) {
       const int j = tid < 10 ? tid : tid - 10;
       float* dst = tid < 10 ? (j < 9 ? a.cw + cc * 9 + j : a.cb + cc) : (j < 9 ? a.cmw + cc * 9 + j : a.cmb + cc);
       *dst = scv[tid];
@@ -1134,7 +1294,13 @@ int vanilla_lds_bytes() { return kVaLds; }
 
 std::string vanilla_check(const VaArgs& a) {
   if (a.M < 1 || a.M > 16) return "rows per step 1..16";
-  if (a.G != kVaG || a.NC != a.G / kVaNR || a.NC > kVaMaxNC) return "256 workgroups (32 conv channels x 8 image pairs)";
+  if (a.rem) {
+    if (a.G < kVaNR || a.G > kVaG || a.G % kVaNR || a.NC != a.G / kVaNR) return "remote Alice: 8..256 workgroups, a multiple of 8";
+    if (a.M > a.G) return "remote Alice: a softmax workgroup per row";
+    if (a.Yrem == nullptr || a.lk.sdata[0] == nullptr || a.lk.rdata[0] == nullptr) return "remote Alice: the channel";
+  } else if (a.G != kVaG || a.NC != a.G / kVaNR || a.NC > kVaMaxNC) {
+    return "256 workgroups (32 conv channels x 8 image pairs)";
+  }
   if (a.N1 < 4 || a.N1 % 4) return "fc1 width % 4";
   if ((a.N1 / 4 + a.NC - 1) / a.NC > kVaMaxWC4) return "fc1 too wide for the fc2 tiles";
   if (a.N1 > 16 * kVaMaxRB || a.nrb != (a.N1 + 15) / 16) return "fc1 row blocks";
@@ -1155,7 +1321,8 @@ bool vanilla_fits(const VaArgs& a, int device, std::string* why) {
     if (hipGetDeviceProperties(&pr, device) != hipSuccess) {
       s = "device properties";
     } else {
-      const void* fn = reinterpret_cast<const void*>(&vanilla_epoch_kernel);
+      const void* fn = a.rem ? reinterpret_cast<const void*>(&vanilla_epoch_kernel<true>)
+                             : reinterpret_cast<const void*>(&vanilla_epoch_kernel<false>);
       int nb = 0;
       hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kVaLds);
       if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, kVaThreads, kVaLds);
@@ -1170,7 +1337,8 @@ bool vanilla_fits(const VaArgs& a, int device, std::string* why) {
 hipError_t vanilla_epoch_launch(const VaArgs& a, hipStream_t st) {
   if (!vanilla_check(a).empty()) return hipErrorInvalidValue;
   if (a.S <= 0) return hipSuccess;
-  const void* fn = reinterpret_cast<const void*>(&vanilla_epoch_kernel);
+  const void* fn = a.rem ? reinterpret_cast<const void*>(&vanilla_epoch_kernel<true>)
+                         : reinterpret_cast<const void*>(&vanilla_epoch_kernel<false>);
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kVaLds);
   if (e != hipSuccess) return e;
   e = hipMemsetAsync(a.cnt, 0, (size_t)kVaCounters * kVaStride * sizeof(unsigned), st);

@@ -6,13 +6,20 @@
 // real rows).  The host builds the per-step tables (batch rows, labels, CE scales, dropout
 // seeds: host.h step_seed == ops/rng.py), the two fc1 tile-run tables, zeroes the counters (in
 // the launch), launches and reads the kernel's error word once.
+//
+// Remote Alice (cfg channel / peer / G; BASELINE config 3's remote placements): `run_remote`
+// is Bob's side of a remote Alice's epoch, the launch sending and receiving the per-batch
+// messages on the peer-mapped channel itself (csrc/vanilla.hip REM); her side stays
+// csrc/split.cpp run_alice, so the per-batch run_bob is the drop-in fallback.
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "host.h"
+#include "ipc_p2p.h"
 #include "vanilla.h"
 
 namespace py = pybind11;
@@ -33,7 +40,8 @@ class VanillaEpoch {
   // cfg: layers = [3 dicts {W, b, s0, sb0}] (Bob's model2_sisa, SGD-momentum buffers), lr /
   // momentum / wd (Bob), alice = {w [32, 1, 3, 3], b [32], s0w, s0b} + alice_lr / alice_momentum /
   // alice_wd, x (uint8 shard [N, 784]), y (int64 labels [N]), p1 / p2, B, timeout_s,
-  // workgroups (0: cooperative launch of 256)
+  // workgroups (0: cooperative launch of 256).  Remote Alice: channel (an open IpcChannel) and
+  // peer (her rank) in place of alice / x / y; G workgroups (default 256)
   explicit VanillaEpoch(const py::dict& cfg) {
     auto layers = cfg["layers"].cast<std::vector<py::dict>>();
     TORCH_CHECK(layers.size() == 3, "VanillaEpoch drives model2_sisa's 3 layers");
@@ -49,19 +57,30 @@ class VanillaEpoch {
                   "layer shapes");
     }
     TORCH_CHECK(W_[1].size(1) == W_[0].size(0) && W_[2].size(1) == W_[1].size(0), "layer chain shapes");
-    py::dict al = cfg["alice"].cast<py::dict>();
-    cw_ = va_get(al, "w");
-    cb_ = va_get(al, "b");
-    cmw_ = va_get(al, "s0w");
-    cmb_ = va_get(al, "s0b");
-    for (const at::Tensor* t : {&cw_, &cb_, &cmw_, &cmb_}) va_f32(*t, "conv tensors");
-    TORCH_CHECK(cw_.numel() == 288 && cb_.numel() == 32 && cmw_.numel() == 288 && cmb_.numel() == 32,
-                "conv 32 x 1 x 3 x 3");
-    x_ = va_get(cfg, "x");
-    y_ = va_get(cfg, "y");
-    TORCH_CHECK(x_.is_cuda() && x_.scalar_type() == at::kByte && x_.is_contiguous() && x_.numel() % 784 == 0,
-                "shard pixels uint8 [N, 784]");
-    TORCH_CHECK(y_.is_cuda() && y_.scalar_type() == at::kLong && y_.numel() * 784 == x_.numel(), "labels int64 [N]");
+    rem_ = cfg.contains("channel") && !cfg["channel"].is_none();
+    if (rem_) {
+      const py::object ch = cfg["channel"];
+      TORCH_CHECK(py::isinstance<sl::IpcChannel>(ch), "VanillaEpoch: channel must be an IpcChannel");
+      chan_ = ch.cast<sl::IpcChannel*>();
+      channel_ = ch;   // keep the channel alive with the executor
+      peer_ = cfg["peer"].cast<int>();
+      TORCH_CHECK(chan_->opened() && peer_ >= 0 && peer_ < chan_->size() && peer_ != chan_->rank(),
+                  "VanillaEpoch: an open channel and the Alice's rank");
+    } else {
+      py::dict al = cfg["alice"].cast<py::dict>();
+      cw_ = va_get(al, "w");
+      cb_ = va_get(al, "b");
+      cmw_ = va_get(al, "s0w");
+      cmb_ = va_get(al, "s0b");
+      for (const at::Tensor* t : {&cw_, &cb_, &cmw_, &cmb_}) va_f32(*t, "conv tensors");
+      TORCH_CHECK(cw_.numel() == 288 && cb_.numel() == 32 && cmw_.numel() == 288 && cmb_.numel() == 32,
+                  "conv 32 x 1 x 3 x 3");
+      x_ = va_get(cfg, "x");
+      y_ = va_get(cfg, "y");
+      TORCH_CHECK(x_.is_cuda() && x_.scalar_type() == at::kByte && x_.is_contiguous() && x_.numel() % 784 == 0,
+                  "shard pixels uint8 [N, 784]");
+      TORCH_CHECK(y_.is_cuda() && y_.scalar_type() == at::kLong && y_.numel() * 784 == x_.numel(), "labels int64 [N]");
+    }
     B_ = cfg["B"].cast<int>();
     const double p1 = cfg["p1"].cast<double>(), p2 = cfg["p2"].cast<double>();
     timeout_s_ = cfg.contains("timeout_s") ? cfg["timeout_s"].cast<double>() : 30.0;
@@ -80,7 +99,8 @@ class VanillaEpoch {
     a.C = (int)W_[2].size(0);
     a.C4 = (a.C + 3) & ~3;
     a.M = B_;
-    a.G = sl::kVaG;
+    a.G = rem_ && cfg.contains("G") ? cfg["G"].cast<int>() : sl::kVaG;
+    a.rem = rem_ ? 1 : 0;
     const int wg = cfg.contains("workgroups") ? cfg["workgroups"].cast<int>() : 0;
     a.coop = wg > 0 ? 0 : 1;
     a.fault_step = -1;
@@ -96,9 +116,17 @@ class VanillaEpoch {
     a.dsc2 = p2 > 0 ? (float)(1.0 / (1.0 - p2)) : 1.f;
     a.o = sl::make_opt_raw(1, cfg["lr"].cast<double>(), 0, 0, 0, cfg["wd"].cast<double>(),
                            cfg["momentum"].cast<double>(), 0, nullptr);
-    a.oa = sl::make_opt_raw(1, cfg["alice_lr"].cast<double>(), 0, 0, 0, cfg["alice_wd"].cast<double>(),
-                            cfg["alice_momentum"].cast<double>(), 0, nullptr);
-    why_ = cus < a.G ? "fewer than 256 CUs" : "";
+    a.oa = rem_ ? sl::make_opt_raw(1, 0.0, 0, 0, 0, 0.0, 0.0, 0, nullptr)
+                : sl::make_opt_raw(1, cfg["alice_lr"].cast<double>(), 0, 0, 0, cfg["alice_wd"].cast<double>(),
+                                   cfg["alice_momentum"].cast<double>(), 0, nullptr);
+    why_ = cus < a.G ? "fewer CUs than workgroups" : "";
+    if (why_.empty() && rem_) {
+      // placeholders the check requires; the launch's own are set per chunk
+      a.Yrem = reinterpret_cast<int64_t*>(16);
+      a.lk.sdata[0] = reinterpret_cast<float*>(16);
+      a.lk.rdata[0] = reinterpret_cast<const float*>(16);
+      if (chan_->cap() < act_words(B_)) why_ = "the channel is too small for a batch";
+    }
     if (why_.empty()) why_ = sl::vanilla_check(a);
     if (why_.empty()) why_ = tables();
     if (why_.empty()) {
@@ -148,11 +176,13 @@ class VanillaEpoch {
       setL(a.L1, 0);
       setL(a.L2, 1);
       setL(a.L3, 2);
-      a.img = x_.data_ptr<uint8_t>();
-      a.cw = cw_.data_ptr<float>();
-      a.cb = cb_.data_ptr<float>();
-      a.cmw = cmw_.data_ptr<float>();
-      a.cmb = cmb_.data_ptr<float>();
+      if (!rem_) {
+        a.img = x_.data_ptr<uint8_t>();
+        a.cw = cw_.data_ptr<float>();
+        a.cb = cb_.data_ptr<float>();
+        a.cmw = cmw_.data_ptr<float>();
+        a.cmb = cmb_.data_ptr<float>();
+      }
       std::string why;
       sl::vanilla_fits(a, dev_, &why);
       why_ = why;
@@ -170,22 +200,63 @@ class VanillaEpoch {
   py::tuple run(const at::Tensor& order, at::Tensor& loss_rows, int64_t t_a, int64_t t_b, int64_t fwd_count,
                 int64_t seed_base, const c10::optional<at::Tensor>& trace_all, int64_t trace_step) {
     TORCH_CHECK(ok_, "VanillaEpoch: ", why_);
+    TORCH_CHECK(!rem_, "VanillaEpoch.run: a co-located Alice (run_remote serves a remote one)");
     TORCH_CHECK(order.is_cuda() && order.scalar_type() == at::kLong && order.dim() == 1, "order int64 [n] on the GPU");
     const int64_t n = order.numel();
     const int64_t S = (n + B_ - 1) / B_;
     if (S == 0) return py::make_tuple(t_a, t_b, fwd_count);
-    TORCH_CHECK(loss_rows.is_cuda() && loss_rows.scalar_type() == at::kFloat && loss_rows.numel() >= S * B_,
-                "loss_rows f32 [>= S * B]");
     const at::Device dev = order.device();
     auto lopt = at::TensorOptions().dtype(at::kLong).device(dev);
     rows_ = at::full({S * B_}, -1, lopt);
     rows_.narrow(0, 0, n).copy_(order);
     labels_ = at::full({S * B_}, -100, lopt);
     labels_.narrow(0, 0, n).copy_(y_.index_select(0, order));
+    epoch(n, S, loss_rows, fwd_count, seed_base, trace_all, trace_step, dev);
+    return py::make_tuple(t_a + S, t_b + S, fwd_count + S);
+  }
+
+  // Bob's side of a remote Alice's epoch of n samples (her side: csrc/split.cpp run_alice):
+  // the per-batch messages -- her activation + labels in, the cut gradient out -- go over the
+  // channel from inside the launch, in run_bob's order and sizes.  Returns (t_b, fwd_count)
+  // advanced by the step count.  Raises when an in-launch wait gave up (fail-stop: she is
+  // then stopped at a message of this epoch and times out on her side).
+  py::tuple run_remote(int64_t n, at::Tensor& loss_rows, int64_t t_b, int64_t fwd_count, int64_t seed_base,
+                       const c10::optional<at::Tensor>& trace_all, int64_t trace_step) {
+    TORCH_CHECK(ok_, "VanillaEpoch: ", why_);
+    TORCH_CHECK(rem_, "VanillaEpoch.run_remote: configured with a channel and peer");
+    const int64_t S = n > 0 ? (n + B_ - 1) / B_ : 0;
+    if (S == 0) return py::make_tuple(t_b, fwd_count);
+    epoch(n, S, loss_rows, fwd_count, seed_base, trace_all, trace_step, W_[0].device());
+    return py::make_tuple(t_b + S, fwd_count + S);
+  }
+
+  // (op, peer, bytes) of every message the last run_remote issued, in issue order (run_bob's)
+  std::vector<std::tuple<std::string, int, int64_t>> messages() const { return log_; }
+
+  void set_fault_step(int64_t s) { fault_step_ = (int)s; }
+  bool remote() const { return rem_; }
+  int workgroups() const { return a_.G; }
+  void set_max_steps(int64_t s) { max_steps_ = std::max<int64_t>(1, std::min<int64_t>(s, sl::kVaMaxS)); }
+  at::Tensor table() const { return tab_.clone(); }
+
+ private:
+  // the vanilla activation message's words: split.cpp act_msg_words (M x 5408 activation, then
+  // M int64 labels, padded to 16 bytes)
+  static int64_t act_words(int M) { return ((int64_t)M * 5408 + 2 * (int64_t)M + 3) / 4 * 4; }
+
+  // One epoch of S steps over n samples as launches of at most max_steps_ steps: the per-step
+  // tables (rows, CE scale, dropout seeds), then per chunk (remote: its run of channel messages)
+  // one launch; one read of the error word per chunk.
+  void epoch(int64_t n, int64_t S, at::Tensor& loss_rows, int64_t fwd_count, int64_t seed_base,
+             const c10::optional<at::Tensor>& trace_all, int64_t trace_step, const at::Device& dev) {
+    TORCH_CHECK(loss_rows.is_cuda() && loss_rows.scalar_type() == at::kFloat && loss_rows.numel() >= S * B_,
+                "loss_rows f32 [>= S * B]");
     std::vector<float> tabf(4 * S, 0.f);
     std::vector<int32_t> seeds(4 * S);
+    auto rows_at = [&](int64_t i) { return (int)std::min<int64_t>(B_, n - i * B_); };
     for (int64_t i = 0; i < S; ++i) {
-      const int64_t rows = std::min<int64_t>(B_, n - i * B_);
+      const int64_t rows = rows_at(i);
+      tabf[4 * i] = (float)rows;
       tabf[4 * i + 2] = (float)(1.0 / (double)rows);
       const uint64_t s0 = sl::step_seed((uint64_t)seed_base, 0, (uint64_t)(fwd_count + 1 + i));
       const uint64_t s1 = sl::step_seed((uint64_t)seed_base, 1, (uint64_t)(fwd_count + 1 + i));
@@ -201,6 +272,8 @@ class VanillaEpoch {
     // launches of at most kVaMaxS steps (one launch of S steps is bitwise S one-step launches)
     const int64_t cs = std::min<int64_t>(S, max_steps_);
     xr_ = at::empty({cs * 16 * a_.K1}, at::TensorOptions().dtype(at::kFloat).device(dev));
+    if (rem_) yrem_ = at::empty({cs * B_}, at::TensorOptions().dtype(at::kLong).device(dev));
+    log_.clear();
     for (int64_t s0 = 0; s0 < S; s0 += cs) {
       // a chunk whose wait gave up stops the epoch here (host check between chunks, as HybridEpoch)
       if (s0 > 0 && err_.item<int>() != 0) break;
@@ -208,11 +281,38 @@ class VanillaEpoch {
       sl::VaArgs a = a_;
       a.S = (int)ns;
       a.Xr = xr_.data_ptr<float>();
-      a.rows = rows_.data_ptr<int64_t>() + s0 * B_;
-      a.Y = labels_.data_ptr<int64_t>() + s0 * B_;
       a.loss = loss_rows.data_ptr<float>() + s0 * B_;
       a.adam = tabf_.data_ptr<float>() + 4 * s0;
       a.seeds = reinterpret_cast<const uint32_t*>(seeds_.data_ptr<int32_t>()) + 4 * s0;
+      if (rem_) {
+        std::vector<int64_t> sends, recvs;
+        for (int64_t i = s0; i < s0 + ns; ++i) {
+          recvs.push_back(act_words(rows_at(i)));
+          sends.push_back((int64_t)rows_at(i) * a_.K1);
+          log_.emplace_back("recv", peer_, recvs.back() * 4);
+          log_.emplace_back("send", peer_, sends.back() * 4);
+        }
+        const sl::P2PRun r = chan_->run(peer_, st, sends, recvs);
+        for (int p = 0; p < 2; ++p) {
+          a.lk.sdata[p] = r.sdata[p];
+          a.lk.sflag[p] = r.sflag[p];
+          a.lk.sack[p] = r.sack[p];
+          a.lk.rdata[p] = r.rdata[p];
+          a.lk.rflag[p] = r.rflag[p];
+          a.lk.rack[p] = r.rack[p];
+          a.lk.sprev[p] = r.sprev[p];
+        }
+        a.lk.sgen0 = r.sgen0;
+        a.lk.rgen0 = r.rgen0;
+        a.lk.err = r.err;
+        a.lk.herr = r.herr;
+        a.Yrem = yrem_.data_ptr<int64_t>();
+        a.rows = nullptr;
+        a.Y = nullptr;
+      } else {
+        a.rows = rows_.data_ptr<int64_t>() + s0 * B_;
+        a.Y = labels_.data_ptr<int64_t>() + s0 * B_;
+      }
       if (trace_all.has_value() && s0 == 0) {
         TORCH_CHECK(trace_all->is_cuda() && trace_all->scalar_type() == at::kLong && trace_all->is_contiguous() &&
                         trace_all->numel() % (16LL * a_.G) == 0,
@@ -228,14 +328,8 @@ class VanillaEpoch {
     fault_step_ = -1;
     const int e = err_.item<int>();
     TORCH_CHECK(e == 0, "vanilla split epoch: an in-launch wait gave up (error word ", e, ")");
-    return py::make_tuple(t_a + S, t_b + S, fwd_count + S);
   }
 
-  void set_fault_step(int64_t s) { fault_step_ = (int)s; }
-  void set_max_steps(int64_t s) { max_steps_ = std::max<int64_t>(1, std::min<int64_t>(s, sl::kVaMaxS)); }
-  at::Tensor table() const { return tab_.clone(); }
-
- private:
   // forward (row-major, hybrid_exec.cpp's) and update (column-major) tile runs
   std::string tables() {
     sl::VaArgs& a = a_;
@@ -294,7 +388,12 @@ class VanillaEpoch {
   sl::VaArgs a_{};
   bool ok_ = false;
   std::string why_;
-  at::Tensor HB_, cnt_, err_, shard_n_, tab_, tabf_, seeds_, rows_, labels_, xr_;
+  at::Tensor HB_, cnt_, err_, shard_n_, tab_, tabf_, seeds_, rows_, labels_, xr_, yrem_;
+  bool rem_ = false;
+  sl::IpcChannel* chan_ = nullptr;
+  py::object channel_;
+  int peer_ = -1;
+  std::vector<std::tuple<std::string, int, int64_t>> log_;
 };
 
 }  // namespace
@@ -308,5 +407,10 @@ void sl_register_vanilla(py::module& m) {
       .def("set_fault_step", &VanillaEpoch::set_fault_step)
       .def("set_max_steps", &VanillaEpoch::set_max_steps)
       .def("run", &VanillaEpoch::run, py::arg("order"), py::arg("loss_rows"), py::arg("t_a"), py::arg("t_b"),
-           py::arg("fwd_count"), py::arg("seed_base"), py::arg("trace_all") = py::none(), py::arg("trace_step") = 0);
+           py::arg("fwd_count"), py::arg("seed_base"), py::arg("trace_all") = py::none(), py::arg("trace_step") = 0)
+      .def("run_remote", &VanillaEpoch::run_remote, py::arg("n"), py::arg("loss_rows"), py::arg("t_b"),
+           py::arg("fwd_count"), py::arg("seed_base"), py::arg("trace_all") = py::none(), py::arg("trace_step") = 0)
+      .def("messages", &VanillaEpoch::messages)
+      .def("remote", &VanillaEpoch::remote)
+      .def("workgroups", &VanillaEpoch::workgroups);
 }

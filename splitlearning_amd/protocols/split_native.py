@@ -351,11 +351,68 @@ def native_remote_role(sess, cid: int, mode: str):
     return None
 
 
+def persistent_remote_ok(sess, cid: int, mode: str) -> bool:
+    """Bob's side only (the Alice's side is the same run_alice either way): whether Bob serves
+    this remote Alice's vanilla epoch with ONE persistent launch that speaks the peer-mapped
+    channel itself (`_C.VanillaEpoch.run_remote`, csrc/vanilla.hip REM).  Needs the peer-mapped
+    channel (not RCCL), fp32 SGD-momentum, B <= 16, the flag, no earlier failure, and a GPU of
+    its own: with ranks sharing one GPU the Alice's kernels need CUs the launch would hold, so
+    only an explicit reduced grid (SL_VA_REMOTE_G, the one-GPU tests) runs there."""
+    if mode != "vanilla" or getattr(sess.args, "split_persist", "auto") == "off" or sess.__dict__.get("_va_rem_off"):
+        return False
+    ch = getattr(sess, "split_channel", None)
+    C = sess.ops.C()
+    if ch is None or not hasattr(ch, "host_error") or not hasattr(C, "VanillaEpoch"):
+        return False
+    if getattr(sess.comm, "host_staging", False) and not os.environ.get("SL_VA_REMOTE_G"):
+        return False
+    dt = getattr(sess.args, "dtype", "fp32")
+    if dt != "fp32" or (hasattr(C, "get_compute_dtype") and C.get_compute_dtype() != "fp32"):
+        return False
+    t = sess.tail
+    return (1 <= sess.B <= 16 and sess.bob_slot(cid).cfg.kind == "sgd" and len(t.layers) == 3 and t.tp_size == 1
+            and all(L.W.dtype == torch.float32 for L in t.layers))
+
+
+def _run_remote_persistent(sess, cid: int, n: int, peer: int):
+    """Bob's half of a remote vanilla epoch as one persistent launch; None when the executor
+    declines this configuration (the caller then runs run_bob, which Alice cannot tell apart).
+    A launch that fails mid-epoch raises: the Alice is then stopped at a message of this epoch
+    and times out on her side, so there is no state both sides could roll back to (fail-stop,
+    docs/DEVIATIONS.md)."""
+    bslot = sess.bob_slot(cid)
+    layers = []
+    for L in sess.tail.layers:
+        pw, pb = _param(bslot, f"{L.spec.name}.weight", L.W), _param(bslot, f"{L.spec.name}.bias", L.b)
+        layers.append({"W": pw["p"], "b": pb["p"], "s0": pw["s0"], "sb0": pb["s0"]})
+    bo = bslot.cfg
+    cfg = {"layers": layers, "lr": bo.lr, "momentum": bo.momentum, "wd": bo.weight_decay, "B": sess.B,
+           "p1": sess.tail.layers[0].spec.dropout, "p2": sess.tail.layers[1].spec.dropout,
+           "timeout_s": float(getattr(sess.args, "persist_timeout_s", 30.0)),
+           "channel": sess.split_channel, "peer": int(peer),
+           "G": int(os.environ.get("SL_VA_REMOTE_G", "256")),
+           "workgroups": int(os.environ.get("SL_PERSIST_WORKGROUPS", "0"))}
+    ex = sess.ops.C().VanillaEpoch(cfg)
+    if not ex.ok():
+        sess.__dict__["_va_rem_off"] = True
+        sess.__dict__["split_persist_reason"] = "remote: " + ex.why()
+        return None
+    nb = -(-int(n) // sess.B)
+    loss = torch.empty(max(nb, 1) * sess.B, dtype=torch.float32, device=sess.device)
+    sess.tail._pre = None
+    t_b, fc = ex.run_remote(int(n), loss, bslot.t, sess.tail.fwd_count, sess.tail.seed_base)
+    _bob_done(sess, cid, t_b, fc)
+    sess.__dict__["last_split_losses"] = loss[:int(n)]
+    _count(sess, "remote_persistent")
+    return ex
+
+
 def run_native_remote_epoch(sess, cid: int, order, n: int, mode: str, role: str):
     """This rank's half of one split epoch of a remote Alice_cid (`_C.SplitEpoch` roles 1 / 2,
     csrc/split.cpp run_alice / run_bob): the per-batch messages go over `sess.split_channel`
     on the compute stream.  Same launches and step counts as the Python loop of this
-    placement (the §3.2 overlap order: no look-ahead)."""
+    placement (the §3.2 overlap order: no look-ahead).  Bob's side of a vanilla epoch runs as
+    ONE persistent launch when `persistent_remote_ok` (the same messages, from inside it)."""
     if role == "skip":
         return None
     _count(sess, "remote_" + role)
@@ -364,7 +421,10 @@ def run_native_remote_epoch(sess, cid: int, order, n: int, mode: str, role: str)
     cfg = {"mode": 1 if mode == "vanilla" else 2, "B": sess.B, "channel": sess.split_channel}
     comm = sess.comm
     comm.progress()
-    if role == "alice":
+    ex = _run_remote_persistent(sess, cid, n, host) if role == "bob" and persistent_remote_ok(sess, cid, mode) else None
+    if ex is not None:
+        pass                      # Bob's side ran as one persistent launch
+    elif role == "alice":
         a = sess.alices[cid]
         cfg.update(_alice_cfg(sess, cid, mode))
         cfg.update({"role": 1, "peer": bob})

@@ -301,3 +301,60 @@ def test_persistent_vanilla_refuses_bf16(tmp_path, monkeypatch):
         assert split_native.persistent_vanilla_ok(s, 1) is want, (flag, dt)
         if not want:
             assert "bf16" in s.__dict__.get("split_persist_reason", "")
+
+
+def test_persistent_remote_vanilla_decision(tmp_path, monkeypatch):
+    """Bob's side of a remote Alice's vanilla epoch adopts the persistent launch
+    (`_C.VanillaEpoch.run_remote`, csrc/vanilla.hip REM) only with the peer-mapped channel, fp32,
+    SGD-momentum, B <= 16 and a GPU of its own (ranks sharing one GPU need an explicit reduced grid,
+    SL_VA_REMOTE_G); never for U-shape or with --split_persist off.  The GPU objects are stubbed."""
+    import torch
+    from splitlearning_amd.config import parse_args
+    from splitlearning_amd.data.mnist import write_shards
+    from splitlearning_amd.parallel.dist import Comm, Placement
+    from splitlearning_amd.protocols import VanillaSession
+    from splitlearning_amd.protocols import split_native
+
+    class _C:
+        VanillaEpoch = object
+
+        def get_compute_dtype(self):
+            return "fp32"
+
+    class _Ops:
+        c = _C()
+
+        def C(self):
+            return self.c
+
+    class _Chan:
+        def host_error(self):
+            return 0
+
+    monkeypatch.delenv("SL_VA_REMOTE_G", raising=False)
+
+    def sess(*flags):
+        args = parse_args(["--vanilla", "--world_size", "2", "--num_samples", "300", "--no_tqdm",
+                           "--datapath", str(tmp_path / "d"), "--log_dir", str(tmp_path / "l")] + list(flags))
+        write_shards(args, verbose=False)
+        dev = torch.device("cpu")
+        s = VanillaSession(args, Comm(0, 1, dev, Placement.make(2, 1, 1)), dev)
+        s.ops = _Ops()
+        s.split_channel = _Chan()
+        return s
+
+    s = sess()
+    assert split_native.persistent_remote_ok(s, 1, "vanilla")
+    assert not split_native.persistent_remote_ok(s, 1, "ushape")
+    assert not split_native.persistent_remote_ok(sess("--split_persist", "off"), 1, "vanilla")
+    assert not split_native.persistent_remote_ok(sess("--batch_size", "32"), 1, "vanilla")
+    s = sess()
+    s.split_channel = object()            # RCCL link: the kernel speaks the peer-mapped protocol only
+    assert not split_native.persistent_remote_ok(s, 1, "vanilla")
+    s = sess()
+    s.comm.host_staging = True            # ranks share one GPU
+    assert not split_native.persistent_remote_ok(s, 1, "vanilla")
+    monkeypatch.setenv("SL_VA_REMOTE_G", "64")
+    assert split_native.persistent_remote_ok(s, 1, "vanilla")
+    s._va_rem_off = True                  # an earlier decline in this session
+    assert not split_native.persistent_remote_ok(s, 1, "vanilla")

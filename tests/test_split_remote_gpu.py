@@ -34,6 +34,22 @@ def test_remote_split_epoch_is_bitwise_python_loop(kind, B):
     assert out.stdout.count("PASS") == 2, text[-3000:]
 
 
+@pytest.mark.parametrize("B", [16, 5])
+def test_remote_vanilla_persistent_bob_matches_per_batch(B):
+    """Bob's side of a remote Alice's vanilla epoch as ONE persistent launch that sends and
+    receives the per-batch messages on the peer-mapped channel itself (csrc/vanilla.hip REM),
+    her side the unchanged run_alice: within fp32 rounding of the per-batch run_bob, one launch
+    bitwise its chunked launches, run_bob's message sequence, executors mixed on one channel
+    (scripts/vanilla_remote_one_gpu.py; Bob on 64 of the one GPU's CUs, a scaled tail)."""
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "vanilla_remote_one_gpu.py"), str(B), "64"],
+                         capture_output=True, text=True, timeout=115, cwd=ROOT)
+    text = out.stdout + out.stderr
+    assert out.returncode == 0, text[-3000:]
+    assert out.stdout.count("one launch bitwise chunked: True") == 2, text[-3000:]
+    assert "message sequence equal True" in out.stdout, text[-3000:]
+    assert out.stdout.count("PASS") == 2, text[-3000:]
+
+
 @pytest.mark.parametrize("mode,n,ws,port", [("ushape", 2, 2, 29793), ("vanilla", 4, 5, 29795)])
 def test_bench_split_schedule_with_remote_alices(tmp_path, mode, n, ws, port):
     out_json = tmp_path / "b.json"
