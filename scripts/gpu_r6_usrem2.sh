@@ -1,0 +1,22 @@
+#!/bin/bash
+# round 6: U-shape remote bf16 (Adam-bound comparison), the vanilla prefetch A/B (ab/run.sh), the
+# vanilla / remote regression tests and the vanilla bench.  A faulting / aborting / timed-out step
+# ends the call.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export PYTHONUNBUFFERED=1
+O=gpurun_out/r6_usrem2
+mkdir -p $O
+step() {
+  local name=$1 t=$2; shift 2
+  timeout -k 10 $t "$@" > $O/$name.log 2>&1
+  local rc=$?
+  echo "$name rc $rc"; grep -E "rank|PASS|passed|failed|Error|us/step" $O/$name.log | tail -12
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name"; exit $rc; fi
+  return 0
+}
+step us16bf 200 python -u scripts/ushape_remote_one_gpu.py 16 2 bf16
+step us5bf 200 python -u scripts/ushape_remote_one_gpu.py 5 2 bf16
+step ab 900 bash ab/run.sh
+step tests 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_vanilla_persist_gpu.py tests/test_golden_gpu.py tests/test_long_launch_gpu.py tests/test_split_remote_gpu.py -k "vanilla or remote"
+step bench_va 300 python bench.py --mode vanilla --steps 20 --warmup 5 --json_out $O/bench_vanilla.json

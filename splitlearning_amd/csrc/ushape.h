@@ -25,7 +25,26 @@ constexpr int kUsStride = 32;     // counter words 128 B apart
 // F2[8] / L[8] / D[8] (fc2 partials / h2 / dlogits, per-XCD shards), DZ[8] (dz1 slices per row
 // group), DX[32] (cut-gradient partials per channel), CW[32] (conv gradient partials per channel)
 constexpr int kUsXC = 0, kUsPC = 32, kUsF2 = 40, kUsL = 48, kUsD = 56, kUsDZ = 64, kUsDX = 72, kUsCW = 104;
-constexpr int kUsCounters = 136;
+constexpr int kUsFin = 136;       // remote Alice: the launch's closing arrivals (the last dz2's ack)
+constexpr int kUsCounters = 137;
+
+// A REMOTE Alice (UsArgs::rem): her conv front and head run in her process (csrc/split.cpp
+// run_alice, unchanged) and the launch speaks the peer-mapped channel (csrc/ipc_p2p.h) itself,
+// in run_bob's order: per step i it receives her activation (generation rgen0 + 1 + 2 i), sends
+// h2 (sgen0 + 1 + 2 i), receives her premasked dz2 (rgen0 + 2 + 2 i) and sends the cut gradient
+// (sgen0 + 2 + 2 i), each on the parity slot of its generation.
+struct UsLink {
+  float* sdata[2];          // her slot data[bob][par]
+  uint32_t* sflag[2];       // her flag words [bob][par][chunk]
+  const uint32_t* sack[2];  // own ack words [alice][par][chunk]
+  const float* rdata[2];    // own slot data[alice][par]
+  const uint32_t* rflag[2]; // own flag words [alice][par][chunk]
+  uint32_t* rack[2];        // her ack words [bob][par][chunk]
+  uint32_t sgen0, rgen0;
+  int sprev[2];             // chunk counts of the messages two generations before sends 0 (h2_0), 1 (dx_0)
+  int* err;
+  int* herr;
+};
 
 struct UsArgs {
   // Bob: fc1 [N1][5408], fc2 [N2][N1], Adam moments of each
@@ -36,7 +55,7 @@ struct UsArgs {
   float *W3, *m3, *v3, *b3, *mb3, *vb3;
   int N1, N2, C, M, S;
   SlOpt ob, oa;                // Bob's / Alice's Adam (lr, betas, eps, wd; step scalars per step in tabf)
-  const float* tabf;           // [S][8] {ss_b, ib_b, ss_a, ib_a, CE scale (1 / the step's rows), -, -, -}
+  const float* tabf;           // [S][8] {ss_b, ib_b, ss_a, ib_a, CE scale (1 / the step's rows), rows, -, -}
   const uint8_t* img;          // Alice's shard pixels [N][784]
   const int64_t* rows;         // [S * M] shard row of every batch row (-1: padding)
   const int64_t* Y;            // [S * M] labels (ignore for padding)
@@ -59,6 +78,10 @@ struct UsArgs {
   int coop;
   int bf16;                    // products on bf16 operands (fc1's on bf16 MFMA), fp32 accumulation and state
   int fault_step;              // tests: this step's first wait is never met; -1 off
+  // remote Alice: the <.., true> instantiation; RG row groups of 128 fc1 rows, G = 32 RG
+  // workgroups (so a one-GPU test can leave CUs to her kernels); tabf [5] = the step's rows
+  int rem, RG, G;
+  UsLink lk;
 };
 
 std::string ushape_check(const UsArgs& a);

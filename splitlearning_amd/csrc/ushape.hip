@@ -47,7 +47,24 @@
 // Every sum runs in a fixed order: a launch is deterministic and one launch of S steps is
 // bitwise S one-step launches.  Results agree with the per-batch executor and torch to fp32
 // rounding (different summation orders; the hardware square root / reciprocal in Adam).
+//
+// REMOTE Alice (the <.., true> instantiations; BASELINE config 2: one Bob and one Alice on two
+// GPUs, reference data_entities.py:65-81 over RPC).  Her conv front and head run in her process
+// (csrc/split.cpp run_alice, unchanged) and the launch exchanges run_bob's four messages per step
+// on the peer-mapped channel (csrc/ipc_p2p.h) itself, in place of the conv jobs and the CE:
+//   in   her activation of step i: workgroup (rg, c) copies rows rg + RG t of channel c's slice
+//        into XS (flags polled relaxed, one acquire, system-scope loads) -> XC[c];
+//   out  h2 after the L shards (workgroups 0, 1: its <= 2 chunks, gathered from H2);
+//   in   her premasked dz2 (every workgroup reads the <= 2 chunks into its dz2 slab) -> D;
+//   out  the cut gradient after every channel's DX partials (workgroup c: chunk c, the row
+//        groups' partials summed in order, as the conv jobs sum them).
+// Sends are system-scope write-through stores, drained, released, then the chunk's flag; each
+// send first waits for her ack of the message two generations back.  Her activation and dz2 of
+// step i - 1 are acked at step i after the F2 seam (every workgroup has read them by then), the
+// last dz2 after a closing seam.  Without conv jobs the grid is 32 RG workgroups for RG row groups
+// (a one-GPU test runs a narrower fc1 on 64 CUs next to her kernels).
 #include "ushape.h"
+#include "ipc_ar.h"
 #include "persist.h"
 
 #include <string>
@@ -101,6 +118,23 @@ __device__ __forceinline__ bool us_wait(const UsArgs& a, int n, int* s_ok, F tgt
   return *s_ok != 0;
 }
 
+// one lane: bounded wait until the channel flag / ack word *f reaches generation `want` (remote
+// Alice); a timeout raises the launch's error word and the channel's
+__device__ __forceinline__ bool us_pwait(const UsArgs& a, const uint32_t* f, uint32_t want) {
+  if ((int32_t)(ipc_poll_flag(f) - want) >= 0) return true;
+  const uint64_t t0 = wall_clock64();
+  while ((int32_t)(ipc_poll_flag(f) - want) < 0) {
+    if (failed(a.err)) return false;
+    __builtin_amdgcn_s_sleep(1);
+    if ((int64_t)(wall_clock64() - t0) > a.timeout) {
+      __hip_atomic_fetch_or(a.err, 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ipc_fail(a.lk.err, a.lk.herr);
+      return false;
+    }
+  }
+  return true;
+}
+
 // arrivals per shard s of a seam whose producers are workgroups 0 .. n - 1 (shard w % 8)
 __device__ __forceinline__ unsigned us_shard_n(int n, int s) { return n > s ? (unsigned)((n - 1 - s) / 8 + 1) : 0u; }
 
@@ -150,7 +184,8 @@ __device__ __forceinline__ us_bf16x4 us_bf4(f32x4 v) {
   return us_bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
 }
 
-template <bool BF>
+// REM: the Alice is remote (the channel phases above in place of her conv jobs and head)
+template <bool BF, bool REM>
 __global__ void __launch_bounds__(kUsThreads) ushape_epoch_kernel(UsArgs a) {
   auto R = [](float v) { return BF ? bfr(v) : v; };
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -177,6 +212,7 @@ __global__ void __launch_bounds__(kUsThreads) ushape_epoch_kernel(UsArgs a) {
 
   const int w = blockIdx.x, rg = w >> 5, cc = w & 31;
   const int M = a.M, N1 = a.N1, N2 = a.N2, C = a.C;
+  const int RG = REM ? a.RG : kUsRG, G = REM ? a.G : kUsG;
   const int nb = 128 * rg;
   const __amdgpu_buffer_rsrc_t rHB = rs_of(a.HB);
   const int bXS = 4 * a.oXS, bPP = 4 * a.oPP, bP2 = 4 * a.oP2, bH2 = 4 * a.oH2, bDL = 4 * a.oDL, bDZ = 4 * a.oDZ,
@@ -206,13 +242,13 @@ __global__ void __launch_bounds__(kUsThreads) ushape_epoch_kernel(UsArgs a) {
       sW2[512 + q * 128 + j] = ok ? a.m2[off] : 0.f;
       sW2[1024 + q * 128 + j] = ok ? a.v2[off] : 0.f;
     }
-    for (int e = tid; e < kUsW3; e += kUsThreads) {
+    for (int e = tid; !REM && e < kUsW3; e += kUsThreads) {
       const bool ok = e < C * N2;
       sW3[e] = ok ? a.W3[e] : 0.f;
       sW3[kUsW3 + e] = ok ? a.m3[e] : 0.f;
       sW3[2 * kUsW3 + e] = ok ? a.v3[e] : 0.f;
     }
-    if (tid < kUsCP) {
+    if (!REM && tid < kUsCP) {
       const bool ok = tid < C;
       sb3[tid] = ok ? a.b3[tid] : 0.f;
       sb3[kUsCP + tid] = ok ? a.mb3[tid] : 0.f;
@@ -231,7 +267,7 @@ __global__ void __launch_bounds__(kUsThreads) ushape_epoch_kernel(UsArgs a) {
       sb2[1] = ok ? a.mb2[w] : 0.f;
       sb2[2] = ok ? a.vb2[w] : 0.f;
     }
-    if (tid < 10) {
+    if (!REM && tid < 10) {
       // {w[9], b} of channel cc, then their m, then their v
       const int j = tid;
       scv[j] = j < 9 ? a.cw[cc * 9 + j] : a.cb[cc];
@@ -303,10 +339,67 @@ __global__ void __launch_bounds__(kUsThreads) ushape_epoch_kernel(UsArgs a) {
     }
   };
 
-  // ---- prologue: Alice's forward of batch 0
-  img_put(0, img_word(0));
-  __syncthreads();
-  conv_fwd(0);
+  // ---------------------------------------------------------------- remote Alice (REM)
+  auto rows_of = [&](int s) { return (int)a.tabf[8 * s + 5]; };
+  auto nchunks = [](int n) { return (n + kIpcChunk - 1) / kIpcChunk; };
+  // her activation of step s -> XS[s & 1]: workgroup (rg, cc) rows m = rg + RG t (t < 16 / RG) of
+  // channel cc's 169 columns (padding rows zero); false when a wait gave up
+  auto recv_act = [&](int s) -> bool {
+    const int Ms = rows_of(s);
+    const uint32_t gen = a.lk.rgen0 + 1u + 2u * (uint32_t)s;
+    const int par = (int)(gen & 1u);
+    if (threadIdx.x < 64) {
+      const int lane = threadIdx.x, t = lane >> 1, m = rg + RG * t;
+      bool ok = true;
+      if (t < 16 / RG && m < Ms) {
+        const int base = m * (kUsCh * kUsP) + cc * kUsP;
+        ok = us_pwait(a, a.lk.rflag[par] + ((lane & 1) ? base + kUsP - 1 : base) / kIpcChunk, gen);
+      }
+      ok = __all(ok);
+      ipc_acquire();
+      if (lane == 0) *s_ok = ok ? 1 : 0;
+    }
+    __syncthreads();
+    if (*s_ok == 0) return false;
+    const __amdgpu_buffer_rsrc_t rR = ipc_rsrc(a.lk.rdata[par]);
+    for (int e = threadIdx.x; e < (16 / RG) * kUsP; e += kUsThreads) {
+      const int t = e / kUsP, p = e - t * kUsP, m = rg + RG * t;
+      float v = 0.f;
+      if (m < Ms)
+        v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rR, (m * (kUsCh * kUsP) + cc * kUsP + p) * 4, 0, 17));
+      hst1(rHB, bXS + ((((s & 1) * kUsCh + cc) * 16 + m) * kUsKP + p) * 4, v);
+    }
+    return true;
+  };
+  // one chunk of a message to her: wait for her ack of the message two generations back on the
+  // slot, fill(e, v) -> the float4 at e (< len), system-scope stores, drain, release, flag
+  auto send_chunk = [&](int c, uint32_t gen, int prev, int len, auto fill) -> bool {
+    const int par = (int)(gen & 1u);
+    if (threadIdx.x == 0) {
+      const bool ok = prev == 0 || us_pwait(a, a.lk.sack[par] + (c < prev ? c : 0), gen - 2u);
+      ipc_acquire();
+      *s_ok = ok ? 1 : 0;
+    }
+    __syncthreads();
+    if (*s_ok == 0) return false;
+    const int e = c * kIpcChunk + 4 * (int)threadIdx.x;
+    if ((int)threadIdx.x < kIpcThreads && e < len) ipc_st4(ipc_rsrc(a.lk.sdata[par]), e, __builtin_bit_cast(float4, fill(e)));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) ipc_raise_flag(a.lk.sflag[par] + c, gen);
+    __syncthreads();
+    return true;
+  };
+  int i_end = 0;   // steps completed (remote: the closing ack)
+
+  // ---- prologue: Alice's forward of batch 0 (remote: her message of it)
+  if constexpr (REM) {
+    if (!recv_act(0)) goto fin;
+  } else {
+    img_put(0, img_word(0));
+    __syncthreads();
+    conv_fwd(0);
+  }
   us_arrive(a, kUsXC + cc);
 
   for (int i = 0; i < a.S; ++i) {
@@ -316,12 +409,12 @@ __global__ void __launch_bounds__(kUsThreads) ushape_epoch_kernel(UsArgs a) {
     const float cs = a.tabf[8 * i + 4];
     asm volatile("" : "+v"(ss_b), "+v"(ib_b), "+v"(ss_a), "+v"(ib_a));   // held in VGPRs (res_update)
     // the next batch's images, in flight across the step (into LDS in the conv phase)
-    const uint32_t pimg = more ? img_word(i + 1) : 0u;
+    const uint32_t pimg = (!REM && more) ? img_word(i + 1) : 0u;
 
     // ================= F: x_i of channel cc, the forward partial over its columns
     if (!us_wait(a, 1, s_ok, [&](int, int& idx) {
           idx = kUsXC + cc;
-          return i == a.fault_step ? 0xffffffffu : 8u * (unsigned)(i + 1);
+          return i == a.fault_step ? 0xffffffffu : (unsigned)RG * (unsigned)(i + 1);
         }))
       break;
     {
@@ -407,9 +500,21 @@ __global__ void __launch_bounds__(kUsThreads) ushape_epoch_kernel(UsArgs a) {
     if (w < N2) {
       if (!us_wait(a, 8, s_ok, [&](int l, int& idx) {
             idx = kUsF2 + l;
-            return 32u * (unsigned)(i + 1);
+            return (unsigned)(G / 8) * (unsigned)(i + 1);
           }))
         break;
+      if constexpr (REM) {
+        // every workgroup has read her activation of this step and her dz2 of the last one
+        if (threadIdx.x == 0) {
+          const uint32_t ga = a.lk.rgen0 + 1u + 2u * (uint32_t)i;
+          for (int c = w; c < nchunks(rows_of(i) * (kUsCh * kUsP)); c += N2)
+            ipc_raise_flag(a.lk.rack[ga & 1u] + c, ga, 0);
+          if (i > 0) {
+            const uint32_t gd = ga - 1u;
+            for (int c = w; c < nchunks(rows_of(i - 1) * N2); c += N2) ipc_raise_flag(a.lk.rack[gd & 1u] + c, gd, 0);
+          }
+        }
+      }
       {
         US_IDX();
         const int sl = tid >> 2, mg = tid & 3;   // producers 2 sl, 2 sl + 1
@@ -444,8 +549,29 @@ __global__ void __launch_bounds__(kUsThreads) ushape_epoch_kernel(UsArgs a) {
       us_arrive(a, kUsL + (w & 7));
     }
 
+    // ================= (remote) h2 to her: workgroups c < its chunks, after the L shards
+    if constexpr (REM) {
+      const int len = rows_of(i) * N2;
+      if (w < nchunks(len)) {
+        if (!us_wait(a, 8, s_ok, [&](int l, int& idx) {
+              idx = kUsL + l;
+              return (unsigned)(i + 1) * us_shard_n(N2, l);
+            }))
+          break;
+        const uint32_t gen = a.lk.sgen0 + 1u + 2u * (uint32_t)i;
+        const int prev = i > 0 ? nchunks(rows_of(i - 1) * N2) : a.lk.sprev[0];
+        if (!send_chunk(w, gen, prev, len, [&](int e) {
+              const int m = e / N2, j = e - m * N2;   // N2 % 4 == 0: one row
+              f32x4 v;
+#pragma unroll
+              for (int q = 0; q < 4; ++q) v[q] = hld1(rHB, bH2 + ((par * kUsN2P + j + q) * 16 + m) * 4);
+              return v;
+            }))
+          break;
+      }
+    }
     // ================= CE: workgroup m = w < M: model3 logits of row m, softmax-CE, dlogits
-    if (w < M) {
+    if (!REM && w < M) {
       if (!us_wait(a, 8, s_ok, [&](int l, int& idx) {
             idx = kUsL + l;
             return (unsigned)(i + 1) * us_shard_n(N2, l);
@@ -487,6 +613,26 @@ __global__ void __launch_bounds__(kUsThreads) ushape_epoch_kernel(UsArgs a) {
     }
 
     // ================= D: dz2 (old head), dz1 of my 4 rows (old W2); then the small Adam steps
+    if constexpr (REM) {
+      // her premasked dz2 (scaled by her CE) -> the dz2 slab
+      const int Mi = rows_of(i), len = Mi * N2;
+      const uint32_t gen = a.lk.rgen0 + 2u + 2u * (uint32_t)i;
+      if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        const bool ok = __all(lane < nchunks(len) ? us_pwait(a, a.lk.rflag[gen & 1u] + lane, gen) : true);
+        ipc_acquire();
+        if (lane == 0) *s_ok = ok ? 1 : 0;
+      }
+      __syncthreads();
+      if (*s_ok == 0) break;
+      const __amdgpu_buffer_rsrc_t rR = ipc_rsrc(a.lk.rdata[gen & 1u]);
+      for (int e = threadIdx.x; e < 16 * kUsN2P; e += kUsThreads) {
+        const int m = e / kUsN2P, j = e - m * kUsN2P;
+        sdz2[m * kUsN2P + j] =
+            (m < Mi && j < N2) ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rR, (m * N2 + j) * 4, 0, 17)) : 0.f;
+      }
+      __syncthreads();
+    } else {
     if (!us_wait(a, 8, s_ok, [&](int l, int& idx) {
           idx = kUsD + l;
           return (unsigned)(i + 1) * us_shard_n(M, l);
@@ -517,6 +663,7 @@ __global__ void __launch_bounds__(kUsThreads) ushape_epoch_kernel(UsArgs a) {
       }
     }
     __syncthreads();
+    }
     {
       US_IDX();
       const int o = tid >> 3, part = tid & 7, m = o >> 2, q = o & 3;
@@ -562,14 +709,14 @@ __global__ void __launch_bounds__(kUsThreads) ushape_epoch_kernel(UsArgs a) {
         for (int m = 0; m < 16; ++m) g += sdz2[m * kUsN2P + w];
         res_update<true>(a.ob, ss_b, ib_b, sb2[0], g, sb2[1], sb2[2]);
       }
-      for (int e = tid; e < C * N2; e += kUsThreads) {
+      for (int e = tid; !REM && e < C * N2; e += kUsThreads) {
         const int cls = e / N2, j = e - cls * N2;
         float g = 0.f;
 #pragma unroll
         for (int m = 0; m < 16; ++m) g = fmaf(R(sdl[m * kUsCP + cls]), R(sh2[m * kUsN2P + j]), g);
         res_update<true>(a.oa, ss_a, ib_a, sW3[e], g, sW3[kUsW3 + e], sW3[2 * kUsW3 + e]);
       }
-      if (tid >= 32 && tid < 32 + C) {
+      if (!REM && tid >= 32 && tid < 32 + C) {
         const int cls = tid - 32;
         float g = 0.f;
 #pragma unroll
@@ -631,6 +778,39 @@ __global__ void __launch_bounds__(kUsThreads) ushape_epoch_kernel(UsArgs a) {
     }
     us_arrive(a, kUsDX + cc);
 
+    if constexpr (REM) {
+      // ================= (remote) the cut gradient to her, her activation of batch i + 1 in
+      const int len = rows_of(i) * (kUsCh * kUsP);
+      if (w < nchunks(len)) {
+        if (!us_wait(a, kUsCh, s_ok, [&](int l, int& idx) {
+              idx = kUsDX + l;
+              return (unsigned)RG * (unsigned)(i + 1);
+            }))
+          break;
+        const uint32_t gen = a.lk.sgen0 + 2u + 2u * (uint32_t)i;
+        const int prev = i > 0 ? nchunks(rows_of(i - 1) * (kUsCh * kUsP)) : a.lk.sprev[1];
+        bool sent = true;
+        for (int c = w; sent && c < nchunks(len); c += G)   // 85 chunks at B = 16: more than a narrow grid
+          sent = send_chunk(c, gen, prev, len, [&](int e) {
+              const int m = e / (kUsCh * kUsP), k0 = e - m * (kUsCh * kUsP);
+              f32x4 v;
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                const int c = (k0 + q) / kUsP, p = (k0 + q) - c * kUsP;
+                float gx = 0.f;
+                for (int g = 0; g < RG; ++g)   // the row groups' partials in order, as the conv jobs
+                  gx += hld1(rHB, bDX + (((((par * kUsCh + c) * kUsRG + g) * kUsKP + p) * 16 + m) * 4));
+                v[q] = gx;
+              }
+              return v;
+            });
+        if (!sent) break;
+      }
+      if (more) {
+        if (!recv_act(i + 1)) break;
+        us_arrive(a, kUsXC + cc);
+      }
+    } else {
     // ================= C: conv job: backward, the channel's step, forward of batch i + 1
     if (!us_wait(a, 1, s_ok, [&](int, int& idx) {
           idx = kUsDX + cc;
@@ -699,6 +879,7 @@ __global__ void __launch_bounds__(kUsThreads) ushape_epoch_kernel(UsArgs a) {
       conv_fwd(i + 1);
       us_arrive(a, kUsXC + cc);
     }
+    }
 
     // ================= U: fc1's Adam step in registers (dW = dz1^T x_i on MFMA)
     {
@@ -723,6 +904,24 @@ __global__ void __launch_bounds__(kUsThreads) ushape_epoch_kernel(UsArgs a) {
         // lane: dW[n = 16 r + li][16 kb + 4 lq + j] = g[j]
         res_update4<true>(a.ob, ss_b, ib_b, Wr[kb], g, Mr[kb], Vr[kb]);
         asm volatile("" ::: "memory");
+      }
+    }
+    i_end = i + 1;
+  }
+
+fin:
+  if constexpr (REM) {
+    // the last step's dz2: acked once every workgroup has read it (a closing seam)
+    if (i_end == a.S && a.S > 0) {
+      us_arrive(a, kUsFin);
+      const int s = a.S - 1;
+      const uint32_t gd = a.lk.rgen0 + 2u + 2u * (uint32_t)s;
+      const int nch = nchunks(rows_of(s) * N2);
+      if (w < nch && us_wait(a, 1, s_ok, [&](int, int& idx) {
+            idx = kUsFin;
+            return (unsigned)G;
+          })) {
+        if (threadIdx.x == 0) ipc_raise_flag(a.lk.rack[gd & 1u] + w, gd, 0);
       }
     }
   }
@@ -764,7 +963,7 @@ __global__ void __launch_bounds__(kUsThreads) ushape_epoch_kernel(UsArgs a) {
       a.mb2[w] = sb2[1];
       a.vb2[w] = sb2[2];
     }
-    if (w == 0) {
+    if (!REM && w == 0) {
       for (int e = tid; e < C * N2; e += kUsThreads) {
         a.W3[e] = sW3[e];
         a.m3[e] = sW3[kUsW3 + e];
@@ -776,7 +975,7 @@ __global__ void __launch_bounds__(kUsThreads) ushape_epoch_kernel(UsArgs a) {
         a.vb3[tid] = sb3[2 * kUsCP + tid];
       }
     }
-    if (rg == 0 && tid < 10) {
+    if (!REM && rg == 0 && tid < 10) {
       const int j = tid;
       if (j < 9) {
         a.cw[cc * 9 + j] = scv[j];
@@ -794,12 +993,26 @@ __global__ void __launch_bounds__(kUsThreads) ushape_epoch_kernel(UsArgs a) {
 
 std::string ushape_check(const UsArgs& a) {
   if (a.M < 1 || a.M > 16) return "rows per step 1..16";
+  if (a.rem) {
+    if (a.RG != 1 && a.RG != 2 && a.RG != 4 && a.RG != 8) return "remote Alice: 1, 2, 4 or 8 row groups";
+    if (a.G != 32 * a.RG || a.N1 > 128 * a.RG) return "remote Alice: 32 workgroups per 128-row group";
+    if (a.N2 > a.G || a.N2 % 4) return "remote Alice: fc2 width % 4, one h2 workgroup per column";
+    if (a.lk.sdata[0] == nullptr || a.lk.rdata[0] == nullptr) return "remote Alice: the channel";
+  }
   if (a.N1 < 1 || a.N1 > kUsRG * 128) return "fc1 width <= 1024";
   if (a.N2 < 1 || a.N2 > kUsN2P) return "fc2 width <= 128";
   if (a.C < 1 || a.C > kUsCP || a.C * a.N2 > kUsW3) return "head classes <= 16, classes x fc2 width <= 1024";
   if (a.ob.kind != 2 || a.oa.kind != 2) return "Adam on both sides";
   if (a.S < 0) return "steps";
   return "";
+}
+
+static const void* us_kernel(const UsArgs& a) {
+  if (a.rem)
+    return a.bf16 ? reinterpret_cast<const void*>(&ushape_epoch_kernel<true, true>)
+                  : reinterpret_cast<const void*>(&ushape_epoch_kernel<false, true>);
+  return a.bf16 ? reinterpret_cast<const void*>(&ushape_epoch_kernel<true, false>)
+                : reinterpret_cast<const void*>(&ushape_epoch_kernel<false, false>);
 }
 
 bool ushape_fits(const UsArgs& a, int device, std::string* why) {
@@ -809,13 +1022,12 @@ bool ushape_fits(const UsArgs& a, int device, std::string* why) {
     if (hipGetDeviceProperties(&pr, device) != hipSuccess) {
       s = "device properties";
     } else {
-      const void* fn = a.bf16 ? reinterpret_cast<const void*>(&ushape_epoch_kernel<true>)
-                              : reinterpret_cast<const void*>(&ushape_epoch_kernel<false>);
+      const void* fn = us_kernel(a);
       int nb = 0;
       hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kUsLds);
       if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, kUsThreads, kUsLds);
       if (e != hipSuccess || nb < 1) s = "occupancy";
-      else if ((int64_t)nb * pr.multiProcessorCount < kUsG) s = "workgroups not co-resident";
+      else if ((int64_t)nb * pr.multiProcessorCount < (a.rem ? a.G : kUsG)) s = "workgroups not co-resident";
     }
   }
   if (why) *why = s;
@@ -825,16 +1037,16 @@ bool ushape_fits(const UsArgs& a, int device, std::string* why) {
 hipError_t ushape_epoch_launch(const UsArgs& a, hipStream_t st) {
   if (!ushape_check(a).empty()) return hipErrorInvalidValue;
   if (a.S <= 0) return hipSuccess;
-  const void* fn = a.bf16 ? reinterpret_cast<const void*>(&ushape_epoch_kernel<true>)
-                          : reinterpret_cast<const void*>(&ushape_epoch_kernel<false>);
+  const void* fn = us_kernel(a);
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kUsLds);
   if (e != hipSuccess) return e;
   e = hipMemsetAsync(a.cnt, 0, (size_t)kUsCounters * kUsStride * sizeof(unsigned), st);
   if (e != hipSuccess) return e;
   UsArgs arg = a;
   void* params[] = {&arg};
-  if (!a.coop) return hipLaunchKernel(fn, dim3(kUsG), dim3(kUsThreads), params, (size_t)kUsLds, st);
-  return hipLaunchCooperativeKernel(fn, dim3(kUsG), dim3(kUsThreads), params, (unsigned)kUsLds, st);
+  const int G = a.rem ? a.G : kUsG;
+  if (!a.coop) return hipLaunchKernel(fn, dim3(G), dim3(kUsThreads), params, (size_t)kUsLds, st);
+  return hipLaunchCooperativeKernel(fn, dim3(G), dim3(kUsThreads), params, (unsigned)kUsLds, st);
 }
 
 }  // namespace sl

@@ -80,14 +80,14 @@ struct VaArgs {
   //   LA [2][nrb][kVaSlots][16 n][16 m] forward partials    H1 [2][N1][16 m] h1
   //   FP [2][NC][N2][16 m] fc2 partials                      LP [2][HW][16][C4] logit partials
   //   DL [2][16][C4] dlogits                                 DZ [2][16][N2] dz2
-  //   DP [2][8][N1][16 m] dz1 partials                       ZP [G][kVaRuns][8][64] f32x4
+  //   DP [2][8][N1][16 m] dz1 partials
   //   DX [ncb][kVaDxSlots][16 m][256] cut-gradient partials
   //   CWP [2][32][8][16] conv gradient partials per (channel, image pair)
   // the batches' activations, one [16][K1] slot per step of the launch (each written once,
-  // before any read, so the forward and update passes read it with plain L2-cached loads)
+  // before any read; read with sc1 loads like every handed-off byte)
   float* Xr;
   float* HB;
-  int oLA, oH1, oFP, oLP, oDL, oDZ, oDP, oZP, oDX, oCWP;
+  int oLA, oH1, oFP, oLP, oDL, oDZ, oDP, oDX, oCWP;
   unsigned* cnt;          // [kVaCounters][kVaStride] (zeroed per launch)
   const int* shard_n;     // [kVaSeams][8] arrivals per seam shard and step
   int* err;               // nonzero after a wait gave up (2 timeout)

@@ -152,6 +152,7 @@ __device__ __forceinline__ bool va_pwait(const VaArgs& a, const uint32_t* f, uin
 
 constexpr int kSt = 16;   // fc1 W / buf loads and stores: sc1 (write-through stores, L1-bypassing loads)
 constexpr int kVaFwdRing = 6;   // forward-pass register ring depth (tiles; kVaFwdRing - 1 in flight)
+constexpr int kVaFwdPre = 2;    // of them loaded early, under the seam-X wait (VGPR budget: 3 spill)
 
 // f(integral_constant<int, I>) for I in [B, E): compile-time ring and buffer indices in the
 // unrolled tile loops
@@ -174,6 +175,10 @@ constexpr int OFF_U = OFF_W2 + ((kVaMaxWR * PW2 * 4 + 15) & ~15);
 constexpr int U_SA = 0;
 constexpr int U_DZB = U_SA + 16 * 64 * 16;
 constexpr int kUUpd = U_DZB + kVaRuns * 256 * 4;
+// union, forward-pass view: the flush's last-row-block accumulators [8 waves][64] f32x4 at U_SA,
+// the earlier row blocks' [kVaRuns - 1][8 waves][64] f32x4 behind them (no global round trip)
+constexpr int U_ZP = U_SA + 8 * 64 * 16;
+constexpr int kUFwd = U_ZP + (kVaRuns - 1) * 8 * 64 * 16;
 // union, fc2 view
 constexpr int U_SH1 = 0;
 constexpr int U_SDZ2 = U_SH1 + 16 * PH * 4;
@@ -182,7 +187,8 @@ constexpr int U_SDL = U_RED + 16 * 32 * 16;
 constexpr int U_SH2 = U_SDL + 16 * kVaMaxC * 4;
 constexpr int U_SDZH = U_SH2 + 16 * 4 * 4;
 constexpr int kUFc2 = U_SDZH + 16 * 4 * 4;
-constexpr int kU = kUUpd > kUFc2 ? kUUpd : kUFc2;
+constexpr int kU0 = kUUpd > kUFc2 ? kUUpd : kUFc2;
+constexpr int kU = kU0 > kUFwd ? kU0 : kUFwd;
 constexpr int OFF_W3 = OFF_U + kU;                       // W3 columns {W, buf}[4][kVaMaxC]
 constexpr int OFF_B3 = OFF_W3 + 2 * 4 * kVaMaxC * 4;     // b3 {W, buf}[kVaMaxC]
 constexpr int OFF_B2 = OFF_B3 + 2 * kVaMaxC * 4;         // b2 {W, buf}[4] (+ pad)
@@ -218,6 +224,7 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* sw2 = reinterpret_cast<float*>(smem + OFF_W2);
   f32x4* sa = reinterpret_cast<f32x4*>(smem + OFF_U + U_SA);
+  f32x4* szp = reinterpret_cast<f32x4*>(smem + OFF_U + U_ZP);
   float* sdzb = reinterpret_cast<float*>(smem + OFF_U + U_DZB);
   float* sh1 = reinterpret_cast<float*>(smem + OFF_U + U_SH1);
   float* sdz2 = reinterpret_cast<float*>(smem + OFF_U + U_SDZ2);
@@ -261,7 +268,7 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
   const int cc = w & 31, cg = w >> 5;
   const __amdgpu_buffer_rsrc_t rHB = rs_of(a.HB);
   const int bLA = 4 * a.oLA, bH1 = 4 * a.oH1, bFP = 4 * a.oFP, bLP = 4 * a.oLP, bDL = 4 * a.oDL, bDZ = 4 * a.oDZ,
-            bDP = 4 * a.oDP, bZP = 4 * a.oZP, bDX = 4 * a.oDX, bCW = 4 * a.oCWP;
+            bDP = 4 * a.oDP, bDX = 4 * a.oDX, bCW = 4 * a.oCWP;
   const __amdgpu_buffer_rsrc_t rX = rs_of(a.Xr);
   const __amdgpu_buffer_rsrc_t rW1 = rs_of(a.L1.W), rM1 = rs_of(a.L1.m);
 
@@ -424,9 +431,10 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
     }
   };
   f32x4 zlast = zv;
+  // a finished row block's per-wave accumulator -> LDS (read by this workgroup's flush only)
   auto zp_store = [&](int k, f32x4 z) {
     VA_IDX();
-    hst4(rHB, bZP + (((w * kVaRuns + k) * 8 + r) * 64 + lane) * 16, z);
+    szp[(k * 8 + r) * 64 + lane] = z;
   };
   // The forward pass keeps kVaFwdRing - 1 tiles of W (sc1 loads: tiles another workgroup's
   // update run just wrote) and x in flight in a register ring, every load issued after the
@@ -436,6 +444,22 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
   // own k-slice of each tile with no LDS staging and no workgroup barrier per tile (the staged
   // form: a 16 KB LDS round trip and a barrier per tile, 4.3 TB/s).  Same products in the same
   // order at every depth and in both forms: the form and the depth change timing only.
+  // The ring's first W tiles are loaded early (fwd_prefetch), under the seam-X wait: once every
+  // update run of the step has arrived (XD), W no longer waits for anything, only x does.
+  constexpr int kPre = kVaFwdPre;
+  f32x4 wpre[kPre > 0 ? kPre : 1][2];
+  auto fwd_prefetch = [&]() {
+#pragma unroll
+    for (int d = 0; d < kPre; ++d)
+      if (d < nt) load_w(t_begin + d, wpre[d]);
+  };
+  // every update run of step i has stored and drained its tiles (the W the forward pass reads)
+  auto wait_all_xd = [&](int i) {
+    return va_wait_many(a, ncb, s_ok, [&](int l, int& idx) {
+      idx = va_XD(l);
+      return (unsigned)(i + 1) * (unsigned)a.tab[a.oU + G + 1 + ncb + l];
+    });
+  };
   auto fwd_pass = [&](int step) {
     if (nt <= 0) return;
     constexpr int D = kVaFwdRing;
@@ -444,7 +468,12 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
 #pragma unroll
     for (int d = 0; d < D - 1; ++d)
       if (d < nt) {
-        load_w(t_begin + d, wr[d]);
+        if (d < kPre) {
+          wr[d][0] = wpre[d][0];
+          wr[d][1] = wpre[d][1];
+        } else {
+          load_w(t_begin + d, wr[d]);
+        }
         load_xv(step, t_begin + d, xr[d]);
       }
     f32x4 z = zv;
@@ -497,7 +526,7 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
           for (int ww = 0; ww < 8; ++ww) parts[ww] = sa[ww * 64 + 16 * mg + nn];
         } else {
 #pragma unroll
-          for (int ww = 0; ww < 8; ++ww) parts[ww] = hld4(rHB, bZP + (((w * kVaRuns + k) * 8 + ww) * 64 + 16 * mg + nn) * 16);
+          for (int ww = 0; ww < 8; ++ww) parts[ww] = szp[(k * 8 + ww) * 64 + 16 * mg + nn];
         }
         f32x4 v = parts[0];
 #pragma unroll
@@ -747,6 +776,7 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
   va_arrive(a, va_seam(4, w & 7));
   if (!va_seam_wait(a, 4, 1u, s_ok, s_sn)) goto done;
   if constexpr (REM) ack_act(0);
+  fwd_prefetch();
   fwd_pass(0);
   flush(0);
 
@@ -1135,6 +1165,10 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
         if (!recv_act(i + 1)) break;
         va_arrive(a, va_seam(4, w & 7));
         VA_MARK(12);
+        if constexpr (kVaFwdPre > 0) {
+          if (!wait_all_xd(i)) break;
+          fwd_prefetch();
+        }
         if (!va_seam_wait(a, 4, (unsigned)(i + 2), s_ok, s_sn)) break;
         VA_MARK(13);
         ack_act(i + 1);
@@ -1224,6 +1258,10 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
       conv_fwd(i + 1);
       va_arrive(a, va_seam(4, w & 7));
       VA_MARK(12);
+      if constexpr (kVaFwdPre > 0) {
+        if (!wait_all_xd(i)) break;
+        fwd_prefetch();
+      }
       if (!va_seam_wait(a, 4, (unsigned)(i + 2), s_ok, s_sn)) break;
       VA_MARK(13);
       // ================= V: the forward pass of batch i + 1 over the updated fc1

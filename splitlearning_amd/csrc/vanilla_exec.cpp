@@ -144,7 +144,6 @@ class VanillaEpoch {
       a.oDL = take(2LL * 16 * a.C4);
       a.oDZ = take(2LL * 16 * a.N2);
       a.oDP = take(2LL * sl::kVaNR * 16 * a.N1);
-      a.oZP = take((int64_t)a.G * sl::kVaRuns * 8 * 64 * 4);
       a.oDX = take((int64_t)a.ncb * sl::kVaDxSlots * 16 * 256);
       a.oCWP = take(2LL * 32 * 8 * 16);
       HB_ = at::zeros({off}, opt);

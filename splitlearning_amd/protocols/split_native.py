@@ -353,33 +353,65 @@ def native_remote_role(sess, cid: int, mode: str):
 
 def persistent_remote_ok(sess, cid: int, mode: str) -> bool:
     """Bob's side only (the Alice's side is the same run_alice either way): whether Bob serves
-    this remote Alice's vanilla epoch with ONE persistent launch that speaks the peer-mapped
-    channel itself (`_C.VanillaEpoch.run_remote`, csrc/vanilla.hip REM).  Needs the peer-mapped
-    channel (not RCCL), fp32 SGD-momentum, B <= 16, the flag, no earlier failure, and a GPU of
-    its own: with ranks sharing one GPU the Alice's kernels need CUs the launch would hold, so
-    only an explicit reduced grid (SL_VA_REMOTE_G, the one-GPU tests) runs there."""
-    if mode != "vanilla" or getattr(sess.args, "split_persist", "auto") == "off" or sess.__dict__.get("_va_rem_off"):
+    this remote Alice's epoch with ONE persistent launch that speaks the peer-mapped channel
+    itself (`_C.VanillaEpoch.run_remote` / `_C.UShapeEpoch.run_remote`, csrc/vanilla.hip and
+    csrc/ushape.hip REM).  Needs the peer-mapped channel (not RCCL), B <= 16, the flag, no
+    earlier decline, vanilla: fp32 SGD-momentum; U-shape: Adam, fp32 or bf16 as the compute
+    dtype; and a GPU of its own: with ranks sharing one GPU the Alice's kernels need CUs the
+    launch would hold, so only an explicit reduced grid (SL_VA_REMOTE_G / SL_US_REMOTE_G, the
+    one-GPU tests) runs there."""
+    if mode not in ("vanilla", "ushape") or getattr(sess.args, "split_persist", "auto") == "off":
+        return False
+    if sess.__dict__.get("_va_rem_off" if mode == "vanilla" else "_us_rem_off"):
         return False
     ch = getattr(sess, "split_channel", None)
     C = sess.ops.C()
-    if ch is None or not hasattr(ch, "host_error") or not hasattr(C, "VanillaEpoch"):
+    if ch is None or not hasattr(ch, "host_error") or not hasattr(C, "VanillaEpoch" if mode == "vanilla" else "UShapeEpoch"):
         return False
-    if getattr(sess.comm, "host_staging", False) and not os.environ.get("SL_VA_REMOTE_G"):
+    if getattr(sess.comm, "host_staging", False) and not os.environ.get("SL_VA_REMOTE_G" if mode == "vanilla" else "SL_US_REMOTE_G"):
         return False
     dt = getattr(sess.args, "dtype", "fp32")
-    if dt != "fp32" or (hasattr(C, "get_compute_dtype") and C.get_compute_dtype() != "fp32"):
-        return False
+    cdt = C.get_compute_dtype() if hasattr(C, "get_compute_dtype") else "fp32"
     t = sess.tail
-    return (1 <= sess.B <= 16 and sess.bob_slot(cid).cfg.kind == "sgd" and len(t.layers) == 3 and t.tp_size == 1
-            and all(L.W.dtype == torch.float32 for L in t.layers))
+    if not (1 <= sess.B <= 16 and t.tp_size == 1 and all(L.W.dtype == torch.float32 for L in t.layers)):
+        return False
+    if mode == "vanilla":
+        return dt == "fp32" and cdt == "fp32" and sess.bob_slot(cid).cfg.kind == "sgd" and len(t.layers) == 3
+    return dt in ("fp32", "bf16") and cdt == dt and sess.bob_slot(cid).cfg.kind == "adam" and len(t.layers) == 2
 
 
-def _run_remote_persistent(sess, cid: int, n: int, peer: int):
+def _run_remote_persistent_ushape(sess, cid: int, n: int, peer: int):
+    """Bob's half of a remote U-shape epoch as one persistent launch (`_C.UShapeEpoch.run_remote`),
+    as `_run_remote_persistent` for vanilla."""
+    bslot = sess.bob_slot(cid)
+    L1, L2 = sess.tail.layers
+    cfg = {"fc1": _six(bslot, L1.spec.name, L1.W, L1.b), "fc2": _six(bslot, L2.spec.name, L2.W, L2.b),
+           "bob_opt": _adam(bslot.cfg), "B": sess.B,
+           "timeout_s": float(getattr(sess.args, "persist_timeout_s", 30.0)),
+           "channel": sess.split_channel, "peer": int(peer),
+           "G": int(os.environ.get("SL_US_REMOTE_G", "256")),
+           "workgroups": int(os.environ.get("SL_PERSIST_WORKGROUPS", "0")),
+           "bf16": getattr(sess.args, "dtype", "fp32") == "bf16"}
+    ex = sess.ops.C().UShapeEpoch(cfg)
+    if not ex.ok():
+        sess.__dict__["_us_rem_off"] = True
+        sess.__dict__["split_persist_reason"] = "remote: " + ex.why()
+        return None
+    sess.tail._pre = None
+    t_b = ex.run_remote(int(n), bslot.t)
+    _bob_done(sess, cid, t_b, sess.tail.fwd_count + -(-int(n) // sess.B))
+    _count(sess, "remote_persistent")
+    return ex
+
+
+def _run_remote_persistent(sess, cid: int, n: int, peer: int, mode: str = "vanilla"):
     """Bob's half of a remote vanilla epoch as one persistent launch; None when the executor
     declines this configuration (the caller then runs run_bob, which Alice cannot tell apart).
     A launch that fails mid-epoch raises: the Alice is then stopped at a message of this epoch
     and times out on her side, so there is no state both sides could roll back to (fail-stop,
     docs/DEVIATIONS.md)."""
+    if mode == "ushape":
+        return _run_remote_persistent_ushape(sess, cid, n, peer)
     bslot = sess.bob_slot(cid)
     layers = []
     for L in sess.tail.layers:
@@ -421,7 +453,7 @@ def run_native_remote_epoch(sess, cid: int, order, n: int, mode: str, role: str)
     cfg = {"mode": 1 if mode == "vanilla" else 2, "B": sess.B, "channel": sess.split_channel}
     comm = sess.comm
     comm.progress()
-    ex = _run_remote_persistent(sess, cid, n, host) if role == "bob" and persistent_remote_ok(sess, cid, mode) else None
+    ex = _run_remote_persistent(sess, cid, n, host, mode) if role == "bob" and persistent_remote_ok(sess, cid, mode) else None
     if ex is not None:
         pass                      # Bob's side ran as one persistent launch
     elif role == "alice":

@@ -358,3 +358,60 @@ def test_persistent_remote_vanilla_decision(tmp_path, monkeypatch):
     assert split_native.persistent_remote_ok(s, 1, "vanilla")
     s._va_rem_off = True                  # an earlier decline in this session
     assert not split_native.persistent_remote_ok(s, 1, "vanilla")
+
+
+def test_persistent_remote_ushape_decision(tmp_path, monkeypatch):
+    """The U-shape counterpart (`_C.UShapeEpoch.run_remote`, csrc/ushape.hip REM): Adam on Bob's
+    side, fp32 or bf16 as the compute dtype, the peer-mapped channel, a GPU of its own unless
+    SL_US_REMOTE_G sets a reduced grid.  The GPU objects are stubbed."""
+    import torch
+    from splitlearning_amd.config import parse_args
+    from splitlearning_amd.data.mnist import write_shards
+    from splitlearning_amd.parallel.dist import Comm, Placement
+    from splitlearning_amd.protocols import UShapeSession
+    from splitlearning_amd.protocols import split_native
+
+    class _C:
+        UShapeEpoch = object
+
+        def __init__(self, dt):
+            self.dt = dt
+
+        def get_compute_dtype(self):
+            return self.dt
+
+    class _Ops:
+        def __init__(self, dt):
+            self.c = _C(dt)
+
+        def C(self):
+            return self.c
+
+    class _Chan:
+        def host_error(self):
+            return 0
+
+    monkeypatch.delenv("SL_US_REMOTE_G", raising=False)
+
+    def sess(dt="fp32", *flags):
+        args = parse_args(["--world_size", "2", "--num_samples", "300", "--no_tqdm", "--dtype", dt,
+                           "--datapath", str(tmp_path / "d"), "--log_dir", str(tmp_path / "l")] + list(flags))
+        write_shards(args, verbose=False)
+        dev = torch.device("cpu")
+        s = UShapeSession(args, Comm(0, 1, dev, Placement.make(2, 1, 1)), dev)
+        s.ops = _Ops(dt)
+        s.split_channel = _Chan()
+        return s
+
+    assert split_native.persistent_remote_ok(sess(), 1, "ushape")
+    assert split_native.persistent_remote_ok(sess("bf16"), 1, "ushape")
+    assert not split_native.persistent_remote_ok(sess(), 1, "vanilla")       # U-shape's Adam Bob
+    s = sess()
+    s.ops = _Ops("bf16")                                                    # --dtype fp32, bf16 kernels
+    assert not split_native.persistent_remote_ok(s, 1, "ushape")
+    assert not split_native.persistent_remote_ok(sess("fp32", "--split_persist", "off"), 1, "ushape")
+    s = sess()
+    s.comm.host_staging = True
+    assert not split_native.persistent_remote_ok(s, 1, "ushape")
+    monkeypatch.setenv("SL_US_REMOTE_G", "64")
+    assert split_native.persistent_remote_ok(s, 1, "ushape")

@@ -50,6 +50,22 @@ def test_remote_vanilla_persistent_bob_matches_per_batch(B):
     assert out.stdout.count("PASS") == 2, text[-3000:]
 
 
+@pytest.mark.parametrize("B,dtype", [(16, "fp32"), (5, "fp32"), (16, "bf16")])
+def test_remote_ushape_persistent_bob_matches_per_batch(B, dtype):
+    """Bob's side of a remote Alice's U-shape epoch (BASELINE config 2's placement) as ONE
+    persistent launch exchanging run_bob's four messages per step on the peer-mapped channel
+    (csrc/ushape.hip REM), her side the unchanged run_alice: within fp32 rounding of the
+    per-batch run_bob (bf16: of the per-batch bf16 executor), one launch bitwise its chunked
+    launches, run_bob's message sequence (scripts/ushape_remote_one_gpu.py; 2 row groups = 64 CUs)."""
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "ushape_remote_one_gpu.py"), str(B), "2", dtype],
+                         capture_output=True, text=True, timeout=115, cwd=ROOT)
+    text = out.stdout + out.stderr
+    assert out.returncode == 0, text[-3000:]
+    assert out.stdout.count("one launch bitwise chunked: True") == 2, text[-3000:]
+    assert "message sequence equal True" in out.stdout, text[-3000:]
+    assert out.stdout.count("PASS") == 2, text[-3000:]
+
+
 @pytest.mark.parametrize("mode,n,ws,port", [("ushape", 2, 2, 29793), ("vanilla", 4, 5, 29795)])
 def test_bench_split_schedule_with_remote_alices(tmp_path, mode, n, ws, port):
     out_json = tmp_path / "b.json"
