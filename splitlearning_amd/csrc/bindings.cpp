@@ -767,6 +767,9 @@ PYBIND11_MODULE(_C, m) {
     sl::g_bf16 = d == "bf16" ? 1 : 0;
   });
   m.def("get_compute_dtype", []() { return std::string(sl::g_bf16 ? "bf16" : "fp32"); });
+  // gemm_nn_dgrad's split over the reduction: 0 = its own choice (default), else forced (sweeps)
+  m.def("set_gemm_nn_splits", [](int s) { sl::g_nn_splits = s < 0 ? 0 : s; });
+  m.def("set_gemm_nn_form", [](int wm) { sl::g_nn_wm = (wm == 2 || wm == 4) ? wm : 0; });
   // hand-off stress test (csrc/handoff.hip, tests/test_handoff_gpu.py): G workgroups x R rounds
   // of the persistent kernels' publication primitive in `mode`; returns {mismatching words,
   // rounds completed by the slowest workgroup, error word, kernel ms, first mismatch [7]...}

@@ -431,7 +431,7 @@ hipError_t dgrad_reduce(const float* P, int S, int64_t slab, const float* hprev,
                         int ldo, int M, int K, hipStream_t st);
 
 // dX[M, K] = mask(dZ[M, R] . W[R, K]): 256 x 128 tiles when they fill the chip, else 128 x 128
-// tiles split over the reduction until ~2 workgroups per CU (slices >= 256 deep, <= 8).
+// tiles split over the reduction (the choice below).
 hipError_t gemm_nn_dgrad(const float* dZ, int ldz, const float* W, int ldw, const float* hprev, int ldh, float scale,
                          float* dX, int ldx, int M, int R, int K, float* ws, int64_t ws_elems, hipStream_t st) {
   if (M <= 0 || K <= 0) return hipSuccess;
@@ -439,17 +439,34 @@ hipError_t gemm_nn_dgrad(const float* dZ, int ldz, const float* W, int ldw, cons
   constexpr int64_t kMax = 0x7fff0000;
   if ((int64_t)M * ldz * 4 > kMax || (int64_t)R * ldw * 4 > kMax) return hipErrorInvalidValue;
   const int64_t t4 = (int64_t)((M + 255) / 256) * ((K + 127) / 128);
-  if (t4 >= 384) {
+  if (t4 >= 384 && g_nn_wm != 2) {
     gemm_nn_f32x32_kernel<4><<<(unsigned)t4, 512, 0, st>>>(dZ, ldz, W, ldw, dX, ldx, M, K, R, hprev, ldh, scale, R,
                                                           nullptr);
+    return hipGetLastError();
+  }
+  if (g_nn_wm == 4 && g_nn_splits > 0) {   // A/B: the 256 x 128 form split over the reduction
+    const int S4 = std::max(1, std::min<int>(g_nn_splits, (int)std::min<int64_t>(64, ws ? ws_elems / ((int64_t)M * K) : 0)));
+    const int kc4 = S4 > 1 ? ((R + S4 - 1) / S4 + 15) / 16 * 16 : R;
+    gemm_nn_f32x32_kernel<4><<<dim3((unsigned)t4, S4), 512, 0, st>>>(dZ, ldz, W, ldw, dX, ldx, M, K, R, hprev, ldh,
+                                                                    scale, kc4, S4 > 1 ? ws : nullptr);
+    if (S4 > 1) return dgrad_reduce(ws, S4, (int64_t)M * K, hprev, ldh, scale, dX, ldx, M, K, st);
     return hipGetLastError();
   }
   const int64_t t2 = (int64_t)((M + 127) / 128) * ((K + 127) / 128);
   if (t2 > 0x7fffffff) return hipErrorInvalidValue;
   int S = 1;
   if (ws == nullptr) ws_elems = 0;
-  const int rmin = t2 < 32 ? 64 : 256;   // a grid of a few tiles: shorter slices (as gemm_nt_rows)
-  while (S < 8 && t2 * S * 2 <= 640 && R / (S * 2) >= rmin && (int64_t)S * 2 * M * K <= ws_elems) S *= 2;
+  // The split over the reduction (profiles/r6_gemm/nn_sweep_form2.txt, every S 1-32 at the eval /
+  // large-batch shapes against hipBLASLt): a long reduction takes 8 slices (workgroups are then
+  // short, so the last one to finish trails the grid by little; the slab reduce costs ~6 %), a
+  // short one ~640 / tiles slices of >= 128 (beyond that the slab reduce and the fixed costs of
+  // a workgroup win).  M = 200: 60 -> 82 % of hipBLASLt at R = 5000, 55 -> 72 % at R = 1000;
+  // M = 1000: 72 -> 97 %, 76 -> 75 %.
+  const int64_t smax = ws_elems / std::max<int64_t>(1, (int64_t)M * K);
+  if (R >= 2048) S = 8;
+  else S = (int)std::min<int64_t>(6, std::max<int64_t>(1, (640 + t2 / 2) / std::max<int64_t>(1, t2)));
+  while (S > 1 && (R / S < (t2 < 32 ? 64 : 128) || S > smax)) --S;
+  if (g_nn_splits > 0) S = std::max(1, std::min<int>(g_nn_splits, (int)std::min<int64_t>(64, ws_elems / ((int64_t)M * K))));
   const int kc = S > 1 ? ((R + S - 1) / S + 15) / 16 * 16 : R;
   gemm_nn_f32x32_kernel<2><<<dim3((unsigned)t2, S), 256, 0, st>>>(dZ, ldz, W, ldw, dX, ldx, M, K, R, hprev, ldh,
                                                                  scale, kc, S > 1 ? ws : nullptr);

@@ -124,7 +124,8 @@ def test_linear_fwd_wide_k_uses_the_k_loop_form(cuda):
 
 @pytest.mark.parametrize("M,N,K", [(16, 5000, 5408), (16, 1000, 5000), (16, 100, 1000), (16, 10, 100),
                                     (3, 37, 52), (16, 1000, 628), (64, 1000, 5000), (40, 1000, 604),
-                                    (16, 12, 8), (200, 1000, 5000), (1000, 100, 1000)])
+                                    (16, 12, 8), (200, 1000, 5000), (1000, 100, 1000), (200, 5000, 5408),
+                                    (1000, 1000, 5000), (300, 24, 40), (130, 2052, 132)])
 @pytest.mark.parametrize("masked", [False, True])
 def test_linear_dgrad(cuda, M, N, K, masked):
     """The split-N + reduce pair (the mask fused into the reduce), or one masked launch."""
