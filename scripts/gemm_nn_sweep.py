@@ -33,10 +33,13 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--M", type=int, nargs="+", default=[200, 1000])
     ap.add_argument("--form", type=int, default=0, help="0: the kernel's choice of tile; 2: 128 x 128; 4: 256 x 128")
+    ap.add_argument("--nt", action="store_true", help="the forward (NT) product Y = X W^T instead (gemm_nt)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     C = H.C()
     C.set_gemm_nn_form(a.form)
+    if a.nt:
+        return sweep_nt(a, C, dev)
     for M in a.M:
         for N, K in ((5000, 5408), (1000, 5000)):
             torch.manual_seed(0)
@@ -56,6 +59,28 @@ def main():
                 t = bench(lambda: C.gemm_nn_dgrad(dz, w, h, 2.0, out, ws), a.reps)
                 line.append(f"S{S}: {fl / t / 1e12:5.1f} TF ({100 * t_mm / t:3.0f} %{', ERR %.1e' % err if err > 1e-4 else ''})")
             C.set_gemm_nn_splits(0)
+            print(" | ".join(line), flush=True)
+
+
+def sweep_nt(a, C, dev):
+    """gemm_nt's small-grid split over K (Y[M, N] = X[M, K] W[N, K]^T, bias + ReLU fused)."""
+    for M in a.M:
+        for N, K in ((5000, 5408), (1000, 5000)):
+            torch.manual_seed(0)
+            x = torch.randn(M, K, device=dev)
+            w = torch.randn(N, K, device=dev) / K ** 0.5
+            b = torch.randn(N, device=dev)
+            ref = torch.relu(x @ w.t() + b)
+            fl = 2.0 * M * N * K
+            t_mm = bench(lambda: torch.mm(x, w.t()), a.reps)
+            line = [f"NT M={M} N={N} K={K}: torch.mm {fl / t_mm / 1e12:6.1f} TF"]
+            for S in a.splits:
+                C.set_gemm_nt_splits(S)
+                y = H.linear_fwd(x, w, b, True, 0.0, 1)
+                err = ((y - ref).abs().max() / ref.abs().max()).item()
+                t = bench(lambda: H.linear_fwd(x, w, b, True, 0.0, 1), a.reps)
+                line.append(f"S{S}: {fl / t / 1e12:5.1f} TF ({100 * t_mm / t:3.0f} %{', ERR %.1e' % err if err > 1e-4 else ''})")
+            C.set_gemm_nt_splits(0)
             print(" | ".join(line), flush=True)
 
 

@@ -770,6 +770,7 @@ PYBIND11_MODULE(_C, m) {
   // gemm_nn_dgrad's split over the reduction: 0 = its own choice (default), else forced (sweeps)
   m.def("set_gemm_nn_splits", [](int s) { sl::g_nn_splits = s < 0 ? 0 : s; });
   m.def("set_gemm_nn_form", [](int wm) { sl::g_nn_wm = (wm == 2 || wm == 4) ? wm : 0; });
+  m.def("set_gemm_nt_splits", [](int s) { sl::g_nt_splits = s < 0 ? 0 : s; });
   // hand-off stress test (csrc/handoff.hip, tests/test_handoff_gpu.py): G workgroups x R rounds
   // of the persistent kernels' publication primitive in `mode`; returns {mismatching words,
   // rounds completed by the slowest workgroup, error word, kernel ms, first mismatch [7]...}

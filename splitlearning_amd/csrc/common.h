@@ -225,6 +225,7 @@ extern int g_variant[24];
 extern int g_bf16;      // compute dtype of the GEMM-shaped kernels: 0 = exact fp32, 1 = bf16 operands
 extern int g_nn_splits;  // gemm_nn_dgrad's reduction split: 0 = its own choice, else forced (A/B sweeps)
 extern int g_nn_wm;      // gemm_nn_dgrad's tile form: 0 = its own choice, 2 / 4 forced (A/B sweeps)
+extern int g_nt_splits;  // gemm_nt's small-grid split over K: 0 = its own choice, else forced (sweeps)
 }
 
 #define SL_CHECK_LAUNCH() (hipGetLastError())

@@ -586,6 +586,10 @@ static hipError_t gemm_nt_rows(const float* X, int ldx, const float* W, int ldw,
   const int kmin = t2 < 32 ? 64 : t2 < 256 ? 256 : 512;
   int S = 1;
   while (S < 8 && t2 * S * 2 <= 640 && K / (S * 2) >= kmin && (int64_t)S * 2 * M * N <= ws_elems) S *= 2;
+  // a long reduction over >= 80 tiles: 6 slices (profiles/r6_gemm/nt_sweep.txt, against
+  // hipBLASLt: M = 200, N = 5000, K = 5408 78 -> 90 %, M = 1000 81 -> 89 %)
+  if (t2 >= 80 && K >= 4096 && (int64_t)6 * M * N <= ws_elems) S = 6;
+  if (g_nt_splits > 0) S = std::max(1, std::min<int>(g_nt_splits, (int)std::min<int64_t>(64, ws_elems / ((int64_t)M * N))));
   return launch_gemm_f32x32<2, 16>(X, ldx, W, ldw, Y, ldy, M, N, K, e, S, ws, st);
 }
 

@@ -30,6 +30,7 @@ int g_variant[24] = {0};
 int g_bf16 = 0;
 int g_nn_splits = 0;
 int g_nn_wm = 0;
+int g_nt_splits = 0;
 
 hipError_t gemm_nt(const float* X, int ldx, const float* W, int ldw, float* Y, int ldy, int M, int N, int K, Epi e,
                    bool bf16, float* ws, int64_t ws_elems, hipStream_t st);
