@@ -9,7 +9,9 @@ Covered, T = 2 ranks on cuda:0 / cuda:1 (scripts/*_one_gpu.py with SL_RANK_DEVIC
   epoch, bitwise the Python loop of the same placement with the same message sequence;
 * the hybrid and register-resident persistent epochs tensor-parallel over the two devices
   (in-launch fc2 exchange): replicated state bitwise equal across ranks and close to fp32 torch;
-* the mid-epoch failure of those epochs survived across devices (rolled back, launch-per-stage).
+* the mid-epoch failure of those epochs survived across devices (rolled back, launch-per-stage);
+* Bob's persistent vanilla / U-shape epochs of a remote Alice on the full grid of his own device,
+  her per-batch side on the other (the in-launch channel protocol over xGMI).
 Reference: split_nn.py:183-186 (one process per role, mp.spawn)."""
 import os
 import subprocess
@@ -49,3 +51,16 @@ def test_persistent_tp2_across_devices(kind):
 @pytest.mark.parametrize("kind", ["hybrid", "resident"])
 def test_persistent_tp2_failure_survived_across_devices(kind):
     _run(os.path.join(ROOT, "scripts", "persist_fallback_one_gpu.py"), "2", kind)
+
+
+def test_remote_vanilla_persistent_across_devices():
+    """Bob's vanilla epoch of a remote Alice as one persistent launch speaking the channel from
+    inside (csrc/vanilla.hip REM), the full 256-workgroup grid on his own device, her per-batch
+    run_alice on the other (scripts/vanilla_remote_one_gpu.py)."""
+    _run(os.path.join(ROOT, "scripts", "vanilla_remote_one_gpu.py"), "16", "256")
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_remote_ushape_persistent_across_devices(dtype):
+    """The U-shape counterpart (csrc/ushape.hip REM), 8 row groups = the full 256-workgroup grid."""
+    _run(os.path.join(ROOT, "scripts", "ushape_remote_one_gpu.py"), "16", "8", dtype)
