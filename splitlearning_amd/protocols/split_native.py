@@ -143,7 +143,11 @@ def persistent_vanilla_ok(sess, cid: int) -> bool:
         sess.__dict__["split_persist_reason"] = f"dtype {dt if dt != 'fp32' else C.get_compute_dtype()}: fp32 only"
         return False
     a = sess.alices[cid]
-    return (1 <= sess.B <= 16 and a.slot.cfg.kind == "sgd" and sess.bob_slot(cid).cfg.kind == "sgd"
+    if not 1 <= sess.B <= 16:
+        # every product's MFMA row block is the batch (csrc/vanilla.hip): larger batches run per batch
+        sess.__dict__["split_persist_reason"] = f"batch {sess.B} > 16: per-batch executor"
+        return False
+    return (a.slot.cfg.kind == "sgd" and sess.bob_slot(cid).cfg.kind == "sgd"
             and len(sess.tail.layers) == 3 and all(L.W.dtype == torch.float32 for L in sess.tail.layers))
 
 
@@ -232,7 +236,10 @@ def persistent_ushape_ok(sess, cid: int) -> bool:
         sess.__dict__["split_persist_reason"] = f"dtype {dt} with compute dtype {cdt}"
         return False
     a = sess.alices[cid]
-    return (1 <= sess.B <= 16 and a.slot.cfg.kind == "adam" and sess.bob_slot(cid).cfg.kind == "adam"
+    if not 1 <= sess.B <= 16:
+        sess.__dict__["split_persist_reason"] = f"batch {sess.B} > 16: per-batch executor"
+        return False
+    return (a.slot.cfg.kind == "adam" and sess.bob_slot(cid).cfg.kind == "adam"
             and len(sess.tail.layers) == 2 and all(L.W.dtype == torch.float32 for L in sess.tail.layers))
 
 

@@ -262,6 +262,37 @@ def test_split_persist_flag_and_cpu_decision(tmp_path):
     assert not persistent_vanilla_ok(s, 1)
 
 
+def test_split_persist_batch_bound_is_reported(tmp_path, monkeypatch):
+    """--batch_size > 16 keeps the per-batch executor (the persistent epochs' MFMA row block is the
+    batch) and says so in split_persist_reason (bench.py reports it), instead of dropping silently."""
+    import torch
+    from splitlearning_amd.config import parse_args
+    from splitlearning_amd.data.mnist import write_shards
+    from splitlearning_amd.parallel.dist import Comm, Placement
+    from splitlearning_amd.protocols import VanillaSession
+    from splitlearning_amd.protocols import split_native
+
+    class _C:
+        VanillaEpoch = object
+
+        def get_compute_dtype(self):
+            return "fp32"
+
+    class _Ops:
+        def C(self):
+            return _C()
+
+    monkeypatch.setattr(split_native, "native_split_ok", lambda sess, cid, mode: True)
+    args = parse_args(["--vanilla", "--world_size", "2", "--num_samples", "300", "--no_tqdm", "--batch_size", "32",
+                       "--datapath", str(tmp_path / "d"), "--log_dir", str(tmp_path / "l")])
+    write_shards(args, verbose=False)
+    dev = torch.device("cpu")
+    s = VanillaSession(args, Comm(0, 1, dev, Placement.make(2, 1, 1)), dev)
+    s.ops = _Ops()
+    assert not split_native.persistent_vanilla_ok(s, 1)
+    assert "batch 32 > 16" in s.split_persist_reason
+
+
 def test_persistent_vanilla_refuses_bf16(tmp_path, monkeypatch):
     """csrc/vanilla.hip is exact fp32 only: with --dtype bf16 (fp32 master weights, bf16 operands
     through the global compute-dtype switch) the persistent vanilla epoch must not be chosen, and
