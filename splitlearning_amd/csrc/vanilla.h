@@ -27,9 +27,9 @@ constexpr int kVaStride = 32;       // counter words 128 B apart
 constexpr int kVaSeams = 5;         // F: fc2 partials, L: logit partials, D: dlogits, Z: dz2, X: next batch
 // counter words: the seams' 8 shards each, then P[NC] (dz1 partials per fc2 column block),
 // R[nrb] (forward partials per fc1 row block), XD[ncb] (cut-gradient partials per fc1 column
-// block), CW[32] (conv gradient partials per channel)
+// block), CW[32] (conv gradient partials per channel), CX[32] (next-batch activations per channel)
 constexpr int kVaMaxS = 6000;      // steps per launch (the activation slots' 32-bit offsets)
-constexpr int kVaCounters = kVaSeams * 8 + kVaMaxNC + kVaMaxRB + kVaMaxCB + 32;
+constexpr int kVaCounters = kVaSeams * 8 + kVaMaxNC + kVaMaxRB + kVaMaxCB + 32 + 32;
 
 // A REMOTE Alice (VaArgs::rem): her conv front runs in her own process (csrc/split.cpp
 // run_alice, unchanged) and the launch speaks the peer-mapped channel's protocol

@@ -77,6 +77,7 @@ __device__ __forceinline__ int va_P(int b) { return kVaSeams * 8 + b; }
 __device__ __forceinline__ int va_R(int rb) { return kVaSeams * 8 + kVaMaxNC + rb; }
 __device__ __forceinline__ int va_XD(int cb) { return kVaSeams * 8 + kVaMaxNC + kVaMaxRB + cb; }
 __device__ __forceinline__ int va_CW(int c) { return kVaSeams * 8 + kVaMaxNC + kVaMaxRB + kVaMaxCB + c; }
+__device__ __forceinline__ int va_CX(int c) { return kVaSeams * 8 + kVaMaxNC + kVaMaxRB + kVaMaxCB + 32 + c; }
 
 __device__ __forceinline__ bool va_spin(const VaArgs& a, const unsigned* p, unsigned tgt) {
   if (poll(p) >= tgt) return true;
@@ -152,7 +153,10 @@ __device__ __forceinline__ bool va_pwait(const VaArgs& a, const uint32_t* f, uin
 
 constexpr int kSt = 16;   // fc1 W / buf loads and stores: sc1 (write-through stores, L1-bypassing loads)
 constexpr int kVaFwdRing = 6;   // forward-pass register ring depth (tiles; kVaFwdRing - 1 in flight)
-constexpr int kVaFwdPre = 2;    // of them loaded early, under the seam-X wait (VGPR budget: 3 spill)
+constexpr int kVaFwdPre = 2;
+// seam X of a co-located Alice: her 32 x 8 conv jobs arrive on one counter per channel (8 each)
+// and wave 0's 32 lanes poll them, instead of 8 shards of 32 arrivals (off: no faster)
+constexpr bool kVaSeamXByChannel = false;   // A/B: 137.0 vs 136.4 us (shards), profiles/r6_vanilla_direct/seam_x_per_channel_ab.txt    // of them loaded early, under the seam-X wait (VGPR budget: 3 spill)
 
 // f(integral_constant<int, I>) for I in [B, E): compile-time ring and buffer indices in the
 // unrolled tile loops
@@ -765,6 +769,20 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
     return true;
   };
 
+  // seam X: every activation of the next batch published (arrive, `between`, then wait);
+  // REM: every workgroup's share of her message (8 shards), co-located: per channel (kVaSeamXByChannel)
+  auto seam_x = [&](unsigned mult, auto between) -> bool {
+    if (!REM && kVaSeamXByChannel) va_arrive(a, va_CX(cc));
+    else va_arrive(a, va_seam(4, w & 7));
+    if (!between()) return false;
+    if (!REM && kVaSeamXByChannel)
+      return va_wait_many(a, 32, s_ok, [&](int l, int& idx) {
+        idx = va_CX(l);
+        return mult * 8u;
+      });
+    return va_seam_wait(a, 4, mult, s_ok, s_sn);
+  };
+
   // ---- prologue: Alice's forward of batch 0 (REM: her message of it), then the forward pass
   if constexpr (REM) {
     if (!recv_act(0)) goto done;
@@ -773,8 +791,7 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
     __syncthreads();
     conv_fwd(0);
   }
-  va_arrive(a, va_seam(4, w & 7));
-  if (!va_seam_wait(a, 4, 1u, s_ok, s_sn)) goto done;
+  if (!seam_x(1u, [] { return true; })) goto done;
   if constexpr (REM) ack_act(0);
   fwd_prefetch();
   fwd_pass(0);
@@ -1256,13 +1273,15 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
     __syncthreads();
     if (more) {
       conv_fwd(i + 1);
-      va_arrive(a, va_seam(4, w & 7));
-      VA_MARK(12);
-      if constexpr (kVaFwdPre > 0) {
-        if (!wait_all_xd(i)) break;
-        fwd_prefetch();
-      }
-      if (!va_seam_wait(a, 4, (unsigned)(i + 2), s_ok, s_sn)) break;
+      if (!seam_x((unsigned)(i + 2), [&] {
+            VA_MARK(12);
+            if constexpr (kVaFwdPre > 0) {
+              if (!wait_all_xd(i)) return false;
+              fwd_prefetch();
+            }
+            return true;
+          }))
+        break;
       VA_MARK(13);
       // ================= V: the forward pass of batch i + 1 over the updated fc1
       fwd_pass(i + 1);
