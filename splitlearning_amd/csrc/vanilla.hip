@@ -153,10 +153,11 @@ __device__ __forceinline__ bool va_pwait(const VaArgs& a, const uint32_t* f, uin
 
 constexpr int kSt = 16;   // fc1 W / buf loads and stores: sc1 (write-through stores, L1-bypassing loads)
 constexpr int kVaFwdRing = 6;   // forward-pass register ring depth (tiles; kVaFwdRing - 1 in flight)
-constexpr int kVaFwdPre = 2;
+constexpr int kVaFwdPre = 2;    // of them loaded early, under the seam-X wait (VGPR budget: 3 spill)
 // seam X of a co-located Alice: her 32 x 8 conv jobs arrive on one counter per channel (8 each)
-// and wave 0's 32 lanes poll them, instead of 8 shards of 32 arrivals (off: no faster)
-constexpr bool kVaSeamXByChannel = false;   // A/B: 137.0 vs 136.4 us (shards), profiles/r6_vanilla_direct/seam_x_per_channel_ab.txt    // of them loaded early, under the seam-X wait (VGPR budget: 3 spill)
+// and wave 0's 32 lanes poll them, instead of 8 shards of 32 arrivals.  Off: no faster (137.0
+// vs 136.4 us, profiles/r6_vanilla_direct/seam_x_per_channel_ab.txt)
+constexpr bool kVaSeamXByChannel = false;
 
 // f(integral_constant<int, I>) for I in [B, E): compile-time ring and buffer indices in the
 // unrolled tile loops
