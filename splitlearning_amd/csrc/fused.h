@@ -39,6 +39,7 @@ struct WgGroup {
   int afirst;           // load the first chunk's A / dZ before W / m / v (set by wgrad_group)
   int pol;              // W / state load and store cache policy preset (set by wgrad_group; variant 21)
   int rt;               // row tiles per workgroup of the streaming form (set by wgrad_group; 0 = tiled form)
+  int pin;              // streaming form: layer-0 rows [0, pin) plain both ways, the rest non-temporal (variant 23)
 };
 
 int head3_slices(int N2);

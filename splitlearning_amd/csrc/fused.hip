@@ -592,6 +592,8 @@ wgrad_stream_kernel(WgGroup grp, int M, SlOpt o) {
   const int lbytes = L.N * L.ldw * 4;   // grp.pol != 0 only for layers under 2 GB
   // one tile's state for this thread: W / m / v of (row 16 by + r, columns k .. k + 3), and the
   // wave's dZ[lane][16 by + r] in lanes 0-15
+  // a pinned tile (layer 0, rows < grp.pin): plain both ways
+  const auto pinned = [&](int by) { return l0 && by * 16 < grp.pin; };
   auto ld_tile = [&](int by, f32x4& p, f32x4& q0, f32x4& q1, float& dzl) {
     const int n = by * 16 + r;
     dzl = (lane < 16 && lane < M && n < L.N) ? L.dz[(int64_t)lane * L.ldz + n] : 0.f;
@@ -605,9 +607,10 @@ wgrad_stream_kernel(WgGroup grp, int M, SlOpt o) {
         q0 = *reinterpret_cast<const f32x4*>(L.s0 + off);
         if (ADAM) q1 = *reinterpret_cast<const f32x4*>(L.s1 + off);
       } else {
-        p = ld_pol(L.W, lbytes, (int)(off * 4), plw);
-        q0 = ld_pol(L.s0, lbytes, (int)(off * 4), pls);
-        if (ADAM) q1 = ld_pol(L.s1, lbytes, (int)(off * 4), pls);
+        const bool pn = pinned(by);
+        p = ld_pol(L.W, lbytes, (int)(off * 4), pn ? 0 : plw);
+        q0 = ld_pol(L.s0, lbytes, (int)(off * 4), pn ? 0 : pls);
+        if (ADAM) q1 = ld_pol(L.s1, lbytes, (int)(off * 4), pn ? 0 : pls);
       }
     }
   };
@@ -652,9 +655,10 @@ wgrad_stream_kernel(WgGroup grp, int M, SlOpt o) {
       const int64_t off = (int64_t)n * L.ldw + k;
       if (grp.pol != 0) {
         const int boff = (int)(off * 4);
-        if (o.kind != 0) st_pol(L.W, lbytes, boff, p, psw);
-        st_pol(L.s0, lbytes, boff, q0, pss);
-        if (ADAM) st_pol(L.s1, lbytes, boff, q1, pss);
+        const bool pn = pinned(by);
+        if (o.kind != 0) st_pol(L.W, lbytes, boff, p, pn ? 0 : psw);
+        st_pol(L.s0, lbytes, boff, q0, pn ? 0 : pss);
+        if (ADAM) st_pol(L.s1, lbytes, boff, q1, pn ? 0 : pss);
       } else if (grp.wt) {
         const int boff = (int)(off * 4);
         if (o.kind != 0) st_wt(L.W, L.N, L.ldw, boff, p);
@@ -770,6 +774,22 @@ static void set_traversal(WgGroup& gg) {
   const int64_t st0 = (int64_t)gg.d[0].N * gg.d[0].ldw * 4 * (gg.d[0].s1 ? 3 : 2);
   const int v21 = g_variant[21];
   gg.pol = !gg.wt ? 0 : (v21 == 6 ? 0 : (v21 != 0 ? v21 : (st0 > (256ll << 20) ? 1 : 0)));
+  // A layer-0 stream of over 1 GB (concat's fc1: 2.6 GB of W / m / v, 519 KB per row) instead
+  // pins a fixed subset of its rows in the Infinity Cache -- plain loads and stores of their W /
+  // m / v, ~65 % of the 256 MB, so those rows never reach HBM -- and streams every other row
+  // non-temporal past it.  ws = 9 concat on one GPU (profiles/r6_pin/): 92.5 -> 96.4-97.6 k on one
+  // box, 320 rows the best of 192 - 576 on another.  Variant 23 forces a row count (-1: off).
+  gg.pin = 0;
+  const int64_t row0 = (int64_t)gg.d[0].ldw * 4 * (gg.d[0].s1 ? 3 : 2);
+  const int v23 = g_variant[23];
+  if (gg.wt && v23 >= 0) {
+    int pin = v23 > 0 ? v23 : (st0 > (1ll << 30) ? (int)((256ll << 20) * 65 / 100 / row0) : 0);
+    pin = pin / 16 * 16;
+    if (pin > 0) {
+      gg.pin = pin;
+      gg.pol = 2;
+    }
+  }
 }
 
 hipError_t wgrad_group(const WgGroup& g, int M, SlOpt o, hipStream_t st) {
