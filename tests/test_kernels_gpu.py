@@ -330,6 +330,43 @@ def test_wgrad_stream_form_is_bitwise_the_tiled_form(cuda, kind, rt, pol, M, sha
 
 
 @pytest.mark.parametrize("kind", ["sgd", "adam"])
+@pytest.mark.parametrize("rt,pin", [(-1, 32), (8, 32), (8, 1008), (40, 496)])
+def test_wgrad_pinned_rows_are_bitwise_unpinned(cuda, kind, rt, pin):
+    """The pinned-row cache policy (variant 23: the first `pin` rows of layer 0 plain, the rest
+    non-temporal; csrc/fused.hip set_traversal -- concat's fc1 by default) changes cache hints
+    only: W / states / biases / look-ahead slabs bitwise equal to the unpinned shipped policy,
+    with the pinned boundary inside a tile run, past the last row, and on the tiled form."""
+    C = hip_ops.C()
+    cfg = OptimCfg("adam", 1e-3, weight_decay=1e-5) if kind == "adam" else OptimCfg("sgd", 1e-2, momentum=0.9)
+    g = torch.Generator().manual_seed(7)
+    M, shapes, mn = 16, [(1000, 5408), (200, 1000), (100, 200)], 16
+    base = [(torch.randn(M, N, generator=g), torch.randn(M, K, generator=g), torch.randn(N, K, generator=g),
+             torch.randn(N, generator=g)) for N, K in shapes]
+    xn = torch.randn(mn, shapes[0][1], generator=g).to(cuda)
+    outs = []
+    try:
+        C.set_variant(22, rt)
+        for v23 in (-1, pin):
+            C.set_variant(23, v23)
+            layers = []
+            for dz, a, w, b in base:
+                w, b = w.to(cuda), b.to(cuda)
+                sw = {"m": torch.full_like(w, 0.01), "v": torch.full_like(w, 0.02)} if kind == "adam" else \
+                    {"buf": torch.full_like(w, 0.01)}
+                sb = {k: torch.full_like(b, 0.01) for k in sw}
+                layers.append((dz.to(cuda), a.to(cuda), w, sw, b, sb))
+            pn = hip_ops.lookahead_slabs(cuda, shapes[0][1], mn, shapes[0][0])
+            hip_ops.wgrad_group_(layers, M, cfg, 3, x_next=xn, p_next=pn)
+            torch.cuda.synchronize()
+            outs.append([t.clone() for L in layers for t in (L[2], L[4], *L[3].values(), *L[5].values())] + [pn])
+    finally:
+        C.set_variant(22, 0)
+        C.set_variant(23, 0)
+    for x, y in zip(outs[0], outs[1]):
+        assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("kind", ["sgd", "adam"])
 def test_conv_local_epoch_matches_steps(cuda, kind):
     """The C++-looped epoch == the per-step calls (bitwise), incl. a partial last batch."""
     x = _shard(300, cuda)
