@@ -585,7 +585,10 @@ static hipError_t gemm_nt_rows(const float* X, int ldx, const float* W, int ldw,
   const int64_t t2 = (int64_t)((M + 127) / 128) * ((N + 127) / 128);
   const int kmin = t2 < 32 ? 64 : t2 < 256 ? 256 : 512;
   int S = 1;
-  while (S < 8 && t2 * S * 2 <= 640 && K / (S * 2) >= kmin && (int64_t)S * 2 * M * N <= ws_elems) S *= 2;
+  // up to 8 slices, or one workgroup per CU for a grid of under 32 tiles (M = 200, N = 1000, K =
+  // 5000: 16 tiles x 16 slices, 48 -> 74 % of hipBLASLt; profiles/r6_gemm/nt_sweep_wide.txt)
+  const int smax2 = t2 < 32 ? std::max<int>(8, (int)(256 / std::max<int64_t>(1, t2))) : 8;
+  while (S < smax2 && t2 * S * 2 <= 640 && K / (S * 2) >= kmin && (int64_t)S * 2 * M * N <= ws_elems) S *= 2;
   // a long reduction over >= 80 tiles: 6 slices (profiles/r6_gemm/nt_sweep.txt, against
   // hipBLASLt: M = 200, N = 5000, K = 5408 78 -> 90 %, M = 1000 81 -> 89 %)
   if (t2 >= 80 && K >= 4096 && (int64_t)6 * M * N <= ws_elems) S = 6;

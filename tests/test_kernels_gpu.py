@@ -75,13 +75,15 @@ def test_conv_bwd(cuda, kind):
 
 @pytest.mark.parametrize("M,N,K", [(16, 5000, 5408), (16, 1000, 5000), (16, 100, 1000), (5, 10, 100),
                                     (16, 37, 52), (200, 100, 1000), (1000, 5000, 5408), (8000, 1000, 5000),
-                                    (129, 130, 36), (300, 10, 100), (1000, 100, 1000), (14000, 5000, 5408)])
+                                    (129, 130, 36), (300, 10, 100), (1000, 100, 1000), (14000, 5000, 5408),
+                                    (200, 1000, 5000)])
 @pytest.mark.parametrize("relu,drop", [(False, 0.0), (True, 0.0), (True, 0.5)])
 @pytest.mark.parametrize("gemm", [0, 2])
 def test_linear_fwd(cuda, M, N, K, relu, drop, gemm):
     """M <= 128: the skinny split-K kernels; M > 128: the in-tree LDS-tiled MFMA GEMM with its
     fused epilogue (gemm 0, the default: 14000 x 5000 x 5408 takes the tail split of its last
-    partial round, 1000 x 100 x 1000 the deep split-K of a small grid) or hipBLASLt + the
+    partial round, 1000 x 100 x 1000 the deep split-K of a small grid, 200 x 1000 x 5000 16 slices
+    of a 16-tile grid) or hipBLASLt + the
     in-tree epilogue (gemm 2: variant 11)."""
     if gemm and M <= 128:
         pytest.skip("the tiled GEMM serves M > 128")
