@@ -56,11 +56,12 @@ struct VaArgs {
   int NC, HW;             // fc2 column blocks (G = 8 NC), head workgroups (N2 / 4)
   int nrb, ncb, ntile;    // fc1 row blocks, column blocks, tiles
   // device table (int): the forward pass's row-major runs as hybrid.h (tile0[G + 1], rbw0[nrb],
-  // rbn[nrb], hn[NC]), then the update pass's column-major runs (tile t: column block t / nrb,
-  // row block t % nrb): u0[G + 1], cbw0[ncb] (first workgroup touching the column block),
-  // cbn[ncb] (workgroups touching it)
+  // rbn[nrb], hn[NC]), then the update pass's runs: cbn[ncb] (workgroups touching the column
+  // block) at oU; per workgroup {v0, v1, rb0, nb} at oUW: its run [v0, v1) of the row band
+  // [rb0, rb0 + nb) walked column-major (tile v: column block v / nb, row block rb0 + v % nb);
+  // per workgroup and column block its dx slot (-1: untouched) at oUS ([G][ncb])
   const int* tab;
-  int oU;                 // offset of u0 in tab
+  int oU, oUW, oUS;
   // Alice: uint8 shard pixels [N, 784], the batch rows of every step ([S * M] shard row
   // indices, -1 = padding), her conv weights / bias and their momentum buffers
   const uint8_t* img;

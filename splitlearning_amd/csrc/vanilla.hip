@@ -249,7 +249,7 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
   int* s_fns = reinterpret_cast<int*>(smem + OFF_TABC);   // [32]: forward slots of row block rlo + j
   int* s_slot = s_fns + 32;                                // [kVaRuns]: w - first forward toucher
   int* s_sn = s_slot + kVaRuns;                            // [kVaSeams * 8]
-  int* s_dxs = s_sn + kVaSeams * 8;                        // [kVaMaxCB]: w - first update toucher
+  int* s_dxs = s_sn + kVaSeams * 8;                        // [kVaMaxCB]: this run's dx slot per column block
   constexpr int MC = kVaMaxC;
   const f32x4 zv = {0.f, 0.f, 0.f, 0.f};
 
@@ -267,8 +267,10 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
   const int nt = t_end - t_begin;
   const int rbA = nt > 0 ? t_begin / ncb : 0;
   const int nruns = nt > 0 ? (t_end - 1) / ncb - rbA + 1 : 0;
-  // update-pass tile run (column-major) [u_begin, u_begin + unt)
-  const int u_begin = a.tab[a.oU + w], unt = a.tab[a.oU + w + 1] - u_begin;
+  // update-pass tile run [u_begin, u_begin + unt) of the row band [u_rb0, u_rb0 + u_nb), walked
+  // column-major (tile v: column block v / u_nb, row block u_rb0 + v % u_nb)
+  const int u_begin = a.tab[a.oUW + 4 * w], unt = a.tab[a.oUW + 4 * w + 1] - u_begin;
+  const int u_rb0 = a.tab[a.oUW + 4 * w + 2], u_nb = a.tab[a.oUW + 4 * w + 3];
   // conv job: channel cc, images 2 cg, 2 cg + 1
   const int cc = w & 31, cg = w >> 5;
   const __amdgpu_buffer_rsrc_t rHB = rs_of(a.HB);
@@ -323,7 +325,7 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
     }
     if (tid < kVaRuns) s_slot[tid] = tid < nruns ? w - a.tab[G + 1 + rbA + tid] : -1;
     if (tid < kVaSeams * 8) s_sn[tid] = a.shard_n[tid];
-    if (tid < kVaMaxCB) s_dxs[tid] = tid < ncb ? w - a.tab[a.oU + G + 1 + tid] : -1;
+    if (tid < kVaMaxCB) s_dxs[tid] = tid < ncb ? a.tab[a.oUS + w * ncb + tid] : -1;
     if (tid < 16 * kVaRuns) {
       const int k = tid >> 4, j = tid & 15;
       const int rb = rbA + k, n = 16 * rb + j;
@@ -462,7 +464,7 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
   auto wait_all_xd = [&](int i) {
     return va_wait_many(a, ncb, s_ok, [&](int l, int& idx) {
       idx = va_XD(l);
-      return (unsigned)(i + 1) * (unsigned)a.tab[a.oU + G + 1 + ncb + l];
+      return (unsigned)(i + 1) * (unsigned)a.tab[a.oU + l];
     });
   };
   auto fwd_pass = [&](int step) {
@@ -552,7 +554,7 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
   auto load_u = [&](int t, f32x4 (&p)[2], f32x4 (&mm)[2]) {
     VA_IDX();
     const int rh = r >> 2, cq = r & 3;
-    const int cb = t / nrb, rb = t - (t / nrb) * nrb;
+    const int cb = t / u_nb, rb = u_rb0 + t - (t / u_nb) * u_nb;
     const int k = cb * 256 + 64 * cq + 4 * li;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -608,7 +610,7 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
   };
   auto upd_pass = [&](int step, float ss, float ib) {
     if (unt <= 0) return;
-    int ccb = u_begin / nrb;
+    int ccb = u_begin / u_nb;
     stage_x(ccb, step);
 #pragma unroll
     for (int c = 0; c < 4; ++c) dacc[c] = zv;
@@ -616,7 +618,7 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
     auto tile = [&](auto cur_c, int j) {
       constexpr int cur = decltype(cur_c)::value, nb = cur ^ 1;
       const int t = u_begin + j;
-      const int cb = t / nrb, rb = t - (t / nrb) * nrb;
+      const int cb = t / u_nb, rb = u_rb0 + t - (t / u_nb) * u_nb;
       if (cb != ccb) {   // uniform: the run enters its next column block
         flush_dx(ccb);
         ccb = cb;
@@ -733,7 +735,7 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
     if (w >= nch) return true;
     if (!va_wait_many(a, ncb, s_ok, [&](int l, int& idx) {
           idx = va_XD(l);
-          return (unsigned)(i + 1) * (unsigned)a.tab[a.oU + G + 1 + ncb + l];
+          return (unsigned)(i + 1) * (unsigned)a.tab[a.oU + l];
         }))
       return false;
     const uint32_t sg = a.lk.sgen0 + 1u + (uint32_t)i;
@@ -752,7 +754,7 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
       const int e = c * kIpcChunk + 4 * (int)threadIdx.x;
       if ((int)threadIdx.x < kIpcThreads && e < len) {
         const int m = e / K1, k = e - m * K1, cb = k >> 8, kk = k & 255;
-        const int ns = a.tab[a.oU + G + 1 + ncb + cb];
+        const int ns = a.tab[a.oU + cb];
         f32x4 parts[kVaDxSlots];
 #pragma unroll
         for (int sl = 0; sl < kVaDxSlots; ++sl)
@@ -1135,7 +1137,7 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
         const bool item = e < (unt + nruns) * 64;
         const int j = e >> 6, nn = (e >> 2) & 15, mg = e & 3;
         const bool upd = j < unt;
-        const int rb = upd ? (u_begin + j) - ((u_begin + j) / nrb) * nrb : rbA + (j - unt);
+        const int rb = upd ? u_rb0 + (u_begin + j) - ((u_begin + j) / u_nb) * u_nb : rbA + (j - unt);
         const int n = 16 * rb + nn;
         f32x4 v = zv;
         if (item && n < N1) {
@@ -1202,7 +1204,7 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
       const int k0 = cc * 169, cblo = k0 >> 8, cbhi = (k0 + 168) >> 8;
       if (!va_wait_many(a, cbhi - cblo + 1, s_ok, [&](int l, int& idx) {
             idx = va_XD(cblo + l);
-            return (unsigned)(i + 1) * (unsigned)a.tab[a.oU + G + 1 + ncb + cblo + l];
+            return (unsigned)(i + 1) * (unsigned)a.tab[a.oU + cblo + l];
           }))
         break;
     }
@@ -1218,7 +1220,7 @@ __global__ void __launch_bounds__(kVaThreads) vanilla_epoch_kernel(VaArgs a) {
         const int m = 2 * cg + bl;
         if (m < M && cy > 0.f) {
           const int k = cc * 169 + p, cb = k >> 8, kk = k & 255;
-          const int ns = a.tab[a.oU + G + 1 + ncb + cb];
+          const int ns = a.tab[a.oU + cb];
           float parts[kVaDxSlots];
 #pragma unroll
           for (int s = 0; s < kVaDxSlots; ++s)

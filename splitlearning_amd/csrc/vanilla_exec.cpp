@@ -14,6 +14,7 @@
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 
+#include <cstdlib>
 #include <string>
 #include <tuple>
 #include <vector>
@@ -362,18 +363,69 @@ class VanillaEpoch {
     }
     for (int b = 0; b < NC; ++b)
       if (tab[G + 1 + 2 * nrb + b] < 1) return "an fc2 column block without fc1 rows";
-    // update runs: u0[G + 1], cbw0[ncb], cbn[ncb]
+    // update runs: G balanced column-major runs over all tiles (tile v: column block v / nrb, row
+    // block v % nrb), as before, but dealt to the workgroups by the row band their first tile
+    // falls in -- run k goes to a workgroup of XCD x (w % 8 == x under round-robin dispatch)
+    // when its first row block is in band x of 8 -- so the runs of one XCD stage the dz1 of
+    // ~1/4 of the row blocks instead of all of them (the staging is an L2 <- fabric fetch).
+    // Each run keeps its slot among the workgroups touching its column blocks.
     a.oU = (int)tab.size();
-    const int base = a.oU;
-    tab.resize(base + G + 1 + 2 * ncb, 0);
-    for (int w = 0; w <= G; ++w) tab[base + w] = (int)((int64_t)w * T / G);
-    for (int w = 0; w < G; ++w)
-      if (tab[base + w + 1] - tab[base + w] > sl::kVaMaxRun) return "an update run longer than 28 tiles";
-    for (int cb = 0; cb < ncb; ++cb) {
-      const int w0 = wg_of(tab, base, cb * nrb), w1 = wg_of(tab, base, (cb + 1) * nrb - 1);
-      tab[base + G + 1 + cb] = w0;
-      tab[base + G + 1 + ncb + cb] = w1 - w0 + 1;
-      if (w1 - w0 + 1 > sl::kVaDxSlots) return "an fc1 column block spans more workgroups than the dx slots";
+    tab.resize(a.oU + ncb, 0);
+    a.oUW = (int)tab.size();
+    tab.resize(a.oUW + 4 * G, 0);
+    a.oUS = (int)tab.size();
+    std::vector<int> run_of(G, -1);
+    // SL_VA_XCD_RUNS=0: runs dealt in order (A/B)
+    const char* env_x = std::getenv("SL_VA_XCD_RUNS");
+    const bool xcd_runs = !(env_x && env_x[0] == '0');
+    if (G % 8 == 0 && nrb >= 64 && xcd_runs) {
+      std::vector<int> used(G, 0), spill;
+      std::vector<int> next(8, 0);
+      for (int k = 0; k < G; ++k) {
+        const int v0 = (int)((int64_t)k * T / G);
+        const int x = (int)((int64_t)(v0 % nrb) * 8 / nrb);
+        if (next[x] < G / 8) {
+          const int w = x + 8 * next[x]++;
+          run_of[w] = k;
+          used[w] = 1;
+        } else {
+          spill.push_back(k);
+        }
+      }
+      size_t q = 0;
+      for (int w = 0; w < G && q < spill.size(); ++w)
+        if (!used[w]) run_of[w] = spill[q++];
+    } else {
+      for (int w = 0; w < G; ++w) run_of[w] = w;
+    }
+    auto fill = [&]() -> std::string {
+      tab.resize(a.oUS);
+      tab.resize(a.oUS + (size_t)G * ncb, -1);
+      std::vector<int> cnt(ncb, 0);
+      for (int k = 0; k < G; ++k) {
+        // slots per column block in run order (the sum order of the cut-gradient partials)
+        int w = -1;
+        for (int x = 0; x < G; ++x)
+          if (run_of[x] == k) { w = x; break; }
+        if (w < 0) return "update run table";
+        const int v0 = (int)((int64_t)k * T / G), v1 = (int)((int64_t)(k + 1) * T / G);
+        if (v1 - v0 > sl::kVaMaxRun) return "an update run longer than 28 tiles";
+        tab[a.oUW + 4 * w] = v0;
+        tab[a.oUW + 4 * w + 1] = v1;
+        tab[a.oUW + 4 * w + 2] = 0;
+        tab[a.oUW + 4 * w + 3] = nrb;
+        if (v1 <= v0) continue;
+        for (int cb = v0 / nrb; cb <= (v1 - 1) / nrb; ++cb) {
+          tab[a.oUS + (size_t)w * ncb + cb] = cnt[cb]++;
+          if (cnt[cb] > sl::kVaDxSlots) return "an fc1 column block spans more workgroups than the dx slots";
+        }
+      }
+      for (int cb = 0; cb < ncb; ++cb) tab[a.oU + cb] = cnt[cb];
+      return "";
+    };
+    {
+      const std::string e = fill();
+      if (!e.empty()) return e;
     }
     tab_ = at::tensor(tab, at::TensorOptions().dtype(at::kInt)).to(W_[0].device());
     return "";
