@@ -85,3 +85,41 @@ def test_persistent_vanilla_mid_epoch_failure_falls_back(cuda, tmp_path):
     a, b = _states(sq, "vanilla"), _states(sp, "vanilla")
     for k in a:
         assert torch.equal(a[k], b[k]), k
+
+
+def test_persistent_vanilla_update_runs_partition_the_tiles(cuda, tmp_path):
+    """The update-pass table (csrc/vanilla_exec.cpp tables): the G balanced column-major runs
+    partition fc1's tiles, each column block counts the runs touching it and numbers them in run
+    order (the dx partials' sum order, as when runs were dealt in order), and the runs are dealt
+    to workgroups by the row band they start in (workgroup w on XCD w % 8 stages ~1/4 of the row
+    blocks' dz1, not all of them)."""
+    from splitlearning_amd.protocols.split_native import _va_cfg
+    s = _session("vanilla", tmp_path, True, cuda, 16, persist=True)
+    ex = s.ops.C().VanillaEpoch(_va_cfg(s, 1))
+    assert ex.ok(), ex.why()
+    G = ex.workgroups()
+    tab = ex.table().cpu().tolist()
+    N1, K1 = s.tail.layers[0].W.shape
+    nrb, ncb, NC = (N1 + 15) // 16, (K1 + 255) // 256, G // 8
+    oU = G + 1 + 2 * nrb + NC
+    oUW, oUS = oU + ncb, oU + ncb + 4 * G
+    assert len(tab) == oUS + G * ncb
+    cbn = tab[oU:oU + ncb]
+    runs = [tab[oUW + 4 * w:oUW + 4 * w + 4] for w in range(G)]
+    assert all(r[2] == 0 and r[3] == nrb for r in runs)
+    T = nrb * ncb
+    assert sorted((r[0], r[1]) for r in runs) == [(k * T // G, (k + 1) * T // G) for k in range(G)]
+    seen = [0] * ncb
+    for v0, v1, _, _ in sorted(runs):
+        w = next(x for x in range(G) if runs[x][0] == v0 and runs[x][1] == v1)
+        for cb in range(ncb):
+            slot = tab[oUS + w * ncb + cb]
+            touches = v1 > v0 and v0 // nrb <= cb <= (v1 - 1) // nrb
+            assert (slot >= 0) == touches, (w, cb)
+            if touches:
+                assert slot == seen[cb], (w, cb)
+                seen[cb] += 1
+    assert seen == cbn
+    if G % 8 == 0 and nrb >= 64:
+        home = sum(1 for w in range(G) if (runs[w][0] % nrb) * 8 // nrb == w % 8)
+        assert home >= G - G // 16, home
