@@ -93,6 +93,9 @@ head_fwd_kernel(const float* __restrict__ P2, int S2, int64_t slab2, Epi e2, con
   // executor, us per server step: TP = 1 172.1 -> 170.3, TP = 8 52.6 -> 51.2 with head_bwd's
   // partial logits ahead of its W3 (profiles/r3h_head_load_order_ab.txt)
   const bool sfirst = !IPC && S2 <= 16;
+  // gridDim.z > 1 (wide heads: SISA-concat's k x 100 logits, no IPC): workgroup z takes output
+  // groups z, z + Z, ... (each group JU x 8 outputs); every z reduces the slabs, z = 0 stores h2
+  const int j00 = JU * (int)blockIdx.z, jstep = JU * (int)gridDim.z;
   f32x4 sv0 = {0.f, 0.f, 0.f, 0.f}, sv1 = sv0;
   if (sfirst) {
     const int cc = tid & (HS - 1), sg = tid >> 5;
@@ -102,7 +105,7 @@ head_fwd_kernel(const float* __restrict__ P2, int S2, int64_t slab2, Epi e2, con
       if (sg + 8 < S2) sv1 = src[(sg + 8) * (slab2 >> 2)];
     }
   }
-  load_w(0);
+  load_w(j00);
   if constexpr (IPC) {
     __shared__ int s_ok;
     if (wv == 0) {
@@ -163,7 +166,7 @@ head_fwd_kernel(const float* __restrict__ P2, int S2, int64_t slab2, Epi e2, con
       const int col = 4 * (qa + tid);
 #pragma unroll
       for (int i = 0; i < 4; ++i) o[i] = apply_epi(e2, v[i], m, col + i);
-      reinterpret_cast<f32x4*>(h2 + (int64_t)m * N2)[qa + tid] = o;
+      if (blockIdx.z == 0) reinterpret_cast<f32x4*>(h2 + (int64_t)m * N2)[qa + tid] = o;
     }
     hs[tid] = o;
   }
@@ -171,8 +174,8 @@ head_fwd_kernel(const float* __restrict__ P2, int S2, int64_t slab2, Epi e2, con
   // 2. partial logits: half-wave h (32 lanes = the slice's columns) owns output 8 j + 2 wv + h
   const f32x4 h = BF ? bfr4(hs[c]) : hs[c];
   float* dst = plog + ((int64_t)q * M + m) * C;
-  for (int j0 = 0; j0 * 8 < C; j0 += JU) {
-    if (j0) load_w(j0);
+  for (int j0 = j00; j0 * 8 < C; j0 += jstep) {
+    if (j0 != j00) load_w(j0);
 #pragma unroll
     for (int j = 0; j < JU; ++j) {
       const f32x4 wj = BF ? bfr4(w[j]) : w[j];
@@ -735,6 +738,10 @@ hipError_t server_head3(const float* P2, int S2, int64_t slab2, Epi e2, const fl
     return hipErrorInvalidValue;
   const IpcStep none{};
   const IpcStep& ip = ipc ? *ipc : none;
+  // a wide head's output groups (104 logits each) spread over gridDim.z: C = 800 (SISA-concat,
+  // k = 8) ran 128 workgroups of 8 groups each
+  dim3 gf = g;
+  if (ipc == nullptr) gf.z = (unsigned)std::max(1, std::min(8, (C + 103) / 104));
   if (ipc != nullptr) {
     if (g_bf16)
       head_fwd_kernel<true, true><<<g, 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C, ip);
@@ -742,9 +749,9 @@ hipError_t server_head3(const float* P2, int S2, int64_t slab2, Epi e2, const fl
       head_fwd_kernel<false, true><<<g, 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C, ip);
   } else {
     if (g_bf16)
-      head_fwd_kernel<true, false><<<g, 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C, none);
+      head_fwd_kernel<true, false><<<gf, 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C, none);
     else
-      head_fwd_kernel<false, false><<<g, 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C, none);
+      head_fwd_kernel<false, false><<<gf, 256, 0, st>>>(P2, S2, slab2, e2, W3, ldw3, h2, ws, M, N2, C, none);
   }
   launch_head_bwd(ws, b3, W3, ldw3, y, ignore, scale, e2.dscale, h2, dlog, dz2, loss_rows, M, N2, C, Q, Q, st, G,
                   gscale);
