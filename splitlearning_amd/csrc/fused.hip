@@ -246,6 +246,27 @@ head_bwd_kernel(const float* __restrict__ plog, const float* __restrict__ b3, co
         if (s < Qp) v += pv[s];
       lg[tid] = v;
     }
+  } else if (C <= 1024 && Qp <= 8) {
+    // wide heads (SISA-concat's k x 100 logits): up to 4 outputs per thread, all 32 partial
+    // loads in flight before the first sum (a loop per output took one round trip each), the
+    // same sums in the same order
+    float pw[4][8], bw[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int o = tid + 256 * u;
+      bw[u] = (o < C && b3) ? b3[o] : 0.f;
+#pragma unroll
+      for (int s = 0; s < 8; ++s) pw[u][s] = (o < C && s < Qp) ? plog[((int64_t)s * M + m) * C + o] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int o = tid + 256 * u;
+      float v = bw[u];
+#pragma unroll
+      for (int s = 0; s < 8; ++s)
+        if (s < Qp) v += pw[u][s];
+      if (o < C) lg[o] = v;
+    }
   } else {
     for (int o = tid; o < C; o += 256) {
       float v = b3 ? b3[o] : 0.f;
