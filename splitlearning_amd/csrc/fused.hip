@@ -612,7 +612,10 @@ wgrad_stream_kernel(WgGroup grp, int M, SlOpt o) {
   const bool kin = k < L.K;
   const f32x4 zv = {0.f, 0.f, 0.f, 0.f};
   int plw = 0, pls = 0, psw = 16, pss = 16;
-  pol_aux(grp.pol, plw, pls, psw, pss);
+  // with layer 0 pinned, the small layers (concat's fc2 / fc3, 70 MB) keep the over-the-cache
+  // form (W plain, m / v non-temporal): W2 / W3 are read again by the next kernels (fc2 forward
+  // 10.7 -> 8 us per concat step with W2 in the Infinity Cache)
+  pol_aux(l0 || grp.pin == 0 ? grp.pol : 1, plw, pls, psw, pss);
   const int lbytes = L.N * L.ldw * 4;   // grp.pol != 0 only for layers under 2 GB
   // one tile's state for this thread: W / m / v of (row 16 by + r, columns k .. k + 3), and the
   // wave's dZ[lane][16 by + r] in lanes 0-15
