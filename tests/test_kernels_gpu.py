@@ -418,7 +418,9 @@ def test_server_head3(cuda, M, S2, N2, C):
 @pytest.mark.parametrize("M,G", [(16, 2), (16, 4), (9, 8)])
 def test_server_head_grouped_cross_entropy(cuda, M, G):
     """G cross-entropy groups of 100 logits (SISA-concat's k heads): per-(row, group) label,
-    scale and loss; ignored (row, group) pairs give zero loss and zero dlogits."""
+    scale and loss; ignored (row, group) pairs give zero loss and zero dlogits.  G = 4 / 8 (C =
+    400 / 800) take head_fwd's output groups over gridDim.z and head_bwd's wide partial-logit
+    reads (csrc/fused.hip)."""
     g = torch.Generator().manual_seed(G)
     N2, C = 1000, 100 * G
     P2 = (torch.randn(4, M, N2, generator=g) * 0.5).to(cuda)
