@@ -133,12 +133,14 @@ __device__ __forceinline__ bool hy_seam_wait(const HyArgs& a, int seam, unsigned
 // store write-through; W and m kept 149.2, W write-through 148.0;
 // profiles/r4w_hybrid_per_array_cache_policy_ab.txt).  When it fits (TP = 2 / 4), every
 // array write-through: 85.5 / 58.6 against 87.1 / 60.7 plain and 96.9 / 63.4 non-temporal.
-// The same workgroup (same CU) reads a tile again next step.  On top, one workgroup in 8
-// keeps its m tiles plain as well (13.5 MB more in the cache): 142.5-142.8 vs 144.8-145.0
-// (one in 2 or 4: 143.3-143.8).
+// The same workgroup (same CU) reads a tile again next step.  On top, one workgroup in 4
+// keeps its m tiles plain as well (27 MB more in the cache).  Round 4: one in 8 142.5-142.8 vs
+// 144.8-145.0 without (one in 2 or 4: 143.3-143.8); on the round-6 kernel one in 4 is the better
+// (two boxes, interleaved: 136.4-137.2 vs 137.4-138.1; a third neutral; all m plain 136.5-136.8
+// vs 133.8-135.5 -- profiles/r6_hybrid/keep_m_ab.txt).
 constexpr int kStW = 0, kStM = 2, kStV = 2;
 constexpr int kLdW = 0, kLdM = 2, kLdV = 2;
-constexpr int kKeepM = 7;
+constexpr int kKeepM = 3;
 constexpr int kStFit = 16;
 
 // fc2 column block of fc2 column (= fc1 shard row) float4 group n4: blocks [q0_b, q0_{b+1})
